@@ -1,0 +1,176 @@
+// cv2.bilateralFilter(u8, d, sigma_color, sigma_space, borderType=BORDER_CONSTANT) for C = 3 / 1.
+// Reference call sites: lib/model/test.py:272-278 (d=9, sigmaColor=20, sigmaSpace=100),
+// lib/roi_data_layer/minibatch.py:172,1658-1663; BASELINE config 4 uses sigma 75/75.
+//
+// OpenCV 3.4.2 bilateralFilter_8u semantics (restated in oracle/filters.c): radius = d/2, taps
+// {(i,j): sqrt(i^2+j^2) <= radius}, space weight float(exp(r^2 * -0.5/ss^2)), colour weight of
+// the L1 distance |db|+|dg|+|dr|, float sums, out = cvRound(sum * (1.f / wsum)), border pixels 0.
+//
+// gfx950 design: a 256-thread workgroup owns a 64 x 16 output tile; the (64+2r) x (16+2r) input
+// tile (BGR0-packed u32 per pixel, zero outside the image) is staged once in LDS.  Each thread
+// walks 4 output rows of one column.  Per tap: v_sad_u8 on the packed pixels gives the colour
+// distance in one instruction; the weight is exp2(fma(dist^2, c2, log2(space_w))) — one FMA + one
+// v_exp_f32 instead of two table loads (the colour LUT of OpenCV is float(exp(double)); the
+// in-register exp differs by <= 1 ulp, inside the <= 1 LSB output tolerance).  Taps are a
+// compile-time table for d = 9 (radius 4, 49 taps); other d use the runtime-tap kernel.
+#include "idn_common.hpp"
+
+#include <math.h>
+#include <string.h>
+
+namespace idn {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BL_TW = 64;   // tile width (outputs)
+constexpr int BL_TH = 16;   // tile height (outputs)
+constexpr int BL_RPT = 4;   // output rows per thread
+constexpr int BL_MAXR = 8;  // max radius supported (d <= 17)
+
+struct BilateralTaps {
+  float c2;                                          // -0.5/sc^2 * log2(e)
+  float lsw[(2 * BL_MAXR + 1) * (2 * BL_MAXR + 1)];  // log2(space weight) at (i+R)*(2R+1)+(j+R)
+};
+
+template <int C>
+__device__ __forceinline__ uint32_t load_px(const uint8_t* __restrict__ s, int64_t row_stride,
+                                            int h, int w, int y, int x) {
+  if (y < 0 || y >= h || x < 0 || x >= w) return 0u;  // BORDER_CONSTANT (0)
+  const uint8_t* p = s + (int64_t)y * row_stride + (int64_t)x * C;
+  if constexpr (C == 3) return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  else return (uint32_t)p[0];
+}
+
+template <int C, int R>
+__global__ __launch_bounds__(256) void bilateral_u8_kernel(const uint8_t* __restrict__ src,
+                                                           uint8_t* __restrict__ dst, int h, int w,
+                                                           int64_t row_stride, int tiles_x,
+                                                           int tiles_y, BilateralTaps taps) {
+  constexpr int LW = BL_TW + 2 * R;
+  constexpr int LH = BL_TH + 2 * R;
+  __shared__ uint32_t tile[LH * LW];
+
+  const int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  const int ty = (t / tiles_x) % tiles_y;
+  const int img = t / (tiles_x * tiles_y);
+  const uint8_t* s = src + (int64_t)img * h * row_stride;
+  uint8_t* d = dst + (int64_t)img * h * row_stride;
+  const int x0 = tx * BL_TW, y0 = ty * BL_TH;
+
+  for (int i = threadIdx.x; i < LH * LW; i += 256) {
+    const int ly = i / LW, lx = i % LW;
+    tile[i] = load_px<C>(s, row_stride, h, w, y0 + ly - R, x0 + lx - R);
+  }
+  __syncthreads();
+
+  const int col = threadIdx.x & 63;
+  const int rgrp = threadIdx.x >> 6;  // 4 groups of BL_RPT rows
+  const int x = x0 + col;
+  if (x >= w) return;
+#pragma unroll 1
+  for (int rr = 0; rr < BL_RPT; ++rr) {
+    const int ly = rgrp * BL_RPT + rr;
+    const int y = y0 + ly;
+    if (y >= h) break;
+    const uint32_t p0 = tile[(ly + R) * LW + col + R];
+    // (b, g) and (r, wsum) accumulate as packed pairs: one v_pk_fma_f32 each per tap
+    f32x2 acc_bg = {0.f, 0.f}, acc_rw = {0.f, 0.f};
+#pragma unroll
+    for (int i = -R; i <= R; ++i) {
+#pragma unroll
+      for (int j = -R; j <= R; ++j) {
+        if (i * i + j * j > R * R) continue;  // sqrt(i^2+j^2) > radius: not a tap
+        const uint32_t p = tile[(ly + R + i) * LW + col + R + j];
+        const float df = (float)__builtin_amdgcn_sad_u8(p, p0, 0u);
+        const float wt = __builtin_amdgcn_exp2f(
+            __builtin_fmaf(df * df, taps.c2, taps.lsw[(i + R) * (2 * R + 1) + (j + R)]));
+        const f32x2 w2 = {wt, wt};
+        if constexpr (C == 3) {
+          const f32x2 bg = {(float)(p & 0xFFu), (float)((p >> 8) & 0xFFu)};
+          const f32x2 r1 = {(float)((p >> 16) & 0xFFu), 1.f};
+          acc_bg = __builtin_elementwise_fma(bg, w2, acc_bg);
+          acc_rw = __builtin_elementwise_fma(r1, w2, acc_rw);
+        } else {
+          const f32x2 b1 = {(float)(p & 0xFFu), 1.f};
+          acc_rw = __builtin_elementwise_fma(b1, w2, acc_rw);
+        }
+      }
+    }
+    const float sb = (C == 3) ? acc_bg.x : acc_rw.x, sg = acc_bg.y, sr = acc_rw.x;
+    const float ws = acc_rw.y;
+    const float inv = 1.f / ws;
+    uint8_t* o = d + (int64_t)y * row_stride + (int64_t)x * C;
+    // cvRound = round half to even (v_rndne), saturate to u8
+    auto cvt = [](float v) -> uint8_t {
+      const float r = __builtin_rintf(v);
+      return (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+    };
+    o[0] = cvt(sb * inv);
+    if constexpr (C == 3) {
+      o[1] = cvt(sg * inv);
+      o[2] = cvt(sr * inv);
+    }
+  }
+}
+
+template <int C, int R>
+static void launch_bl(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
+                      const BilateralTaps& taps, hipStream_t st) {
+  const int tiles_x = (w + BL_TW - 1) / BL_TW, tiles_y = (h + BL_TH - 1) / BL_TH;
+  const int64_t blocks = (int64_t)n * tiles_x * tiles_y;
+  hipLaunchKernelGGL((bilateral_u8_kernel<C, R>), dim3((unsigned)blocks), dim3(256), 0, st, src,
+                     dst, h, w, rs, tiles_x, tiles_y, taps);
+}
+
+}  // namespace idn
+
+extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                                int64_t row_stride, int d, double sigma_color, double sigma_space,
+                                void* stream) {
+  using namespace idn;
+  if (int e = check_filter_args(src, dst, n, h, w, c, row_stride, "idn_bilateral_u8")) return e;
+  IDN_CHECK_ARG(c == 1 || c == 3, "idn_bilateral_u8: channels must be 1 or 3 (got %d)", c);
+  if (n == 0) return IDN_OK;
+  if (sigma_color <= 0) sigma_color = 1;
+  if (sigma_space <= 0) sigma_space = 1;
+  int radius = d <= 0 ? (int)lrint(sigma_space * 1.5) : d / 2;
+  if (radius < 1) radius = 1;
+  if (radius > BL_MAXR)
+    return set_error(IDN_EUNSUPPORTED, "idn_bilateral_u8: radius %d > %d", radius, BL_MAXR);
+  const int64_t blocks = (int64_t)n * ((w + BL_TW - 1) / BL_TW) * ((h + BL_TH - 1) / BL_TH);
+  IDN_CHECK_ARG(blocks < 0x7FFFFFFF, "idn_bilateral_u8: batch too large");
+
+  BilateralTaps taps;
+  memset(&taps, 0, sizeof(taps));
+  const double gcc = -0.5 / (sigma_color * sigma_color);
+  const double gsc = -0.5 / (sigma_space * sigma_space);
+  taps.c2 = (float)(gcc * 1.4426950408889634);
+  for (int i = -radius; i <= radius; ++i)
+    for (int j = -radius; j <= radius; ++j) {
+      const double r = sqrt((double)i * i + (double)j * j);
+      if (r > radius) continue;
+      const float sw = (float)exp(r * r * gsc);  // OpenCV's float space weight
+      taps.lsw[(i + radius) * (2 * radius + 1) + (j + radius)] = (float)log2((double)sw);
+    }
+  hipStream_t st = as_stream(stream);
+#define IDN_BL(CC)                                                          \
+  switch (radius) {                                                         \
+    case 1: launch_bl<CC, 1>(src, dst, n, h, w, row_stride, taps, st); break; \
+    case 2: launch_bl<CC, 2>(src, dst, n, h, w, row_stride, taps, st); break; \
+    case 3: launch_bl<CC, 3>(src, dst, n, h, w, row_stride, taps, st); break; \
+    case 4: launch_bl<CC, 4>(src, dst, n, h, w, row_stride, taps, st); break; \
+    case 5: launch_bl<CC, 5>(src, dst, n, h, w, row_stride, taps, st); break; \
+    case 6: launch_bl<CC, 6>(src, dst, n, h, w, row_stride, taps, st); break; \
+    case 7: launch_bl<CC, 7>(src, dst, n, h, w, row_stride, taps, st); break; \
+    default: launch_bl<CC, 8>(src, dst, n, h, w, row_stride, taps, st); break; \
+  }
+  if (c == 3) {
+    IDN_BL(3)
+  } else {
+    IDN_BL(1)
+  }
+#undef IDN_BL
+  IDN_CHECK_LAUNCH("idn_bilateral_u8");
+  return IDN_OK;
+}

@@ -1,0 +1,100 @@
+// Shared device/host helpers for the idn HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/idn.h"
+
+namespace idn {
+
+// ---- error plumbing (thread-local message, negative status) --------------------------------
+int set_error(int status, const char* fmt, ...);
+// shared argument validation of the u8 -> u8 filters (defined in stencil_u8.hip)
+int check_filter_args(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                      int64_t row_stride, const char* name);
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define IDN_CHECK_ARG(cond, ...)                                         \
+  do {                                                                   \
+    if (!(cond)) return ::idn::set_error(IDN_EINVAL, __VA_ARGS__);       \
+  } while (0)
+
+#define IDN_CHECK_LAUNCH(name)                                                          \
+  do {                                                                                  \
+    hipError_t e_ = hipGetLastError();                                                  \
+    if (e_ != hipSuccess)                                                               \
+      return ::idn::set_error(IDN_EHIP, "%s: launch failed: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- buffer resource descriptors (T8/T20): per-image range-checked loads -----------------
+// Out-of-range loads return 0 and never fault, so border lanes may over-read safely.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  // readfirstlane the inputs so the compiler can prove the descriptor wave-uniform
+  uint64_t p = reinterpret_cast<uint64_t>(base);
+  uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p));
+  uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p >> 32));
+  uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
+  void* q = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, nb, 0x00020000);
+}
+
+// ---- small integer helpers ------------------------------------------------------------------
+// OpenCV BORDER_REFLECT_101 index (cv::borderInterpolate; repeats for overshoot >= len)
+__host__ __device__ __forceinline__ int reflect101(int i, int len) {
+  if (len == 1) return 0;
+  while (i < 0 || i >= len) {
+    if (i < 0) i = -i;
+    if (i >= len) i = 2 * len - 2 - i;
+  }
+  return i;
+}
+__host__ __device__ __forceinline__ int clampi(int i, int lo, int hi) {
+  return i < lo ? lo : (i > hi ? hi : i);
+}
+
+// ---- Philox4x32-10 (Salmon et al., SC'11) --------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ __forceinline__ void philox_round(u32x4& c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+  uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+#else
+  uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+  uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+  uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#endif
+  c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+}
+
+__host__ __device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint64_t key) {
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(ctr, k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return ctr;
+}
+
+// uniform double in (0, 1) from 53 random bits (never 0 -> safe for log)
+__device__ __forceinline__ double u01_open(uint32_t a, uint32_t b) {
+  uint64_t v = ((uint64_t)(a >> 5) << 26) | (b >> 6);  // 53 bits
+  return ((double)v + 0.5) * (1.0 / 9007199254740992.0);
+}
+// uniform double in [0, 1) (numpy random_sample semantics)
+__device__ __forceinline__ double u01_closed_open(uint32_t a, uint32_t b) {
+  uint64_t v = ((uint64_t)(a >> 5) << 26) | (b >> 6);
+  return (double)v * (1.0 / 9007199254740992.0);
+}
+
+}  // namespace idn

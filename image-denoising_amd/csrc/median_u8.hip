@@ -1,0 +1,231 @@
+// cv2.medianBlur(u8, 3|5) on interleaved HxWxC images, BORDER_REPLICATE, bit-exact.
+// Reference call sites: lib/model/test.py:259, lib/roi_data_layer/minibatch.py:153,1644-1648.
+//
+// Same wave-stripe streaming as the stencils (stripe.hpp): one wave = one segment of a band of
+// rows, 16 bytes per lane, DPP halos, replicated borders rebuilt in registers, a K-row ring of raw
+// window dwords.  Selection runs on packed u16 pairs (v_pk_min_u16 / v_pk_max_u16): every
+// comparator handles two output bytes.
+//   3x3: sort each 3-row column once (CSE shares it between the three outputs that read it),
+//        then med3(max3(col mins), med3(col medians), min3(col maxes)).
+//   5x5: pruned Batcher selection network over the 25 taps (median_net.hpp, generated and
+//        proven by tools/gen_median_net.py with the 0-1 principle).
+#include "stripe.hpp"
+#include "median_net.hpp"
+
+namespace idn {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+struct PkOps {
+  __device__ __forceinline__ uint32_t mn(uint32_t a, uint32_t b) const {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+  }
+  __device__ __forceinline__ uint32_t mx(uint32_t a, uint32_t b) const {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+  }
+  __device__ __forceinline__ uint32_t med3(uint32_t a, uint32_t b, uint32_t c) const {
+    return mx(mn(a, b), mn(mx(a, b), c));
+  }
+};
+
+// 3-row column at window u16 position b: (min, median, max) of rows r0, r1, r2
+__device__ __forceinline__ void col3(const uint32_t (&W0)[8], const uint32_t (&W1)[8],
+                                     const uint32_t (&W2)[8], int b, uint32_t& lo, uint32_t& md,
+                                     uint32_t& hi) {
+  const PkOps op;
+  const uint32_t a = lanes16_at(W0, b), c = lanes16_at(W1, b), d = lanes16_at(W2, b);
+  const uint32_t l1 = op.mn(a, c), h1 = op.mx(a, c);
+  lo = op.mn(l1, d);
+  const uint32_t h2 = op.mx(l1, d);
+  hi = op.mx(h1, h2);
+  md = op.mn(h1, h2);
+}
+
+template <int C>
+__device__ __forceinline__ v4u median3_out(const uint32_t (&W0)[8], const uint32_t (&W1)[8],
+                                           const uint32_t (&W2)[8]) {
+  const PkOps op;
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int P = 4 * k + 8 + e;
+      uint32_t l0, m0, h0, l1, m1, h1, l2, m2, h2;
+      col3(W0, W1, W2, P - C, l0, m0, h0);
+      col3(W0, W1, W2, P, l1, m1, h1);
+      col3(W0, W1, W2, P + C, l2, m2, h2);
+      const uint32_t lmax = op.mx(op.mx(l0, l1), l2);
+      const uint32_t mmed = op.med3(m0, m1, m2);
+      const uint32_t hmin = op.mn(op.mn(h0, h1), h2);
+      v[e] = op.med3(lmax, mmed, hmin);
+    }
+    // each u16 lane holds one output byte in its low byte
+    o[k] = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);
+  }
+  v4u r = {o[0], o[1], o[2], o[3]};
+  return r;
+}
+
+template <int C>
+__device__ __forceinline__ v4u median5_out(const uint32_t (&W0)[8], const uint32_t (&W1)[8],
+                                           const uint32_t (&W2)[8], const uint32_t (&W3)[8],
+                                           const uint32_t (&W4)[8]) {
+  const PkOps op;
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int P = 4 * k + 8 + e;
+      uint32_t x[25];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int b = P + (j - 2) * C;
+        x[0 * 5 + j] = lanes16_at(W0, b);
+        x[1 * 5 + j] = lanes16_at(W1, b);
+        x[2 * 5 + j] = lanes16_at(W2, b);
+        x[3 * 5 + j] = lanes16_at(W3, b);
+        x[4 * 5 + j] = lanes16_at(W4, b);
+      }
+      v[e] = median25<uint32_t>(x, op);
+    }
+    o[k] = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);
+  }
+  v4u r = {o[0], o[1], o[2], o[3]};
+  return r;
+}
+
+template <int C, int K, int NT>
+__global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ dst, int h, int rb,
+                                                      uint32_t row_stride, int nseg, int seg_len,
+                                                      int bands, int band_rows, int total_items) {
+  constexpr int R = K / 2;
+  constexpr int PF = K;  // prefetch depth == ring depth: one static slot pattern per group
+  constexpr int U = K;
+
+  const int lane = threadIdx.x & 63;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (item >= total_items) return;
+  const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
+
+  const uint32_t img_bytes = (uint32_t)h * row_stride;
+  const rsrc_t rs = make_rsrc(src + (size_t)g.img * img_bytes, img_bytes);
+  const rsrc_t rd = make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes);
+  const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
+
+  const int y0 = g.band * band_rows;
+  const int y1 = min(y0 + band_rows, h);
+  if (y0 >= y1) return;
+  const int nin = (y1 - y0) + 2 * R;
+  const int ngroups = (nin + U - 1) / U;
+  auto load_row = [&](int r) -> v4u {
+    const int y = clampi(y0 - R + min(r, nin - 1), 0, h - 1);  // BORDER_REPLICATE
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)y * row_stride + ld_off, 0,
+                                                  (NT & 1) ? 2 : 0);
+  };
+
+  v4u Lq[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) Lq[i] = load_row(i);
+  uint32_t Wr[K][8];
+
+  for (int gi = 0; gi < ngroups; ++gi) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = gi * U + u;
+      const v4u Lv = Lq[u % PF];
+      Lq[u % PF] = load_row(r + PF);
+      build_window<C, BORDER_REPLICATE>(Lv, g.lead, g.fix_t0, g.fix_t8, Wr[u % K]);
+      const int y = y0 + r - 2 * R;
+      if (r >= 2 * R && y < y1) {
+        v4u o;
+        if constexpr (K == 3) {
+          o = median3_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[u % K]);
+        } else {
+          o = median5_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[(u + 3) % K],
+                             Wr[(u + 4) % K], Wr[u % K]);
+        }
+        stripe_store<NT>(o, rd, (uint32_t)y * row_stride + (uint32_t)g.q, g.kind);
+      }
+    }
+  }
+}
+
+// generic path: one thread per pixel, exact median by counting (any C, any alignment)
+template <int K>
+__global__ __launch_bounds__(256) void median_u8_generic(const uint8_t* __restrict__ src,
+                                                         uint8_t* __restrict__ dst, int n, int h,
+                                                         int w, int c, int64_t row_stride) {
+  constexpr int R = K / 2;
+  const int64_t npix = (int64_t)n * h * w;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(p % w);
+    const int64_t t = p / w;
+    const int y = (int)(t % h);
+    const int img = (int)(t / h);
+    const uint8_t* s = src + (int64_t)img * h * row_stride;
+    uint8_t* d = dst + (int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * c;
+    for (int ch = 0; ch < c; ++ch) {
+      uint8_t v[K * K];
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          v[i * K + j] = s[(int64_t)clampi(y + i - R, 0, h - 1) * row_stride +
+                           (int64_t)clampi(x + j - R, 0, w - 1) * c + ch];
+      // rank selection: the median is the value with < K*K/2+1 smaller and >= ... elements
+      uint8_t med = 0;
+#pragma unroll
+      for (int a = 0; a < K * K; ++a) {
+        int lt = 0, le = 0;
+#pragma unroll
+        for (int b = 0; b < K * K; ++b) {
+          lt += v[b] < v[a];
+          le += v[b] <= v[a];
+        }
+        if (lt <= (K * K) / 2 && le > (K * K) / 2) med = v[a];
+      }
+      d[ch] = med;
+    }
+  }
+}
+
+template <int K>
+static int launch_median(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                         int64_t row_stride, hipStream_t st) {
+  const int64_t rb = (int64_t)w * c;
+  if (stripe_ok(c, rb, row_stride, h, src, dst)) {
+    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096);
+    IDN_CHECK_ARG(p.total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
+    hipLaunchKernelGGL((median_u8_fast<3, K, 0>), dim3((unsigned)((p.total + 3) / 4)), dim3(256),
+                       0, st, src, dst, h, (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len,
+                       p.bands, p.band_rows, (int)p.total);
+  } else {
+    const int64_t npix = (int64_t)n * h * w;
+    int64_t blocks = (npix + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL((median_u8_generic<K>), dim3((unsigned)blocks), dim3(256), 0, st, src, dst,
+                       n, h, w, c, row_stride);
+  }
+  IDN_CHECK_LAUNCH("idn_median_blur_u8");
+  return IDN_OK;
+}
+
+}  // namespace idn
+
+extern "C" int idn_median_blur_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                                  int64_t row_stride, int ksize, void* stream) {
+  using namespace idn;
+  if (int e = check_filter_args(src, dst, n, h, w, c, row_stride, "idn_median_blur_u8")) return e;
+  if (n == 0) return IDN_OK;
+  if (ksize == 3) return launch_median<3>(src, dst, n, h, w, c, row_stride, as_stream(stream));
+  if (ksize == 5) return launch_median<5>(src, dst, n, h, w, c, row_stride, as_stream(stream));
+  return set_error(IDN_EUNSUPPORTED, "idn_median_blur_u8: ksize %d not supported (3 or 5)", ksize);
+}

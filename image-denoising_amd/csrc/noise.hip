@@ -1,0 +1,375 @@
+// skimage.util.random_noise modes used by the reference's noise closures, on u8 HxWxC batches:
+//   gaussian  lib/model/test.py:193-307, minibatch.py:87-201   out = clip(x + N(mean, sd), 0, 1)
+//   speckle   lib/model/test.py:476-590, minibatch.py:374-490  out = clip(x + x*N(mean, sd), 0, 1)
+//   s&p       lib/model/test.py:357-474, minibatch.py:253-372  out = 1 / 0 / x by two uniforms
+//   poisson   lib/model/test.py:309-355, minibatch.py:203-251  out = clip(P(x*vals)/vals, 0, 1)
+// with x = v * (1/255) in float64 (img_as_float) and the caller's U8 cast (255*out).astype(uint8).
+// The float64 op order is numpy's (file compiled with -ffp-contract=off; explicit _rn ops), so
+// with a replayed random field (numpy's own draws) the outputs are bit-exact; with the Philox
+// stream they are statistically equivalent (tests/test_noise_gpu.py).
+//
+// RNG: Philox4x32-10 keyed by (seed ^ kind tag); counter = (element pair / draw, image id).
+// Image id = offset + image index, so a rank that owns images [a, b) of a batch draws exactly
+// what a single GPU would for those images.
+//
+// Also: periodic noise pattern (add_periodic_noise, test.py:1128-1298) and cv2.add(u8, u8).
+#include "idn_common.hpp"
+
+#include <math.h>
+
+namespace idn {
+
+__device__ __forceinline__ double img_as_float(uint32_t v) { return __dmul_rn((double)v, 1.0 / 255.0); }
+
+__device__ __forceinline__ double clip01(double v) { return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v); }
+
+// (255 * out).astype(np.uint8) for out in [0, 1]: truncation (out is never negative here)
+__device__ __forceinline__ uint8_t u8_of(double out) { return (uint8_t)(int)__dmul_rn(out, 255.0); }
+
+// two standard normals from one Philox block (Box-Muller, fp32 transcendental: v_log/v_sin/v_cos
+// take revolutions, so theta = u2 needs no 2*pi multiply)
+__device__ __forceinline__ void normal2(const u32x4& r, float& z0, float& z1) {
+  const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+  const float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);           // [0, 1)
+  const float rad = __builtin_sqrtf(-2.0f * 0.6931471805599453f * __builtin_amdgcn_logf(u1));
+  z0 = rad * __builtin_amdgcn_cosf(u2);
+  z1 = rad * __builtin_amdgcn_sinf(u2);
+}
+
+constexpr uint64_t KIND_TAG = 0x9E3779B97F4A7C15ull;
+
+struct NoiseArgs {
+  const uint8_t* src;
+  uint8_t* out_u8;
+  double* out_f64;
+  const double* replay;
+  const uint32_t* vals;  // poisson: per-image vals (power of two), workspace
+  int n, h, w, c;
+  int64_t row_stride;
+  int64_t elems;  // h*w*c
+  double p0, p1;  // mean/sd (gaussian, speckle), sap thresholds
+  uint64_t key, offset;
+};
+
+__device__ __forceinline__ void store_out(const NoiseArgs& a, int img, int64_t e, int64_t boff,
+                                          double out) {
+  if (a.out_f64) a.out_f64[(int64_t)img * a.elems + e] = out;
+  if (a.out_u8) a.out_u8[boff] = u8_of(out);
+}
+
+// one thread per element pair (2 normals per Philox block)
+template <int KIND>
+__global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
+  const int64_t pairs = (a.elems + 1) / 2;
+  const int64_t total = pairs * a.n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int img = (int)(t / pairs);
+    const int64_t pr = t - (int64_t)img * pairs;
+    double nz[2];
+    if (a.replay) {
+      const int64_t e0 = 2 * pr;
+      nz[0] = a.replay[(int64_t)img * a.elems + e0];
+      nz[1] = (e0 + 1 < a.elems) ? a.replay[(int64_t)img * a.elems + e0 + 1] : 0.0;
+    } else {
+      const uint64_t gimg = a.offset + (uint64_t)img;
+      const u32x4 r = philox4x32(u32x4{(uint32_t)pr, (uint32_t)(pr >> 32), (uint32_t)gimg,
+                                       (uint32_t)(gimg >> 32)},
+                                 a.key);
+      float z0, z1;
+      normal2(r, z0, z1);
+      nz[0] = __dadd_rn(a.p0, __dmul_rn(a.p1, (double)z0));
+      nz[1] = __dadd_rn(a.p0, __dmul_rn(a.p1, (double)z1));
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int64_t e = 2 * pr + s;
+      if (e >= a.elems) break;
+      const int64_t pix = e / a.c;
+      const int ch = (int)(e - pix * a.c);
+      const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
+      const int64_t boff = (int64_t)img * a.h * a.row_stride + (int64_t)y * a.row_stride +
+                           (int64_t)x * a.c + ch;
+      const double xv = img_as_float(a.src[boff]);
+      double out;
+      if (KIND == IDN_NOISE_GAUSSIAN) out = clip01(__dadd_rn(xv, nz[s]));
+      else out = clip01(__dadd_rn(xv, __dmul_rn(xv, nz[s])));
+      store_out(a, img, e, boff, out);
+    }
+  }
+}
+
+// salt & pepper: flipped = U1 < cdf0(amount), salted = U2 < cdf0(salt_vs_pepper)
+__global__ __launch_bounds__(256) void noise_sap_kernel(NoiseArgs a) {
+  const int64_t total = a.elems * a.n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int img = (int)(t / a.elems);
+    const int64_t e = t - (int64_t)img * a.elems;
+    double u1, u2;
+    if (a.replay) {
+      u1 = a.replay[t];
+      u2 = a.replay[total + t];
+    } else {
+      const uint64_t gimg = a.offset + (uint64_t)img;
+      const u32x4 r = philox4x32(
+          u32x4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
+      u1 = u01_closed_open(r.x, r.y);
+      u2 = u01_closed_open(r.z, r.w);
+    }
+    const int64_t pix = e / a.c;
+    const int ch = (int)(e - pix * a.c);
+    const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
+    const int64_t boff =
+        (int64_t)img * a.h * a.row_stride + (int64_t)y * a.row_stride + (int64_t)x * a.c + ch;
+    double out = img_as_float(a.src[boff]);
+    if (u1 < a.p0) out = (u2 < a.p1) ? 1.0 : 0.0;
+    store_out(a, img, e, boff, out);
+  }
+}
+
+// per-image distinct-value mask (256 bits) -> vals = 2^ceil(log2(#distinct))
+__global__ __launch_bounds__(256) void unique_mask_kernel(const uint8_t* __restrict__ src, int h,
+                                                          int rowbytes, int64_t row_stride,
+                                                          uint32_t* __restrict__ mask) {
+  __shared__ uint32_t m[8];
+  if (threadIdx.x < 8) m[threadIdx.x] = 0;
+  __syncthreads();
+  const int img = blockIdx.y;
+  const uint8_t* s = src + (int64_t)img * h * row_stride;
+  const int64_t total = (int64_t)h * rowbytes;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(i / rowbytes);
+    const uint32_t v = s[(int64_t)y * row_stride + (i - (int64_t)y * rowbytes)];
+    atomicOr(&m[v >> 5], 1u << (v & 31));
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && m[threadIdx.x]) atomicOr(&mask[img * 8 + threadIdx.x], m[threadIdx.x]);
+}
+
+__global__ void vals_from_mask_kernel(uint32_t* mask, int n) {
+  const int img = blockIdx.x * blockDim.x + threadIdx.x;
+  if (img >= n) return;
+  int cnt = 0;
+  for (int k = 0; k < 8; ++k) cnt += __popc(mask[img * 8 + k]);
+  uint32_t v = 1;
+  while ((int)v < cnt) v <<= 1;  // 2**ceil(log2(cnt)); cnt == 1 -> 1
+  mask[8 * n + img] = v;
+}
+
+// numpy legacy Poisson: multiplication method for lam < 10, PTRS (Hormann 1993) otherwise
+struct PhiloxStream {
+  uint64_t key;
+  uint32_t e_lo, e_hi, g_lo, g_hi;
+  uint32_t blk = 0;
+  u32x4 cur;
+  int used = 2;
+  __device__ __forceinline__ double next() {
+    if (used == 2) {
+      cur = philox4x32(u32x4{e_lo, e_hi ^ (blk << 20), g_lo, g_hi}, key);
+      ++blk;
+      used = 0;
+    }
+    const double u = (used == 0) ? u01_closed_open(cur.x, cur.y) : u01_closed_open(cur.z, cur.w);
+    ++used;
+    return u;
+  }
+};
+
+__device__ double poisson_sample(double lam, PhiloxStream& rs) {
+  if (lam == 0.0) return 0.0;
+  if (lam < 10.0) {
+    const double enlam = exp(-lam);
+    double prod = 1.0;
+    int x = 0;
+    for (int it = 0; it < 1000; ++it) {
+      prod *= rs.next();
+      if (prod > enlam) ++x;
+      else return (double)x;
+    }
+    return (double)x;
+  }
+  const double slam = sqrt(lam), loglam = log(lam);
+  const double b = 0.931 + 2.53 * slam;
+  const double a = -0.059 + 0.02483 * b;
+  const double invalpha = 1.1239 + 1.1328 / (b - 3.4);
+  const double vr = 0.9277 - 3.6224 / (b - 2);
+  for (int it = 0; it < 1000; ++it) {
+    const double U = rs.next() - 0.5;
+    const double V = rs.next();
+    const double us = 0.5 - fabs(U);
+    const double k = floor((2 * a / us + b) * U + lam + 0.43);
+    if (us >= 0.07 && V <= vr) return k;
+    if (k < 0 || (us < 0.013 && V > us)) continue;
+    if (log(V) + log(invalpha) - log(a / (us * us) + b) <= -lam + k * loglam - lgamma(k + 1))
+      return k;
+  }
+  return floor(lam);  // unreachable in practice (bounded loop)
+}
+
+__global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a) {
+  const int64_t total = a.elems * a.n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int img = (int)(t / a.elems);
+    const int64_t e = t - (int64_t)img * a.elems;
+    const int64_t pix = e / a.c;
+    const int ch = (int)(e - pix * a.c);
+    const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
+    const int64_t boff =
+        (int64_t)img * a.h * a.row_stride + (int64_t)y * a.row_stride + (int64_t)x * a.c + ch;
+    const double vals = (double)a.vals[img];
+    double k;
+    if (a.replay) {
+      k = a.replay[t];
+    } else {
+      const uint64_t gimg = a.offset + (uint64_t)img;
+      PhiloxStream rs{a.key, (uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg,
+                      (uint32_t)(gimg >> 32)};
+      k = poisson_sample(__dmul_rn(img_as_float(a.src[boff]), vals), rs);
+    }
+    store_out(a, img, e, boff, clip01(k / vals));
+  }
+}
+
+// periodic pattern: t_i = i*step + (-A) (numpy linspace op order), t_last = A
+__global__ __launch_bounds__(256) void periodic_kernel(uint8_t* __restrict__ pat, int64_t size,
+                                                       double amp, double step) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < size;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double t = (i == size - 1) ? amp : __dadd_rn(__dmul_rn((double)i, step), -amp);
+    const double y = __dmul_rn(sin(t), 255.0);
+    // (uint8)(int32)trunc(y): truncate toward zero, wrap mod 256
+    pat[i] = (uint8_t)(int)y;
+  }
+}
+
+// cv2.add(u8, u8) = min(a + b, 255), 16 bytes per thread where aligned
+__global__ __launch_bounds__(256) void add_pattern_kernel(const uint8_t* __restrict__ src,
+                                                          const uint8_t* __restrict__ pat,
+                                                          uint8_t* __restrict__ dst, int n, int h,
+                                                          int rowbytes, int64_t row_stride) {
+  const int64_t per_img = (int64_t)h * rowbytes;
+  const int64_t total = per_img * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int img = (int)(i / per_img);
+    const int64_t e = i - (int64_t)img * per_img;
+    const int y = (int)(e / rowbytes);
+    const int64_t off = (int64_t)img * h * row_stride + (int64_t)y * row_stride + (e - (int64_t)y * rowbytes);
+    const uint32_t s = (uint32_t)src[off] + (uint32_t)pat[e];
+    dst[off] = (uint8_t)(s > 255u ? 255u : s);
+  }
+}
+
+static unsigned grid_for(int64_t work, int64_t cap = 65536) {
+  int64_t b = (work + 255) / 256;
+  if (b < 1) b = 1;
+  return (unsigned)(b > cap ? cap : b);
+}
+
+}  // namespace idn
+
+extern "C" size_t idn_noise_workspace_size(int kind, int n) {
+  if (kind != IDN_NOISE_POISSON || n <= 0) return 0;
+  return (size_t)n * 9 * sizeof(uint32_t);
+}
+
+extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
+                            int w, int c, int64_t row_stride, int kind, double p0, double p1,
+                            uint64_t seed, uint64_t offset, const double* replay, void* workspace,
+                            size_t ws_bytes, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(src, "idn_noise_u8: null src");
+  IDN_CHECK_ARG(out_u8 || out_f64, "idn_noise_u8: at least one of out_u8 / out_f64 is required");
+  IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c >= 1 && c <= 4, "idn_noise_u8: bad shape");
+  IDN_CHECK_ARG(row_stride >= (int64_t)w * c, "idn_noise_u8: row_stride < w*c");
+  IDN_CHECK_ARG(kind >= 0 && kind <= 3, "idn_noise_u8: unknown noise kind %d", kind);
+  IDN_CHECK_ARG((const void*)out_u8 != (const void*)src || kind != IDN_NOISE_POISSON,
+                "idn_noise_u8: poisson cannot run in place");
+  if (n == 0) return IDN_OK;
+  hipStream_t st = as_stream(stream);
+  NoiseArgs a;
+  a.src = src;
+  a.out_u8 = out_u8;
+  a.out_f64 = out_f64;
+  a.replay = replay;
+  a.vals = nullptr;
+  a.n = n;
+  a.h = h;
+  a.w = w;
+  a.c = c;
+  a.row_stride = row_stride;
+  a.elems = (int64_t)h * w * c;
+  a.key = seed ^ (KIND_TAG * (uint64_t)(kind + 1));
+  a.offset = offset;
+  switch (kind) {
+    case IDN_NOISE_GAUSSIAN:
+    case IDN_NOISE_SPECKLE: {
+      IDN_CHECK_ARG(p1 >= 0.0, "idn_noise_u8: var must be >= 0");
+      a.p0 = p0;             // mean
+      a.p1 = pow(p1, 0.5);   // var ** 0.5 (random_noise)
+      const int64_t work = (a.elems + 1) / 2 * n;
+      if (kind == IDN_NOISE_GAUSSIAN)
+        hipLaunchKernelGGL(noise_gauss_kernel<IDN_NOISE_GAUSSIAN>, dim3(grid_for(work)), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL(noise_gauss_kernel<IDN_NOISE_SPECKLE>, dim3(grid_for(work)), dim3(256), 0, st, a);
+      break;
+    }
+    case IDN_NOISE_SAP: {
+      IDN_CHECK_ARG(p0 >= 0.0 && p0 <= 1.0 && p1 >= 0.0 && p1 <= 1.0,
+                    "idn_noise_u8: amount / salt_vs_pepper must be in [0, 1]");
+      // np.random.choice([True, False], p=[p, 1-p]): True iff random_sample < cdf[0]
+      a.p0 = p0 / (p0 + (1.0 - p0));
+      a.p1 = p1 / (p1 + (1.0 - p1));
+      hipLaunchKernelGGL(noise_sap_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      break;
+    }
+    default: {  // POISSON
+      const size_t need = idn_noise_workspace_size(kind, n);
+      IDN_CHECK_ARG(workspace && ws_bytes >= need,
+                    "idn_noise_u8: poisson needs %zu workspace bytes (got %zu)", need, ws_bytes);
+      uint32_t* mask = (uint32_t*)workspace;
+      if (hipMemsetAsync(mask, 0, (size_t)n * 8 * sizeof(uint32_t), st) != hipSuccess)
+        return set_error(IDN_EHIP, "idn_noise_u8: memset failed");
+      const int64_t per_img = (int64_t)h * w * c;
+      unsigned gx = grid_for(per_img, 64);
+      hipLaunchKernelGGL(unique_mask_kernel, dim3(gx, (unsigned)n), dim3(256), 0, st, src, h, w * c,
+                         row_stride, mask);
+      hipLaunchKernelGGL(vals_from_mask_kernel, dim3((n + 255) / 256), dim3(256), 0, st, mask, n);
+      a.vals = mask + 8 * n;
+      hipLaunchKernelGGL(noise_poisson_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      break;
+    }
+  }
+  IDN_CHECK_LAUNCH("idn_noise_u8");
+  return IDN_OK;
+}
+
+extern "C" int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, double amplitude,
+                                       void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(pattern, "idn_periodic_pattern_u8: null pattern");
+  IDN_CHECK_ARG(h > 0 && w > 0 && c > 0, "idn_periodic_pattern_u8: bad shape");
+  const int64_t size = (int64_t)h * w * c;
+  // numpy.linspace(-A, A, size): step = (A - (-A)) / (size - 1)
+  const double step = size > 1 ? (amplitude - (-amplitude)) / (double)(size - 1) : 0.0;
+  hipLaunchKernelGGL(periodic_kernel, dim3(grid_for(size)), dim3(256), 0, as_stream(stream),
+                     pattern, size, amplitude, step);
+  IDN_CHECK_LAUNCH("idn_periodic_pattern_u8");
+  return IDN_OK;
+}
+
+extern "C" int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n,
+                                  int h, int w, int c, int64_t row_stride, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(src && pattern && dst, "idn_add_pattern_u8: null pointer");
+  IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c > 0, "idn_add_pattern_u8: bad shape");
+  IDN_CHECK_ARG(row_stride >= (int64_t)w * c, "idn_add_pattern_u8: row_stride < w*c");
+  if (n == 0) return IDN_OK;
+  hipLaunchKernelGGL(add_pattern_kernel, dim3(grid_for((int64_t)n * h * w * c)), dim3(256), 0,
+                     as_stream(stream), src, pattern, dst, n, h, w * c, row_stride);
+  IDN_CHECK_LAUNCH("idn_add_pattern_u8");
+  return IDN_OK;
+}

@@ -1,0 +1,204 @@
+// Shared building blocks of the "wave stripe" kernels (stencil, median): one wave owns one
+// <=1008-byte segment of a band of rows; lane l holds the 16-byte chunk
+// [seg_start - 8 + 16 l, +16) of the current row; the 8-byte halos come from the neighbouring
+// lanes through DPP wave shifts; row and segment edges rebuild border bytes in registers.
+#pragma once
+
+#include "idn_common.hpp"
+
+namespace idn {
+
+enum Border { BORDER_REFLECT101 = 0, BORDER_REPLICATE = 1 };
+
+// lane i <- lane i-1 (wave_shr:1), lane 0 gets 0
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+// lane i <- lane i+1 (wave_shl:1), lane 63 gets 0
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+// byte P (0..31) of the 8-dword window W (window byte 0 = chunk byte -8)
+__device__ __forceinline__ uint32_t wbyte(const uint32_t (&W)[8], int P) {
+  return (W[P >> 2] >> (8 * (P & 3))) & 0xFFu;
+}
+// 4 bytes of the window starting at window byte P (P compile-time after unrolling)
+__device__ __forceinline__ uint32_t wdword(const uint32_t (&W)[8], int P) {
+  const int lo = P >> 2, s = P & 3;
+  if (s == 0) return W[lo];
+  return __builtin_amdgcn_alignbyte(W[lo + 1], W[lo], s);
+}
+__device__ __forceinline__ uint32_t even_u16(uint32_t x) { return x & 0x00FF00FFu; }
+__device__ __forceinline__ uint32_t odd_u16(uint32_t x) { return (x >> 8) & 0x00FF00FFu; }
+
+// u16-lane view of the window: for window byte b, the register holding bytes (b, b+2) in its
+// two u16 lanes.  SE[j] = bytes (4j, 4j+2), SO[j] = (4j+1, 4j+3); b = 4m+2 / 4m+3 straddle two
+// dwords and are formed with one v_alignbyte_b32 (a 2-byte funnel shift).
+struct Lanes16 {
+  uint32_t SE[8], SO[8];
+  __device__ __forceinline__ uint32_t at(int b) const {
+    const int m = b >> 2;
+    switch (b & 3) {
+      case 0: return SE[m];
+      case 1: return SO[m];
+      case 2: return __builtin_amdgcn_alignbyte(SE[m + 1], SE[m], 2);
+      default: return __builtin_amdgcn_alignbyte(SO[m + 1], SO[m], 2);
+    }
+  }
+};
+
+// Build the 4 bytes at row positions [p0, p0+4) (p0 < 0) that lie left of the row start from
+// the 16 bytes L (row bytes 0..15).
+template <int C, int BORDER>
+__device__ __forceinline__ uint32_t lead_fix(const uint32_t (&L)[4], int p0) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int p = p0 + b;                // negative row byte
+    const int pix = (p - (C - 1)) / C;   // floor(p / C) for p < 0
+    const int ch = p - pix * C;
+    const int src = (BORDER == BORDER_REFLECT101) ? (-pix * C + ch) : ch;  // < 16 for C <= 4
+    r |= ((L[src >> 2] >> (8 * (src & 3))) & 0xFFu) << (8 * b);
+  }
+  return r;
+}
+
+// Bytes at row positions rb + k (k = k0..k0+3) rebuilt from window bytes; `base` = window byte of
+// row position rb.
+template <int C, int BORDER>
+__device__ __forceinline__ uint32_t tail_fix(const uint32_t (&W)[8], int base, int k0) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int k = k0 + b;
+    const int src = (BORDER == BORDER_REFLECT101) ? base - 2 * C - (k / C) * C + (k % C)
+                                                  : base - C + (k % C);
+    r |= wbyte(W, src) << (8 * b);
+  }
+  return r;
+}
+
+// Assemble the 8-dword window of one row for this lane (DPP halos + border fixups).
+template <int C, int BORDER>
+__device__ __forceinline__ void build_window(const v4u& Lv, bool lead, bool fix_t0, bool fix_t8,
+                                             uint32_t (&W)[8]) {
+  W[2] = Lv.x;
+  W[3] = Lv.y;
+  W[4] = Lv.z;
+  W[5] = Lv.w;
+  if (lead) {  // chunk starts 8 bytes left of the row: rebuild from row bytes 0..15
+    const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
+    W[2] = lead_fix<C, BORDER>(L, -8);
+    W[3] = lead_fix<C, BORDER>(L, -4);
+    W[4] = L[0];
+    W[5] = L[1];
+  }
+  W[0] = from_prev_lane(W[4]);
+  W[1] = from_prev_lane(W[5]);
+  W[6] = from_next_lane(W[2]);
+  W[7] = from_next_lane(W[3]);
+  if (fix_t0) {  // row end at chunk end: window bytes 24.. are past the row
+    const uint32_t a = tail_fix<C, BORDER>(W, 24, 0);
+    const uint32_t b = tail_fix<C, BORDER>(W, 24, 4);
+    W[6] = a;
+    W[7] = b;
+  }
+  if (fix_t8) {  // row end mid-chunk: window byte 16 == rb
+    const uint32_t a = tail_fix<C, BORDER>(W, 16, 0);
+    const uint32_t b = tail_fix<C, BORDER>(W, 16, 4);
+    W[4] = a;
+    W[5] = b;
+  }
+}
+
+// u16-lane view of a raw window: the register holding window bytes (b, b+2) in its two lanes.
+__device__ __forceinline__ uint32_t lanes16_at(const uint32_t (&W)[8], int b) {
+  const int m = b >> 2;
+  switch (b & 3) {
+    case 0: return W[m] & 0x00FF00FFu;
+    case 1: return __builtin_amdgcn_perm(0u, W[m], 0x0C030C01u);
+    case 2: return __builtin_amdgcn_alignbyte(W[m + 1], W[m], 2) & 0x00FF00FFu;
+    default: return __builtin_amdgcn_perm(0u, __builtin_amdgcn_alignbyte(W[m + 1], W[m], 2), 0x0C030C01u);
+  }
+}
+
+// Work-item geometry of a stripe launch (all wave-uniform).
+struct StripeGeom {
+  int seg, band, img;
+  int seg_start, seg_end, q;
+  bool lead, fix_t0, fix_t8;
+  int kind;  // 0 none, 1 full 16 B, 2 low 8 B, 3 high 8 B
+};
+
+__device__ __forceinline__ StripeGeom stripe_geom(int item, int lane, int rb, int nseg,
+                                                  int seg_len, int bands) {
+  StripeGeom g;
+  g.seg = item % nseg;
+  const int tq = item / nseg;
+  g.band = tq % bands;
+  g.img = tq / bands;
+  g.seg_start = g.seg * seg_len;
+  g.seg_end = min(g.seg_start + seg_len, rb);
+  g.q = g.seg_start - 8 + 16 * lane;
+  g.lead = (g.seg_start == 0) && (lane == 0);
+  const bool last_seg = (g.seg_end == rb);
+  const int tail = (rb - g.seg_start + 8) & 15;
+  g.fix_t0 = last_seg && tail == 0 && (g.q + 16 == rb);
+  g.fix_t8 = last_seg && tail == 8 && (g.q + 8 == rb);
+  const int o_lo = max(g.q, g.seg_start), o_hi = min(g.q + 16, g.seg_end);
+  g.kind = (o_hi <= o_lo) ? 0 : (o_lo == g.q && o_hi == g.q + 16) ? 1 : (o_lo == g.q) ? 2 : 3;
+  return g;
+}
+
+template <int NT>
+__device__ __forceinline__ void stripe_store(const v4u& o, rsrc_t rd, uint32_t off, int kind) {
+  constexpr int aux = (NT & 2) ? 2 : 0;
+  if (kind == 1) {
+    __builtin_amdgcn_raw_buffer_store_b128(o, rd, off, 0, aux);
+  } else if (kind == 2) {
+    v2u lo2 = {o.x, o.y};
+    __builtin_amdgcn_raw_buffer_store_b64(lo2, rd, off, 0, aux);
+  } else if (kind == 3) {
+    v2u hi2 = {o.z, o.w};
+    __builtin_amdgcn_raw_buffer_store_b64(hi2, rd, off + 8u, 0, aux);
+  }
+}
+
+// Host-side stripe geometry: segments of <= 1008 bytes, bands sized to one resident round.
+struct StripePlan {
+  int nseg, seg_len, bands, band_rows;
+  int64_t total;
+};
+
+inline int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+inline StripePlan plan_stripe(int n, int h, int64_t rb, int K, int U, int64_t cap) {
+  StripePlan p;
+  p.nseg = (int)((rb + 1007) / 1008);
+  p.seg_len = (int)(((rb + p.nseg - 1) / p.nseg + 7) / 8 * 8);
+  int band_rows = env_int("IDN_BAND_ROWS", 0);
+  if (band_rows <= 0) {
+    int64_t bands = cap / ((int64_t)n * p.nseg);
+    if (bands < 1) bands = 1;
+    band_rows = (int)((h + bands - 1) / bands);
+    if (band_rows < 24) band_rows = 24;
+    while ((band_rows + (K - 1)) % U != 0 && band_rows < h) ++band_rows;
+  }
+  p.band_rows = band_rows;
+  p.bands = (h + band_rows - 1) / band_rows;
+  p.total = (int64_t)n * p.bands * p.nseg;
+  return p;
+}
+
+inline bool stripe_ok(int c, int64_t rb, int64_t row_stride, int h, const void* src,
+                      const void* dst) {
+  return c == 3 && rb % 8 == 0 && row_stride % 8 == 0 && rb >= 32 &&
+         (int64_t)h * row_stride < (int64_t)0x7FFFFFFF && ((uintptr_t)src & 7) == 0 &&
+         ((uintptr_t)dst & 7) == 0 && env_int("IDN_FORCE_GENERIC", 0) == 0;
+}
+
+}  // namespace idn

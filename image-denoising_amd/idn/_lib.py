@@ -1,0 +1,77 @@
+"""ctypes binding of the HIP C-ABI library (include/idn.h -> idn/libidn_hip.so).
+
+The library is the only compute path: there is no CPU fallback.  If the .so is missing (not
+built) or cannot be loaded, every op raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libidn_hip.so"
+
+_c_u8p = ctypes.c_void_p
+_c_f64p = ctypes.c_void_p
+_c_int = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_u64 = ctypes.c_uint64
+_c_dbl = ctypes.c_double
+_c_size = ctypes.c_size_t
+_c_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/idn.h exactly
+SIGNATURES = {
+    "idn_version": (ctypes.c_char_p, []),
+    "idn_last_error": (ctypes.c_char_p, []),
+    "idn_gaussian_blur_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp]),
+    "idn_box_blur_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp]),
+    "idn_median_blur_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp]),
+    "idn_bilateral_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_dbl, _c_dbl, _c_vp]),
+    "idn_noise_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
+                              _c_dbl, _c_dbl, _c_u64, _c_u64, _c_f64p, _c_vp, _c_size, _c_vp]),
+    "idn_noise_workspace_size": (_c_size, [_c_int, _c_int]),
+    "idn_periodic_pattern_u8": (_c_int, [_c_u8p, _c_int, _c_int, _c_int, _c_dbl, _c_vp]),
+    "idn_add_pattern_u8": (_c_int, [_c_u8p, _c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
+    "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_int,
+                                        _c_vp, _c_size, _c_vp]),
+    "idn_wavelet_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    "idn_blob_f32": (_c_int, [_c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_int,
+                              ctypes.POINTER(ctypes.c_double), _c_int, _c_vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class IdnError(RuntimeError):
+    """A C-ABI call returned a negative idn_status."""
+
+
+def load(required: bool = False):
+    """Load libidn_hip.so and bind the declared symbols (raises if the library is missing;
+    with required=True also if any symbol of include/idn.h is not exported)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise IdnError(
+                    f"{LIB_PATH} is missing: build it with `python -m idn._build` "
+                    "(or __graft_entry__.build()); idn has no CPU fallback")
+            lib = ctypes.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name, None)
+                if fn is None:
+                    if required:
+                        raise IdnError(f"{LIB_PATH.name} does not export {name}")
+                    continue
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().idn_last_error()
+        raise IdnError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

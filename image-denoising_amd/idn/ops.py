@@ -1,0 +1,210 @@
+"""Tensor-level ops over the HIP C-ABI (device tensors in, device tensors out).
+
+Every function takes uint8 images shaped (H, W, C) or (N, H, W, C) living on a ROCm device
+(torch "cuda" tensors) and launches on torch's current stream.  Names and argument meaning follow
+the OpenCV / scikit-image calls the reference makes on its preprocessing path:
+
+  gaussian_blur(x, ksize)                 cv2.GaussianBlur(x, (ksize, ksize), 0)
+  blur(x, ksize=3)                        cv2.blur(x, (ksize, ksize))
+  median_blur(x, ksize)                   cv2.medianBlur(x, ksize)
+  bilateral_filter(x, d, sc, ss)          cv2.bilateralFilter(x, d, sc, ss, BORDER_CONSTANT)
+  random_noise(x, mode, ...)              skimage.util.random_noise (+ U8 cast)
+  periodic_pattern / add_pattern          add_periodic_noise's linspace/sin pattern, cv2.add
+  denoise_wavelet(x, wavelet, levels)     skimage.restoration.denoise_wavelet (0.14.2 wrapper)
+  blob(x, ...)                            lib/utils/blob.py prep_im_for_blob + im_list_to_blob
+
+There is no CPU path: a CPU tensor raises, a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+PIXEL_MEANS = (102.9801, 115.9465, 122.7717)  # lib/model/config.py:252 (BGR)
+
+NOISE_KINDS = {"gaussian": 0, "speckle": 1, "s&p": 2, "sap": 2, "poisson": 3}
+WAVELETS = {"db1": 0, "haar": 0, "bior1.5": 1}
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _as_batch(x: torch.Tensor, name: str) -> Tuple[torch.Tensor, bool]:
+    if not isinstance(x, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor, got {type(x).__name__}")
+    if x.device.type != "cuda":
+        raise ValueError(f"{name}: idn runs on the GPU only; got a {x.device} tensor "
+                         "(move it with .cuda(); there is no CPU fallback)")
+    squeeze = False
+    if x.dim() == 3:
+        x = x.unsqueeze(0)
+        squeeze = True
+    if x.dim() != 4:
+        raise ValueError(f"{name}: expected (H,W,C) or (N,H,W,C), got shape {tuple(x.shape)}")
+    return x, squeeze
+
+
+def _u8_batch(x: torch.Tensor, name: str) -> Tuple[torch.Tensor, bool]:
+    x, sq = _as_batch(x, name)
+    if x.dtype != torch.uint8:
+        raise TypeError(f"{name}: expected uint8 images, got {x.dtype}")
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return x, sq
+
+
+def _finish(out: torch.Tensor, squeeze: bool) -> torch.Tensor:
+    return out[0] if squeeze else out
+
+
+def _filter(fn_name: str, x: torch.Tensor, *args, out: Optional[torch.Tensor] = None):
+    xb, sq = _u8_batch(x, fn_name)
+    n, h, w, c = xb.shape
+    y = torch.empty_like(xb) if out is None else out.view(n, h, w, c)
+    lib = _lib.load()
+    rc = getattr(lib, fn_name)(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c, *args, _stream())
+    _lib.check(rc, fn_name)
+    return _finish(y, sq)
+
+
+def gaussian_blur(x: torch.Tensor, ksize: int = 5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cv2.GaussianBlur(x, (ksize, ksize), 0); ksize in {3, 5}; bit-exact."""
+    return _filter("idn_gaussian_blur_u8", x, int(ksize), out=out)
+
+
+def blur(x: torch.Tensor, ksize: int = 3, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cv2.blur(x, (ksize, ksize)); ksize 3; bit-exact."""
+    return _filter("idn_box_blur_u8", x, int(ksize), out=out)
+
+
+def median_blur(x: torch.Tensor, ksize: int = 3, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cv2.medianBlur(x, ksize); ksize in {3, 5}; bit-exact."""
+    return _filter("idn_median_blur_u8", x, int(ksize), out=out)
+
+
+def bilateral_filter(x: torch.Tensor, d: int = 9, sigma_color: float = 20.0,
+                     sigma_space: float = 100.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cv2.bilateralFilter(x, d, sigma_color, sigma_space, borderType=BORDER_CONSTANT)."""
+    return _filter("idn_bilateral_u8", x, int(d), float(sigma_color), float(sigma_space), out=out)
+
+
+# ---- noise generators ------------------------------------------------------------------------
+
+def _empty_like_img(xb: torch.Tensor, dtype) -> torch.Tensor:
+    return torch.empty(xb.shape, dtype=dtype, device=xb.device)
+
+
+def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, var: float = 0.01,
+                 amount: float = 0.05, salt_vs_pepper: float = 0.5, seed: int = 0,
+                 offset: int = 0, replay: Optional[torch.Tensor] = None, out: str = "u8",
+                 out_u8: Optional[torch.Tensor] = None):
+    """skimage.util.random_noise(x, mode, ...) on a uint8 batch, plus the caller's U8 cast.
+
+    out="u8"   -> (255 * random_noise(...)).astype(np.uint8)   (denoise-branch input)
+    out="f64"  -> random_noise(...) as float64 in [0, 1]        ("plain" branch result)
+    out="both" -> (u8, f64)
+    replay: None draws from the Philox stream keyed by (seed, offset + image index); otherwise the
+    random field numpy would have drawn (gaussian/speckle: N(mean, sqrt(var)) field of x.shape;
+    s&p: float64 [2, *x.shape] random_sample fields for `flipped` then `salted`; poisson: the
+    Poisson draws), which makes the result bit-exact with the reference.
+    """
+    kind = NOISE_KINDS.get(mode.lower())
+    if kind is None:
+        raise ValueError(f"random_noise: unsupported mode {mode!r}; supported: {sorted(NOISE_KINDS)}")
+    xb, sq = _u8_batch(x, "random_noise")
+    n, h, w, c = xb.shape
+    want_u8 = out in ("u8", "both")
+    want_f64 = out in ("f64", "both")
+    if not (want_u8 or want_f64):
+        raise ValueError("random_noise: out must be 'u8', 'f64' or 'both'")
+    y8 = (out_u8.view(n, h, w, c) if out_u8 is not None else _empty_like_img(xb, torch.uint8)) if want_u8 else None
+    y64 = _empty_like_img(xb, torch.float64) if want_f64 else None
+    if kind in (0, 1):
+        p0, p1 = float(mean), float(var)
+    elif kind == 2:
+        p0, p1 = float(amount), float(salt_vs_pepper)
+    else:
+        p0 = p1 = 0.0
+    rp = None
+    if replay is not None:
+        rp = replay
+        if rp.device != xb.device or rp.dtype != torch.float64:
+            raise ValueError("random_noise: replay must be a float64 tensor on the same device")
+        need = (2 if kind == 2 else 1) * xb.numel()
+        if rp.numel() != need:
+            raise ValueError(f"random_noise: replay has {rp.numel()} elements, expected {need}")
+        rp = rp.contiguous()
+    lib = _lib.load()
+    ws = None
+    ws_bytes = lib.idn_noise_workspace_size(kind, n)
+    if ws_bytes:
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=xb.device)
+    rc = lib.idn_noise_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
+                          y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c, kind,
+                          p0, p1, int(seed) & (2 ** 64 - 1), int(offset),
+                          rp.data_ptr() if rp is not None else None,
+                          ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+    _lib.check(rc, "idn_noise_u8")
+    if out == "u8":
+        return _finish(y8, sq)
+    if out == "f64":
+        return _finish(y64, sq)
+    return _finish(y8, sq), _finish(y64, sq)
+
+
+_PATTERN_CACHE: dict = {}
+
+
+def periodic_pattern(h: int, w: int, c: int, amplitude: float, device=None) -> torch.Tensor:
+    """U8(255*sin(linspace(-A, A, h*w*c))).reshape(h, w, c); cached per (h, w, c, A, device)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (h, w, c, float(amplitude), str(dev))
+    pat = _PATTERN_CACHE.get(key)
+    if pat is None:
+        pat = torch.empty((h, w, c), dtype=torch.uint8, device=dev)
+        rc = _lib.load().idn_periodic_pattern_u8(pat.data_ptr(), h, w, c, float(amplitude), _stream())
+        _lib.check(rc, "idn_periodic_pattern_u8")
+        _PATTERN_CACHE[key] = pat
+    return pat
+
+
+def add_pattern(x: torch.Tensor, pattern: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cv2.add(x, pattern) (u8 saturating), pattern broadcast over the batch."""
+    xb, sq = _u8_batch(x, "add_pattern")
+    n, h, w, c = xb.shape
+    if tuple(pattern.shape) != (h, w, c) or pattern.dtype != torch.uint8:
+        raise ValueError(f"add_pattern: pattern must be uint8 {(h, w, c)}, got {tuple(pattern.shape)}")
+    y = torch.empty_like(xb) if out is None else out.view(n, h, w, c)
+    rc = _lib.load().idn_add_pattern_u8(xb.data_ptr(), pattern.contiguous().data_ptr(), y.data_ptr(),
+                                        n, h, w, c, w * c, _stream())
+    _lib.check(rc, "idn_add_pattern_u8")
+    return _finish(y, sq)
+
+
+def periodic_noise(x: torch.Tensor, amplitude: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """add_periodic_noise: cv2.add(img, U8(255*sin(linspace(-A, A, img.size))).reshape(h,w,3))."""
+    xb, _ = _as_batch(x, "periodic_noise")
+    _, h, w, c = xb.shape
+    return add_pattern(x, periodic_pattern(h, w, c, amplitude, xb.device), out=out)
+
+
+# ---- blob epilogue -----------------------------------------------------------------------------
+
+def blob(x: torch.Tensor, pixel_means=PIXEL_MEANS, out_hw: Optional[Tuple[int, int]] = None,
+         flip: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """prep_im_for_blob (scale 1.0) + im_list_to_blob: float32 NHWC, mean-subtracted, zero-padded."""
+    xb, _ = _u8_batch(x, "blob")
+    n, h, w, c = xb.shape
+    oh, ow = out_hw if out_hw is not None else (h, w)
+    y = torch.empty((n, oh, ow, 3), dtype=torch.float32, device=xb.device) if out is None else out
+    m = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(pixel_means, np.float64).reshape(-1)])
+    rc = _lib.load().idn_blob_f32(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c, oh, ow, m,
+                                  1 if flip else 0, _stream())
+    _lib.check(rc, "idn_blob_f32")
+    return y

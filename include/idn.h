@@ -1,0 +1,140 @@
+/*
+ * idn.h — C-ABI of the MI355X-native noise-injection + denoising filter bank.
+ *
+ * One shared library (image-denoising_amd/idn/libidn_hip.so, hipcc --offload-arch=gfx950)
+ * exports every function below with C linkage.  No torch types cross this boundary:
+ * plain device pointers, sizes and a hipStream_t passed as `void*`.
+ *
+ * Conventions (all entry points)
+ *   - Images are uint8 HxWxC, channel-interleaved (cv2.imread layout: BGR, C=3), row pitch
+ *     `row_stride` bytes (>= W*C), a batch of `n` images laid back to back with image pitch
+ *     h*row_stride.  f64 arrays use the same element order with pitch W*C elements.
+ *   - Pointers are DEVICE pointers owned by the caller; nothing is allocated inside a call.
+ *     Calls that need scratch take (workspace, ws_bytes) and expose idn_*_workspace_size().
+ *   - Every call is stream-ordered on `stream` (NULL = default stream) and capture-safe
+ *     (no sync, no malloc).  The RNG position is explicit: (seed, offset) keys a Philox4x32-10
+ *     stream; element e of image i draws counter (offset + i, e), so results do not depend on
+ *     how a batch is split across launches or ranks.
+ *   - Return IDN_OK (0) or a negative idn_status; idn_last_error() returns a thread-local
+ *     message for the last failing call on the calling thread.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   cv2.GaussianBlur / cv2.blur / cv2.medianBlur / cv2.bilateralFilter calls inside the noise
+ *   closures and the post-dispatch denoise hook: lib/model/test.py:193-1607,1787-1831 and
+ *   lib/roi_data_layer/minibatch.py:87-1516,1636-1673; skimage random_noise calls at the same
+ *   sites; lib/utils/blob.py:17-47 (prep_im_for_blob / im_list_to_blob).
+ */
+#ifndef IDN_H_
+#define IDN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum idn_status {
+  IDN_OK = 0,
+  IDN_EINVAL = -1,        /* bad shape / stride / parameter                         */
+  IDN_EUNSUPPORTED = -2,  /* valid but unsupported combination (e.g. ksize 7)        */
+  IDN_EHIP = -3,          /* HIP runtime error (launch failure, ...)                */
+  IDN_EWORKSPACE = -4     /* workspace missing or too small                         */
+} idn_status;
+
+/* noise kinds for idn_noise_u8 (skimage.util.random_noise modes used on the path) */
+typedef enum idn_noise_kind {
+  IDN_NOISE_GAUSSIAN = 0, /* out = clip(x + N(mean, sqrt(var)), 0, 1)                */
+  IDN_NOISE_SPECKLE = 1,  /* out = clip(x + x*N(mean, sqrt(var)), 0, 1)              */
+  IDN_NOISE_SAP = 2,      /* salt & pepper, amount = p0, salt_vs_pepper = p1          */
+  IDN_NOISE_POISSON = 3   /* out = clip(Poisson(x*vals)/vals, 0, 1), vals per image    */
+} idn_noise_kind;
+
+/* wavelet families for idn_wavelet_denoise_u8 */
+typedef enum idn_wavelet {
+  IDN_WAVELET_DB1 = 0,    /* Haar ('db1', skimage default)                           */
+  IDN_WAVELET_BIOR15 = 1  /* 'bior1.5' (the reference's in-branch choice)             */
+} idn_wavelet;
+
+/* ---- library ------------------------------------------------------------------------- */
+const char* idn_version(void);
+const char* idn_last_error(void);
+
+/* ---- denoising filters (u8 -> u8, src != dst) ------------------------------------------ */
+
+/* cv2.GaussianBlur(img, (ksize, ksize), 0), ksize in {3, 5}, BORDER_REFLECT_101.
+ * Replaces e.g. lib/model/test.py:224, lib/roi_data_layer/minibatch.py:1636-1639. Bit-exact. */
+int idn_gaussian_blur_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                         int64_t row_stride, int ksize, void* stream);
+
+/* cv2.blur(img, (ksize, ksize)), ksize = 3, BORDER_REFLECT_101.
+ * Replaces lib/model/test.py:241,1767, lib/roi_data_layer/minibatch.py:1640-1643. Bit-exact. */
+int idn_box_blur_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                    int64_t row_stride, int ksize, void* stream);
+
+/* cv2.medianBlur(img, ksize), ksize in {3, 5}, BORDER_REPLICATE.
+ * Replaces lib/model/test.py:259, lib/roi_data_layer/minibatch.py:1644-1648. Bit-exact. */
+int idn_median_blur_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                       int64_t row_stride, int ksize, void* stream);
+
+/* cv2.bilateralFilter(img, d, sigma_color, sigma_space, borderType=BORDER_CONSTANT), c = 3
+ * (or 1).  Replaces lib/model/test.py:278, lib/roi_data_layer/minibatch.py:1658-1663.
+ * <= 1 LSB vs OpenCV (fp32 summation order). */
+int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                     int64_t row_stride, int d, double sigma_color, double sigma_space,
+                     void* stream);
+
+/* ---- noise generators (skimage.util.random_noise, as called on the path) --------------- */
+
+/* Apply one random_noise mode to a batch of u8 images.
+ *   out_u8  (nullable): U8(255*out)  == (255*out).astype(np.uint8), the denoise-branch input
+ *   out_f64 (nullable): out itself (float64 in [0,1]), what the "plain" branches return
+ *   p0, p1: GAUSSIAN/SPECKLE: mean, var; SAP: amount, salt_vs_pepper; POISSON: unused
+ *   replay  (nullable): caller-provided random field, which makes the result bit-exact with
+ *     numpy's legacy stream:  GAUSSIAN/SPECKLE: f64 N(mean,sqrt(var)) field (n*h*w*c);
+ *     SAP: f64 [2][n*h*w*c] = (random_sample for `flipped`, random_sample for `salted`);
+ *     POISSON: f64 per-element Poisson draws (n*h*w*c).  NULL = Philox stream (seed, offset).
+ *   workspace: POISSON needs idn_noise_workspace_size() bytes (per-image `vals`); else unused.
+ * Replaces skimage random_noise at lib/model/test.py:193-590, minibatch.py:87-490. */
+int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
+                 int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
+                 uint64_t offset, const double* replay, void* workspace, size_t ws_bytes,
+                 void* stream);
+size_t idn_noise_workspace_size(int kind, int n);
+
+/* Periodic noise pattern of add_periodic_noise (lib/model/test.py:1128-1298):
+ * pattern[i] = U8(255*sin(t_i)), t = np.linspace(-A, A, h*w*c), written as u8 HxWxC (pitch w*c).
+ * Image independent: build once per (h, w, c, A) and reuse. */
+int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, double amplitude,
+                            void* stream);
+
+/* cv2.add(img, pattern) on u8 (saturating), pattern broadcast over the batch. */
+int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n, int h,
+                       int w, int c, int64_t row_stride, void* stream);
+
+/* ---- wavelet denoise (skimage 0.14.2 denoise_wavelet, BayesShrink, soft, YCbCr) -------- */
+
+/* out_u8 = (255*denoise_wavelet(img, method='BayesShrink', mode='soft', wavelet=wavelet,
+ *           multichannel=True, convert2ycbcr=True, wavelet_levels=levels)).astype(uint8),
+ * c = 3.  levels <= 0 selects skimage's default max(dwt_max_level - 3, 1).  in_f64 (nullable)
+ * replaces src when the caller holds a float image in [0,1] (the reference's f64 branches).
+ * Replaces lib/model/test.py:197-201,1807-1810, minibatch.py:1653-1656,
+ * minibatch_before_curvelet.py:85-87. */
+int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8, int n,
+                           int h, int w, int64_t row_stride, int wavelet, int levels,
+                           void* workspace, size_t ws_bytes, void* stream);
+size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels);
+
+/* ---- blob epilogue (lib/utils/blob.py:17-47) -------------------------------------------- */
+
+/* blob[i, y, x, ch] = float32(float64(img[i,y,x,ch]) - mean[ch]) for y<h, x<w; zero elsewhere
+ * in the (n, out_h, out_w, 3) float32 NHWC blob (im_list_to_blob's zero padding).  flip != 0
+ * mirrors x (minibatch.py:1676-1677).  c must be 3.  Scale 1.0 only (the 600x1000 case). */
+int idn_blob_f32(const uint8_t* src, float* blob, int n, int h, int w, int c,
+                 int64_t row_stride, int out_h, int out_w, const double mean[3], int flip,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IDN_H_ */

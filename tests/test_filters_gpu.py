@@ -1,0 +1,160 @@
+"""GPU parity: HIP stencil / median / bilateral filters vs the C oracle (oracle/filters.c).
+
+Integer filters must be bit-exact.  Shapes cover the fast path's segment tails (row bytes
+% 16 == 0 and == 8), multi-segment rows, the 600x1000 BASELINE shape, tiny images (vertical
+reflection of h < ksize) and shapes only the generic path accepts (W*C % 8 != 0).
+"""
+import numpy as np
+import pytest
+
+from conftest import textured
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    (2, 600, 1000),  # BASELINE shape: 3 segments of 1000 B, tail 8
+    (3, 64, 96),     # rb 288: one segment, tail 8
+    (2, 40, 104),    # rb 312: tail 0
+    (1, 33, 336),    # rb 1008: exactly one full segment
+    (2, 17, 344),    # rb 1032: two segments
+    (1, 5, 16),      # rb 48, h 5
+    (2, 2, 24),      # h 2 < ksize
+    (1, 1, 40),      # single row
+    (2, 37, 53),     # rb 159: generic path
+    (1, 9, 11),      # generic path, tiny
+]
+
+
+def _run(fn, img, *args):
+    import torch
+    x = torch.from_numpy(img).cuda()
+    y = fn(x, *args)
+    torch.cuda.synchronize()
+    return y.cpu().numpy()
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("k", [3, 5])
+def test_gaussian_blur_bitexact(dev, shape, k):
+    import idn
+    import oracle
+    img = textured(*shape, seed=sum(shape) + k)
+    got = _run(idn.gaussian_blur, img, k)
+    ref = oracle.cv.gaussian_blur(img, k)
+    assert np.array_equal(got, ref), f"mismatches: {np.argwhere(got != ref)[:8]}"
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_box_blur_bitexact(dev, shape):
+    import idn
+    import oracle
+    img = textured(*shape, seed=sum(shape))
+    got = _run(idn.blur, img, 3)
+    ref = oracle.cv.blur(img, 3)
+    assert np.array_equal(got, ref), f"mismatches: {np.argwhere(got != ref)[:8]}"
+
+
+@pytest.mark.parametrize("k", [3, 5])
+def test_stencil_random_extremes(dev, k):
+    """i.i.d. full-range bytes incl. all-0 / all-255 rows exercise the SWAR lane bounds."""
+    import idn
+    import oracle
+    rs = np.random.RandomState(k)
+    img = rs.randint(0, 256, size=(2, 50, 1000, 3)).astype(np.uint8)
+    img[0, :7] = 255
+    img[1, -6:] = 0
+    img[1, :, :5] = 255
+    for fn, ref in ((idn.gaussian_blur, oracle.cv.gaussian_blur(img, k)),):
+        assert np.array_equal(_run(fn, img, k), ref)
+    if k == 3:
+        assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+
+
+def test_generic_path_forced(dev, monkeypatch):
+    import idn
+    import oracle
+    monkeypatch.setenv("IDN_FORCE_GENERIC", "1")
+    img = textured(2, 31, 200, seed=9)
+    assert np.array_equal(_run(idn.gaussian_blur, img, 5), oracle.cv.gaussian_blur(img, 5))
+    assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+
+
+@pytest.mark.parametrize("band_rows", ["7", "32", "600"])
+def test_band_split_invariance(dev, monkeypatch, band_rows):
+    import idn
+    import oracle
+    monkeypatch.setenv("IDN_BAND_ROWS", band_rows)
+    img = textured(2, 100, 1000, seed=int(band_rows))
+    assert np.array_equal(_run(idn.gaussian_blur, img, 5), oracle.cv.gaussian_blur(img, 5))
+
+
+def test_rejects_cpu_tensor():
+    import torch
+    import idn
+    with pytest.raises(ValueError):
+        idn.gaussian_blur(torch.zeros(4, 4, 3, dtype=torch.uint8), 5)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("k", [3, 5])
+def test_median_blur_bitexact(dev, shape, k):
+    import idn
+    import oracle
+    img = textured(*shape, seed=sum(shape) * 7 + k)
+    got = _run(idn.median_blur, img, k)
+    ref = oracle.cv.median_blur(img, k)
+    assert np.array_equal(got, ref), f"mismatches: {np.argwhere(got != ref)[:8]}"
+
+
+@pytest.mark.parametrize("k", [3, 5])
+def test_median_saltpepper_extremes(dev, k):
+    """s&p-like data (config 3): runs of 0 / 255 around real values, incl. all-equal windows"""
+    import idn
+    import oracle
+    rs = np.random.RandomState(40 + k)
+    img = textured(2, 60, 1000, seed=k)
+    m = rs.random_sample(img.shape)
+    img[m < 0.2] = 0
+    img[(m >= 0.2) & (m < 0.4)] = 255
+    img[0, 10:20] = 255
+    assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k))
+
+
+def test_median_generic_forced(dev, monkeypatch):
+    import idn
+    import oracle
+    monkeypatch.setenv("IDN_FORCE_GENERIC", "1")
+    img = textured(2, 23, 64, seed=5)
+    for k in (3, 5):
+        assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k))
+
+
+BILATERAL_CASES = [(9, 20.0, 100.0), (9, 75.0, 75.0), (5, 30.0, 10.0), (3, 10.0, 10.0)]
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 37, 53), (1, 600, 1000), (2, 5, 7)])
+@pytest.mark.parametrize("case", BILATERAL_CASES)
+def test_bilateral_within_1lsb(dev, shape, case):
+    """<= 1 LSB vs OpenCV semantics (fp32 sum order / exp ulps); pre-round values within 1e-4 rel"""
+    import idn
+    import oracle
+    d, sc, ss = case
+    img = textured(*shape, seed=d + int(sc))
+    got = _run(idn.bilateral_filter, img, d, sc, ss)
+    ref = oracle.cv.bilateral_filter(img, d, sc, ss)
+    diff = np.abs(got.astype(np.int32) - ref.astype(np.int32))
+    assert diff.max() <= 1
+    # any 1-LSB difference must sit on a rounding boundary of the exact value
+    pre = oracle.cv.bilateral_prefilter_f32(img, d, sc, ss)
+    frac = np.abs(pre - np.floor(pre) - 0.5)
+    assert np.all(frac[diff > 0] < 1e-3)
+    assert (diff > 0).mean() < 1e-3
+
+
+def test_bilateral_gray(dev):
+    import idn
+    import oracle
+    img = textured(1, 40, 64, c=1, seed=3)
+    got = _run(idn.bilateral_filter, img, 9, 20.0, 100.0)
+    ref = oracle.cv.bilateral_filter(img, 9, 20.0, 100.0)
+    assert np.abs(got.astype(int) - ref.astype(int)).max() <= 1

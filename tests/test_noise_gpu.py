@@ -1,0 +1,225 @@
+"""GPU parity of the noise generators, periodic pattern and blob epilogue.
+
+Replay mode (numpy's own random field fed to the kernel) must reproduce skimage's random_noise
+bit-exactly (u8 and float64), checked against the golden fixtures (tests/golden) and the oracle.
+Philox mode is checked statistically: moments / KS distance of the generated noise and the
+s&p flip rates, at BASELINE's full 600x1000 size.
+"""
+import hashlib
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from test_oracle import make_img, oracle_noise, replay_field
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD / "golden.npz", allow_pickle=False), json.loads((GOLD / "golden.json").read_text())
+
+
+MODE = {"gaussian": "gaussian", "speckle": "speckle", "s&p": "s&p", "poisson": "poisson"}
+
+
+def gpu_noise(img, case, field):
+    import torch
+    import idn
+    x = torch.from_numpy(img).cuda()
+    kw = dict(case["kw"])
+    rp = torch.from_numpy(np.ascontiguousarray(field, np.float64)).cuda()
+    u8, f64 = idn.ops.random_noise(x, case["mode"], replay=rp, out="both", **kw)
+    torch.cuda.synchronize()
+    return u8.cpu().numpy(), f64.cpu().numpy()
+
+
+def test_replay_bitexact_small(dev, gold):
+    g, m = gold
+    for case in m["noise"]:
+        if case["key"] is None:
+            continue
+        img = g["in_" + case["input"]]
+        field = replay_field(case["mode"], case["kw"], case["seed"], img)
+        u8, f64 = gpu_noise(img, case, field)
+        assert sha(f64) == case["sha_f64"], case
+        assert np.array_equal(u8, g[case["key"] + "_u8"]), case
+
+
+def test_replay_bitexact_full_size(dev, gold):
+    _, m = gold
+    big = make_img(600, 1000, 5)
+    for case in m["noise"]:
+        if case["key"] is not None:
+            continue
+        field = replay_field(case["mode"], case["kw"], case["seed"], big)
+        u8, f64 = gpu_noise(big, case, field)
+        assert sha(f64) == case["sha_f64"], case
+        assert sha(u8) == case["sha_u8"], case
+
+
+def test_replay_batch_matches_per_image(dev):
+    """a batch of 3 images with per-image fields == three single-image calls (oracle)"""
+    import torch
+    import idn
+    import oracle
+    imgs = np.stack([make_img(30, 44, s) for s in (1, 2, 3)])
+    for mode, kw in (("gaussian", {"var": 1.5}), ("speckle", {"var": 1.0}),
+                     ("s&p", {"amount": 0.2}), ("poisson", {})):
+        fields = [replay_field(mode, dict(kw, var=kw.get("var", 0)), 77 + i, imgs[i]) for i in range(3)]
+        if mode == "s&p":
+            field = np.stack([np.stack([f[0] for f in fields]), np.stack([f[1] for f in fields])])
+        else:
+            field = np.stack(fields)
+        x = torch.from_numpy(imgs).cuda()
+        u8, f64 = idn.ops.random_noise(x, mode, replay=torch.from_numpy(field).cuda(), out="both", **kw)
+        for i in range(3):
+            ref = oracle_noise(mode, kw, imgs[i], fields[i])
+            assert np.array_equal(f64[i].cpu().numpy(), ref)
+            assert np.array_equal(u8[i].cpu().numpy(), oracle.sk.to_u8(255 * ref))
+
+
+def _philox(img, mode, **kw):
+    import torch
+    import idn
+    x = torch.from_numpy(img).cuda()
+    u8, f64 = idn.ops.random_noise(x, mode, out="both", **kw)
+    return u8.cpu().numpy(), f64.cpu().numpy()
+
+
+def test_philox_gaussian_statistics(dev):
+    """unclipped region: out - x ~ N(0, sqrt(var)); KS distance against the normal CDF"""
+    from math import erf, sqrt
+    img = np.full((1, 600, 1000, 3), 128, np.uint8)
+    var = 0.0025  # small so clipping never triggers around 0.5
+    _, f64 = _philox(img, "gaussian", var=var, seed=3)
+    z = np.sort(((f64 - 128 / 255.0) / sqrt(var)).reshape(-1))
+    assert abs(z.mean()) < 5e-3 and abs(z.std() - 1) < 5e-3
+    cdf = 0.5 * (1 + np.vectorize(erf)(z[:: 97] / sqrt(2)))
+    emp = (np.arange(z.size)[::97] + 0.5) / z.size
+    assert np.abs(cdf - emp).max() < 3e-3
+
+
+def test_philox_speckle_and_determinism(dev):
+    img = make_img(600, 1000, 5)[None]
+    a8, a = _philox(img, "speckle", var=0.5, seed=11, offset=3)
+    b8, b = _philox(img, "speckle", var=0.5, seed=11, offset=3)
+    c8, _ = _philox(img, "speckle", var=0.5, seed=12, offset=3)
+    assert np.array_equal(a, b) and np.array_equal(a8, b8)
+    assert (a8 != c8).mean() > 0.5
+    # small variance, mid-range x: no clipping within 5 sigma, so n = (out - x) / x is unbiased
+    _, a = _philox(img, "speckle", var=0.0025, seed=11, offset=3)
+    x = img.astype(np.float64) * (1.0 / 255.0)
+    m = (x > 0.1) & (x < 0.75)
+    n = (a[m] - x[m]) / x[m]
+    assert abs(n.mean()) < 5e-4 and abs(n.std() - 0.05) < 5e-4
+
+
+def test_philox_offset_is_image_id(dev):
+    """image i of a batch with offset o == image 0 of a single call with offset o + i"""
+    import torch
+    import idn
+    imgs = np.stack([make_img(40, 60, s) for s in range(4)])
+    x = torch.from_numpy(imgs).cuda()
+    full = idn.ops.random_noise(x, "gaussian", var=1.0, seed=5, offset=10).cpu().numpy()
+    for i in range(4):
+        one = idn.ops.random_noise(x[i:i + 1], "gaussian", var=1.0, seed=5, offset=10 + i).cpu().numpy()
+        assert np.array_equal(full[i], one[0])
+
+
+def test_philox_sap_rates(dev):
+    img = make_img(600, 1000, 5)[None]
+    for amount in (0.2, 0.4, 0.8):
+        u8, f64 = _philox(img, "s&p", amount=amount, seed=7)
+        x = img.astype(np.float64) * (1.0 / 255.0)  # img_as_float
+        salt = (f64 == 1.0) & (x != 1.0)
+        pep = (f64 == 0.0) & (x != 0.0)
+        keep = f64 == x
+        assert abs(salt.mean() - amount / 2) < 3e-3
+        assert abs(pep.mean() - amount / 2) < 3e-3
+        assert np.all(salt | pep | keep)
+        assert np.all(u8[salt] == 255) and np.all(u8[pep] == 0)
+
+
+def test_philox_poisson_statistics(dev):
+    import oracle
+    rs = np.random.RandomState(0)
+    img = rs.randint(0, 256, (1, 600, 1000, 3)).astype(np.uint8)
+    vals = oracle.sk.poisson_vals(img[0])
+    assert vals == 256
+    _, f64 = _philox(img, "poisson", seed=9)
+    lam = img.astype(np.float64) / 255 * vals
+    k = f64 * vals
+    assert np.all(k == np.round(k))
+    for lo, hi in ((0.5, 3), (3, 10), (10, 30), (100, 200)):
+        sel = (lam >= lo) & (lam < hi) & (f64 < 1)
+        r = (k[sel] - lam[sel])
+        assert abs(r.mean()) < 0.02 * np.sqrt(lam[sel].mean())
+        assert abs((r ** 2).mean() / lam[sel].mean() - 1) < 0.02
+
+
+def test_poisson_vals_per_image(dev):
+    """vals = 2**ceil(log2(#unique)) per image: image with 3 distinct values -> vals 4"""
+    import torch
+    import idn
+    a = np.zeros((2, 8, 16, 3), np.uint8)
+    a[0, :, :8] = 10
+    a[0, :, 8:] = 200
+    a[0, 0, 0, 0] = 77           # 4 distinct values incl. 0? -> {10, 200, 77} + none = 3 -> 4
+    a[1] = np.arange(8 * 16 * 3).reshape(8, 16, 3) % 256  # 256 distinct -> 256 (and 0 present)
+    lam = np.zeros(a.shape)
+    x = torch.from_numpy(a).cuda()
+    rp = torch.zeros(a.shape, dtype=torch.float64, device="cuda")
+    rp[0] = 3.0
+    rp[1] = 3.0
+    _, f64 = idn.ops.random_noise(x, "poisson", replay=rp, out="both")
+    f = f64.cpu().numpy()
+    assert np.allclose(f[0], 3.0 / 4) and np.allclose(f[1], 3.0 / 256)
+    del lam
+
+
+def test_periodic_pattern_gpu(dev, gold):
+    import oracle
+    import idn
+    _, m = gold
+    for case in m["periodic"]:
+        pat = idn.ops.periodic_pattern(case["h"], case["w"], 3, case["amp"]).cpu().numpy()
+        ref = oracle.sk.periodic_pattern(case["h"], case["w"], 3, case["amp"])
+        diff = np.flatnonzero(pat.reshape(-1) != ref.reshape(-1))
+        assert set(diff.tolist()) <= set(case["near_int_idx"]), (case["amp"], diff[:10])
+
+
+def test_periodic_noise_add(dev):
+    import torch
+    import idn
+    import oracle
+    img = make_img(600, 1000, 5)
+    x = torch.from_numpy(np.stack([img, img[::-1].copy()])).cuda()
+    got = idn.ops.periodic_noise(x, 100.0).cpu().numpy()
+    pat = idn.ops.periodic_pattern(600, 1000, 3, 100.0).cpu().numpy()
+    assert np.array_equal(got[0], oracle.sk.add_saturate(img, pat))
+    assert np.array_equal(got[1], oracle.sk.add_saturate(img[::-1], pat))
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_blob_bitexact(dev, flip):
+    import torch
+    import idn
+    import oracle
+    imgs = np.stack([make_img(600, 1000, s) for s in (1, 2)])
+    x = torch.from_numpy(imgs).cuda()
+    got = idn.ops.blob(x, flip=flip).cpu().numpy()
+    ref = oracle.sk.blob_f32(list(imgs), flip=flip)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    padded = idn.ops.blob(x[:1, :500, :700], out_hw=(600, 1000)).cpu().numpy()
+    refp = oracle.sk.blob_f32([imgs[0, :500, :700], np.zeros((600, 1000, 3), np.uint8)])[:1]
+    refp[0, 500:] = 0
+    refp[0, :, 700:] = 0
+    assert np.array_equal(padded, refp)
