@@ -1,0 +1,653 @@
+// Wavelet denoiser: skimage 0.14.2 denoise_wavelet(img, method='BayesShrink', mode='soft',
+// wavelet=db1|bior1.5, multichannel=True, convert2ycbcr=True, wavelet_levels=L) followed by the
+// caller's (255 * out).astype(np.uint8).
+// Reference call sites: lib/model/test.py:197-201,1807-1810, lib/roi_data_layer/minibatch.py:
+// 1653-1656, minibatch_before_curvelet.py:85-87.  Restated in numpy in oracle/wavelet.py (pinned
+// against pywt 1.1.1 / skimage 0.18.3 fixtures).
+//
+// Pipeline per image (all images of the batch in every launch; grid.z = image x channel):
+//   1 wl_color      u8 BGR (or f64) -> three fp32 YCbCr planes (BGR data treated as RGB, as the
+//                   reference does) + per-channel min / max (u32 atomics on positive floats)
+//   2 wl_dwt  x L   one separable 2-D analysis level per launch: a 256-thread workgroup stages a
+//                   (2T+F-2)^2 input tile in LDS (pywt 'symmetric' extension), filters rows, then
+//                   columns, and writes the aa / ad / da / dd bands.  Level 1 applies the
+//                   (x - min) / (max - min) channel normalisation while staging.
+//   3 wl_sumsq      per detail band: sum of squares in fp64, fixed-order tree (deterministic)
+//   4 wl_median     sigma = median(|finest dd| != 0) / 0.6744897501960817: exact radix select on
+//                   the float bits (3 passes of 11/11/10 bits, LDS histograms), both middle ranks
+//   5 wl_thresh     BayesShrink t = var / sqrt(max(mean(d^2) - var, eps)) per band
+//   6 wl_idwt x L-1 synthesis levels L..2 (stage-2 valid convolution of pywt's
+//                   upsampling_convolution_valid_sf) with the soft threshold d*max(1-t/|d|, 0)
+//                   applied to every detail read; output cropped to the next level's size
+//   7 wl_idwt_final level 1 for all three channels of a pixel at once, fused with clip [0,1],
+//                   de-normalisation, YCbCr -> RGB, clip [0,1] and the U8 cast
+// Storage and arithmetic are fp64 (`wreal`): the BayesShrink threshold var/sqrt(mean(d^2) - var)
+// is ill-conditioned when a band is noise dominated, so fp32 bands moved outputs by up to 5e-5.
+// The analysis filters multiply then add (no FMA), as pywt's C loop does: a detail coefficient of
+// two equal samples is then exactly 0 (-S*x + S*x), which the "nonzero" median relies on.
+#include "idn_common.hpp"
+
+#include <math.h>
+
+#include <algorithm>
+
+namespace idn {
+
+using wreal = double;  // workspace / arithmetic type of the transform
+constexpr wreal S2 = 0.7071067811865476;
+constexpr wreal B1 = 0.016572815184059706;
+constexpr wreal B2 = 0.12153397801643785;
+
+template <int WV> struct Wav;
+template <> struct Wav<IDN_WAVELET_DB1> {
+  static constexpr int F = 2;
+  static constexpr wreal dlo[2] = {S2, S2};
+  static constexpr wreal dhi[2] = {-S2, S2};
+  static constexpr wreal rlo[2] = {S2, S2};
+  static constexpr wreal rhi[2] = {S2, -S2};
+};
+template <> struct Wav<IDN_WAVELET_BIOR15> {
+  static constexpr int F = 10;
+  static constexpr wreal dlo[10] = {B1, -B1, -B2, B2, S2, S2, B2, -B2, -B1, B1};
+  static constexpr wreal dhi[10] = {0, 0, 0, 0, -S2, S2, 0, 0, 0, 0};
+  static constexpr wreal rlo[10] = {0, 0, 0, 0, S2, S2, 0, 0, 0, 0};
+  static constexpr wreal rhi[10] = {B1, B1, -B2, -B2, S2, -S2, B2, B2, -B1, -B1};
+};
+
+inline int wl_filter_len(int wv) { return wv == IDN_WAVELET_DB1 ? 2 : 10; }
+
+// pywt dwt_max_level: floor(log2(n / (F - 1))) with integer division, 0 if n < F - 1
+inline int wl_max_level(int n, int F) {
+  if (F <= 1 || n < F - 1) return 0;
+  int q = n / (F - 1), l = 0;
+  while (q > 1) {
+    q >>= 1;
+    ++l;
+  }
+  return l;
+}
+
+constexpr int WL_MAXL = 12;
+constexpr int WL_STATS = 256;  // doubles of per-image stats
+
+struct WlLayout {
+  int n, h, w, F, L;
+  int H[WL_MAXL + 1], W[WL_MAXL + 1];  // H[0] = h; H[l] = band height of level l
+  size_t off_band[WL_MAXL + 1];        // element offset of level l's 3x4 bands inside an image
+  size_t img_floats;                   // wreal elements per image (planes + bands)
+  size_t stats_off;                    // byte offset of the stats region (after all images)
+  size_t bytes;
+};
+
+// stats region per image (doubles): [0..6) min/max as u32 pairs, [8..) sumsq[3][L][3],
+// [8+9L..) median[3], thr as double[3][L][3] after that, [255] degenerate flag
+struct WlStats {
+  __host__ __device__ static int sumsq(int c, int l, int b, int L) { return 8 + (c * L + l) * 3 + b; }
+  __host__ __device__ static int median(int c, int L) { return 8 + 9 * L + c; }
+  __host__ __device__ static int thr(int c, int l, int b, int L) { return 8 + 9 * L + 3 + (c * L + l) * 3 + b; }
+  static constexpr int FLAG = 255;
+  static constexpr int DIAG = 248;  // [248..251) nonzero count of the finest dd per channel
+  static constexpr int MN64 = 200;  // [200..203) fp64 channel min (u64 bits), [203..206) max
+  static constexpr int MX64 = 203;
+};
+
+inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
+  WlLayout Lt;
+  Lt.n = n;
+  Lt.h = h;
+  Lt.w = w;
+  Lt.F = wl_filter_len(wv);
+  if (levels <= 0) {
+    const int ml = std::min(wl_max_level(h, Lt.F), wl_max_level(w, Lt.F));
+    levels = std::max(ml - 3, 1);
+  }
+  Lt.L = levels;
+  Lt.H[0] = h;
+  Lt.W[0] = w;
+  size_t off = (size_t)3 * h * w;
+  for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
+    Lt.H[l] = (Lt.H[l - 1] + Lt.F - 1) / 2;
+    Lt.W[l] = (Lt.W[l - 1] + Lt.F - 1) / 2;
+    Lt.off_band[l] = off;
+    off += (size_t)12 * Lt.H[l] * Lt.W[l];
+  }
+  Lt.img_floats = (off + 63) / 64 * 64;
+  Lt.stats_off = (size_t)n * Lt.img_floats * sizeof(wreal);
+  Lt.bytes = Lt.stats_off + (size_t)n * WL_STATS * sizeof(double);
+  return Lt;
+}
+
+__device__ __forceinline__ int sym_idx(int i, int n) {  // pywt 'symmetric' (half-sample)
+  const int period = 2 * n;
+  i %= period;
+  if (i < 0) i += period;
+  return i < n ? i : period - 1 - i;
+}
+
+// ---- 1: colour transform + min / max -----------------------------------------------------------
+__global__ void wl_init_stats(double* stats, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * WL_STATS) return;
+  const int k = i % WL_STATS;
+  uint32_t* u = reinterpret_cast<uint32_t*>(stats + (i - k));
+  if (k < 3) {
+    u[2 * k] = 0xFFFFFFFFu;  // min (float bits, positive)
+    u[2 * k + 1] = 0u;       // max
+  } else if (k >= WlStats::MN64 && k < WlStats::MN64 + 3) {
+    reinterpret_cast<unsigned long long*>(stats)[i] = ~0ull;
+  } else {
+    stats[i] = 0.0;
+  }
+}
+
+// skimage rgb2ycbcr: arr @ ycbcr_from_rgb.T + [16, 128, 128].  numpy's matmul (OpenBLAS dgemm) rounds
+// each dot product as an fma chain over k; reproduced exactly, because the set of exactly-zero finest
+// detail coefficients (and so sigma) depends on the last bit of Y (oracle/filters.c, same chain).
+__device__ __forceinline__ double dot3(double x0, double x1, double x2, double m0, double m1, double m2) {
+  return __fma_rn(x2, m2, __fma_rn(x1, m1, __dmul_rn(x0, m0)));
+}
+__device__ __forceinline__ void ycbcr64(double x0, double x1, double x2, double (&o)[3]) {
+  o[0] = __dadd_rn(dot3(x0, x1, x2, 65.481, 128.553, 24.966), 16.0);
+  o[1] = __dadd_rn(dot3(x0, x1, x2, -37.797, -74.203, 112.0), 128.0);
+  o[2] = __dadd_rn(dot3(x0, x1, x2, 112.0, -93.786, -18.214), 128.0);
+}
+
+__device__ __forceinline__ void load_rgb64(const uint8_t* __restrict__ src,
+                                           const double* __restrict__ in64, int img, int h, int w,
+                                           int64_t row_stride, int y, int x, double (&v)[3]) {
+  if (in64) {
+    const double* s = in64 + (((int64_t)img * h + y) * w + x) * 3;
+    v[0] = s[0];
+    v[1] = s[1];
+    v[2] = s[2];
+  } else {
+    const uint8_t* s = src + (int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3;
+    v[0] = (double)s[0] * (1.0 / 255.0);
+    v[1] = (double)s[1] * (1.0 / 255.0);
+    v[2] = (double)s[2] * (1.0 / 255.0);
+  }
+}
+
+__global__ __launch_bounds__(256) void wl_color(const uint8_t* __restrict__ src,
+                                                const double* __restrict__ in64, int h, int w,
+                                                int64_t row_stride, wreal* __restrict__ ws,
+                                                size_t img_floats, double* __restrict__ stats) {
+  const int img = blockIdx.y;
+  const int64_t np = (int64_t)h * w;
+  wreal* P = ws + img * img_floats;
+  float lmn[3] = {INFINITY, INFINITY, INFINITY}, lmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  double dmn[3] = {INFINITY, INFINITY, INFINITY}, dmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    double x0, x1, x2;
+    if (in64) {
+      const double* s = in64 + ((int64_t)img * np + p) * 3;
+      x0 = s[0];
+      x1 = s[1];
+      x2 = s[2];
+    } else {
+      const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
+      const uint8_t* s = src + (int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3;
+      x0 = (double)s[0] * (1.0 / 255.0);
+      x1 = (double)s[1] * (1.0 / 255.0);
+      x2 = (double)s[2] * (1.0 / 255.0);
+    }
+    double yc[3];
+    ycbcr64(x0, x1, x2, yc);
+    P[p] = yc[0];
+    P[np + p] = yc[1];
+    P[2 * np + p] = yc[2];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      lmn[c] = fminf(lmn[c], (float)yc[c]);
+      lmx[c] = fmaxf(lmx[c], (float)yc[c]);
+      dmn[c] = fmin(dmn[c], yc[c]);
+      dmx[c] = fmax(dmx[c], yc[c]);
+    }
+  }
+  uint32_t* u = reinterpret_cast<uint32_t*>(stats + (size_t)img * WL_STATS);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float a = lmn[c], b = lmx[c];
+    for (int o = 32; o > 0; o >>= 1) {
+      a = fminf(a, __shfl_xor(a, o));
+      b = fmaxf(b, __shfl_xor(b, o));
+    }
+    double da = dmn[c], db = dmx[c];
+    for (int o = 32; o > 0; o >>= 1) {
+      da = fmin(da, __shfl_xor(da, o));
+      db = fmax(db, __shfl_xor(db, o));
+    }
+    // YCbCr of [0,1] inputs is positive: float order == unsigned bit order
+    if ((threadIdx.x & 63) == 0 && a <= b) {
+      atomicMin(&u[2 * c], __float_as_uint(a));
+      atomicMax(&u[2 * c + 1], __float_as_uint(b));
+      unsigned long long* u64 = reinterpret_cast<unsigned long long*>(stats + (size_t)img * WL_STATS);
+      atomicMin(&u64[WlStats::MN64 + c], (unsigned long long)__double_as_longlong(da));
+      atomicMax(&u64[WlStats::MX64 + c], (unsigned long long)__double_as_longlong(db));
+    }
+  }
+}
+
+__device__ __forceinline__ void wl_minmax(const double* st, int c, float& mn, float& mx) {
+  const uint32_t* u = reinterpret_cast<const uint32_t*>(st);
+  mn = __uint_as_float(u[2 * c]);
+  mx = __uint_as_float(u[2 * c + 1]);
+}
+
+__device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn, double& mx) {
+  const unsigned long long* u64 = reinterpret_cast<const unsigned long long*>(st);
+  mn = __longlong_as_double((long long)u64[WlStats::MN64 + c]);
+  mx = __longlong_as_double((long long)u64[WlStats::MX64 + c]);
+}
+
+// ---- 2: one analysis level ----------------------------------------------------------------------
+constexpr int DT = 16;  // output tile (DT x DT coefficients per band)
+
+template <int WV>
+__global__ __launch_bounds__(256) void wl_dwt(wreal* __restrict__ ws, size_t img_floats,
+                                              const double* __restrict__ stats, int level,
+                                              size_t in_off, int Hin, int Win, size_t out_off,
+                                              int Ho, int Wo, int tiles_x) {
+  using Wv = Wav<WV>;
+  constexpr int F = Wv::F;
+  constexpr int NI = 2 * DT + F - 2;  // staged input rows / cols
+  __shared__ wreal xin[NI][NI + 1];
+  __shared__ wreal vl[DT][NI + 1], vh[DT][NI + 1];
+
+  const int img = blockIdx.z / 3, c = blockIdx.z % 3;
+  wreal* base = ws + img * img_floats;
+  const wreal* X = base + in_off + (size_t)c * ((level == 1) ? (size_t)Hin * Win : (size_t)4 * Hin * Win);
+  // level 1 reads plane c; deeper levels read band 'aa' (slot 0) of channel c of the level above
+  const size_t bsz = (size_t)Ho * Wo;
+  wreal* out = base + out_off + (size_t)c * 4 * bsz;  // [aa, ad, da, dd]
+  wreal mn = 0, inv = 1;
+  bool norm = false;
+  if (level == 1) {
+    wreal mx;
+    wl_minmax64(stats + (size_t)img * WL_STATS, c, mn, mx);
+    inv = mx - mn;
+    norm = true;
+  }
+  const int ti = blockIdx.x / tiles_x, tj = blockIdx.x % tiles_x;
+  const int i0 = ti * DT, j0 = tj * DT;
+  const int r0 = 2 * i0 + 2 - F, q0 = 2 * j0 + 2 - F;  // input coordinate of staged [0][0]
+  for (int k = threadIdx.x; k < NI * NI; k += 256) {
+    const int r = k / NI, q = k % NI;
+    wreal v = X[(size_t)sym_idx(r0 + r, Hin) * Win + sym_idx(q0 + q, Win)];
+    if (norm) v = (v - mn) / inv;  // skimage: channel = out - min; channel /= max - min
+    xin[r][q] = v;
+  }
+  __syncthreads();
+  // axis 0 first (pywt dwtn order): output row i uses staged rows 2ii + F-1-p
+  for (int k = threadIdx.x; k < DT * NI; k += 256) {
+    const int ii = k / NI, q = k % NI;
+    wreal lo = 0, hi = 0;
+#pragma unroll
+    for (int p = 0; p < F; ++p) {
+      const wreal v = xin[2 * ii + F - 1 - p][q];
+      if (Wv::dlo[p] != 0) lo = lo + Wv::dlo[p] * v;  // no FMA: pywt's mul-then-add
+      if (Wv::dhi[p] != 0) hi = hi + Wv::dhi[p] * v;
+    }
+    vl[ii][q] = lo;
+    vh[ii][q] = hi;
+  }
+  __syncthreads();
+  const int ii = threadIdx.x / DT, jj = threadIdx.x % DT;
+  const int i = i0 + ii, j = j0 + jj;
+  if (i < Ho && j < Wo) {
+    wreal aa = 0, ad = 0, da = 0, dd = 0;
+#pragma unroll
+    for (int q = 0; q < F; ++q) {  // then axis 1: output column j uses staged cols 2jj + F-1-q
+      const wreal l = vl[ii][2 * jj + F - 1 - q], hh = vh[ii][2 * jj + F - 1 - q];
+      if (Wv::dlo[q] != 0) {
+        aa = aa + Wv::dlo[q] * l;   // key 'aa': axis 0 low, axis 1 low
+        da = da + Wv::dlo[q] * hh;  // key 'da': axis 0 high, axis 1 low
+      }
+      if (Wv::dhi[q] != 0) {
+        ad = ad + Wv::dhi[q] * l;   // key 'ad': axis 0 low, axis 1 high
+        dd = dd + Wv::dhi[q] * hh;
+      }
+    }
+    const size_t o = (size_t)i * Wo + j;
+    out[o] = aa;
+    out[bsz + o] = ad;
+    out[2 * bsz + o] = da;
+    out[3 * bsz + o] = dd;
+  }
+}
+
+// ---- 3: sum of squares per detail band ----------------------------------------------------------
+__global__ __launch_bounds__(1024) void wl_sumsq(const wreal* __restrict__ ws, size_t img_floats,
+                                                 double* __restrict__ stats, WlLayout Lt) {
+  // block = (img, c, l, b)
+  int t = blockIdx.x;
+  const int b = t % 3;
+  t /= 3;
+  const int l = t % Lt.L;
+  t /= Lt.L;
+  const int c = t % 3;
+  const int img = t / 3;
+  const int lev = l + 1;
+  const size_t bsz = (size_t)Lt.H[lev] * Lt.W[lev];
+  const wreal* d = ws + img * img_floats + Lt.off_band[lev] + (size_t)c * 4 * bsz + (size_t)(b + 1) * bsz;
+  double s = 0.0;
+  for (size_t k = threadIdx.x; k < bsz; k += 1024) {
+    const double v = d[k];
+    s += v * v;
+  }
+  __shared__ double red[16];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int k = 0; k < 16; ++k) tot += red[k];
+    stats[(size_t)img * WL_STATS + WlStats::sumsq(c, l, b, Lt.L)] = tot;
+  }
+}
+
+// ---- 4: sigma = median(|finest dd| != 0) / ppf(0.75) ------------------------------------------
+// The median is over the NONZERO coefficients, so which coefficients are exactly zero must match
+// the reference: the analysis runs in fp64 with pywt's op order (normalise (Y - min)/(max - min),
+// axis 0 then axis 1, multiply then add), under which equal samples give an exact 0.
+// exact rank selection over nonzero non-negative doubles: 6 passes of <= 11 bits on the bits
+__device__ unsigned long long radix_select64(const double* __restrict__ d, size_t n, uint32_t rank,
+                                             uint32_t* hist) {
+  unsigned long long prefix = 0, pmask = 0;
+  for (int pass = 0; pass < 6; ++pass) {
+    const int sh = (pass < 5) ? 52 - 11 * pass : 0;
+    const int wd = (pass < 5) ? 11 : 8;
+    const int nb = 1 << wd;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(d[k]) & 0x7FFFFFFFFFFFFFFFull;
+      if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    __shared__ uint32_t sel_bin, sel_rank;
+    if (threadIdx.x == 0) {
+      uint32_t acc = 0;
+      int bin = 0;
+      for (; bin < nb - 1; ++bin) {
+        if (acc + hist[bin] > rank) break;
+        acc += hist[bin];
+      }
+      sel_bin = (uint32_t)bin;
+      sel_rank = rank - acc;
+    }
+    __syncthreads();
+    prefix |= (unsigned long long)sel_bin << sh;
+    pmask |= (unsigned long long)(nb - 1) << sh;
+    rank = sel_rank;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(1024) void wl_median(const wreal* __restrict__ ws, size_t img_floats,
+                                                  double* __restrict__ stats, WlLayout Lt) {
+  const int img = blockIdx.x / 3, c = blockIdx.x % 3;
+  const size_t bsz = (size_t)Lt.H[1] * Lt.W[1];
+  const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t cnt_s;
+  if (threadIdx.x == 0) cnt_s = 0;
+  __syncthreads();
+  uint32_t cnt = 0;
+  for (size_t k = threadIdx.x; k < bsz; k += 1024) cnt += d[k] != 0.0;  // -0.0 == 0.0
+  atomicAdd(&cnt_s, cnt);
+  __syncthreads();
+  const uint32_t total = cnt_s;
+  double med;
+  if (total == 0) {
+    med = NAN;  // np.median of an empty selection
+  } else {
+    const uint32_t klo = (total - 1) / 2, khi = total / 2;
+    const double vlo = __longlong_as_double((long long)radix_select64(d, bsz, klo, hist));
+    const double vhi =
+        (khi == klo) ? vlo : __longlong_as_double((long long)radix_select64(d, bsz, khi, hist));
+    med = (vlo + vhi) / 2.0;  // np.median: mean of the two middle values
+  }
+  if (threadIdx.x == 0) {
+    stats[(size_t)img * WL_STATS + WlStats::median(c, Lt.L)] = med;
+    stats[(size_t)img * WL_STATS + WlStats::DIAG + c] = (double)total;  // diagnostics
+  }
+}
+
+// ---- 5: BayesShrink thresholds ------------------------------------------------------------------
+__global__ void wl_thresh(double* __restrict__ stats, WlLayout Lt) {
+  const int img = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  double* st = stats + (size_t)img * WL_STATS;
+  bool bad = false;
+  for (int c = 0; c < 3; ++c) {
+    double mn, mx;
+    wl_minmax64(st, c, mn, mx);
+    if (!(mx > mn)) bad = true;  // 0.14.2 divides by zero -> NaN everywhere -> U8 0
+    const double sigma = st[WlStats::median(c, Lt.L)] / 0.6744897501960817;
+    if (!(sigma == sigma)) bad = true;
+    const double var = sigma * sigma;
+    for (int l = 0; l < Lt.L; ++l)
+      for (int b = 0; b < 3; ++b) {
+        const int lev = l + 1;
+        const double cnt = (double)Lt.H[lev] * Lt.W[lev];
+        const double dvar = st[WlStats::sumsq(c, l, b, Lt.L)] / cnt;
+        const double t = var / sqrt(fmax(dvar - var, 2.220446049250313e-16));
+        st[WlStats::thr(c, l, b, Lt.L)] = t;
+      }
+  }
+  st[WlStats::FLAG] = bad ? 1.0 : 0.0;
+}
+
+__device__ __forceinline__ wreal soft(wreal d, wreal t) {
+  const wreal s = 1.0 - t / fabs(d);  // |d| == 0 -> -inf -> 0 (pywt.threshold 'soft')
+  return d * fmax(s, 0.0);
+}
+
+// ---- 6: one synthesis level (levels L..2), output = approx of level l-1 -------------------------
+template <int WV>
+__global__ __launch_bounds__(256) void wl_idwt(wreal* __restrict__ ws, size_t img_floats,
+                                               const double* __restrict__ stats, int level, int L,
+                                               size_t in_off, int Nh, int Nw, size_t out_off,
+                                               int Hout, int Wout, size_t out_chan_stride) {
+  using Wv = Wav<WV>;
+  constexpr int F = Wv::F, HF = F / 2;
+  const int img = blockIdx.z / 3, c = blockIdx.z % 3;
+  wreal* base = ws + img * img_floats;
+  const size_t bsz = (size_t)Nh * Nw;
+  const wreal* A = base + in_off + (size_t)c * 4 * bsz;
+  const wreal* AD = A + bsz;
+  const wreal* DA = A + 2 * bsz;
+  const wreal* DD = A + 3 * bsz;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const wreal tad = st[WlStats::thr(c, level - 1, 0, L)];
+  const wreal tda = st[WlStats::thr(c, level - 1, 1, L)];
+  const wreal tdd = st[WlStats::thr(c, level - 1, 2, L)];
+  wreal* out = base + out_off + (size_t)c * out_chan_stride;
+  const int64_t total = (int64_t)Hout * Wout;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(k / Wout), q = (int)(k - (int64_t)p * Wout);
+    const int m = p >> 1, r = p & 1, nn = q >> 1, s = q & 1;
+    wreal acc = 0;
+#pragma unroll
+    for (int j = 0; j < HF; ++j) {
+      const int row = m + HF - 1 - j;
+      const wreal fa0 = Wv::rlo[2 * j], fa1 = Wv::rlo[2 * j + 1];
+      const wreal fd0 = Wv::rhi[2 * j], fd1 = Wv::rhi[2 * j + 1];
+      const wreal fa = r ? fa1 : fa0, fd = r ? fd1 : fd0;
+#pragma unroll
+      for (int kk = 0; kk < HF; ++kk) {
+        const int col = nn + HF - 1 - kk;
+        const wreal ga0 = Wv::rlo[2 * kk], ga1 = Wv::rlo[2 * kk + 1];
+        const wreal gd0 = Wv::rhi[2 * kk], gd1 = Wv::rhi[2 * kk + 1];
+        const wreal ga = s ? ga1 : ga0, gd = s ? gd1 : gd0;
+        const size_t o = (size_t)row * Nw + col;
+        if ((fa0 != 0 || fa1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fa * ga * A[o];
+        if ((fa0 != 0 || fa1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fa * gd * (soft(AD[o], tad));
+        if ((fd0 != 0 || fd1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fd * ga * (soft(DA[o], tda));
+        if ((fd0 != 0 || fd1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fd * gd * (soft(DD[o], tdd));
+      }
+    }
+    out[(size_t)p * Wout + q] = acc;
+  }
+}
+
+// ---- 7: level 1 synthesis of all channels + colour + casts --------------------------------------
+template <int WV>
+__global__ __launch_bounds__(256) void wl_idwt_final(const wreal* __restrict__ ws,
+                                                     size_t img_floats,
+                                                     const double* __restrict__ stats, int L,
+                                                     size_t in_off, int Nh, int Nw, int h, int w,
+                                                     uint8_t* __restrict__ out_u8,
+                                                     int64_t row_stride,
+                                                     float* __restrict__ out_f32) {
+  using Wv = Wav<WV>;
+  constexpr int F = Wv::F, HF = F / 2;
+  const int img = blockIdx.y;
+  const wreal* base = ws + img * img_floats + in_off;
+  const size_t bsz = (size_t)Nh * Nw;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const bool bad = st[WlStats::FLAG] != 0.0;
+  wreal t[3][3], mn[3], sc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    wreal mx;
+    wl_minmax64(st, c, mn[c], mx);
+    sc[c] = mx - mn[c];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) t[c][b] = st[WlStats::thr(c, 0, b, L)];
+  }
+  const int64_t total = (int64_t)h * w;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(k / w), q = (int)(k - (int64_t)p * w);
+    const int m = p >> 1, r = p & 1, nn = q >> 1, s = q & 1;
+    double ych[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const wreal* A = base + (size_t)c * 4 * bsz;
+      wreal acc = 0;
+#pragma unroll
+      for (int j = 0; j < HF; ++j) {
+        const int row = m + HF - 1 - j;
+        const wreal fa0 = Wv::rlo[2 * j], fa1 = Wv::rlo[2 * j + 1];
+        const wreal fd0 = Wv::rhi[2 * j], fd1 = Wv::rhi[2 * j + 1];
+        const wreal fa = r ? fa1 : fa0, fd = r ? fd1 : fd0;
+#pragma unroll
+        for (int kk = 0; kk < HF; ++kk) {
+          const int col = nn + HF - 1 - kk;
+          const wreal ga0 = Wv::rlo[2 * kk], ga1 = Wv::rlo[2 * kk + 1];
+          const wreal gd0 = Wv::rhi[2 * kk], gd1 = Wv::rhi[2 * kk + 1];
+          const wreal ga = s ? ga1 : ga0, gd = s ? gd1 : gd0;
+          const size_t o = (size_t)row * Nw + col;
+          if ((fa0 != 0 || fa1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fa * ga * A[o];
+          if ((fa0 != 0 || fa1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fa * gd * (soft(A[bsz + o], t[c][0]));
+          if ((fd0 != 0 || fd1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fd * ga * (soft(A[2 * bsz + o], t[c][1]));
+          if ((fd0 != 0 || fd1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fd * gd * (soft(A[3 * bsz + o], t[c][2]));
+        }
+      }
+      // inner denoise_wavelet clip (0.14.2), then * (max - min) + min
+      const double v = fmin(fmax((double)acc, 0.0), 1.0);
+      ych[c] = v * sc[c] + mn[c];
+    }
+    // ycbcr2rgb: (arr - [16,128,128]) @ inv(ycbcr_from_rgb).T (numpy.linalg.inv, full precision,
+    // fma-chain dot as numpy's matmul), then clip [0, 1]
+    const double Y = ych[0] - 16.0, Cb = ych[1] - 128.0, Cr = ych[2] - 128.0;
+    double o3[3];
+    o3[0] = dot3(Y, Cb, Cr, 0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937);
+    o3[1] = dot3(Y, Cb, Cr, 0.004566210045662101, -0.0015363236860449021, -0.003188110949655707);
+    o3[2] = dot3(Y, Cb, Cr, 0.004566210045662101, 0.007910716233554741, 1.1977497040511743e-08);
+    const int y = p, x = q;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double v = fmin(fmax(o3[c], 0.0), 1.0);
+      if (bad) v = 0.0;
+      if (out_u8)
+        out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3 + c] =
+            (uint8_t)(int)(255.0 * v);
+      if (out_f32) out_f32[(((int64_t)img * h + y) * w + x) * 3 + c] = (float)v;
+    }
+  }
+}
+
+template <int WV>
+static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float* out_f32,
+                  const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st) {
+  wreal* wsf = (wreal*)ws;
+  double* stats = (double*)((char*)ws + Lt.stats_off);
+  const int n = Lt.n;
+  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n);
+  {
+    const int64_t np = (int64_t)Lt.h * Lt.w;
+    int gx = (int)((np + 255) / 256);
+    if (gx > 256) gx = 256;
+    hipLaunchKernelGGL(wl_color, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w, row_stride,
+                       wsf, Lt.img_floats, stats);
+  }
+  for (int l = 1; l <= Lt.L; ++l) {
+    const size_t in_off = (l == 1) ? 0 : Lt.off_band[l - 1];
+    const int tx = (Lt.W[l] + DT - 1) / DT, ty = (Lt.H[l] + DT - 1) / DT;
+    hipLaunchKernelGGL((wl_dwt<WV>), dim3(tx * ty, 1, n * 3), dim3(256), 0, st, wsf, Lt.img_floats,
+                       stats, l, in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
+                       tx);
+  }
+  hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
+  hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
+  hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  for (int l = Lt.L; l >= 2; --l) {
+    const int64_t tot = (int64_t)Lt.H[l - 1] * Lt.W[l - 1];
+    int gx = (int)((tot + 255) / 256);
+    if (gx > 1024) gx = 1024;
+    // the level-(l-1) 'aa' slot (consumed by the analysis already) receives the reconstruction
+    hipLaunchKernelGGL((wl_idwt<WV>), dim3(gx, 1, n * 3), dim3(256), 0, st, wsf, Lt.img_floats, stats,
+                       l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Lt.H[l - 1],
+                       Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1]);
+  }
+  {
+    const int64_t tot = (int64_t)Lt.h * Lt.w;
+    int gx = (int)((tot + 255) / 256);
+    if (gx > 2048) gx = 2048;
+    hipLaunchKernelGGL((wl_idwt_final<WV>), dim3(gx, n), dim3(256), 0, st, wsf, Lt.img_floats, stats,
+                       Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h, Lt.w, out_u8, row_stride, out_f32);
+  }
+  return IDN_OK;
+}
+
+}  // namespace idn
+
+extern "C" size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels) {
+  using namespace idn;
+  if (n <= 0 || h <= 0 || w <= 0 || (wavelet != IDN_WAVELET_DB1 && wavelet != IDN_WAVELET_BIOR15))
+    return 0;
+  return wl_layout(n, h, w, wavelet, levels).bytes;
+}
+
+extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,
+                                      float* out_f32, int n, int h, int w, int64_t row_stride,
+                                      int wavelet, int levels, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(src || in_f64, "idn_wavelet_denoise_u8: no input");
+  IDN_CHECK_ARG(out_u8 || out_f32, "idn_wavelet_denoise_u8: no output");
+  IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0, "idn_wavelet_denoise_u8: bad shape");
+  IDN_CHECK_ARG(row_stride >= (int64_t)w * 3, "idn_wavelet_denoise_u8: row_stride < w*3");
+  IDN_CHECK_ARG(wavelet == IDN_WAVELET_DB1 || wavelet == IDN_WAVELET_BIOR15,
+                "idn_wavelet_denoise_u8: unknown wavelet %d", wavelet);
+  if (n == 0) return IDN_OK;
+  const WlLayout Lt = wl_layout(n, h, w, wavelet, levels);
+  IDN_CHECK_ARG(Lt.L >= 1 && Lt.L <= WL_MAXL, "idn_wavelet_denoise_u8: levels %d out of range", Lt.L);
+  // pywt needs every level's input at least one sample long; skimage warns but proceeds
+  for (int l = 1; l <= Lt.L; ++l)
+    IDN_CHECK_ARG(Lt.H[l - 1] >= 1 && Lt.W[l - 1] >= 1, "idn_wavelet_denoise_u8: image too small");
+  if (!workspace || ws_bytes < Lt.bytes)
+    return set_error(IDN_EWORKSPACE, "idn_wavelet_denoise_u8: needs %zu workspace bytes (got %zu)",
+                     Lt.bytes, ws_bytes);
+  hipStream_t st = as_stream(stream);
+  if (wavelet == IDN_WAVELET_DB1) wl_run<IDN_WAVELET_DB1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+  else wl_run<IDN_WAVELET_BIOR15>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+  IDN_CHECK_LAUNCH("idn_wavelet_denoise_u8");
+  return IDN_OK;
+}

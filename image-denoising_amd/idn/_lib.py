@@ -33,8 +33,8 @@ SIGNATURES = {
     "idn_noise_workspace_size": (_c_size, [_c_int, _c_int]),
     "idn_periodic_pattern_u8": (_c_int, [_c_u8p, _c_int, _c_int, _c_int, _c_dbl, _c_vp]),
     "idn_add_pattern_u8": (_c_int, [_c_u8p, _c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
-    "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_int,
-                                        _c_vp, _c_size, _c_vp]),
+    "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_i64,
+                                        _c_int, _c_int, _c_vp, _c_size, _c_vp]),
     "idn_wavelet_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "idn_blob_f32": (_c_int, [_c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_int,
                               ctypes.POINTER(ctypes.c_double), _c_int, _c_vp]),

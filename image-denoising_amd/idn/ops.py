@@ -208,3 +208,59 @@ def blob(x: torch.Tensor, pixel_means=PIXEL_MEANS, out_hw: Optional[Tuple[int, i
                                   1 if flip else 0, _stream())
     _lib.check(rc, "idn_blob_f32")
     return y
+
+
+# ---- wavelet denoise ---------------------------------------------------------------------------
+
+_WS_CACHE: dict = {}
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    """grow-only per-device scratch (the C-ABI never allocates)."""
+    key = str(device)
+    ws = _WS_CACHE.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _WS_CACHE[key] = ws
+    return ws
+
+
+def denoise_wavelet(x: torch.Tensor, wavelet: str = "bior1.5", levels: Optional[int] = None,
+                    out: str = "u8", out_u8: Optional[torch.Tensor] = None):
+    """(255 * skimage.restoration.denoise_wavelet(x, method='BayesShrink', mode='soft',
+    wavelet=wavelet, multichannel=True, convert2ycbcr=True, wavelet_levels=levels)).astype(uint8)
+    with skimage 0.14.2's clipping.  x: uint8 (N,)H,W,3 or float64 (N,)H,W,3 in [0, 1].
+    out: 'u8' | 'f32' (float result before the cast) | 'both'."""
+    wv = WAVELETS.get(wavelet)
+    if wv is None:
+        raise ValueError(f"denoise_wavelet: unsupported wavelet {wavelet!r} (db1/haar/bior1.5)")
+    xb, sq = _as_batch(x, "denoise_wavelet")
+    if xb.shape[-1] != 3:
+        raise ValueError("denoise_wavelet: multichannel YCbCr path needs 3 channels")
+    n, h, w, _ = xb.shape
+    if xb.dtype == torch.uint8:
+        src, src64 = xb.contiguous(), None
+    elif xb.dtype == torch.float64:
+        src, src64 = None, xb.contiguous()
+    else:
+        raise TypeError(f"denoise_wavelet: expected uint8 or float64, got {xb.dtype}")
+    want_u8 = out in ("u8", "both")
+    want_f32 = out in ("f32", "both")
+    y8 = (out_u8.view(n, h, w, 3) if out_u8 is not None else
+          torch.empty((n, h, w, 3), dtype=torch.uint8, device=xb.device)) if want_u8 else None
+    y32 = torch.empty((n, h, w, 3), dtype=torch.float32, device=xb.device) if want_f32 else None
+    lib = _lib.load()
+    lv = -1 if levels is None else int(levels)
+    nbytes = lib.idn_wavelet_workspace_size(n, h, w, wv, lv)
+    ws = _workspace(nbytes, xb.device)
+    rc = lib.idn_wavelet_denoise_u8(src.data_ptr() if src is not None else None,
+                                    src64.data_ptr() if src64 is not None else None,
+                                    y8.data_ptr() if y8 is not None else None,
+                                    y32.data_ptr() if y32 is not None else None,
+                                    n, h, w, w * 3, wv, lv, ws.data_ptr(), nbytes, _stream())
+    _lib.check(rc, "idn_wavelet_denoise_u8")
+    if out == "u8":
+        return _finish(y8, sq)
+    if out == "f32":
+        return _finish(y32, sq)
+    return _finish(y8, sq), _finish(y32, sq)

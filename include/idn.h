@@ -117,12 +117,14 @@ int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst,
 /* out_u8 = (255*denoise_wavelet(img, method='BayesShrink', mode='soft', wavelet=wavelet,
  *           multichannel=True, convert2ycbcr=True, wavelet_levels=levels)).astype(uint8),
  * c = 3.  levels <= 0 selects skimage's default max(dwt_max_level - 3, 1).  in_f64 (nullable)
- * replaces src when the caller holds a float image in [0,1] (the reference's f64 branches).
+ * replaces src when the caller holds a float image in [0,1] (the reference's f64 branches, dense
+ * n*h*w*3).  out_f32 (nullable) receives the float result before the U8 cast (dense n*h*w*3).
+ * Computed in fp32 with fp64 reductions: |out - reference| <= 1e-5 before the cast.
  * Replaces lib/model/test.py:197-201,1807-1810, minibatch.py:1653-1656,
  * minibatch_before_curvelet.py:85-87. */
-int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8, int n,
-                           int h, int w, int64_t row_stride, int wavelet, int levels,
-                           void* workspace, size_t ws_bytes, void* stream);
+int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,
+                           float* out_f32, int n, int h, int w, int64_t row_stride, int wavelet,
+                           int levels, void* workspace, size_t ws_bytes, void* stream);
 size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels);
 
 /* ---- blob epilogue (lib/utils/blob.py:17-47) -------------------------------------------- */

@@ -41,6 +41,8 @@ def lib():
         L.oracle_bilateral_u8.restype = None
         L.oracle_bilateral_f32.argtypes = [u8p, u8p, i, i, i, i, i64, i, d, d]
         L.oracle_bilateral_f32.restype = None
+        L.oracle_matmul3_fma.argtypes = [u8p, u8p, i64, u8p, u8p, u8p]
+        L.oracle_matmul3_fma.restype = None
         _lib = L
     return _lib
 
@@ -103,3 +105,15 @@ def bilateral_prefilter_f32(img, d, sigma_color, sigma_space) -> np.ndarray:
     lib().oracle_bilateral_f32(a.ctypes.data, out.ctypes.data, n, h, w, c, w * c, d,
                                float(sigma_color), float(sigma_space))
     return _unsq(out, sq)
+
+
+def matmul3_fma(x: np.ndarray, M: np.ndarray, pre=(0.0, 0.0, 0.0), post=(0.0, 0.0, 0.0)) -> np.ndarray:
+    """(x - pre) @ M.T + post with numpy/OpenBLAS's fma-chain rounding (see filters.c)."""
+    a = np.ascontiguousarray(x, np.float64)
+    out = np.empty_like(a)
+    Mc = np.ascontiguousarray(M, np.float64)
+    pr = np.ascontiguousarray(pre, np.float64)
+    po = np.ascontiguousarray(post, np.float64)
+    lib().oracle_matmul3_fma(a.ctypes.data, out.ctypes.data, a.size // 3, Mc.ctypes.data,
+                             pr.ctypes.data, po.ctypes.data)
+    return out

@@ -211,3 +211,21 @@ void oracle_bilateral_f32(const uint8_t* src, float* out, int n, int h, int w, i
       }
   }
 }
+
+/* numpy `arr @ M.T` for (n,3) x (3,3) float64 as OpenBLAS's dgemm kernels evaluate it on x86-64
+ * with FMA (an fma chain over k, checked bit-for-bit against numpy 1.26 / 2.2 in this image), with
+ * skimage's offsets: out = fma(x2', M[k][2], fma(x1', M[k][1], x0' * M[k][0])) + post[k], where
+ * x' = x - pre (rgb2ycbcr: pre = 0, post = [16,128,128]; ycbcr2rgb: pre = [16,128,128], post = 0).
+ * Used by oracle/wavelet.py so the oracle does not depend on the host BLAS kernel. */
+void oracle_matmul3_fma(const double* in, double* out, int64_t n, const double* M,
+                        const double* pre, const double* post) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    const double x0 = in[3 * i] - pre[0], x1 = in[3 * i + 1] - pre[1], x2 = in[3 * i + 2] - pre[2];
+    for (int k = 0; k < 3; ++k) {
+      const double* m = M + 3 * k;
+      const double d = fma(x2, m[2], fma(x1, m[1], x0 * m[0]));
+      out[3 * i + k] = d + post[k];
+    }
+  }
+}

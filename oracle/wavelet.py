@@ -7,7 +7,9 @@ numpy restatement of the wavelet denoiser the reference calls:
                                                                   minibatch.py:1653-1656
   denoise_wavelet(im, ..., wavelet_levels=3)  (default 'db1')     minibatch_before_curvelet.py:85-87
 
-with scikit-image 0.14.2's wrapper semantics (requirements.txt:160): img_as_float, rgb2ycbcr on
+with scikit-image 0.14.2's wrapper semantics (the two colour matmuls use numpy/OpenBLAS's fma-chain
+rounding, reproduced in C by oracle/filters.c:oracle_matmul3_fma, so zero sets of the finest dd do
+not depend on the host BLAS kernel) (requirements.txt:160): img_as_float, rgb2ycbcr on
 the (BGR-as-RGB) data, per channel min/max normalisation, `_wavelet_threshold` (pywt wavedecn,
 'symmetric' mode, level default max(dwt_max_level - 3, 1), sigma = median(|finest dd| != 0) /
 0.6744897501960817, BayesShrink thresholds var / sqrt(max(mean(d^2) - var, eps)) per detail band,
@@ -161,12 +163,13 @@ def wavelet_threshold(img2d: np.ndarray, w: str, levels=None) -> np.ndarray:
 def denoise_wavelet(img, wavelet: str = "bior1.5", levels=None) -> np.ndarray:
     """skimage 0.14.2 denoise_wavelet(img, method='BayesShrink', mode='soft', wavelet=wavelet,
     multichannel=True, convert2ycbcr=True, wavelet_levels=levels) -> float64 [0, 1]."""
+    from .cv import matmul3_fma
     x = img.astype(np.float64) * (1.0 / 255.0) if img.dtype == np.uint8 else np.asarray(img, np.float64)
-    out = x @ YCBCR_FROM_RGB.T + YCBCR_OFFSET
+    out = matmul3_fma(x, YCBCR_FROM_RGB, post=YCBCR_OFFSET)  # rgb2ycbcr
     for i in range(3):
         mn, mx = out[..., i].min(), out[..., i].max()
         ch = (out[..., i] - mn) / (mx - mn)
         ch = np.clip(wavelet_threshold(ch, wavelet, levels), 0, 1)
         out[..., i] = ch * (mx - mn) + mn
-    out = (out - YCBCR_OFFSET) @ RGB_FROM_YCBCR.T
+    out = matmul3_fma(out, RGB_FROM_YCBCR, pre=YCBCR_OFFSET)  # ycbcr2rgb
     return np.clip(out, 0, 1)

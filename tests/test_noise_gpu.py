@@ -142,8 +142,9 @@ def test_philox_sap_rates(dev):
         salt = (f64 == 1.0) & (x != 1.0)
         pep = (f64 == 0.0) & (x != 0.0)
         keep = f64 == x
-        assert abs(salt.mean() - amount / 2) < 3e-3
-        assert abs(pep.mean() - amount / 2) < 3e-3
+        inner = (x > 0) & (x < 1)  # flips on already-black / white pixels are invisible
+        assert abs(salt[inner].mean() - amount / 2) < 3e-3
+        assert abs(pep[inner].mean() - amount / 2) < 3e-3
         assert np.all(salt | pep | keep)
         assert np.all(u8[salt] == 255) and np.all(u8[pep] == 0)
 
