@@ -36,6 +36,15 @@ SIGNATURES = {
     "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_i64,
                                         _c_int, _c_int, _c_vp, _c_size, _c_vp]),
     "idn_wavelet_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    "idn_gaussian_blur_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp]),
+    "idn_box_blur_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp]),
+    "idn_shader_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_dbl, _c_vp]),
+    "idn_bloom_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_vp, _c_vp, _c_int,
+                              _c_vp, _c_vp]),
+    "idn_blob_from_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                   ctypes.POINTER(ctypes.c_double), _c_int, _c_vp]),
+    "idn_resize_linear_f32": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_dbl,
+                                       _c_dbl, _c_vp]),
     "idn_blob_f32": (_c_int, [_c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_int,
                               ctypes.POINTER(ctypes.c_double), _c_int, _c_vp]),
 }

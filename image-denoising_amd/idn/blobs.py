@@ -1,0 +1,60 @@
+"""Drop-in for lib/utils/blob.py (im_list_to_blob 17-30, prep_im_for_blob 33-47) on the GPU.
+
+Accepts numpy images (as the reference passes them) or device tensors; computes on the GPU and
+returns numpy by default (the detector is fed from host memory, network.py:476-485) or a device
+tensor with as_tensor=True.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+def _to_device(im):
+    if isinstance(im, torch.Tensor):
+        return im if im.device.type == "cuda" else im.cuda()
+    return torch.from_numpy(np.ascontiguousarray(im)).cuda()
+
+
+def im_scale_for(shape, target_size: int, max_size: int) -> float:
+    """prep_im_for_blob's scale rule (blob.py:37-43)."""
+    im_size_min = float(min(shape[0:2]))
+    im_size_max = float(max(shape[0:2]))
+    im_scale = float(target_size) / float(im_size_min)
+    if np.round(im_scale * im_size_max) > max_size:
+        im_scale = float(max_size) / float(im_size_max)
+    return im_scale
+
+
+def prep_im_for_blob(im, pixel_means, target_size, max_size, flip: bool = False,
+                     as_tensor: bool = False):
+    """im (uint8 BGR or float64) -> (float32 mean-subtracted, resized image, im_scale).
+
+    `flip` folds the roidb 'flipped' column reversal (minibatch.py:1675) into the same pass."""
+    x = _to_device(im)
+    means = np.asarray(pixel_means, np.float64).reshape(-1)
+    if x.dtype == torch.uint8:
+        f = ops.blob(x, means, flip=flip)[0]
+    elif x.dtype == torch.float64:
+        f = ops.blob_from_f64(x, means, flip=flip)[0]
+    elif x.dtype == torch.float32:
+        f = ops.blob_from_f64(x.double(), means, flip=flip)[0]  # f32 -> f64 is exact
+    else:
+        raise TypeError(f"prep_im_for_blob: unsupported dtype {x.dtype}")
+    im_scale = im_scale_for(f.shape, target_size, max_size)
+    if im_scale != 1.0:
+        f = ops.resize_linear(f, im_scale, im_scale)
+    return (f if as_tensor else f.cpu().numpy()), im_scale
+
+
+def im_list_to_blob(ims, as_tensor: bool = False):
+    """Zero-padded NHWC float32 blob of prepared images (numpy or device tensors)."""
+    xs = [_to_device(im) for im in ims]
+    hmax = max(int(x.shape[0]) for x in xs)
+    wmax = max(int(x.shape[1]) for x in xs)
+    blob = torch.zeros((len(xs), hmax, wmax, 3), dtype=torch.float32, device=xs[0].device)
+    for i, x in enumerate(xs):
+        blob[i, : x.shape[0], : x.shape[1], :] = x.float()
+    return blob if as_tensor else blob.cpu().numpy()

@@ -264,3 +264,94 @@ def denoise_wavelet(x: torch.Tensor, wavelet: str = "bior1.5", levels: Optional[
     if out == "f32":
         return _finish(y32, sq)
     return _finish(y8, sq), _finish(y32, sq)
+
+
+# ---- float64 filters, shader, bloom ------------------------------------------------------------
+
+def _f64_batch(x: torch.Tensor, name: str):
+    xb, sq = _as_batch(x, name)
+    if xb.dtype != torch.float64:
+        raise TypeError(f"{name}: expected float64, got {xb.dtype}")
+    return xb.contiguous(), sq
+
+
+def gaussian_blur_f64(x: torch.Tensor, ksize: int = 3) -> torch.Tensor:
+    """cv2.GaussianBlur on a float64 image (the train_v0 post hook after a float64 noise branch)."""
+    xb, sq = _f64_batch(x, "gaussian_blur_f64")
+    n, h, w, c = xb.shape
+    y = torch.empty_like(xb)
+    _lib.check(_lib.load().idn_gaussian_blur_f64(xb.data_ptr(), y.data_ptr(), n, h, w, c, int(ksize),
+                                                 _stream()), "idn_gaussian_blur_f64")
+    return _finish(y, sq)
+
+
+def blur_f64(x: torch.Tensor, ksize: int = 3) -> torch.Tensor:
+    """cv2.blur on a float64 image (test_v0 default branch, train_v0 'mean' post hook)."""
+    xb, sq = _f64_batch(x, "blur_f64")
+    n, h, w, c = xb.shape
+    y = torch.empty_like(xb)
+    _lib.check(_lib.load().idn_box_blur_f64(xb.data_ptr(), y.data_ptr(), n, h, w, c, int(ksize),
+                                            _stream()), "idn_box_blur_f64")
+    return _finish(y, sq)
+
+
+def shader(x: torch.Tensor, factor: float = 3.0) -> torch.Tensor:
+    """add_shader: PIL ImageEnhance.Brightness(factor) of the image, returned in RGB order."""
+    xb, sq = _u8_batch(x, "shader")
+    n, h, w, c = xb.shape
+    y = torch.empty_like(xb)
+    _lib.check(_lib.load().idn_shader_u8(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c, float(factor),
+                                         _stream()), "idn_shader_u8")
+    return _finish(y, sq)
+
+
+def bloom(x: torch.Tensor, rng=None, **flare_kw) -> torch.Tensor:
+    """add_bloom: Automold.add_sun_flare(img, flare_center=(100,100), angle=-pi/4) per image, the
+    random draws taken from `rng` (default: the global `random`, like the reference)."""
+    import math
+    from . import automold
+    xb, sq = _u8_batch(x, "bloom")
+    n, h, w, c = xb.shape
+    kw = dict(flare_center=(100, 100), angle=-math.pi / 4)
+    kw.update(flare_kw)
+    circ, wts = zip(*[automold.sun_flare_circles(h, w, rng=rng, **kw) for _ in range(n)])
+    circ, wts = np.stack(circ), np.stack(wts)
+    rmax = int(circ[..., 2].max()) if circ.size else 0
+    spans = torch.from_numpy(automold.span_table(max(rmax, 1))).to(xb.device)
+    circ_t = torch.from_numpy(np.ascontiguousarray(circ)).to(xb.device)
+    wts_t = torch.from_numpy(np.ascontiguousarray(wts)).to(xb.device)
+    y = torch.empty_like(xb)
+    _lib.check(_lib.load().idn_bloom_u8(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c,
+                                        circ_t.data_ptr(), wts_t.data_ptr(), circ.shape[1],
+                                        spans.data_ptr(), _stream()), "idn_bloom_u8")
+    return _finish(y, sq)
+
+
+def blob_from_f64(x: torch.Tensor, pixel_means=PIXEL_MEANS, out_hw: Optional[Tuple[int, int]] = None,
+                  flip: bool = False) -> torch.Tensor:
+    """prep_im_for_blob on a float64 image (the reference's float64 plain-noise branches)."""
+    xb, _ = _f64_batch(x, "blob_from_f64")
+    n, h, w, c = xb.shape
+    oh, ow = out_hw if out_hw is not None else (h, w)
+    y = torch.empty((n, oh, ow, 3), dtype=torch.float32, device=xb.device)
+    m = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(pixel_means, np.float64).reshape(-1)])
+    _lib.check(_lib.load().idn_blob_from_f64(xb.data_ptr(), y.data_ptr(), n, h, w, oh, ow, m,
+                                             1 if flip else 0, _stream()), "idn_blob_from_f64")
+    return y
+
+
+def resize_linear(x: torch.Tensor, fx: float, fy: float) -> torch.Tensor:
+    """cv2.resize(x, None, None, fx=fx, fy=fy, interpolation=cv2.INTER_LINEAR) on float32 NHWC."""
+    xb, sq = _as_batch(x, "resize_linear")
+    if xb.dtype != torch.float32:
+        raise TypeError("resize_linear: expected float32")
+    xb = xb.contiguous()
+    n, h, w, c = xb.shape
+    oh, ow = int(round(h * fy)), int(round(w * fx))  # cv::Size(saturate_cast<int>(...))
+    if (oh, ow) == (h, w):
+        return _finish(xb.clone(), sq)  # cv2.resize copies when the size is unchanged
+    y = torch.empty((n, oh, ow, c), dtype=torch.float32, device=xb.device)
+    _lib.check(_lib.load().idn_resize_linear_f32(xb.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow,
+                                                 float(fx), float(fy), _stream()),
+               "idn_resize_linear_f32")
+    return _finish(y, sq)

@@ -1,0 +1,179 @@
+"""Batch executor of noise-spec plans on the GPU.
+
+`Preprocessor(noise, mode)` turns a batch of uint8 BGR images (device tensor (N,H,W,3)) into what
+the reference's per-image loop body produces for each image (lib/model/test.py:189-1831 for
+mode='test_v0', lib/roi_data_layer/minibatch.py:84-1677 for 'train_v0', the README grammar for
+'canonical'): a uint8 or float64 image per input, plus the resolved Plan.  Images whose plans are
+identical run as one sub-batch through each kernel (a mixed batch -- BASELINE config 5 -- is
+grouped by plan), so a homogeneous batch is a single launch per step.
+
+Randomness:
+  rng        Python-level choices (mix noise type, gaussian level, bloom circles): `random`
+             module semantics; default a `random.Random(seed)`
+  noise_rng  'philox'  device Philox4x32 stream keyed by (seed, image id): fast, statistically
+                        equivalent to numpy's draws
+             'numpy'   draw the fields with numpy's global legacy RandomState exactly as
+                        skimage.random_noise does, replay them on the GPU: bit-exact with the
+                        reference for the same numpy state (host RNG cost, like the reference)
+"""
+from __future__ import annotations
+
+import random as _random
+from collections import OrderedDict
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import noise_spec as ns
+from . import ops
+
+
+class Preprocessor:
+    def __init__(self, noise: str, mode: str = "canonical", seed: int = 3,
+                 rng: Optional[_random.Random] = None, noise_rng: str = "philox"):
+        if noise_rng not in ("philox", "numpy"):
+            raise ValueError("noise_rng must be 'philox' or 'numpy'")
+        self.noise = noise
+        self.mode = mode
+        self.seed = int(seed)
+        self.rng = rng if rng is not None else _random.Random(seed)
+        self.noise_rng = noise_rng
+
+    # ---- planning ------------------------------------------------------------------------
+    def plans(self, n: int) -> List[ns.Plan]:
+        return [ns.plan(self.noise, self.mode, self.rng) for _ in range(n)]
+
+    # ---- execution -----------------------------------------------------------------------
+    def __call__(self, batch: torch.Tensor, image_ids: Optional[Sequence[int]] = None,
+                 plans: Optional[Sequence[ns.Plan]] = None):
+        """Returns (outputs, plans): outputs[i] is a device tensor (H,W,3) uint8 or float64."""
+        if batch.dim() == 3:
+            batch = batch.unsqueeze(0)
+        n = batch.shape[0]
+        plans = list(plans) if plans is not None else self.plans(n)
+        ids = list(image_ids) if image_ids is not None else list(range(n))
+        groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
+        for i, p in enumerate(plans):
+            # numpy-stream mode draws image by image, in order, like the reference's loop
+            key = (i,) if self.noise_rng == "numpy" else p.steps
+            groups.setdefault(key, []).append(i)
+        outs: List[Optional[torch.Tensor]] = [None] * n
+        for _, idx in groups.items():
+            steps = plans[idx[0]].steps
+            if len(idx) == n:
+                sub = batch
+            else:
+                sub = batch.index_select(0, torch.as_tensor(idx, device=batch.device))
+            res = self._run_steps(sub, steps, [ids[i] for i in idx])
+            for k, i in enumerate(idx):
+                outs[i] = res[k]
+        return outs, plans
+
+    def run_batch(self, batch: torch.Tensor, image_ids=None, plans=None):
+        """Like __call__ but stacks the outputs when they share dtype and shape."""
+        outs, plans = self(batch, image_ids, plans)
+        if len({(o.dtype, tuple(o.shape)) for o in outs}) == 1:
+            return torch.stack(outs), plans
+        return outs, plans
+
+    def _noise(self, x: torch.Tensor, step: ns.Step, nxt: Optional[ns.Step], ids: List[int]):
+        op = step.op
+        if op == "original":
+            return x
+        if op == "periodic":
+            _, h, w, c = x.shape
+            return ops.periodic_noise(x, ns.periodic_amplitude(step.args[0], h * w * c))
+        if op == "shader":
+            return ops.shader(x, 3.0)
+        if op == "bloom":
+            return ops.bloom(x, rng=self.rng)
+        mode = {"gaussian": "gaussian", "speckle": "speckle", "sap": "s&p", "poisson": "poisson"}[op]
+        kw = {}
+        if op in ("gaussian", "speckle"):
+            kw["var"] = float(step.args[0])
+        elif op == "sap":
+            kw["amount"] = float(step.args[0])
+        out = "u8" if (nxt is not None and nxt.kind == "cast_u8") else "f64"
+        replay = self._numpy_field(x, mode, kw) if self.noise_rng == "numpy" else None
+        offsets = ids
+        if replay is None and offsets != list(range(offsets[0], offsets[0] + len(offsets))):
+            # non-contiguous image ids: one launch per image keeps the (seed, id) stream
+            return torch.cat([ops.random_noise(x[k:k + 1], mode, seed=self.seed, offset=int(i),
+                                               out=out, **kw) for k, i in enumerate(offsets)])
+        return ops.random_noise(x, mode, seed=self.seed, offset=int(offsets[0]), replay=replay,
+                                out=out, **kw)
+
+    def _numpy_field(self, x: torch.Tensor, mode: str, kw) -> torch.Tensor:
+        """The exact draws skimage.random_noise makes from numpy's global RandomState."""
+        host = x.cpu().numpy()
+        fields = []
+        for img in host:
+            if mode in ("gaussian", "speckle"):
+                fields.append(np.random.normal(0.0, kw["var"] ** 0.5, img.shape))
+            elif mode == "s&p":
+                fields.append(np.stack([np.random.random_sample(img.shape),
+                                        np.random.random_sample(img.shape)]))
+            else:
+                xf = img.astype(np.float64) * (1.0 / 255.0)
+                vals = 2 ** np.ceil(np.log2(len(np.unique(xf))))
+                fields.append(np.random.poisson(xf * vals).astype(np.float64))
+        if mode == "s&p":
+            f = np.stack([np.stack([a[0] for a in fields]), np.stack([a[1] for a in fields])])
+        else:
+            f = np.stack(fields)
+        return torch.from_numpy(np.ascontiguousarray(f)).to(x.device)
+
+    def _filter(self, x: torch.Tensor, step: ns.Step) -> torch.Tensor:
+        op, a = step.op, step.args
+        f64 = x.dtype == torch.float64
+        if op == "gaus_blur":
+            return ops.gaussian_blur_f64(x, a[0]) if f64 else ops.gaussian_blur(x, a[0])
+        if op == "mean":
+            return ops.blur_f64(x, a[0]) if f64 else ops.blur(x, a[0])
+        if op == "median":
+            if f64:
+                raise RuntimeError("cv2.error: medianBlur does not support float64 input")
+            return ops.median_blur(x, a[0])
+        if op == "bilateral":
+            if f64:
+                raise RuntimeError("cv2.error: bilateralFilter supports only 8u and 32f images")
+            return ops.bilateral_filter(x, a[0], a[1], a[2])
+        if op == "wavelet":
+            return ops.denoise_wavelet(x, a[0], a[1])
+        raise ValueError(f"unknown filter step {op!r}")
+
+    def _run_steps(self, x: torch.Tensor, steps: Tuple[ns.Step, ...], ids: List[int]):
+        cur = x
+        i = 0
+        while i < len(steps):
+            st = steps[i]
+            nxt = steps[i + 1] if i + 1 < len(steps) else None
+            if st.kind == "noise":
+                cur = self._noise(cur, st, nxt, ids)
+                if nxt is not None and nxt.kind == "cast_u8":
+                    i += 1  # fused into the noise kernel's U8 output
+            elif st.kind == "cast_u8":
+                raise RuntimeError("internal: a U8 cast must follow a noise step")
+            else:
+                cur = self._filter(cur, st)
+            i += 1
+        return list(cur.unbind(0))
+
+
+def blob_from_outputs(outs: Sequence[torch.Tensor], pixel_means=ops.PIXEL_MEANS,
+                      flips: Optional[Sequence[bool]] = None) -> torch.Tensor:
+    """im_list_to_blob(prep_im_for_blob(...)) at scale 1.0 for a list of device images (u8 or f64),
+    zero-padded to the max H, W (lib/utils/blob.py:17-30)."""
+    hmax = max(o.shape[0] for o in outs)
+    wmax = max(o.shape[1] for o in outs)
+    blob = torch.zeros((len(outs), hmax, wmax, 3), dtype=torch.float32, device=outs[0].device)
+    flips = flips or [False] * len(outs)
+    for i, o in enumerate(outs):
+        h, w = o.shape[:2]
+        if o.dtype == torch.uint8:
+            b = ops.blob(o, pixel_means, flip=flips[i])
+        else:
+            b = ops.blob_from_f64(o, pixel_means, flip=flips[i])
+        blob[i, :h, :w] = b[0]
+    return blob

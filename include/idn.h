@@ -127,6 +127,32 @@ int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* ou
                            int levels, void* workspace, size_t ws_bytes, void* stream);
 size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels);
 
+/* ---- float64 filters (the reference's quirk branches blur random_noise's float64 output) -- */
+
+/* cv2.GaussianBlur / cv2.blur on CV_64F images (dense n*h*w*c doubles), BORDER_REFLECT_101.
+ * Reached by train_v0 post hooks after a "plain" noise branch (minibatch.py:1636-1643) and by
+ * test_v0's default branch (test.py:1757-1768).  Within 1e-12 of the double reference. */
+int idn_gaussian_blur_f64(const double* src, double* dst, int n, int h, int w, int c, int ksize,
+                          void* stream);
+int idn_box_blur_f64(const double* src, double* dst, int n, int h, int w, int c, int ksize,
+                     void* stream);
+
+/* ---- shader / bloom noise types ---------------------------------------------------------- */
+
+/* add_shader (test.py:1595-1601): np.array(ImageEnhance.Brightness(PIL image).enhance(factor)).
+ * src is the BGR image; dst is written in PIL's RGB channel order, as the reference returns it. */
+int idn_shader_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                  int64_t row_stride, double factor, void* stream);
+
+/* add_bloom -> Automold add_sun_flare (tools/Automold.py:588-627): per image `ncirc` steps of
+ * {filled LINE_8 circle on the overlay, cv2.addWeighted(overlay, a, out, b, 0)}.
+ * circles: device int32 [n][ncirc][8] = {cx, cy, radius, c0, c1, c2, reset_overlay, 0};
+ * weights: device float [n][ncirc][2] = {a, b}; spans: device int16 half-width table of radius R
+ * at row offset t stored at R*(R+1)/2 + t (idn/automold.py).  <= 1 LSB (float blend order). */
+int idn_bloom_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c, int64_t row_stride,
+                 const int32_t* circles, const float* weights, int ncirc, const int16_t* spans,
+                 void* stream);
+
 /* ---- blob epilogue (lib/utils/blob.py:17-47) -------------------------------------------- */
 
 /* blob[i, y, x, ch] = float32(float64(img[i,y,x,ch]) - mean[ch]) for y<h, x<w; zero elsewhere
@@ -135,6 +161,17 @@ size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels);
 int idn_blob_f32(const uint8_t* src, float* blob, int n, int h, int w, int c,
                  int64_t row_stride, int out_h, int out_w, const double mean[3], int flip,
                  void* stream);
+
+/* blob from a float64 image (dense n*h*w*3): float32(float64(float32(x)) - mean[ch]) -- what
+ * prep_im_for_blob does with the float64 output of the "plain" noise branches. */
+int idn_blob_from_f64(const double* src, float* blob, int n, int h, int w, int out_h, int out_w,
+                      const double mean[3], int flip, void* stream);
+
+/* cv2.resize(im_f32, None, None, fx, fy, INTER_LINEAR) on dense n*h*w*c float32 images
+ * (prep_im_for_blob when the image is not already 600 x 1000: lib/utils/blob.py:44-45,
+ * lib/model/test.py:75-76).  out_h/out_w = round(h*fy), round(w*fx) as cv2 computes them. */
+int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int c, int out_h,
+                          int out_w, double fx, double fy, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,72 @@
+"""CPU: the C-ABI library loads, exports every function include/idn.h declares, and the ctypes
+signature table matches the header (no compute calls: there is no GPU here)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "idn.h"
+
+
+def header_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(idn_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def _lib_path():
+    from idn import _lib
+    p = Path(_lib.LIB_PATH)
+    if not p.exists():
+        pytest.skip("libidn_hip.so not built (run __graft_entry__.build())")
+    return p
+
+
+def test_header_declares_the_path():
+    names = header_functions()
+    for must in ("idn_gaussian_blur_u8", "idn_box_blur_u8", "idn_median_blur_u8",
+                 "idn_bilateral_u8", "idn_noise_u8", "idn_wavelet_denoise_u8", "idn_blob_f32",
+                 "idn_resize_linear_f32", "idn_bloom_u8", "idn_shader_u8"):
+        assert must in names
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(str(_lib_path()))
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, f"declared in idn.h but not exported: {missing}"
+
+
+def test_ctypes_table_covers_header():
+    from idn import _lib
+    assert sorted(_lib.SIGNATURES) == header_functions()
+
+
+def test_version_and_error_without_gpu():
+    """idn_version / idn_last_error are host-only and callable without a device."""
+    lib = ctypes.CDLL(str(_lib_path()))
+    lib.idn_version.restype = ctypes.c_char_p
+    assert lib.idn_version().decode().startswith("idn ")
+    lib.idn_last_error.restype = ctypes.c_char_p
+    assert isinstance(lib.idn_last_error(), (bytes, type(None)))
+
+
+def test_argument_validation_without_gpu():
+    """Bad arguments are rejected on the host before any HIP call (-1 = IDN_EINVAL)."""
+    from idn import _lib
+    lib = _lib.load()
+    rc = lib.idn_gaussian_blur_u8(None, None, 1, 8, 8, 3, 24, 5, None)
+    assert rc == -1
+    assert b"null" in lib.idn_last_error()
+    rc = lib.idn_median_blur_u8(1, 2, 1, 8, 8, 3, 10, 3, None)  # row_stride < w*c
+    assert rc == -1
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    from idn import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", tmp_path / "nope.so")
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.IdnError):
+        _lib.load()

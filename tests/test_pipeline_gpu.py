@@ -1,0 +1,89 @@
+"""GPU parity of the plugin surface end to end: a noise spec string -> per-image plan -> kernels,
+vs the same plan executed by the oracle with the same numpy draws (noise_rng='numpy' replays
+numpy's global RandomState on the GPU), for the three dispatch modes."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import textured
+
+pytestmark = pytest.mark.gpu
+
+SPECS = {
+    "canonical": ["gaussian_var0.1", "gaussian_median_var1.0", "sap_median_var0.4",
+                  "speckle_bilateral_var0.5", "poisson_gaus_blur", "poisson_wavelet",
+                  "periodic_mean_var100", "original_median", "shader", "bloom",
+                  "sap_wavelet_var0.2", "noise_mix_var_low_median", "speckle_mean_var2.0"],
+    "test_v0": ["gaussian_var1.0", "sap_median_var0.4", "speckle_mean_var1.0", "poisson_wavelet",
+                "anything_else", "noise_mix_var_all", "bloom", "gaussian_wavelet_var0.1",
+                "periodic_bilateral_varsize"],
+    "train_v0": ["gaussian_mean_var0.1", "speckle_var2.0", "gaussian_gaus_blur_var1.5",
+                 "sap_var0.8", "periodic_median_var3.14", "noise_mix_var_medium",
+                 "poisson_median", "sap_bilateral_var0.2"],
+}
+
+
+def _plans(spec, mode, n, seed):
+    from idn import noise_spec as ns
+    out, s = [], seed
+    while len(out) < n:
+        try:
+            out.append(ns.plan(spec, mode, random.Random(s)))
+        except NotImplementedError:
+            pass  # a mix draw landed on a §8f "next" noise type; draw again
+        s += 1000
+    return out
+
+
+@pytest.mark.parametrize("mode,spec", [(m, s) for m, ss in SPECS.items() for s in ss])
+def test_plan_parity(dev, mode, spec):
+    import torch
+    from idn.pipeline import Preprocessor
+    from plan_oracle import run_plan
+    imgs = textured(3, 320, 416, seed=len(spec) + len(mode))
+    plans = _plans(spec, mode, 3, seed=5)
+    pre = Preprocessor(spec, mode, rng=random.Random(77), noise_rng="numpy")
+    np.random.seed(123)
+    outs, _ = pre(torch.from_numpy(imgs).cuda(), image_ids=[0, 1, 2], plans=plans)
+    torch.cuda.synchronize()
+    np.random.seed(123)
+    orng = random.Random(77)
+    for i, p in enumerate(plans):
+        ref, wl = run_plan(imgs[i], p.steps, orng)
+        got = outs[i].cpu().numpy()
+        assert got.dtype == ref.dtype == (np.uint8 if p.out_dtype == "u8" else np.float64), p
+        if got.dtype == np.float64:
+            assert np.abs(got - ref).max() <= 1e-12, p
+            continue
+        d = np.abs(got.astype(int) - ref.astype(int))
+        has_bil = any(s.op == "bilateral" for s in p.steps)
+        has_bloom = any(s.op == "bloom" for s in p.steps)
+        if wl:
+            # fp64 wavelet vs numpy: last-bit differences flip U8 casts only at integer boundaries
+            assert d.max() <= 2 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
+        elif has_bil or has_bloom:
+            assert d.max() <= 1 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
+        else:
+            assert d.max() == 0, (p, d.max(), (d > 0).mean())
+
+
+def test_philox_batch_groups_by_plan(dev):
+    """A mixed batch is grouped by plan; results equal running each image alone with its id."""
+    import torch
+    from idn.pipeline import Preprocessor
+    imgs = torch.from_numpy(textured(4, 64, 96, seed=3)).cuda()
+    plans = _plans("noise_mix_var_low_median", "canonical", 4, seed=9)
+    pre = Preprocessor("noise_mix_var_low_median", "canonical", seed=5)
+    outs, _ = pre(imgs, image_ids=[10, 11, 12, 13], plans=plans)
+    for i in range(4):
+        alone, _ = pre(imgs[i:i + 1], image_ids=[10 + i], plans=[plans[i]])
+        assert torch.equal(outs[i], alone[0]), plans[i]
+
+
+def test_reference_failures_reproduced(dev):
+    from idn import noise_spec as ns
+    with pytest.raises(RuntimeError):
+        ns.plan("gaussian_median_var0.1", "train_v0", random.Random(0))
+    with pytest.raises(NameError):
+        ns.plan("bloom", "train_v0", random.Random(0))
