@@ -37,7 +37,20 @@ OPS = {
     "median3": ("3x3 median", lambda idn, x, y: idn.median_blur(x, 3, out=y), 6, "median_u8"),
     "bilateral": ("bilateral d=9 s=75/75",
                   lambda idn, x, y: idn.bilateral_filter(x, 9, 75.0, 75.0, out=y), 6, "bilateral_u8"),
+    # skimage random_noise('gaussian', var=1.0) + U8 cast, Philox stream (BASELINE config 2 noise)
+    "noise_gaussian": ("gaussian_var1.0 noise",
+                       lambda idn, x, y: idn.ops.random_noise(x, "gaussian", var=1.0, seed=3, out="u8",
+                                                              out_u8=y), 6, "noise_gauss"),
+    # 3-level Haar BayesShrink soft threshold (BASELINE config 5 denoiser), fp64 pipeline
+    "wavelet_haar3": ("3-level Haar wavelet",
+                      lambda idn, x, y: idn.ops.denoise_wavelet(x, "db1", 3, out_u8=y), 6, "wl_"),
 }
+# arithmetic type each op computes in (the filters are integer SWAR / fixed point)
+DTYPE = {"noise_gaussian": "f64", "wavelet_haar3": "f64", "bilateral": "f32"}
+PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
+          "wavelet_haar3": "skimage 0.14 denoise_wavelet within 1e-5",
+          "bilateral": "cv2.bilateralFilter within 1 LSB"}
+METRIC = "Mpix/s filtered (5\u00d75 Gaussian, 1000\u00d7600) at 1/2/4/8 GPUs; % HBM roofline"
 
 
 def synth_batch(torch, n, dev, seed=3):
@@ -68,6 +81,9 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "median5": lambda a: oracle.cv.median_blur(a, 5),
         "median3": lambda a: oracle.cv.median_blur(a, 3),
         "bilateral": lambda a: oracle.cv.bilateral_filter(a, 9, 75.0, 75.0),
+        "noise_gaussian": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_gaussian(
+            a, np.random.normal(0.0, 1.0, a.shape))),
+        "wavelet_haar3": lambda a: oracle.sk.to_u8(255 * oracle.wavelet.denoise_wavelet(a[0], "db1", 3)),
     }[op]
     rs = np.random.RandomState(3)
     img = np.clip(128 + rs.uniform(-64, 64, size=(1, H, W, C)), 0, 255).astype(np.uint8)
@@ -79,14 +95,18 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         el = time.perf_counter() - t0
         if el >= budget_s or n_img >= 2000:
             break
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    if op in ("noise_gaussian", "wavelet_haar3"):
+        threads, src = 1, "numpy, single thread"
+    else:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+        src = "oracle/filters.c OpenMP"
     return {
         "value": round(n_img * H * W / el / 1e6, 3),
         "unit": "Mpix/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n_img} x {H}x{W}x3 u8 images, oracle/filters.c ({op}) OpenMP "
-                  f"{threads} threads, {el:.1f} s (cv2 not installed: restatement, not cv2)",
+        "sample": f"{n_img} x {H}x{W}x3 u8 images, oracle ({op}: {src}) "
+                  f"{threads} threads, {el:.1f} s (cv2/skimage not installed: restatement)",
     }
 
 
@@ -166,7 +186,8 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": f"Mpix/s filtered ({label}, 1000x600) at {world} GPU(s); % HBM roofline",
+            "metric": METRIC if args.op == "gauss5" else
+                      f"Mpix/s filtered ({label}, 1000x600) at 1/2/4/8 GPUs; % HBM roofline",
             "value": round(value, 1),
             "unit": "Mpix/s",
             "n_gpus": world,
@@ -176,11 +197,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": DTYPE.get(args.op, "u8"),
             "data": "synthetic (on-device textured pattern, seed 3+rank)",
             "config": {
-                "workload": f"{label} blur, batch {args.batch}x600x1000x3 uint8 per GPU, "
-                            "cv2 semantics bit-exact",
+                "workload": f"{label}, batch {args.batch}x600x1000x3 uint8 per GPU, "
+                            + PARITY.get(args.op, "cv2 semantics bit-exact"),
                 "op": args.op,
                 "batch_per_gpu": args.batch,
                 "image": [H, W, C],

@@ -223,3 +223,57 @@ def test_bilateral_oracle_self_consistent():
         b = oracle.cv.bilateral_filter(img, 9, sc, ss)
         f = oracle.cv.bilateral_prefilter_f32(img, 9, sc, ss)
         assert np.abs(b.astype(np.float64) - f).max() <= 0.5 + 1e-3
+
+
+def test_cvf_float64_filters_vs_scipy():
+    """oracle/cvf.py float64 Gaussian/box (cv2 summation order) vs scipy.ndimage (mirror)."""
+    import numpy as np
+    import scipy.ndimage as nd
+    import oracle
+    x = np.random.RandomState(5).rand(2, 23, 31, 3)
+    for k, w in ((3, np.array([1, 2, 1]) / 4.0), (5, np.array([1, 4, 6, 4, 1]) / 16.0)):
+        ref = nd.correlate1d(nd.correlate1d(x, w, axis=2, mode="mirror"), w, axis=1, mode="mirror")
+        assert np.abs(oracle.cvf.gaussian_blur_f64(x, k) - ref).max() < 1e-15
+    ref = nd.uniform_filter(x, size=(1, 3, 3, 1), mode="mirror")
+    assert np.abs(oracle.cvf.blur_f64(x, 3) - ref).max() < 1e-14
+    one = x[:, :1, :1]
+    assert np.allclose(oracle.cvf.blur_f64(one, 3), one)
+
+
+def test_cvf_resize_vs_torch_bilinear():
+    """INTER_LINEAR restatement vs torch bilinear (align_corners=False, same sampling grid) on
+    upscales, where both clamp identically (OpenCV rounds the source coordinate to float32 before
+    flooring, torch keeps its own float formula: agreement to ~1e-5 relative)."""
+    import numpy as np
+    import torch
+    import oracle
+    rs = np.random.RandomState(6)
+    for s, hw in ((1.6, (40, 55)), (2.0, (37, 53)), (1.25, (40, 56))):
+        x = rs.uniform(-128, 128, size=(*hw, 3)).astype(np.float32)
+        r = oracle.cvf.resize_linear_f32(x, s, s)
+        t = torch.nn.functional.interpolate(torch.from_numpy(x).permute(2, 0, 1)[None],
+                                            scale_factor=s, mode="bilinear", align_corners=False,
+                                            recompute_scale_factor=False)[0].permute(1, 2, 0).numpy()
+        assert r.shape == t.shape
+        assert np.abs(r - t).max() < 4e-3  # |x| <= 128: coefficient rounding differs at ~1e-5 rel
+    assert np.array_equal(oracle.cvf.resize_linear_f32(x, 1.0, 1.0), x)
+
+
+def test_bloom_circle_tables_agree():
+    """Two restatements of cv2.circle(LINE_8, filled): the oracle's span drawing and the span
+    table the GPU kernel consumes (idn.automold.circle_half_widths)."""
+    import numpy as np
+    import oracle
+    from idn import automold
+    for R in (0, 1, 2, 3, 7, 8, 27, 64, 125, 399):
+        n = 2 * R + 3
+        img = np.zeros((n, n, 1), np.uint8)
+        oracle.automold.circle_fill(img, (R + 1, R + 1), R, (1,))
+        half = automold.circle_half_widths(R)
+        for t in range(-R - 1, R + 2):
+            row = img[R + 1 + t, :, 0]
+            hw = half[abs(t)] if abs(t) <= R else -1
+            expect = np.zeros(n, np.uint8)
+            if hw >= 0:
+                expect[R + 1 - hw: R + 2 + hw] = 1
+            assert np.array_equal(row, expect), (R, t)
