@@ -125,8 +125,8 @@ def load_traffic(op: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--op", default="gauss5", choices=sorted(OPS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

@@ -104,13 +104,14 @@ template <int C, int K, int NT>
 __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict__ src,
                                                       uint8_t* __restrict__ dst, int h, int rb,
                                                       uint32_t row_stride, int nseg, int seg_len,
-                                                      int bands, int band_rows, int total_items) {
+                                                      int bands, int band_rows, int total_items,
+                                                      int map) {
   constexpr int R = K / 2;
   constexpr int PF = K;  // prefetch depth == ring depth: one static slot pattern per group
   constexpr int U = K;
 
   const int lane = threadIdx.x & 63;
-  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int item = stripe_item(map, nseg);
   if (item >= total_items) return;
   const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
 
@@ -202,11 +203,12 @@ static int launch_median(const uint8_t* src, uint8_t* dst, int n, int h, int w, 
                          int64_t row_stride, hipStream_t st) {
   const int64_t rb = (int64_t)w * c;
   if (stripe_ok(c, rb, row_stride, h, src, dst)) {
-    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096);
+    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096, env_int("IDN_MEDIAN_MAP", 0),
+                                     env_int("IDN_MEDIAN_ROWS", 32));
     IDN_CHECK_ARG(p.total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
-    hipLaunchKernelGGL((median_u8_fast<3, K, 0>), dim3((unsigned)((p.total + 3) / 4)), dim3(256),
-                       0, st, src, dst, h, (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len,
-                       p.bands, p.band_rows, (int)p.total);
+    hipLaunchKernelGGL((median_u8_fast<3, K, 0>), dim3(p.grid), dim3(p.block), 0, st, src, dst, h,
+                       (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len, p.bands, p.band_rows,
+                       (int)p.total, p.map);
   } else {
     const int64_t npix = (int64_t)n * h * w;
     int64_t blocks = (npix + 255) / 256;

@@ -4,21 +4,26 @@
 // Reference call sites: lib/model/test.py:224,241,1767; lib/roi_data_layer/minibatch.py:119,136,
 // 1636-1643.  OpenCV 3.4.2 semantics restated in oracle/filters.c.
 //
-// Fast path design (one wave = one independent work item, no LDS, no barriers):
-//   * A row of RB = W*C bytes is cut into segments of <= 1008 output bytes.  A wave owns one
-//     segment of one horizontal band of rows of one image and slides down the band.
-//   * Lane l holds the 16-byte chunk [seg_start - 8 + 16 l, +16) of the current row, loaded with
-//     one range-checked buffer_load_dwordx4.  The 2C-byte horizontal halo comes from the two
-//     neighbouring lanes through DPP wave shifts (wave_shr:1 / wave_shl:1), so every byte of HBM
-//     is loaded once per row.  Row/segment edges rebuild the reflected bytes in registers.
-//   * Horizontal taps are formed with v_alignbyte_b32 and summed SWAR: even and odd bytes are
-//     split into two u16 lanes per VGPR (x & 0x00FF00FF, (x >> 8) & 0x00FF00FF), so one 32-bit
-//     add works on two pixels' channels.  Vertical taps come from a K-deep register ring of the
-//     horizontal sums; the Gaussian weights are scaled so the rounded result lands in the high
-//     byte of each u16 lane and one v_perm_b32 packs 4 output bytes.
-//   * Loads are issued PF rows ahead (register queue), stores are whole dwordx4 per lane.
-// Generic path (any C, any alignment): one thread per pixel, same arithmetic, used for shapes
-// the fast path does not accept.
+// Lane layout (shared with the median, stripe.hpp): a row of RB = W*C bytes is cut into
+// segments of <= 1008 output bytes; a wave owns one segment, lane l the 16-byte chunk
+// [seg_start - 8 + 16 l, +16).  The horizontal halo comes from the neighbouring lanes by DPP
+// wave shifts, so each byte is fetched once per row; row/segment edges rebuild the reflected
+// bytes in registers.
+//
+// Arithmetic (vertical first): each input row is split once into even/odd u16 lanes
+// (x & 0x00FF00FF, v_perm), the K vertical taps run on the lane's own 16 bytes from a K-deep
+// register ring (v_mad_u32_u24 for the 6x tap), then the horizontal taps run once per OUTPUT row
+// on the vertical sums, whose 2C-byte halos arrive by DPP (v_pk_mad_u16 for the 6x tap).  The
+// Gaussian weights and the +128 rounding bias are arranged so the cv2 result lands in the high
+// byte of each u16 lane (one v_perm packs 4 bytes); the box mean uses (S*7280 + 33200) >> 16.
+//
+// Memory forms:
+//   stencil_u8_lds  (default, compact rows <= 3024 B)  one 3-wave workgroup per band of NB rows:
+//                   the band's NB + K - 1 input rows are fetched flat into LDS (16 B per lane,
+//                   contiguous lanes, all loads in flight), then each wave walks its segment
+//                   out of LDS.  ~5.7 TB/s on the 600x1000 batch (profiles/).
+//   stencil_u8_vf   (strided rows) the same arithmetic loading each row segment from HBM
+//   stencil_u8_generic  one thread per pixel for shapes the lane layout does not accept
 #include "stripe.hpp"
 
 namespace idn {
@@ -30,87 +35,151 @@ template <> struct Stencil<OP_GAUSS3> { static constexpr int K = 3; };
 template <> struct Stencil<OP_GAUSS5> { static constexpr int K = 5; };
 template <> struct Stencil<OP_BOX3> { static constexpr int K = 3; };
 
-// Horizontal pass: H[2k] / H[2k+1] = even / odd u16 lanes of output dword k (bytes 4k..4k+3).
-template <int C, int OP>
-__device__ __forceinline__ void hpass(const uint32_t (&W)[8], uint32_t (&H)[8]) {
-  Lanes16 V;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    V.SE[j] = even_u16(W[j]);
-    V.SO[j] = __builtin_amdgcn_perm(0u, W[j], 0x0C030C01u);  // (x >> 8) & 0x00FF00FF
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int P = 4 * k + 8 + e;  // window byte of output byte 4k+e
-      uint32_t acc;
-      if constexpr (OP == OP_GAUSS5) {
-        // [1 4 6 4 1]: max 16*255 = 4080 per u16 lane
-        const uint32_t c0 = V.at(P);
-        acc = V.at(P - 2 * C) + V.at(P + 2 * C) + 4u * (V.at(P - C) + V.at(P + C)) +
-              (c0 << 2) + (c0 << 1);
-      } else if constexpr (OP == OP_GAUSS3) {
-        // 4*[1 2 1]: max 4080
-        acc = 4u * (V.at(P - C) + V.at(P + C)) + (V.at(P) << 3);
-      } else {
-        acc = V.at(P - C) + V.at(P) + V.at(P + C);  // max 765
-      }
-      H[2 * k + e] = acc;
+// ---- vertical-first fast path --------------------------------------------------------------
+// Halo rows of a band cost only their unpack (8 ops); the horizontal pass runs per output row.
+// Borders: the lead lane's reflected bytes are rebuilt on the raw row (lead_fix) before the
+// unpack; the tail reflections are rebuilt on the u16 vertical sums (reflection commutes with the
+// separable sums).
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_mad16(uint32_t a, uint32_t k, uint32_t c) {
+  const u16x2 r = __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, k) +
+                  __builtin_bit_cast(u16x2, c);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t k, uint32_t c) {
+  return __umul24(a, k) + c;
+}
+
+// u16 window of vertical sums: SE[m] = window bytes (4m, 4m+2), SO[m] = (4m+1, 4m+3);
+// window byte 0 = chunk byte -8.
+struct VWin {
+  uint32_t SE[8], SO[8];
+  __device__ __forceinline__ uint32_t at(int b) const {  // (b, b+2) as a u16 pair
+    const int m = b >> 2;
+    switch (b & 3) {
+      case 0: return SE[m];
+      case 1: return SO[m];
+      case 2: return __builtin_amdgcn_alignbyte(SE[m + 1], SE[m], 2);
+      default: return __builtin_amdgcn_alignbyte(SO[m + 1], SO[m], 2);
     }
+  }
+  // register and half holding window byte b
+  __device__ __forceinline__ uint32_t reg(int b) const { return (b & 1) ? SO[b >> 2] : SE[b >> 2]; }
+};
+// (a.half[ha], b.half[hb]) -> one u16 pair, one v_perm_b32
+__device__ __forceinline__ uint32_t pick16(uint32_t a, int ha, uint32_t b, int hb) {
+  const uint32_t sel = (uint32_t)(2 * ha) | (uint32_t)(2 * ha + 1) << 8 |
+                       (uint32_t)(4 + 2 * hb) << 16 | (uint32_t)(5 + 2 * hb) << 24;
+  return __builtin_amdgcn_perm(b, a, sel);
+}
+// rebuild window bytes [base, base+8) past the row end (row end = window byte `base`) by
+// BORDER_REFLECT_101 from the bytes before it
+template <int C>
+__device__ __forceinline__ void vwin_tail_fix(VWin& V, int base) {
+  uint32_t nE[2], nO[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      int src[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int k = 4 * m + par + 2 * t;  // window byte base + k
+        src[t] = base - 2 * C - (k / C) * C + (k % C);
+      }
+      const uint32_t r = pick16(V.reg(src[0]), (src[0] >> 1) & 1, V.reg(src[1]), (src[1] >> 1) & 1);
+      (par ? nO : nE)[m] = r;
+    }
+  }
+  const int mb = base >> 2;
+  V.SE[mb] = nE[0];
+  V.SO[mb] = nO[0];
+  V.SE[mb + 1] = nE[1];
+  V.SO[mb + 1] = nO[1];
+}
+
+// one input row -> 8 u16x2 dwords: [0..3] even bytes of chunk dwords 0..3, [4..7] odd bytes
+__device__ __forceinline__ void unpack_row(const v4u& x, uint32_t (&U)[8]) {
+  const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    U[j] = d[j] & 0x00FF00FFu;
+    U[4 + j] = __builtin_amdgcn_perm(0u, d[j], 0x0C030C01u);
   }
 }
 
-// Vertical pass over the ring rows r0..r(K-1) -> 4 output dwords.
+// vertical taps over ring rows r0..r(K-1) (oldest first); raw u16 lanes <= 255
 template <int OP>
-__device__ __forceinline__ v4u vpass(const uint32_t* h0, const uint32_t* h1, const uint32_t* h2,
-                                     const uint32_t* h3, const uint32_t* h4) {
+__device__ __forceinline__ uint32_t vtap(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
+                                         uint32_t r4) {
+  if constexpr (OP == OP_GAUSS5) {
+    // [1 4 6 4 1] + 8 per lane (x16 horizontal weight = the +128 rounding bias): <= 4088
+    const uint32_t t = ((r1 + r3) << 2) + 0x00080008u;
+    return r0 + r4 + mad24(r2, 6u, t);
+  } else if constexpr (OP == OP_GAUSS3) {
+    return r0 + r2 + (r1 << 1);  // [1 2 1]: <= 1020
+  } else {
+    return r0 + r1 + r2;  // <= 765
+  }
+}
+
+// horizontal taps at window byte P of the vertical sums, finished to the output byte:
+// GAUSS: result in the high byte of each u16 lane; BOX: the rounded mean in byte 2 of each of
+// two dwords (lo lane, hi lane)
+template <int C, int OP>
+__device__ __forceinline__ uint32_t htap(const VWin& V, int P) {
+  if constexpr (OP == OP_GAUSS5) {
+    const uint32_t t = (V.at(P - C) + V.at(P + C)) << 2;
+    return V.at(P - 2 * C) + V.at(P + 2 * C) + pk_mad16(V.at(P), 0x00060006u, t);
+  } else if constexpr (OP == OP_GAUSS3) {
+    // 16 * [1 2 1] + 128: (16 S + 128) >> 8 == (S + 8) >> 4
+    const uint32_t x = V.at(P - C) + V.at(P + C) + (V.at(P) << 1);
+    return (x << 4) + 0x00800080u;
+  } else {
+    return V.at(P - C) + V.at(P) + V.at(P + C);  // <= 2295
+  }
+}
+
+template <int OP>
+__device__ __forceinline__ v4u finish(const uint32_t (&A)[8]) {
   uint32_t o[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    uint32_t v[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = 2 * k + e;
-      if constexpr (OP == OP_GAUSS5) {
-        // sum of [1 4 6 4 1]^2 weights = 256; +128 rounds half up; result = high byte of lane
-        const uint32_t a = h0[j] + h4[j] + 0x00800080u;
-        const uint32_t b = h1[j] + h2[j] + h3[j];
-        v[e] = (b << 2) + a + (h2[j] << 1);
-      } else if constexpr (OP == OP_GAUSS3) {
-        // 16 * ([1 2 1]^2 sum) -> (S + 8) >> 4 == (16 S + 128) >> 8
-        v[e] = ((h0[j] + h2[j]) << 2) + (h1[j] << 3) + 0x00800080u;
-      } else {
-        // round(S / 9) == (S*455 + 2075) >> 12 for S in [0, 2295] (exhaustively checked)
-        const uint32_t s = h0[j] + h1[j] + h2[j];
-        const uint32_t lo = ((s & 0xFFFFu) * 455u + 2075u) >> 12;
-        const uint32_t hi = ((s >> 16) * 455u + 2075u) >> 12;
-        v[e] = lo | (hi << 16);
-      }
-    }
     if constexpr (OP == OP_BOX3) {
-      o[k] = v[0] | (v[1] << 8);
+      // round(S/9) == (S*455 + 2075) >> 12 == (S*7280 + 33200) >> 16 (byte 2), S <= 2295
+      const uint32_t e = A[2 * k], od = A[2 * k + 1];
+      const uint32_t el = mad24(e & 0xFFFFu, 7280u, 33200u), eh = mad24(e >> 16, 7280u, 33200u);
+      const uint32_t ol = mad24(od & 0xFFFFu, 7280u, 33200u), oh = mad24(od >> 16, 7280u, 33200u);
+      // bytes: (el.b2, ol.b2, eh.b2, oh.b2)
+      const uint32_t lo = __builtin_amdgcn_perm(ol, el, 0x0C0C0602u);  // el.b2 | ol.b2 << 8
+      const uint32_t hi = __builtin_amdgcn_perm(oh, eh, 0x06020C0Cu);  // eh.b2 << 16 | oh.b2 << 24
+      o[k] = lo | hi;
     } else {
-      o[k] = __builtin_amdgcn_perm(v[1], v[0], 0x07030501u);
+      o[k] = __builtin_amdgcn_perm(A[2 * k + 1], A[2 * k], 0x07030501u);
     }
   }
   v4u r = {o[0], o[1], o[2], o[3]};
   return r;
 }
 
-template <int C, int OP, int PF, int NT>
-__global__ __launch_bounds__(256) void stencil_u8_fast(const uint8_t* __restrict__ src,
-                                                       uint8_t* __restrict__ dst, int h, int rb,
-                                                       uint32_t row_stride, int nseg, int seg_len,
-                                                       int bands, int band_rows, int total_items) {
+// NB > 0: burst form.  The band is exactly NB rows (the launcher sizes it so), all NB + 2R input
+// rows are loaded up front (PF = NB + 2R) and the body is straight-line code.  NB == 0: long
+// bands, a PF-deep load queue and a U-row unrolled loop (U a multiple of K and PF).
+template <int C, int OP, int PF, int NT, int NB>
+__global__ __launch_bounds__(256) void stencil_u8_vf(const uint8_t* __restrict__ src,
+                                                     uint8_t* __restrict__ dst, int h, int rb,
+                                                     uint32_t row_stride, int nseg, int seg_len,
+                                                     int bands, int band_rows, int total_items,
+                                                     int map) {
   constexpr int K = Stencil<OP>::K;
   constexpr int R = K / 2;
-  constexpr int U = (K == 5) ? 5 : 6;  // unroll = lcm(K, PF)
-  static_assert(U % K == 0 && U % PF == 0, "unroll must cover ring and queue");
+  constexpr int U = NB ? NB : (K == 5) ? 5 : 6;
+  static_assert(NB ? PF == NB + 2 * R : (U % K == 0 && U % PF == 0), "queue / unroll shape");
   static_assert(R * C <= 8, "one-side halo must fit in two neighbour dwords");
 
   const int lane = threadIdx.x & 63;
-  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int item = stripe_item(map, nseg);
   if (item >= total_items) return;
   const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
 
@@ -122,45 +191,227 @@ __global__ __launch_bounds__(256) void stencil_u8_fast(const uint8_t* __restrict
   const int y0 = g.band * band_rows;
   const int y1 = min(y0 + band_rows, h);
   if (y0 >= y1) return;
-  const int nin = (y1 - y0) + 2 * R;  // input rows of the band incl. halo
-
-  // Rows are processed in groups of U (static ring / queue slots).  The group count is rounded
-  // up and out-of-band rows are clamped to the band's last input row, so every group runs the
-  // same straight-line code (no phi copies of the ring); only the store is predicated.
-  const int ngroups = (nin + U - 1) / U;
+  const int nin = (y1 - y0) + 2 * R;
   auto load_row = [&](int r) -> v4u {
-    const int y = reflect101(y0 - R + min(r, nin - 1), h);
+    const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
     return __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)y * row_stride + ld_off, 0,
                                                   (NT & 1) ? 2 : 0);
   };
+  const StoreOffs so = store_offs(g);
 
   v4u Lq[PF];
 #pragma unroll
   for (int i = 0; i < PF; ++i) Lq[i] = load_row(i);
 
-  uint32_t Hr[K][8];
+  uint32_t Rg[K][8];  // ring of unpacked input rows; row r lives in slot r % K
 
-  for (int gi = 0; gi < ngroups; ++gi) {
+  // input row r: take it from the queue, refill the queue, rebuild the lead lane, unpack
+  auto take_row = [&](int r, int slot_q, int slot_k, bool refill) {
+    v4u Lv = Lq[slot_q];
+    if (refill) Lq[slot_q] = load_row(r + PF);
+    if (g.lead) {  // chunk = row bytes -8..7: rebuild the reflected 8 bytes
+      const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
+      Lv = v4u{lead_fix<C, BORDER_REFLECT101>(L, -8), lead_fix<C, BORDER_REFLECT101>(L, -4),
+               L[0], L[1]};
+    }
+    unpack_row(Lv, Rg[slot_k]);
+  };
+  // output row from the ring whose newest row sits in slot `nw`
+  auto out_row = [&](int nw, uint32_t row_off) {
+    uint32_t Vs[8];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = gi * U + u;
-      const v4u Lv = Lq[u % PF];
-      Lq[u % PF] = load_row(r + PF);
-      uint32_t W[8];
-      build_window<C, BORDER_REFLECT101>(Lv, g.lead, g.fix_t0, g.fix_t8, W);
-      hpass<C, OP>(W, Hr[u % K]);
-      const int y = y0 + r - 2 * R;
-      if (r >= 2 * R && y < y1) {
-        v4u o;
-        if constexpr (K == 5) {
-          o = vpass<OP>(Hr[(u + 1) % K], Hr[(u + 2) % K], Hr[(u + 3) % K], Hr[(u + 4) % K],
-                        Hr[u % K]);
-        } else {
-          o = vpass<OP>(Hr[(u + 1) % K], Hr[(u + 2) % K], Hr[u % K], nullptr, nullptr);
-        }
-        stripe_store<NT>(o, rd, (uint32_t)y * row_stride + (uint32_t)g.q, g.kind);
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (K == 5) {
+        Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[(nw + 3) % K][j],
+                         Rg[(nw + 4) % K][j], Rg[nw][j]);
+      } else {
+        Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[nw][j], 0u, 0u);
       }
     }
+    VWin V;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      V.SE[2 + j] = Vs[j];
+      V.SO[2 + j] = Vs[4 + j];
+    }
+    if constexpr (R * C > 4) {  // halos: R*C bytes each side
+      V.SE[0] = from_prev_lane(Vs[2]);
+      V.SO[0] = from_prev_lane(Vs[6]);
+      V.SE[7] = from_next_lane(Vs[1]);
+      V.SO[7] = from_next_lane(Vs[5]);
+    } else {
+      V.SE[0] = V.SO[0] = V.SE[7] = V.SO[7] = 0u;
+    }
+    V.SE[1] = from_prev_lane(Vs[3]);
+    V.SO[1] = from_prev_lane(Vs[7]);
+    V.SE[6] = from_next_lane(Vs[0]);
+    V.SO[6] = from_next_lane(Vs[4]);
+    if (g.fix_t0) vwin_tail_fix<C>(V, 24);
+    if (g.fix_t8) vwin_tail_fix<C>(V, 16);
+    uint32_t A[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      A[2 * k] = htap<C, OP>(V, 4 * k + 8);
+      A[2 * k + 1] = htap<C, OP>(V, 4 * k + 9);
+    }
+    stripe_store_nb<NT>(finish<OP>(A), rd, so, row_off);
+  };
+
+  // prologue: the 2R rows above the band only fill the ring
+#pragma unroll
+  for (int r = 0; r < 2 * R; ++r) take_row(r, r % PF, r % K, !NB);
+
+  if constexpr (NB) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int r = 2 * R + u;
+      take_row(r, r % PF, r % K, false);
+      const int y = y0 + u;
+      out_row(r % K, y < y1 ? (uint32_t)y * row_stride : OOB_OFF);
+    }
+  } else {
+    const int nout = y1 - y0;
+    const int ngroups = (nout + U - 1) / U;
+    for (int gi = 0; gi < ngroups; ++gi) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = 2 * R + gi * U + u;  // slots (2R + u) % K / % PF are static
+        take_row(r, (2 * R + u) % PF, (2 * R + u) % K, true);
+        const int y = y0 + gi * U + u;
+        out_row((2 * R + u) % K, y < y1 ? (uint32_t)y * row_stride : OOB_OFF);
+      }
+    }
+  }
+}
+
+// ---- LDS-tiled form --------------------------------------------------------------------------
+// One workgroup = one band of NB output rows of one image, nseg waves (<= 3: rows <= 3024 bytes).
+// The band's NB + 2R input rows are contiguous in HBM (row_stride == row bytes), so the whole
+// tile is fetched flat -- 16 B per lane, consecutive lanes on consecutive addresses, all loads in
+// flight at once -- and staged in LDS; the waves then walk their row segments out of LDS with
+// the vertical-first arithmetic above and store their output rows directly.  Measured on this
+// chip the flat tile fetch sustains ~5.8 TB/s copy-equivalent where per-segment row loads stop
+// near 5.2 (tools/membench3.hip).
+constexpr int TILE_WGT = 192;     // 3 waves
+constexpr int TILE_RBMAX = 3024;  // 3 segments of 1008 bytes
+template <int NB, int K>
+struct TileShape {
+  static constexpr int ROWS = NB + K - 1;
+  static constexpr int BYTES = ROWS * TILE_RBMAX + 16;           // + alignment shift
+  static constexpr int NL = (BYTES + 16 * TILE_WGT - 1) / (16 * TILE_WGT);
+  static constexpr int LDS = NL * 16 * TILE_WGT;
+};
+
+template <int C, int OP, int NB, int NT>
+__global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __restrict__ src,
+                                                          uint8_t* __restrict__ dst, int h, int rb,
+                                                          int nseg, int seg_len, int bands,
+                                                          int total_items, int map) {
+  constexpr int K = Stencil<OP>::K;
+  constexpr int R = K / 2;
+  using TS = TileShape<NB, K>;
+  __shared__ __attribute__((aligned(16))) uint8_t tile[TS::LDS];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int blk = map == 1 ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // waves beyond nseg (rows narrower than 3 segments) only help fetch the tile
+  const int item = blk * nseg + min(wave, nseg - 1);
+  const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
+  const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
+  const rsrc_t rs = make_rsrc(src + (size_t)g.img * img_bytes, img_bytes);
+  const rsrc_t rd = make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes);
+
+  const int y0 = g.band * NB;
+  const int y1 = min(y0 + NB, h);
+  const int ys = max(y0 - R, 0), ye = min(y1 + R, h);
+  const uint32_t base = (uint32_t)ys * (uint32_t)rb;
+  const uint32_t base_al = base & ~15u, shift = base - base_al;
+  const uint32_t nbytes = (uint32_t)ye * (uint32_t)rb - base_al;
+
+  // flat fetch of the tile into LDS (out-of-image lanes read 0 and are not written)
+  {
+    v4u v[TS::NL];
+#pragma unroll
+    for (int i = 0; i < TS::NL; ++i) {
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < nbytes ? base_al + o : OOB_OFF, 0,
+                                                    (NT & 1) ? 2 : 0);
+    }
+#pragma unroll
+    for (int i = 0; i < TS::NL; ++i) {
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
+      if (o < nbytes) *reinterpret_cast<v4u*>(&tile[o]) = v[i];
+    }
+  }
+  __syncthreads();
+  if (wave >= nseg || item >= total_items || y0 >= y1) return;
+
+  const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
+  const int nin = (y1 - y0) + 2 * R;
+  auto lds_row = [&](int r) -> v4u {
+    const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
+    const uint32_t o = (uint32_t)(y - ys) * (uint32_t)rb + shift + ld_off;
+    const v2u a = *reinterpret_cast<const v2u*>(&tile[o]);
+    const v2u b = *reinterpret_cast<const v2u*>(&tile[o + 8]);
+    return v4u{a.x, a.y, b.x, b.y};
+  };
+  const StoreOffs so = store_offs(g);
+  uint32_t Rg[K][8];
+  auto take_row = [&](int r) {
+    v4u Lv = lds_row(r);
+    if (g.lead) {
+      const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
+      Lv = v4u{lead_fix<C, BORDER_REFLECT101>(L, -8), lead_fix<C, BORDER_REFLECT101>(L, -4),
+               L[0], L[1]};
+    }
+    unpack_row(Lv, Rg[r % K]);
+  };
+#pragma unroll
+  for (int r = 0; r < 2 * R; ++r) take_row(r);
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int r = 2 * R + u;
+    take_row(r);
+    const int nw = r % K;
+    uint32_t Vs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (K == 5) {
+        Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[(nw + 3) % K][j],
+                         Rg[(nw + 4) % K][j], Rg[nw][j]);
+      } else {
+        Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[nw][j], 0u, 0u);
+      }
+    }
+    VWin V;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      V.SE[2 + j] = Vs[j];
+      V.SO[2 + j] = Vs[4 + j];
+    }
+    if constexpr (R * C > 4) {
+      V.SE[0] = from_prev_lane(Vs[2]);
+      V.SO[0] = from_prev_lane(Vs[6]);
+      V.SE[7] = from_next_lane(Vs[1]);
+      V.SO[7] = from_next_lane(Vs[5]);
+    } else {
+      V.SE[0] = V.SO[0] = V.SE[7] = V.SO[7] = 0u;
+    }
+    V.SE[1] = from_prev_lane(Vs[3]);
+    V.SO[1] = from_prev_lane(Vs[7]);
+    V.SE[6] = from_next_lane(Vs[0]);
+    V.SO[6] = from_next_lane(Vs[4]);
+    if (g.fix_t0) vwin_tail_fix<C>(V, 24);
+    if (g.fix_t8) vwin_tail_fix<C>(V, 16);
+    uint32_t A[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      A[2 * k] = htap<C, OP>(V, 4 * k + 8);
+      A[2 * k + 1] = htap<C, OP>(V, 4 * k + 9);
+    }
+    const int y = y0 + u;
+    stripe_store_nb<NT>(finish<OP>(A), rd, so, y < y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
   }
 }
 
@@ -280,29 +531,68 @@ static int launch_f64(const double* src, double* dst, int n, int h, int w, int c
 }
 
 // ---- host launchers --------------------------------------------------------------------------
+// Band heights measured best on MI355X (256 x 600 x 1000 x 3 batch, tools/sweep_stencil.py):
+// the tiled kernel with 6-row bands (10 / 8 input rows in LDS, 30 / 24 KB per workgroup, up to
+// 5-6 workgroups per CU).  IDN_STENCIL_TILE=0 forces the stripe form, 2 / 3 pick other heights.
 template <int OP>
 static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
                           int64_t row_stride, hipStream_t st, const char* name) {
+  constexpr int K = Stencil<OP>::K;
+  constexpr int R = K / 2;
   const int64_t rb = (int64_t)w * c;
-  if (stripe_ok(c, rb, row_stride, h, src, dst)) {
-    constexpr int K = Stencil<OP>::K;
-    constexpr int U = (K == 5) ? 5 : 6;
-    constexpr int PF = (K == 5) ? 5 : 6;
-    // one resident round: 5 waves/SIMD x 1024 SIMDs at <= 96 VGPRs
-    const StripePlan p = plan_stripe(n, h, rb, K, U, 5120);
-    IDN_CHECK_ARG(p.total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
-    const dim3 grid((unsigned)((p.total + 3) / 4)), block(256);
-    const int nt = env_int("IDN_STENCIL_NT", 0) & 3;
-#define IDN_LAUNCH_FAST(NTV)                                                                     \
-  hipLaunchKernelGGL((stencil_u8_fast<3, OP, PF, NTV>), grid, block, 0, st, src, dst, h, (int)rb, \
-                     (uint32_t)row_stride, p.nseg, p.seg_len, p.bands, p.band_rows, (int)p.total)
-    switch (nt) {
-      case 1: IDN_LAUNCH_FAST(1); break;
-      case 2: IDN_LAUNCH_FAST(2); break;
-      case 3: IDN_LAUNCH_FAST(3); break;
-      default: IDN_LAUNCH_FAST(0); break;
+  const int tile_mode = env_int("IDN_STENCIL_TILE", 1);
+  const bool ntst = (env_int("IDN_STENCIL_NT", 0) & 2) != 0;  // nontemporal stores (tuning)
+  const int map = env_int("IDN_STENCIL_MAP", 1) == 2 ? 2 : 1;
+  if (tile_mode && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
+      rb <= TILE_RBMAX && h > 2 * R) {
+    const int nseg = (int)((rb + 1007) / 1008);
+    const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
+    constexpr int NB1 = 6, NB2 = K == 5 ? 11 : 10, NB3 = K == 5 ? 8 : 4;
+    const int nb = tile_mode == 2 ? NB2 : tile_mode == 3 ? NB3 : NB1;
+    const int bands = (h + nb - 1) / nb;
+    const int64_t total = (int64_t)n * bands * nseg;
+    IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
+    const dim3 grid((unsigned)((int64_t)n * bands)), block(TILE_WGT);
+#define IDN_LAUNCH_TILE(NBX)                                                                      \
+  if (ntst)                                                                                       \
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, 2>), grid, block, 0, st, src, dst, h, (int)rb, \
+                       nseg, seg_len, bands, (int)total, map);                                    \
+  else                                                                                            \
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, 0>), grid, block, 0, st, src, dst, h, (int)rb, \
+                       nseg, seg_len, bands, (int)total, map)
+    if (tile_mode == 2) {
+      IDN_LAUNCH_TILE(NB2);
+    } else if (tile_mode == 3) {
+      IDN_LAUNCH_TILE(NB3);
+    } else {
+      IDN_LAUNCH_TILE(NB1);
     }
-#undef IDN_LAUNCH_FAST
+#undef IDN_LAUNCH_TILE
+  } else if (stripe_ok(c, rb, row_stride, h, src, dst)) {
+    // strided or wide rows: stripe form.  Rows of <= 4 segments: short bands, one workgroup per
+    // band, all band rows loaded up front; wider rows: long bands of independent waves.
+    constexpr int PF = (K == 5) ? 5 : 6;
+    constexpr int NBS = 6;
+    const bool burst = (rb + 1007) / 1008 <= 4;
+    const StripePlan p = plan_stripe(n, h, rb, K, burst ? 1 : PF, 5120, burst ? map : 0, NBS,
+                                     burst ? NBS : 0);
+    IDN_CHECK_ARG(p.total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
+    const dim3 grid(p.grid), block(p.block);
+#define IDN_LAUNCH_VF(NTV)                                                                        \
+  if (burst)                                                                                      \
+    hipLaunchKernelGGL((stencil_u8_vf<3, OP, NBS + K - 1, NTV, NBS>), grid, block, 0, st, src,    \
+                       dst, h, (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len, p.bands,         \
+                       p.band_rows, (int)p.total, p.map);                                         \
+  else                                                                                            \
+    hipLaunchKernelGGL((stencil_u8_vf<3, OP, PF, NTV, 0>), grid, block, 0, st, src, dst, h,       \
+                       (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len, p.bands, p.band_rows,    \
+                       (int)p.total, p.map)
+    if (ntst) {
+      IDN_LAUNCH_VF(2);
+    } else {
+      IDN_LAUNCH_VF(0);
+    }
+#undef IDN_LAUNCH_VF
   } else {
     const int64_t npix = (int64_t)n * h * w;
     int64_t blocks = (npix + 255) / 256;

@@ -10,13 +10,15 @@ namespace idn {
 
 enum Border { BORDER_REFLECT101 = 0, BORDER_REPLICATE = 1 };
 
-// lane i <- lane i-1 (wave_shr:1), lane 0 gets 0
+// lane i <- lane i-1 (wave_shr:1); lane 0 reads 0 (bound_ctrl).  Lane 0 and lane 63 never consume
+// the halo they would receive (lane 0 outputs only chunk bytes 8..15, lane 63 only 0..7, and
+// R*C <= 8), so no zero-fill (and no extra v_mov) is needed.
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
 }
-// lane i <- lane i+1 (wave_shl:1), lane 63 gets 0
+// lane i <- lane i+1 (wave_shl:1); lane 63 reads 0
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
 }
 
 // byte P (0..31) of the 8-dword window W (window byte 0 = chunk byte -8)
@@ -151,6 +153,23 @@ __device__ __forceinline__ StripeGeom stripe_geom(int item, int lane, int rb, in
   return g;
 }
 
+// Workgroup -> work-item mapping of a stripe launch.
+//   map 0: 4 independent waves per workgroup, item = 4*block + wave (long bands, one round)
+//   map 1: one workgroup = the nseg segments of one short band (whole rows, contiguous in HBM),
+//          blocks renumbered so each XCD walks a contiguous run of bands: vertical neighbours
+//          run on the same XCD at about the same time and their halo rows hit its L2
+//   map 2: as 1 without the XCD renumbering
+__device__ __forceinline__ int xcd_contiguous_block(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+__device__ __forceinline__ int stripe_item(int map, int nseg) {
+  const int wave = threadIdx.x >> 6;
+  if (map == 0) return __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave);
+  const int b = map == 1 ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  return __builtin_amdgcn_readfirstlane(b * nseg + wave);
+}
+
 template <int NT>
 __device__ __forceinline__ void stripe_store(const v4u& o, rsrc_t rd, uint32_t off, int kind) {
   constexpr int aux = (NT & 2) ? 2 : 0;
@@ -165,10 +184,45 @@ __device__ __forceinline__ void stripe_store(const v4u& o, rsrc_t rd, uint32_t o
   }
 }
 
+// Branch-free form of stripe_store: out-of-range buffer offsets drop a store in hardware, so the
+// lane's kind and the row's validity select offsets instead of exec-masked branches.  Lanes of
+// kind 1 issue one 16-byte store; the (at most two) edge lanes of kind 2/3 issue an 8-byte store.
+// >= any image (stripe_ok bounds images below 2^30); the sum of two offsets never wraps
+constexpr uint32_t OOB_OFF = 0x40000000u;
+struct StoreOffs {
+  uint32_t full, half;  // per-lane byte offsets relative to the row start (OOB when unused)
+  bool hi;              // the half store carries bytes 8..15 of the chunk
+};
+__device__ __forceinline__ StoreOffs store_offs(const StripeGeom& g) {
+  StoreOffs s;
+  s.full = g.kind == 1 ? (uint32_t)g.q : OOB_OFF;
+  s.hi = g.kind == 3;
+  s.half = g.kind == 2 ? (uint32_t)g.q : (g.kind == 3 ? (uint32_t)g.q + 8u : OOB_OFF);
+  return s;
+}
+template <int NT>
+__device__ __forceinline__ void stripe_store_nb(const v4u& o, rsrc_t rd, const StoreOffs& so,
+                                                uint32_t row_off) {
+  constexpr int aux = (NT & 2) ? 2 : 0;
+  // row_off == OOB_OFF for a row that must not be written: every offset lands out of range
+  __builtin_amdgcn_raw_buffer_store_b128(o, rd, so.full + row_off, 0, aux);
+  v2u h2 = so.hi ? v2u{o.z, o.w} : v2u{o.x, o.y};
+  __builtin_amdgcn_raw_buffer_store_b64(h2, rd, so.half + row_off, 0, aux);
+}
+
+// BORDER_REFLECT_101 row index for -len < i < 2*len - 1 (one reflection; callers guarantee
+// len > kernel radius), without the loop of reflect101()
+__device__ __forceinline__ int reflect101_1(int i, int len) {
+  i = i < 0 ? -i : i;
+  return i >= len ? 2 * len - 2 - i : i;
+}
+
 // Host-side stripe geometry: segments of <= 1008 bytes, bands sized to one resident round.
 struct StripePlan {
   int nseg, seg_len, bands, band_rows;
   int64_t total;
+  int map;       // see stripe_item()
+  unsigned grid, block;
 };
 
 inline int env_int(const char* name, int dflt) {
@@ -176,11 +230,20 @@ inline int env_int(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-inline StripePlan plan_stripe(int n, int h, int64_t rb, int K, int U, int64_t cap) {
+// map_default: the workgroup mapping used when IDN_STRIPE_MAP is unset; short_rows: band height
+// target of the row-workgroup maps (rounded up so band + halo fills whole unroll groups).
+inline StripePlan plan_stripe(int n, int h, int64_t rb, int K, int U, int64_t cap,
+                              int map_default = 0, int short_rows = 32, int fixed_rows = 0) {
   StripePlan p;
   p.nseg = (int)((rb + 1007) / 1008);
   p.seg_len = (int)(((rb + p.nseg - 1) / p.nseg + 7) / 8 * 8);
-  int band_rows = env_int("IDN_BAND_ROWS", 0);
+  p.map = env_int("IDN_STRIPE_MAP", map_default);
+  if (p.nseg > 4) p.map = 0;  // rows wider than 4 segments: independent waves
+  int band_rows = fixed_rows > 0 ? fixed_rows : env_int("IDN_BAND_ROWS", 0);
+  if (band_rows <= 0 && p.map != 0) {
+    band_rows = short_rows < h ? short_rows : h;
+    while ((band_rows + (K - 1)) % U != 0 && band_rows < h) ++band_rows;
+  }
   if (band_rows <= 0) {
     int64_t bands = cap / ((int64_t)n * p.nseg);
     if (bands < 1) bands = 1;
@@ -191,13 +254,20 @@ inline StripePlan plan_stripe(int n, int h, int64_t rb, int K, int U, int64_t ca
   p.band_rows = band_rows;
   p.bands = (h + band_rows - 1) / band_rows;
   p.total = (int64_t)n * p.bands * p.nseg;
+  if (p.map == 0) {
+    p.block = 256;
+    p.grid = (unsigned)((p.total + 3) / 4);
+  } else {
+    p.block = 64u * (unsigned)p.nseg;
+    p.grid = (unsigned)((int64_t)n * p.bands);
+  }
   return p;
 }
 
 inline bool stripe_ok(int c, int64_t rb, int64_t row_stride, int h, const void* src,
                       const void* dst) {
-  return c == 3 && rb % 8 == 0 && row_stride % 8 == 0 && rb >= 32 &&
-         (int64_t)h * row_stride < (int64_t)0x7FFFFFFF && ((uintptr_t)src & 7) == 0 &&
+  return c == 3 && rb % 8 == 0 && row_stride % 8 == 0 && rb >= 32 && h >= 5 &&
+         (int64_t)h * row_stride < (int64_t)0x40000000 && ((uintptr_t)src & 7) == 0 &&
          ((uintptr_t)dst & 7) == 0 && env_int("IDN_FORCE_GENERIC", 0) == 0;
 }
 

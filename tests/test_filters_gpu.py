@@ -79,13 +79,51 @@ def test_generic_path_forced(dev, monkeypatch):
     assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
 
 
-@pytest.mark.parametrize("band_rows", ["7", "32", "600"])
-def test_band_split_invariance(dev, monkeypatch, band_rows):
+FORMS = [
+    {"IDN_STENCIL_TILE": "1"},                 # LDS tile, 6-row bands (default)
+    {"IDN_STENCIL_TILE": "2"},                 # LDS tile, 11 / 10-row bands
+    {"IDN_STENCIL_TILE": "3"},                 # LDS tile, 8 / 4-row bands
+    {"IDN_STENCIL_TILE": "1", "IDN_STENCIL_MAP": "2", "IDN_STENCIL_NT": "2"},
+    {"IDN_STENCIL_TILE": "0"},                 # stripe form, short bands from HBM
+]
+
+
+@pytest.mark.parametrize("form", FORMS, ids=lambda f: "-".join(f"{k[12:]}{v}" for k, v in f.items()))
+@pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (2, 13, 104), (1, 601, 1000)])
+def test_stencil_forms_agree(dev, monkeypatch, form, shape):
+    """every memory form of the stencil gives cv2's bytes (band tails, 1-3 segments, odd heights)"""
     import idn
     import oracle
-    monkeypatch.setenv("IDN_BAND_ROWS", band_rows)
-    img = textured(2, 100, 1000, seed=int(band_rows))
-    assert np.array_equal(_run(idn.gaussian_blur, img, 5), oracle.cv.gaussian_blur(img, 5))
+    for k, v in form.items():
+        monkeypatch.setenv(k, v)
+    img = textured(*shape, seed=sum(shape))
+    for k in (3, 5):
+        assert np.array_equal(_run(idn.gaussian_blur, img, k), oracle.cv.gaussian_blur(img, k)), k
+    assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+
+
+@pytest.mark.parametrize("w,pad", [(1000, 8), (344, 16), (1400, 0)])
+def test_stencil_row_stride_and_wide_rows(dev, w, pad):
+    """row_stride > W*C (strided rows take the stripe form) and rows wider than the LDS tile"""
+    import torch
+    import idn
+    import oracle
+    from idn import _lib
+    lib = _lib.load()
+    img = textured(2, 41, w, seed=w + pad)
+    wp = w + pad // 3 if pad else w
+    rs = wp * 3 + (pad % 3) if pad else w * 3
+    rs = (rs + 7) // 8 * 8
+    buf = torch.zeros((2, 41, rs), dtype=torch.uint8, device="cuda")
+    buf[:, :, : w * 3] = torch.from_numpy(img.reshape(2, 41, w * 3)).cuda()
+    out = torch.full_like(buf, 77)
+    for k in (3, 5):
+        rc = lib.idn_gaussian_blur_u8(buf.data_ptr(), out.data_ptr(), 2, 41, w, 3, rs, k, None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        got = out[:, :, : w * 3].cpu().numpy().reshape(2, 41, w, 3)
+        assert np.array_equal(got, oracle.cv.gaussian_blur(img, k)), k
+        assert bool((out[:, :, w * 3:] == 77).all())  # padding untouched
 
 
 def test_rejects_cpu_tensor():

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Tuning sweep for the stencil kernels (run on the GPU box): interleaved rounds of each
-(op, IDN_BAND_ROWS, IDN_STENCIL_NT) variant in ONE process, median kernel time via HIP events.
+"""Tuning sweep for the stripe kernels (run on the GPU box): every combination of the given
+environment knobs, interleaved rounds in ONE process, median kernel time via HIP events.  Each
+variant's output is compared with the first variant's (the knobs must not change results).
 
-  python tools/sweep_stencil.py [--batch 256] [--rounds 5] [--ops gauss5,box3]
+  python tools/sweep_stencil.py --ops gauss5,box3 --env IDN_STENCIL_MAP=0,1,2 --env IDN_BAND_ROWS=0,16,36
 """
 import argparse
 import itertools
@@ -22,8 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ops", default="gauss5")
-    ap.add_argument("--bands", default="0,60,100,150,300")
-    ap.add_argument("--nt", default="0,1,2,3")
+    ap.add_argument("--env", action="append", default=[], help="NAME=v1,v2,...")
     args = ap.parse_args()
     import torch
     import idn
@@ -39,15 +39,25 @@ def main():
         "median5": lambda: idn.median_blur(x, 5, out=y),
         "bilateral": lambda: idn.bilateral_filter(x, 9, 75.0, 75.0, out=y),
     }
-    variants = list(itertools.product(args.ops.split(","), args.bands.split(","), args.nt.split(",")))
+    knobs = [(e.split("=")[0], e.split("=")[1].split(",")) for e in args.env]
+    names = [k for k, _ in knobs]
+    combos = list(itertools.product(*[v for _, v in knobs])) or [()]
+    variants = [(op, c) for op in args.ops.split(",") for c in combos]
     res = {v: [] for v in variants}
-    for _ in range(args.rounds):
+    ref = {}
+    bad = set()
+    for rnd in range(args.rounds):
         for v in variants:
-            op, br, nt = v
-            os.environ["IDN_BAND_ROWS"] = br
-            os.environ["IDN_STENCIL_NT"] = nt
+            op, c = v
+            for k, val in zip(names, c):
+                os.environ[k] = val
             fns[op]()
             torch.cuda.synchronize()
+            if rnd == 0:
+                if op not in ref:
+                    ref[op] = y.clone()
+                elif not torch.equal(ref[op], y):
+                    bad.add(v)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(args.iters)]
             for a, b in evs:
@@ -56,16 +66,20 @@ def main():
                 b.record()
             torch.cuda.synchronize()
             res[v].extend(a.elapsed_time(b) for a, b in evs)
+        print(f"round {rnd} done", file=sys.stderr, flush=True)
     nbytes = 6 * args.batch * 600 * 1000
     out = []
     for v, ts in res.items():
         ts.sort()
         med = ts[len(ts) // 2]
-        out.append({"op": v[0], "band_rows": v[1], "nt": v[2], "ms_median": round(med, 4),
-                    "ms_min": round(ts[0], 4), "GBps_median": round(nbytes / med / 1e6, 1)})
+        rec = {"op": v[0], **dict(zip(names, v[1])), "ms_median": round(med, 4),
+               "ms_min": round(ts[0], 4), "GBps_median": round(nbytes / med / 1e6, 1)}
+        if v in bad:
+            rec["MISMATCH"] = True
+        out.append(rec)
     out.sort(key=lambda r: (r["op"], r["ms_median"]))
     for r in out:
-        print(json.dumps(r))
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
