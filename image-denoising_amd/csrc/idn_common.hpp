@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdarg.h>
+#include <stdlib.h>
 
 #include "../../include/idn.h"
 
@@ -45,6 +46,12 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(q, 0, nb, 0x00020000);
 }
 
+// tuning knobs read at launch time (host)
+inline int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
 // ---- small integer helpers ------------------------------------------------------------------
 // OpenCV BORDER_REFLECT_101 index (cv::borderInterpolate; repeats for overshoot >= len)
 __host__ __device__ __forceinline__ int reflect101(int i, int len) {
@@ -64,14 +71,10 @@ struct u32x4 { uint32_t x, y, z, w; };
 
 __host__ __device__ __forceinline__ void philox_round(u32x4& c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-  uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-#else
-  uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
-  uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
-  uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-#endif
+  // one 32x32->64 product per word (v_mad_u64_u32 on the device instead of mul_hi + mul_lo)
+  const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+  const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+  const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
   c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
 }
 

@@ -21,7 +21,8 @@ namespace idn {
 
 __device__ __forceinline__ double img_as_float(uint32_t v) { return __dmul_rn((double)v, 1.0 / 255.0); }
 
-__device__ __forceinline__ double clip01(double v) { return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v); }
+// np.clip(v, 0, 1) for non-NaN v (v_max_f64 / v_min_f64)
+__device__ __forceinline__ double clip01(double v) { return __builtin_fmin(__builtin_fmax(v, 0.0), 1.0); }
 
 // (255 * out).astype(np.uint8) for out in [0, 1]: truncation (out is never negative here)
 __device__ __forceinline__ uint8_t u8_of(double out) { return (uint8_t)(int)__dmul_rn(out, 255.0); }
@@ -97,6 +98,71 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
       store_out(a, img, e, boff, out);
     }
   }
+}
+
+// ---- flat form (compact rows, Philox stream): 16 consecutive elements per thread -------------
+// One 16-byte load / store per lane, image = blockIdx.y, no 64-bit index division.  Stream:
+//   gaussian / speckle  counter (e/4, 0, image id) -> 4 u32 -> two Box-Muller pairs -> the 4
+//                       normals of elements 4q..4q+3
+//   s&p                 counter (e/2, 1, image id) -> (U1, U2) of elements 2q and 2q+1 as 32-bit
+//                       uniforms compared against integer thresholds (|P - p| < 2^-32)
+// The apply is the same float64 expression as the element kernels above.
+__device__ __forceinline__ void normal4(const u32x4& r, float (&z)[4]) {
+  normal2(r, z[0], z[1]);
+  const u32x4 r2{r.z, r.w, 0u, 0u};
+  normal2(r2, z[2], z[3]);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t t_flip,
+                                                           uint32_t t_salt) {
+  const int img = blockIdx.y;
+  const uint32_t chunk = blockIdx.x * 256u + threadIdx.x;
+  const int64_t e0 = (int64_t)chunk * 16;
+  if (e0 >= a.elems) return;
+  const uint64_t gimg = a.offset + (uint64_t)img;
+  const uint8_t* src = a.src + (int64_t)img * a.elems + e0;
+  const v4u raw = *reinterpret_cast<const v4u*>(src);
+  const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
+  uint32_t o[4] = {0u, 0u, 0u, 0u};
+  double* of = a.out_f64 ? a.out_f64 + (int64_t)img * a.elems + e0 : nullptr;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // elements 4k .. 4k+3
+    double outv[4];
+    if constexpr (KIND == IDN_NOISE_SAP) {
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        const uint32_t q = chunk * 8u + (uint32_t)(2 * k + hlf);
+        const u32x4 r = philox4x32(u32x4{q, 1u, (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
+        const uint32_t u1[2] = {r.x, r.z}, u2[2] = {r.y, r.w};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int b = 2 * hlf + j;
+          const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
+          outv[b] = u1[j] < t_flip ? (u2[j] < t_salt ? 1.0 : 0.0) : xv;
+        }
+      }
+    } else {
+      const uint32_t q = chunk * 4u + (uint32_t)k;
+      const u32x4 r = philox4x32(u32x4{q, 0u, (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
+      float z[4];
+      normal4(r, z);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const double nz = __dadd_rn(a.p0, __dmul_rn(a.p1, (double)z[b]));
+        const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
+        if (KIND == IDN_NOISE_GAUSSIAN) outv[b] = clip01(__dadd_rn(xv, nz));
+        else outv[b] = clip01(__dadd_rn(xv, __dmul_rn(xv, nz)));
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      o[k] |= (uint32_t)u8_of(outv[b]) << (8 * b);
+      if (of) of[4 * k + b] = outv[b];
+    }
+  }
+  if (a.out_u8)
+    *reinterpret_cast<v4u*>(a.out_u8 + (int64_t)img * a.elems + e0) = v4u{o[0], o[1], o[2], o[3]};
 }
 
 // salt & pepper: flipped = U1 < cdf0(amount), salted = U2 < cdf0(salt_vs_pepper)
@@ -304,6 +370,11 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
   a.elems = (int64_t)h * w * c;
   a.key = seed ^ (KIND_TAG * (uint64_t)(kind + 1));
   a.offset = offset;
+  // flat form: Philox stream, compact rows, 16-element chunks that never straddle images
+  const bool flat = !replay && row_stride == (int64_t)w * c && a.elems % 16 == 0 &&
+                    ((uintptr_t)src & 15) == 0 && ((uintptr_t)out_u8 & 15) == 0 &&
+                    ((uintptr_t)out_f64 & 7) == 0 && a.elems / 16 < ((int64_t)1 << 31) &&
+                    env_int("IDN_NOISE_FLAT", 1) != 0;
   switch (kind) {
     case IDN_NOISE_GAUSSIAN:
     case IDN_NOISE_SPECKLE: {
@@ -311,7 +382,13 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
       a.p0 = p0;             // mean
       a.p1 = pow(p1, 0.5);   // var ** 0.5 (random_noise)
       const int64_t work = (a.elems + 1) / 2 * n;
-      if (kind == IDN_NOISE_GAUSSIAN)
+      if (flat) {
+        const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
+        if (kind == IDN_NOISE_GAUSSIAN)
+          hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_GAUSSIAN>, grid, dim3(256), 0, st, a, 0u, 0u);
+        else
+          hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SPECKLE>, grid, dim3(256), 0, st, a, 0u, 0u);
+      } else if (kind == IDN_NOISE_GAUSSIAN)
         hipLaunchKernelGGL(noise_gauss_kernel<IDN_NOISE_GAUSSIAN>, dim3(grid_for(work)), dim3(256), 0, st, a);
       else
         hipLaunchKernelGGL(noise_gauss_kernel<IDN_NOISE_SPECKLE>, dim3(grid_for(work)), dim3(256), 0, st, a);
@@ -323,7 +400,18 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
       // np.random.choice([True, False], p=[p, 1-p]): True iff random_sample < cdf[0]
       a.p0 = p0 / (p0 + (1.0 - p0));
       a.p1 = p1 / (p1 + (1.0 - p1));
-      hipLaunchKernelGGL(noise_sap_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      if (flat) {
+        // 32-bit uniform thresholds: P(u < t / 2^32) within 2^-32 of cdf0
+        auto thr = [](double pp) -> uint32_t {
+          const double t = ceil(pp * 4294967296.0);
+          return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+        };
+        const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
+        hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SAP>, grid, dim3(256), 0, st, a,
+                           thr(a.p0), thr(a.p1));
+      } else {
+        hipLaunchKernelGGL(noise_sap_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      }
       break;
     }
     default: {  // POISSON

@@ -225,10 +225,6 @@ struct StripePlan {
   unsigned grid, block;
 };
 
-inline int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
 
 // map_default: the workgroup mapping used when IDN_STRIPE_MAP is unset; short_rows: band height
 // target of the row-workgroup maps (rounded up so band + halo fills whole unroll groups).

@@ -224,3 +224,32 @@ def test_blob_bitexact(dev, flip):
     refp[0, 500:] = 0
     refp[0, :, 700:] = 0
     assert np.array_equal(padded, refp)
+
+
+@pytest.mark.parametrize("flat", ["0", "1"])
+@pytest.mark.parametrize("mode,kw", [("gaussian", {"var": 0.1}), ("speckle", {"var": 1.0}),
+                                     ("s&p", {"amount": 0.4})])
+def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
+    """flat (16 elements / lane) and element kernels: U8 == trunc(255 * f64 out), same output
+    law (first two moments of out - x), deterministic, batch-split invariant"""
+    import oracle
+    import torch
+    import idn
+    monkeypatch.setenv("IDN_NOISE_FLAT", flat)
+    imgs = np.stack([make_img(120, 200, s) for s in range(3)])
+    x = torch.from_numpy(imgs).cuda()
+    u8, f64 = idn.ops.random_noise(x, mode, seed=4, offset=7, out="both", **kw)
+    u8, f64 = u8.cpu().numpy(), f64.cpu().numpy()
+    assert np.array_equal(u8, oracle.sk.to_u8(255 * f64))
+    one8 = idn.ops.random_noise(x[1:2], mode, seed=4, offset=8, **kw).cpu().numpy()
+    assert np.array_equal(one8[0], u8[1])
+    xf = imgs.astype(np.float64) * (1.0 / 255.0)
+    d = (f64 - xf).reshape(-1)
+    ref = {}
+    for f in ("0", "1"):
+        monkeypatch.setenv("IDN_NOISE_FLAT", f)
+        _, g = idn.ops.random_noise(x, mode, seed=99, out="both", **kw)
+        ref[f] = (g.cpu().numpy() - xf).reshape(-1)
+    assert abs(ref["0"].mean() - ref["1"].mean()) < 4e-3
+    assert abs(ref["0"].std() - ref["1"].std()) < 4e-3
+    assert abs(d.mean() - ref["1"].mean()) < 4e-3
