@@ -46,10 +46,81 @@ OPS = {
                       lambda idn, x, y: idn.ops.denoise_wavelet(x, "db1", 3, out_u8=y), 6, "wl_"),
 }
 # arithmetic type each op computes in (the filters are integer SWAR / fixed point)
-DTYPE = {"noise_gaussian": "f64", "wavelet_haar3": "f64", "bilateral": "f32"}
+DTYPE = {"noise_gaussian": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
+         "cfg3": "f64", "cfg4": "f64", "cfg5": "f64"}
 PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
           "wavelet_haar3": "skimage 0.14 denoise_wavelet within 1e-5",
-          "bilateral": "cv2.bilateralFilter within 1 LSB"}
+          "bilateral": "cv2.bilateralFilter within 1 LSB",
+          "cfg2": "Philox noise + cv2.blur bit-exact", "cfg3": "Philox s&p + cv2.medianBlur bit-exact",
+          "cfg4": "Philox speckle + cv2.bilateralFilter within 1 LSB",
+          "cfg5": "Philox/periodic noise + denoise_wavelet within 1e-5"}
+
+def _pipeline(kind):
+    """BASELINE.json configs 2-5 as one step = noise + denoise over the batch (intermediate u8
+    buffers are allocated once, outside the timed region)."""
+    state = {}
+
+    def step(idn, x, y):
+        t = state.get("t")
+        if t is None or t.shape != x.shape:
+            t = state["t"] = x.new_empty(x.shape)
+        ops = idn.ops
+        if kind == "cfg2":    # gaussian_var1.0 + mean 3x3
+            ops.random_noise(x, "gaussian", var=1.0, seed=3, out="u8", out_u8=t)
+            idn.blur(t, 3, out=y)
+        elif kind == "cfg3":  # sap_var0.4 + median 5x5
+            ops.random_noise(x, "s&p", amount=0.4, seed=3, out="u8", out_u8=t)
+            idn.median_blur(t, 5, out=y)
+        elif kind == "cfg4":  # speckle_var1.0 + bilateral d=9 sigma 75/75
+            ops.random_noise(x, "speckle", var=1.0, seed=3, out="u8", out_u8=t)
+            idn.bilateral_filter(t, 9, 75.0, 75.0, out=y)
+        else:                 # cfg5: mixed noise (one type per image, seeded) + Haar L=3 wavelet
+            groups = state.get("groups")
+            if groups is None:
+                import random
+                rng = random.Random(3)
+                kinds = [rng.choice(["gaussian", "s&p", "speckle", "poisson", "periodic",
+                                     "original"]) for _ in range(x.shape[0])]
+                groups = {}
+                for i, k in enumerate(kinds):
+                    groups.setdefault(k, []).append(i)
+                state["groups"] = groups = {k: (v[0], len(v)) for k, v in
+                                            _contiguous(groups).items()}
+            for k, (lo, cnt) in groups.items():
+                xs, ts = x[lo:lo + cnt], t[lo:lo + cnt]
+                if k == "original":
+                    ts.copy_(xs)
+                elif k == "periodic":
+                    ops.periodic_noise(xs, 100.0, out=ts)
+                elif k == "s&p":
+                    ops.random_noise(xs, "s&p", amount=0.4, seed=3, offset=lo, out="u8", out_u8=ts)
+                elif k == "poisson":
+                    ops.random_noise(xs, "poisson", seed=3, offset=lo, out="u8", out_u8=ts)
+                else:
+                    ops.random_noise(xs, k, var=1.0, seed=3, offset=lo, out="u8", out_u8=ts)
+            ops.denoise_wavelet(t, "db1", 3, out_u8=y)
+    return step
+
+
+def _contiguous(groups):
+    """mixed batch: images of one noise type are made contiguous (the bench's synthetic batch
+    is laid out by type, as a type-grouped loader would do)"""
+    out, lo = {}, 0
+    for k in sorted(groups):
+        out[k] = [lo + i for i in range(len(groups[k]))]
+        lo += len(groups[k])
+    return out
+
+
+PIPELINES = {
+    "cfg2": ("gaussian_var1.0 + 3x3 mean (config 2)", 256),
+    "cfg3": ("sap_var0.4 + 5x5 median (config 3)", 1024),
+    "cfg4": ("speckle_var1.0 + bilateral d=9 s=75/75 (config 4)", 512),
+    "cfg5": ("mixed noise + 3-level Haar wavelet (config 5)", 512),
+}
+for _k, (_lbl, _b) in PIPELINES.items():
+    OPS[_k] = (_lbl, _pipeline(_k), 6, "pipeline")
+
 METRIC = "Mpix/s filtered (5\u00d75 Gaussian, 1000\u00d7600) at 1/2/4/8 GPUs; % HBM roofline"
 
 
@@ -84,6 +155,14 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "noise_gaussian": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_gaussian(
             a, np.random.normal(0.0, 1.0, a.shape))),
         "wavelet_haar3": lambda a: oracle.sk.to_u8(255 * oracle.wavelet.denoise_wavelet(a[0], "db1", 3)),
+        "cfg2": lambda a: oracle.cv.blur(oracle.sk.to_u8(255 * oracle.sk.noise_gaussian(
+            a, np.random.normal(0.0, 1.0, a.shape))), 3),
+        "cfg3": lambda a: oracle.cv.median_blur(oracle.sk.to_u8(255 * oracle.sk.noise_sap(
+            a, np.random.random_sample(a.shape), np.random.random_sample(a.shape), 0.4)), 5),
+        "cfg4": lambda a: oracle.cv.bilateral_filter(oracle.sk.to_u8(255 * oracle.sk.noise_speckle(
+            a, np.random.normal(0.0, 1.0, a.shape))), 9, 75.0, 75.0),
+        "cfg5": lambda a: oracle.sk.to_u8(255 * oracle.wavelet.denoise_wavelet(oracle.sk.to_u8(
+            255 * oracle.sk.noise_gaussian(a[0], np.random.normal(0.0, 1.0, a[0].shape))), "db1", 3)),
     }[op]
     rs = np.random.RandomState(3)
     img = np.clip(128 + rs.uniform(-64, 64, size=(1, H, W, C)), 0, 255).astype(np.uint8)
@@ -95,8 +174,11 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         el = time.perf_counter() - t0
         if el >= budget_s or n_img >= 2000:
             break
-    if op in ("noise_gaussian", "wavelet_haar3"):
+    if op in ("noise_gaussian", "wavelet_haar3", "cfg5"):
         threads, src = 1, "numpy, single thread"
+    elif op in ("cfg2", "cfg3", "cfg4"):
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+        src = "numpy noise (1 thread) + oracle/filters.c OpenMP"
     else:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
         src = "oracle/filters.c OpenMP"
@@ -127,7 +209,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU (default: 256, or the "
+                    "config's per-GPU batch for cfg2..cfg5)")
     ap.add_argument("--op", default="gauss5", choices=sorted(OPS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     args = ap.parse_args()
@@ -145,6 +228,8 @@ def main():
     dev = torch.device("cuda", local)
 
     label, call, bpp, kname = OPS[args.op]
+    if args.batch <= 0:
+        args.batch = PIPELINES[args.op][1] if args.op in PIPELINES else 256
     x = synth_batch(torch, args.batch, dev, seed=3 + rank)
     y = torch.empty_like(x)
     torch.cuda.synchronize()
