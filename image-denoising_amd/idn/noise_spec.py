@@ -35,7 +35,13 @@ LEVELS = {
     "sap": (("var0.2", 0.2), ("var0.4", 0.4), ("var0.8", 0.8)),
     "speckle": (("var0.5", 0.5), ("var1.0", 1.0), ("var2.0", 2.0)),
     "periodic": (("var3.14", "pi"), ("var100", 100.0), ("varsize", "size")),
+    # the reference's own additive noises (test.py:767-1572, minibatch.py:669-1490)
+    "uniform": (("var0.2", 0.2), ("var0.6", 0.6), ("var1.2", 1.2)),        # high
+    "brownian": (("var0.9", 0.9), ("var0.09", 0.09), ("var0.009", 0.009)),  # dt
+    "gamma": (("var0.05", 0.05), ("var0.1", 0.1), ("var0.2", 0.2)),         # scale
+    "rayleigh": (("var0.1", 0.1), ("var0.2", 0.2), ("var0.3", 0.3)),        # scale
 }
+ADDITIVE = ("uniform", "gamma", "rayleigh")  # float64 x + noise, unclipped (cv2.add on floats)
 
 # reference in-branch denoiser parameters (test.py:220,241,259,272-274 / minibatch.py likewise)
 BILATERAL_REF = (9, 20.0, 100.0)  # diameter, sigmaColor, sigmaSpace, BORDER_CONSTANT
@@ -158,6 +164,19 @@ def _noise_branch(noise: str, noise_type: str, mode: str):
             val = 0.6  # minibatch.py:367: the plain var0.8 branch draws amount=0.6
         noise_step = Step("noise", "sap" if noise == "sap" else noise, (val,))
     steps = [noise_step]
+    if noise == "brownian":
+        # cv2.add(img, U8(255 * B)) is already u8 (test.py:1095-1124); denoisers run on it
+        if den is not None:
+            steps.append(_filter_step(den))
+        return steps, "u8"
+    if noise in ADDITIVE:
+        if den == "wavelet":  # denoise_wavelet on the unclipped float64 sum
+            return steps + [_filter_step("wavelet")], "u8"
+        if den is not None:
+            return steps + [Step("cast_u8", "u8"), _filter_step(den)], "u8"
+        if mode == "train_v0":  # minibatch.py:787,1324,1464: `im = uniform_noise` (float64)
+            return steps, "f64"
+        return steps + [Step("cast_u8", "u8")], "u8"
     if noise == "periodic":
         # cv2.add(img, pattern) is already u8; denoisers then run on it
         if den is not None:
@@ -191,12 +210,12 @@ def _closure(noise_type: str, mode: str, top_level: bool):
     for noise in ("gaussian", "poisson", "sap", "speckle", "periodic", "brownian", "quant",
                   "uniform", "gamma", "rayleigh"):
         if noise in noise_type:
-            if noise in ("brownian", "quant", "uniform", "gamma", "rayleigh"):
-                if mode == "test_v0" and noise == "quant" and top_level:
+            if noise == "quant":
+                if mode == "test_v0" and top_level:
                     return [Step("noise", "original")], "u8"
                 raise NotImplementedError(
-                    f"noise type {noise!r} is not implemented on the GPU path yet "
-                    "(SURVEY §8f: next rows)")
+                    "noise type 'quant' (MiniBatchKMeans colour quantisation) is not implemented "
+                    "on the GPU path (SURVEY §8f row 4)")
             if mode == "test_v0" and top_level and noise == "sap":
                 return [Step("noise", "original")], "u8"  # test.py:1691-1697
             return _noise_branch(noise, noise_type, mode)
@@ -295,7 +314,8 @@ def _plan_canonical(noise: str, rng) -> Plan:
         if key is None:
             raise ValueError(f"mix spec {noise!r} needs var_low / var_medium / var_high / var_all")
         pool = [t for t in MIX_TEST[key] if t.split("_")[0] in
-                ("gaussian", "poisson", "speckle", "sap", "periodic", "original")]
+                ("gaussian", "poisson", "speckle", "sap", "periodic", "original") + ADDITIVE +
+                ("brownian",)]
         base = rng.choice(pool)
         noise_type = base if den is None else _insert_denoiser(base, den)
         return _plan_canonical(noise_type, rng)._replace_spec(noise)
@@ -304,7 +324,7 @@ def _plan_canonical(noise: str, rng) -> Plan:
     if s.startswith("original_") and den is not None:
         return Plan(noise, s, (Step("noise", "original"), _filter_step(den)), "u8")
     head = s.split("_")[0]
-    if head not in ("gaussian", "sap", "speckle", "poisson", "periodic"):
+    if head not in ("gaussian", "sap", "speckle", "poisson", "periodic") + ADDITIVE + ("brownian",):
         raise ValueError(f"unknown or unsupported noise spec {noise!r}")
     steps, out = _noise_branch(head, s, "canonical")
     return Plan(noise, s, tuple(steps), out)

@@ -158,6 +158,55 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
     return _finish(y8, sq), _finish(y64, sq)
 
 
+ADD_NOISE_KINDS = {"uniform": 4, "gamma": 5, "rayleigh": 6, "brownian": 7}
+GAMMA_SHAPE = 1.99  # a = 1.99 in every gamma closure (lib/model/test.py:1303)
+
+
+def noise_add(x: torch.Tensor, mode: str, level: float, *, seed: int = 0, offset: int = 0,
+              replay: Optional[torch.Tensor] = None, out: str = "u8",
+              out_u8: Optional[torch.Tensor] = None, shape: float = GAMMA_SHAPE):
+    """The reference's own additive noises (lib/model/test.py:767-1572), u8 batch in:
+      uniform  level = high:  out = img_as_float(x) + np.random.uniform(0, high)
+      gamma    level = scale: out = x + scipy.stats.gamma.rvs(1.99, scale=level)
+      rayleigh level = scale: out = x + scipy.stats.rayleigh.rvs(scale=level)
+      brownian level = dt:    u8 = cv2.add(img, U8(255 * cumsum-walk)), f64 = the walk B
+    cv2.add(float64, float64) does not clip: out="f64" is the unclipped sum (what train_v0's plain
+    branches return), out="u8" is (255 * out).astype(np.uint8) with its modulo-256 wrap.
+    replay: numpy's unit draws (random_sample / standard_gamma(1.99) / sqrt(chisquare(2)) /
+    for brownian the normals with element e holding z[e-1]), float64 of x's shape."""
+    kind = ADD_NOISE_KINDS.get(mode.lower())
+    if kind is None:
+        raise ValueError(f"noise_add: unsupported mode {mode!r}; supported: {sorted(ADD_NOISE_KINDS)}")
+    xb, sq = _u8_batch(x, "noise_add")
+    n, h, w, c = xb.shape
+    want_u8 = out in ("u8", "both")
+    want_f64 = out in ("f64", "both")
+    if not (want_u8 or want_f64):
+        raise ValueError("noise_add: out must be 'u8', 'f64' or 'both'")
+    y8 = (out_u8.view(n, h, w, c) if out_u8 is not None else _empty_like_img(xb, torch.uint8)) if want_u8 else None
+    y64 = _empty_like_img(xb, torch.float64) if want_f64 else None
+    p0, p1 = (float(shape), float(level)) if kind == 5 else (float(level), 0.0)
+    rp = None
+    if replay is not None:
+        if replay.device != xb.device or replay.dtype != torch.float64 or replay.numel() != xb.numel():
+            raise ValueError("noise_add: replay must be float64, on the same device, one value per element")
+        rp = replay.contiguous()
+    lib = _lib.load()
+    ws_bytes = lib.idn_noise_add_workspace_size(kind, n, h, w, c)
+    ws = _workspace(ws_bytes, xb.device) if ws_bytes else None
+    rc = lib.idn_noise_add_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
+                              y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c, kind,
+                              p0, p1, int(seed) & (2 ** 64 - 1), int(offset),
+                              rp.data_ptr() if rp is not None else None,
+                              ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+    _lib.check(rc, "idn_noise_add_u8")
+    if out == "u8":
+        return _finish(y8, sq)
+    if out == "f64":
+        return _finish(y64, sq)
+    return _finish(y8, sq), _finish(y64, sq)
+
+
 _PATTERN_CACHE: dict = {}
 
 

@@ -88,6 +88,16 @@ class Preprocessor:
             return ops.shader(x, 3.0)
         if op == "bloom":
             return ops.bloom(x, rng=self.rng)
+        if op in ops.ADD_NOISE_KINDS:
+            out = "u8" if (op == "brownian" or (nxt is not None and nxt.kind == "cast_u8")) else "f64"
+            level = float(step.args[0])
+            if self.noise_rng == "numpy":
+                return ops.noise_add(x, op, level, replay=self._numpy_add_field(x, op), out=out)
+            if ids != list(range(ids[0], ids[0] + len(ids))):
+                return torch.cat([ops.noise_add(x[k:k + 1], op, level, seed=self.seed,
+                                                offset=int(i), out=out)
+                                  for k, i in enumerate(ids)])
+            return ops.noise_add(x, op, level, seed=self.seed, offset=int(ids[0]), out=out)
         mode = {"gaussian": "gaussian", "speckle": "speckle", "sap": "s&p", "poisson": "poisson"}[op]
         kw = {}
         if op in ("gaussian", "speckle"):
@@ -123,6 +133,27 @@ class Preprocessor:
         else:
             f = np.stack(fields)
         return torch.from_numpy(np.ascontiguousarray(f)).to(x.device)
+
+    def _numpy_add_field(self, x: torch.Tensor, op: str) -> torch.Tensor:
+        """numpy's unit draws for the additive closures, image by image, in the reference's
+        order: np.random.uniform -> random_sample; scipy gamma.rvs -> standard_gamma(1.99);
+        scipy rayleigh.rvs -> sqrt(chisquare(2)); brownian -> normal(size=n-1) at elements 1.."""
+        shape = tuple(x.shape[1:])
+        fields = []
+        for _ in range(x.shape[0]):
+            if op == "uniform":
+                f = np.random.random_sample(shape)
+            elif op == "gamma":
+                f = np.random.standard_gamma(ops.GAMMA_SHAPE, shape)
+            elif op == "rayleigh":
+                f = np.sqrt(np.random.chisquare(2, shape))
+            else:
+                size = int(np.prod(shape))
+                f = np.zeros(size)
+                f[1:] = np.random.normal(size=size - 1)
+                f = f.reshape(shape)
+            fields.append(f)
+        return torch.from_numpy(np.ascontiguousarray(np.stack(fields))).to(x.device)
 
     def _filter(self, x: torch.Tensor, step: ns.Step) -> torch.Tensor:
         op, a = step.op, step.args

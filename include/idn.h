@@ -102,6 +102,29 @@ int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, in
                  void* stream);
 size_t idn_noise_workspace_size(int kind, int n);
 
+/* The reference's own additive noises (not skimage), SURVEY §8f:
+ *   IDN_NOISE_UNIFORM   p0 = high   out = img_as_float(x) + U(0, high)         (test.py:767-903)
+ *   IDN_NOISE_GAMMA     p0 = shape, p1 = scale: out = x + gamma.rvs(shape, scale) (1300-1437)
+ *   IDN_NOISE_RAYLEIGH  p0 = scale  out = x + rayleigh.rvs(scale)               (1439-1572)
+ *   IDN_NOISE_BROWNIAN  p0 = dt     out_u8 = sat(img + U8(255 * B)),
+ *                       B = concat([0], cumsum(sqrt(dt) * N(0,1)[h*w*c - 1]))  (905-1126)
+ * cv2.add(float64, float64) is a plain add, so out is unclipped; out_u8 = U8(255*out) wraps
+ * modulo 256 ((uint8)(int32)trunc, |y| >= 2^31 -> 0); out_f64 = out (brownian: the walk B).
+ * replay (float64, N*h*w*c, optional): numpy's unit draws -- random_sample, standard_gamma(shape),
+ * sqrt(chisquare(2)), or for brownian the normals with element e holding z[e-1] (element 0
+ * unused).  Brownian needs idn_noise_add_workspace_size() bytes of workspace. */
+typedef enum idn_noise_add_kind {
+  IDN_NOISE_UNIFORM = 4,
+  IDN_NOISE_GAMMA = 5,
+  IDN_NOISE_RAYLEIGH = 6,
+  IDN_NOISE_BROWNIAN = 7
+} idn_noise_add_kind;
+int idn_noise_add_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
+                     int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
+                     uint64_t offset, const double* replay, void* workspace, size_t ws_bytes,
+                     void* stream);
+size_t idn_noise_add_workspace_size(int kind, int n, int h, int w, int c);
+
 /* Periodic noise pattern of add_periodic_noise (lib/model/test.py:1128-1298):
  * pattern[i] = U8(255*sin(t_i)), t = np.linspace(-A, A, h*w*c), written as u8 HxWxC (pitch w*c).
  * Image independent: build once per (h, w, c, A) and reuse. */

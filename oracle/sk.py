@@ -99,3 +99,32 @@ def blob_f32(imgs, pixel_means=PIXEL_MEANS, flip=False):
     for i, im in enumerate(ims):
         blob[i, 0:im.shape[0], 0:im.shape[1], :] = im
     return blob
+
+
+# ---- the reference's own additive closures (lib/model/test.py:767-1572) --------------------------
+def noise_uniform(img, u, high):
+    """img_as_float(img) + np.random.uniform(0, high) given its random_sample draws u (cv2.add on
+    float64: plain add)."""
+    return img_as_float(img) + (0.0 + high * np.asarray(u, np.float64))
+
+
+def noise_gamma(img, g, scale):
+    """x + scipy gamma.rvs(1.99, loc=0, scale) given standard_gamma(1.99) draws g."""
+    return img_as_float(img) + (np.asarray(g, np.float64) * scale + 0.0)
+
+
+def noise_rayleigh(img, r, scale):
+    """x + scipy rayleigh.rvs(loc=0, scale) given sqrt(chisquare(2)) draws r."""
+    return img_as_float(img) + (np.asarray(r, np.float64) * scale + 0.0)
+
+
+def brownian_walk(z, dt):
+    """B = concat([0], cumsum(sqrt(dt) * z)) for the n-1 normals z (np.cumsum: sequential)."""
+    dB = np.sqrt(dt) * np.asarray(z, np.float64)
+    return np.concatenate((np.zeros(1), np.cumsum(dB)))
+
+
+def noise_brownian(img, z, dt):
+    """cv2.add(img, (B * 255).astype(np.uint8).reshape(img.shape)) (u8 + u8 saturating)."""
+    pat = to_u8(brownian_walk(z, dt) * 255).reshape(img.shape)
+    return add_saturate(img, pat)

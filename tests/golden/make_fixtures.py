@@ -17,6 +17,7 @@ the reference calls, at the reference's call signatures:
                   multichannel=True, convert2ycbcr=True)            lib/model/test.py:197
   denoise_wavelet(..., wavelet_levels=3) (default db1)  minibatch_before_curvelet.py:85-87
   linspace/sin periodic pattern                      lib/model/test.py:1284-1286
+  uniform / gamma / rayleigh / brownian closures     lib/model/test.py:767-1572 (scipy.stats 1.7.1)
   blob: astype(f32) -= PIXEL_MEANS                   lib/utils/blob.py:35-36
 
 Random fields are NOT stored: every case records the numpy legacy seed, and the tests re-draw the
@@ -121,6 +122,40 @@ def main():
         cases.append({"key": None, "input": "big600x1000", "mode": mode, "kw": kw, "seed": seed,
                       "sha_u8": sha(u8(out)), "sha_f64": sha(out)})
     manifest["noise"] = cases
+
+    # ---------------- the reference's own additive closures (scipy.stats + numpy) ----------------
+    # test.py:767-903 (uniform), 1300-1437 (gamma, a = 1.99), 1439-1572 (rayleigh),
+    # 905-1126 (brownian): the closure arithmetic restated line by line with the same calls.
+    from scipy.stats import gamma as sp_gamma, rayleigh as sp_rayleigh
+    add = []
+    for iname, img in imgs.items():
+        image = img_as_float(img)
+        for mode, level in (("uniform", 0.2), ("uniform", 1.2), ("gamma", 0.05), ("gamma", 0.2),
+                            ("rayleigh", 0.1), ("rayleigh", 0.3), ("brownian", 0.9),
+                            ("brownian", 0.009)):
+            seed = 3000 + len(add)
+            np.random.seed(seed)
+            if mode == "uniform":
+                arr = image + np.random.uniform(low=0., high=level, size=img.shape)  # cv2.add
+                o8 = (255 * arr).astype(np.uint8)
+            elif mode == "gamma":
+                arr = image + sp_gamma.rvs(1.99, loc=0., scale=level, size=image.shape)
+                o8 = (arr * 255).astype(np.uint8)
+            elif mode == "rayleigh":
+                arr = image + sp_rayleigh.rvs(loc=0., scale=level, size=image.shape)
+                o8 = (arr * 255).astype(np.uint8)
+            else:
+                h, w = img.shape[:2]
+                n = img.size
+                dB = np.sqrt(level) * np.random.normal(size=(n - 1,))
+                arr = np.concatenate((np.zeros(shape=(1,)), np.cumsum(dB)))
+                brownian = (arr * 255).astype(np.uint8).reshape(h, w, 3)
+                o8 = np.minimum(img.astype(np.int32) + brownian, 255).astype(np.uint8)  # cv2.add
+            key = f"add{len(add)}"
+            arrays[key + "_u8"] = o8
+            add.append({"key": key, "input": iname, "mode": mode, "level": level, "seed": seed,
+                        "sha_f64": sha(np.ascontiguousarray(arr, np.float64))})
+    manifest["additive"] = add
 
     # ---------------- periodic pattern (numpy linspace / sin / uint8 cast) ----------------
     per = []

@@ -31,6 +31,15 @@ def _noise(img, step, nxt, rng):
         return sk.noise_sap(img, r1, r2, step.args[0])
     if op == "poisson":
         return sk.noise_poisson(img, np.random.poisson(sk.poisson_lambda(img)))
+    level = step.args[0]
+    if op == "uniform":
+        return sk.noise_uniform(img, np.random.random_sample(img.shape), level)
+    if op == "gamma":
+        return sk.noise_gamma(img, np.random.standard_gamma(1.99, img.shape), level)
+    if op == "rayleigh":
+        return sk.noise_rayleigh(img, np.sqrt(np.random.chisquare(2, img.shape)), level)
+    if op == "brownian":
+        return sk.noise_brownian(img, np.random.normal(size=img.size - 1), level)
     raise ValueError(op)
 
 

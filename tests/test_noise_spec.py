@@ -143,10 +143,21 @@ def test_unknown_level_unbound_in_test_v0():
         ns.plan("speckle_var9.9", "test_v0", R(0))
 
 
-def test_next_rows_raise_not_implemented():
-    for spec in ("uniform_var0.2", "gamma_var0.1", "rayleigh_var0.1", "brownian_var0.9"):
-        with pytest.raises(NotImplementedError):
-            ns.plan(spec, "train_v0", R(0))
+def test_quant_not_implemented_and_additive_noises_planned():
+    with pytest.raises(NotImplementedError):
+        ns.plan("quant_var3", "train_v0", R(0))  # MiniBatchKMeans: SURVEY §8f row 4
+    assert ops(ns.plan("uniform_var0.6", "train_v0", R(0))) == [("noise", "uniform", 0.6)]
+    assert ns.plan("uniform_var0.6", "train_v0", R(0)).out_dtype == "f64"  # minibatch.py:787
+    assert ops(ns.plan("gamma_var0.2", "test_v0", R(0))) == [("noise", "gamma", 0.2), ("cast_u8", "u8")]
+    assert ops(ns.plan("rayleigh_median_var0.3", "canonical", R(0))) == [
+        ("noise", "rayleigh", 0.3), ("cast_u8", "u8"), ("filter", "median", 3)]
+    # brownian: cv2.add(img, U8(255 B)) is u8; 'var0.09' is not read as 'var0.9'
+    assert ops(ns.plan("brownian_var0.09", "canonical", R(0))) == [("noise", "brownian", 0.09)]
+    assert ops(ns.plan("brownian_wavelet_var0.009", "canonical", R(0))) == [
+        ("noise", "brownian", 0.009), ("filter", "wavelet", "bior1.5", None)]
+    # additive wavelet branches denoise the unclipped float sum (no U8 before the wavelet)
+    assert ops(ns.plan("uniform_wavelet_var1.2", "canonical", R(0))) == [
+        ("noise", "uniform", 1.2), ("filter", "wavelet", "bior1.5", None)]
 
 
 def test_periodic_amplitude():

@@ -39,6 +39,35 @@ def make_img(h, w, seed):
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
+def additive_draws(mode, seed, img):
+    """numpy's unit draws of the additive closures for (mode, seed): the replay field
+    (brownian: element e holds z[e-1], element 0 unused)"""
+    rs = np.random.RandomState(seed)
+    if mode == "uniform":
+        return rs.random_sample(img.shape)
+    if mode == "gamma":
+        return rs.standard_gamma(1.99, img.shape)
+    if mode == "rayleigh":
+        return np.sqrt(rs.chisquare(2, img.shape))
+    f = np.zeros(img.size)
+    f[1:] = rs.normal(size=img.size - 1)
+    return f.reshape(img.shape)
+
+
+def additive_oracle(mode, level, img, field):
+    """(u8, f64) of the oracle restatement given the replay field"""
+    if mode == "uniform":
+        out = sk.noise_uniform(img, field, level)
+    elif mode == "gamma":
+        out = sk.noise_gamma(img, field, level)
+    elif mode == "rayleigh":
+        out = sk.noise_rayleigh(img, field, level)
+    else:
+        z = field.reshape(-1)[1:]
+        return sk.noise_brownian(img, z, level), sk.brownian_walk(z, level)
+    return sk.to_u8(255 * out), out
+
+
 def replay_field(mode, kw, seed, img):
     """re-draw the random field skimage's random_noise drew for (mode, seed)"""
     rs = np.random.RandomState(seed)
@@ -277,3 +306,16 @@ def test_bloom_circle_tables_agree():
             if hw >= 0:
                 expect[R + 1 - hw: R + 2 + hw] = 1
             assert np.array_equal(row, expect), (R, t)
+
+
+def test_additive_noises_vs_fixtures(gold):
+    """uniform / gamma / rayleigh / brownian closures (test.py:767-1572) restated in oracle/sk.py,
+    pinned to fixtures computed with scipy.stats 1.7.1 + numpy at the reference's calls"""
+    g, m = gold
+    assert len(m["additive"]) == 16
+    for case in m["additive"]:
+        img = g["in_" + case["input"]]
+        field = additive_draws(case["mode"], case["seed"], img)
+        u8, f = additive_oracle(case["mode"], case["level"], img, field)
+        assert np.array_equal(u8, g[case["key"] + "_u8"]), case
+        assert sha(np.ascontiguousarray(f, np.float64)) == case["sha_f64"], case

@@ -14,13 +14,16 @@ SPECS = {
     "canonical": ["gaussian_var0.1", "gaussian_median_var1.0", "sap_median_var0.4",
                   "speckle_bilateral_var0.5", "poisson_gaus_blur", "poisson_wavelet",
                   "periodic_mean_var100", "original_median", "shader", "bloom",
-                  "sap_wavelet_var0.2", "noise_mix_var_low_median", "speckle_mean_var2.0"],
+                  "sap_wavelet_var0.2", "noise_mix_var_low_median", "speckle_mean_var2.0",
+                  "uniform_median_var0.6", "gamma_wavelet_var0.1", "brownian_mean_var0.09",
+                  "rayleigh_var0.2", "noise_mix_var_all"],
     "test_v0": ["gaussian_var1.0", "sap_median_var0.4", "speckle_mean_var1.0", "poisson_wavelet",
                 "anything_else", "noise_mix_var_all", "bloom", "gaussian_wavelet_var0.1",
                 "periodic_bilateral_varsize"],
     "train_v0": ["gaussian_mean_var0.1", "speckle_var2.0", "gaussian_gaus_blur_var1.5",
                  "sap_var0.8", "periodic_median_var3.14", "noise_mix_var_medium",
-                 "poisson_median", "sap_bilateral_var0.2"],
+                 "poisson_median", "sap_bilateral_var0.2", "uniform_var0.2",
+                 "rayleigh_gaus_blur_var0.3", "gamma_var0.05", "brownian_wavelet_var0.9"],
 }
 
 
