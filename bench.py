@@ -213,6 +213,9 @@ def main():
                     "config's per-GPU batch for cfg2..cfg5)")
     ap.add_argument("--op", default="gauss5", choices=sorted(OPS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: also time reassembling the filtered batch on every rank with one "
+                         "RCCL all-gather over xGMI per step (reported as 'allgather')")
     args = ap.parse_args()
 
     import torch
@@ -264,6 +267,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
+    gather = None
+    if world > 1 and args.gather:
+        # end-to-end figure = filter step + all-gather of every rank's u8 output
+        full = torch.empty((world * args.batch, H, W, C), dtype=torch.uint8, device=dev)
+        for _ in range(2):
+            dist.all_gather_into_tensor(full, y)
+        torch.cuda.synchronize()
+        barrier()
+        g0 = time.perf_counter()
+        for _ in range(args.steps):
+            dist.all_gather_into_tensor(full, y)
+        torch.cuda.synchronize()
+        barrier()
+        gt = torch.tensor([time.perf_counter() - g0], device=dev, dtype=torch.float64)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        g_ms = float(gt.item()) / args.steps * 1e3
+        del full
+        gather = {"ms_per_step": round(g_ms, 4), "bytes_per_rank": int(y.numel()),
+                  "algbw_GBps": round(y.numel() * (world - 1) / (g_ms * 1e-3) / 1e9, 1)}
+
     pix_step = args.batch * H * W * world
     value = pix_step * args.steps / wall / 1e6
     achieved_gbs = bpp * args.batch * H * W / (avg_kern_ms * 1e-3) / 1e9
@@ -306,6 +329,10 @@ def main():
             },
             "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(args.op),
         }
+        if gather is not None:
+            step_ms = wall / args.steps * 1e3
+            gather["e2e_value"] = round(pix_step / ((step_ms + gather["ms_per_step"]) * 1e-3) / 1e6, 1)
+            rec["allgather"] = gather
         print(json.dumps(rec), flush=True)
 
     if world > 1:

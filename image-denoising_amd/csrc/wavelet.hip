@@ -6,15 +6,18 @@
 // against pywt 1.1.1 / skimage 0.18.3 fixtures).
 //
 // Pipeline per image (all images of the batch in every launch; grid.z = image x channel):
-//   1 wl_color      u8 BGR (or f64) -> three fp32 YCbCr planes (BGR data treated as RGB, as the
-//                   reference does) + per-channel min / max (u32 atomics on positive floats)
+//   1 wl_color_minmax  per-channel fp64 min / max of the YCbCr image (BGR data treated as RGB,
+//                   as the reference does); the YCbCr planes are never stored
 //   2 wl_dwt  x L   one separable 2-D analysis level per launch: a 256-thread workgroup stages a
 //                   (2T+F-2)^2 input tile in LDS (pywt 'symmetric' extension), filters rows, then
-//                   columns, and writes the aa / ad / da / dd bands.  Level 1 applies the
-//                   (x - min) / (max - min) channel normalisation while staging.
-//   3 wl_sumsq      per detail band: sum of squares in fp64, fixed-order tree (deterministic)
+//                   columns, and writes the aa / ad / da / dd bands plus the tile's sums of squares
+//                   of the three detail bands.  Level 1 stages straight from the u8 (or f64) image:
+//                   YCbCr channel + (x - min) / (max - min) normalisation on the fly.
+//   3 wl_sumsq      per detail band: add the tile partials in tile order (deterministic)
 //   4 wl_median     sigma = median(|finest dd| != 0) / 0.6744897501960817: exact radix select on
-//                   the float bits (3 passes of 11/11/10 bits, LDS histograms), both middle ranks
+//                   the float bits (two 11-bit passes over the band, compaction of the selected
+//                   prefix into the consumed input plane, four passes over that), + one pass for
+//                   the upper middle rank
 //   5 wl_thresh     BayesShrink t = var / sqrt(max(mean(d^2) - var, eps)) per band
 //   6 wl_idwt x L-1 synthesis levels L..2 (stage-2 valid convolution of pywt's
 //                   upsampling_convolution_valid_sf) with the soft threshold d*max(1-t/|d|, 0)
@@ -76,6 +79,10 @@ struct WlLayout {
   size_t off_band[WL_MAXL + 1];        // element offset of level l's 3x4 bands inside an image
   size_t img_floats;                   // wreal elements per image (planes + bands)
   size_t stats_off;                    // byte offset of the stats region (after all images)
+  int tiles_x[WL_MAXL + 1], tiles[WL_MAXL + 1];  // DWT tiles per level
+  size_t part_tile0[WL_MAXL + 1];      // first tile index of level l in the partials array
+  size_t part_per_img;                 // partial sums per image: 3 channels x 3 bands x tiles
+  size_t part_off;                     // byte offset of the partial sums region
   size_t bytes;
 };
 
@@ -113,7 +120,16 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   }
   Lt.img_floats = (off + 63) / 64 * 64;
   Lt.stats_off = (size_t)n * Lt.img_floats * sizeof(wreal);
-  Lt.bytes = Lt.stats_off + (size_t)n * WL_STATS * sizeof(double);
+  size_t tiles_tot = 0;
+  for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
+    Lt.tiles_x[l] = (Lt.W[l] + 15) / 16;
+    Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + 15) / 16);
+    Lt.part_tile0[l] = tiles_tot;
+    tiles_tot += (size_t)Lt.tiles[l];
+  }
+  Lt.part_per_img = 9 * tiles_tot;  // [c][b][tile]
+  Lt.part_off = Lt.stats_off + (size_t)n * WL_STATS * sizeof(double);
+  Lt.bytes = Lt.part_off + (size_t)n * Lt.part_per_img * sizeof(double);
   return Lt;
 }
 
@@ -129,12 +145,10 @@ __global__ void wl_init_stats(double* stats, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * WL_STATS) return;
   const int k = i % WL_STATS;
-  uint32_t* u = reinterpret_cast<uint32_t*>(stats + (i - k));
-  if (k < 3) {
-    u[2 * k] = 0xFFFFFFFFu;  // min (float bits, positive)
-    u[2 * k + 1] = 0u;       // max
-  } else if (k >= WlStats::MN64 && k < WlStats::MN64 + 3) {
-    reinterpret_cast<unsigned long long*>(stats)[i] = ~0ull;
+  if (k >= WlStats::MN64 && k < WlStats::MN64 + 3) {
+    reinterpret_cast<unsigned long long*>(stats)[i] = ~0ull;  // min key
+  } else if (k >= WlStats::MX64 && k < WlStats::MX64 + 3) {
+    reinterpret_cast<unsigned long long*>(stats)[i] = 0ull;   // max key
   } else {
     stats[i] = 0.0;
   }
@@ -168,87 +182,81 @@ __device__ __forceinline__ void load_rgb64(const uint8_t* __restrict__ src,
   }
 }
 
-__global__ __launch_bounds__(256) void wl_color(const uint8_t* __restrict__ src,
-                                                const double* __restrict__ in64, int h, int w,
-                                                int64_t row_stride, wreal* __restrict__ ws,
-                                                size_t img_floats, double* __restrict__ stats) {
+// fp64 min / max as order-preserving u64 keys (negative values flip all bits, positive ones the
+// sign bit), so unsigned atomics order any doubles -- f64 inputs outside [0, 1] give negative Cb/Cr
+__device__ __forceinline__ unsigned long long dkey(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dkey_inv(unsigned long long k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+__device__ __forceinline__ void atomicMinD(double* p, double v) {
+  atomicMin(reinterpret_cast<unsigned long long*>(p), dkey(v));
+}
+__device__ __forceinline__ void atomicMaxD(double* p, double v) {
+  atomicMax(reinterpret_cast<unsigned long long*>(p), dkey(v));
+}
+__device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn, double& mx) {
+  const unsigned long long* u64 = reinterpret_cast<const unsigned long long*>(st);
+  mn = dkey_inv(u64[WlStats::MN64 + c]);
+  mx = dkey_inv(u64[WlStats::MX64 + c]);
+}
+
+// per-channel min / max of the YCbCr image (fp64 exact, and fp32 bits for diagnostics); the
+// planes themselves are never stored: the level-1 analysis recomputes Y/Cb/Cr while staging
+__global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict__ src,
+                                                       const double* __restrict__ in64, int h, int w,
+                                                       int64_t row_stride, double* __restrict__ stats) {
   const int img = blockIdx.y;
   const int64_t np = (int64_t)h * w;
-  wreal* P = ws + img * img_floats;
-  float lmn[3] = {INFINITY, INFINITY, INFINITY}, lmx[3] = {-INFINITY, -INFINITY, -INFINITY};
   double dmn[3] = {INFINITY, INFINITY, INFINITY}, dmx[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
        p += (int64_t)gridDim.x * blockDim.x) {
-    double x0, x1, x2;
-    if (in64) {
-      const double* s = in64 + ((int64_t)img * np + p) * 3;
-      x0 = s[0];
-      x1 = s[1];
-      x2 = s[2];
-    } else {
-      const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
-      const uint8_t* s = src + (int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3;
-      x0 = (double)s[0] * (1.0 / 255.0);
-      x1 = (double)s[1] * (1.0 / 255.0);
-      x2 = (double)s[2] * (1.0 / 255.0);
-    }
+    const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
+    double v[3];
+    load_rgb64(src, in64, img, h, w, row_stride, y, x, v);
     double yc[3];
-    ycbcr64(x0, x1, x2, yc);
-    P[p] = yc[0];
-    P[np + p] = yc[1];
-    P[2 * np + p] = yc[2];
+    ycbcr64(v[0], v[1], v[2], yc);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      lmn[c] = fminf(lmn[c], (float)yc[c]);
-      lmx[c] = fmaxf(lmx[c], (float)yc[c]);
       dmn[c] = fmin(dmn[c], yc[c]);
       dmx[c] = fmax(dmx[c], yc[c]);
     }
   }
-  uint32_t* u = reinterpret_cast<uint32_t*>(stats + (size_t)img * WL_STATS);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    float a = lmn[c], b = lmx[c];
-    for (int o = 32; o > 0; o >>= 1) {
-      a = fminf(a, __shfl_xor(a, o));
-      b = fmaxf(b, __shfl_xor(b, o));
-    }
     double da = dmn[c], db = dmx[c];
     for (int o = 32; o > 0; o >>= 1) {
       da = fmin(da, __shfl_xor(da, o));
       db = fmax(db, __shfl_xor(db, o));
     }
-    // YCbCr of [0,1] inputs is positive: float order == unsigned bit order
-    if ((threadIdx.x & 63) == 0 && a <= b) {
-      atomicMin(&u[2 * c], __float_as_uint(a));
-      atomicMax(&u[2 * c + 1], __float_as_uint(b));
-      unsigned long long* u64 = reinterpret_cast<unsigned long long*>(stats + (size_t)img * WL_STATS);
-      atomicMin(&u64[WlStats::MN64 + c], (unsigned long long)__double_as_longlong(da));
-      atomicMax(&u64[WlStats::MX64 + c], (unsigned long long)__double_as_longlong(db));
+    if ((threadIdx.x & 63) == 0 && da <= db) {
+      atomicMinD(stats + (size_t)img * WL_STATS + WlStats::MN64 + c, da);
+      atomicMaxD(stats + (size_t)img * WL_STATS + WlStats::MX64 + c, db);
     }
   }
-}
-
-__device__ __forceinline__ void wl_minmax(const double* st, int c, float& mn, float& mx) {
-  const uint32_t* u = reinterpret_cast<const uint32_t*>(st);
-  mn = __uint_as_float(u[2 * c]);
-  mx = __uint_as_float(u[2 * c + 1]);
-}
-
-__device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn, double& mx) {
-  const unsigned long long* u64 = reinterpret_cast<const unsigned long long*>(st);
-  mn = __longlong_as_double((long long)u64[WlStats::MN64 + c]);
-  mx = __longlong_as_double((long long)u64[WlStats::MX64 + c]);
 }
 
 // ---- 2: one analysis level ----------------------------------------------------------------------
 constexpr int DT = 16;  // output tile (DT x DT coefficients per band)
 
+// channel c of skimage rgb2ycbcr for one pixel (same fma chain as ycbcr64)
+__device__ __forceinline__ double ycbcr_c(const double (&v)[3], int c) {
+  if (c == 0) return __dadd_rn(dot3(v[0], v[1], v[2], 65.481, 128.553, 24.966), 16.0);
+  if (c == 1) return __dadd_rn(dot3(v[0], v[1], v[2], -37.797, -74.203, 112.0), 128.0);
+  return __dadd_rn(dot3(v[0], v[1], v[2], 112.0, -93.786, -18.214), 128.0);
+}
+
 template <int WV>
 __global__ __launch_bounds__(256) void wl_dwt(wreal* __restrict__ ws, size_t img_floats,
                                               const double* __restrict__ stats, int level,
                                               size_t in_off, int Hin, int Win, size_t out_off,
-                                              int Ho, int Wo, int tiles_x) {
+                                              int Ho, int Wo, int tiles_x,
+                                              const uint8_t* __restrict__ src,
+                                              const double* __restrict__ in64, int64_t row_stride,
+                                              double* __restrict__ part, size_t part_per_img,
+                                              size_t part_tile0, int ntiles) {
   using Wv = Wav<WV>;
   constexpr int F = Wv::F;
   constexpr int NI = 2 * DT + F - 2;  // staged input rows / cols
@@ -274,8 +282,15 @@ __global__ __launch_bounds__(256) void wl_dwt(wreal* __restrict__ ws, size_t img
   const int r0 = 2 * i0 + 2 - F, q0 = 2 * j0 + 2 - F;  // input coordinate of staged [0][0]
   for (int k = threadIdx.x; k < NI * NI; k += 256) {
     const int r = k / NI, q = k % NI;
-    wreal v = X[(size_t)sym_idx(r0 + r, Hin) * Win + sym_idx(q0 + q, Win)];
-    if (norm) v = (v - mn) / inv;  // skimage: channel = out - min; channel /= max - min
+    const int yy = sym_idx(r0 + r, Hin), xx = sym_idx(q0 + q, Win);
+    wreal v;
+    if (norm) {  // level 1: the YCbCr channel straight from the source image
+      double px[3];
+      load_rgb64(src, in64, img, Hin, Win, row_stride, yy, xx, px);
+      v = (ycbcr_c(px, c) - mn) / inv;  // skimage: channel = out - min; channel /= max - min
+    } else {
+      v = X[(size_t)yy * Win + xx];
+    }
     xin[r][q] = v;
   }
   __syncthreads();
@@ -295,6 +310,7 @@ __global__ __launch_bounds__(256) void wl_dwt(wreal* __restrict__ ws, size_t img
   __syncthreads();
   const int ii = threadIdx.x / DT, jj = threadIdx.x % DT;
   const int i = i0 + ii, j = j0 + jj;
+  double sq[3] = {0.0, 0.0, 0.0};
   if (i < Ho && j < Wo) {
     wreal aa = 0, ad = 0, da = 0, dd = 0;
 #pragma unroll
@@ -314,13 +330,30 @@ __global__ __launch_bounds__(256) void wl_dwt(wreal* __restrict__ ws, size_t img
     out[bsz + o] = ad;
     out[2 * bsz + o] = da;
     out[3 * bsz + o] = dd;
+    sq[0] = ad * ad;
+    sq[1] = da * da;
+    sq[2] = dd * dd;
+  }
+  // per-tile sums of squares of the three detail bands, fixed order (wl_sumsq adds the tiles)
+  __shared__ double red[3][4];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    double v = sq[b];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) red[b][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int b = threadIdx.x;
+    const double t = (red[b][0] + red[b][1]) + (red[b][2] + red[b][3]);
+    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = t;
   }
 }
 
 // ---- 3: sum of squares per detail band ----------------------------------------------------------
-__global__ __launch_bounds__(1024) void wl_sumsq(const wreal* __restrict__ ws, size_t img_floats,
-                                                 double* __restrict__ stats, WlLayout Lt) {
-  // block = (img, c, l, b)
+__global__ __launch_bounds__(256) void wl_sumsq(double* __restrict__ stats,
+                                                const double* __restrict__ part, WlLayout Lt) {
+  // block = (img, c, l, b): add the level's tile partials in tile order (deterministic)
   int t = blockIdx.x;
   const int b = t % 3;
   t /= 3;
@@ -329,71 +362,107 @@ __global__ __launch_bounds__(1024) void wl_sumsq(const wreal* __restrict__ ws, s
   const int c = t % 3;
   const int img = t / 3;
   const int lev = l + 1;
-  const size_t bsz = (size_t)Lt.H[lev] * Lt.W[lev];
-  const wreal* d = ws + img * img_floats + Lt.off_band[lev] + (size_t)c * 4 * bsz + (size_t)(b + 1) * bsz;
+  const double* p = part + img * Lt.part_per_img + (size_t)(c * 3 + b) * (Lt.part_per_img / 9) +
+                    Lt.part_tile0[lev];
   double s = 0.0;
-  for (size_t k = threadIdx.x; k < bsz; k += 1024) {
-    const double v = d[k];
-    s += v * v;
-  }
-  __shared__ double red[16];
+  for (int k = threadIdx.x; k < Lt.tiles[lev]; k += 256) s += p[k];
+  __shared__ double red[4];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double tot = 0.0;
-    for (int k = 0; k < 16; ++k) tot += red[k];
-    stats[(size_t)img * WL_STATS + WlStats::sumsq(c, l, b, Lt.L)] = tot;
-  }
+  if (threadIdx.x == 0)
+    stats[(size_t)img * WL_STATS + WlStats::sumsq(c, l, b, Lt.L)] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ---- 4: sigma = median(|finest dd| != 0) / ppf(0.75) ------------------------------------------
 // The median is over the NONZERO coefficients, so which coefficients are exactly zero must match
 // the reference: the analysis runs in fp64 with pywt's op order (normalise (Y - min)/(max - min),
 // axis 0 then axis 1, multiply then add), under which equal samples give an exact 0.
-// exact rank selection over nonzero non-negative doubles: 6 passes of <= 11 bits on the bits
-__device__ unsigned long long radix_select64(const double* __restrict__ d, size_t n, uint32_t rank,
-                                             uint32_t* hist) {
-  unsigned long long prefix = 0, pmask = 0;
-  for (int pass = 0; pass < 6; ++pass) {
-    const int sh = (pass < 5) ? 52 - 11 * pass : 0;
-    const int wd = (pass < 5) ? 11 : 8;
-    const int nb = 1 << wd;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
-    __syncthreads();
-    for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
-      const unsigned long long key = (unsigned long long)__double_as_longlong(d[k]) & 0x7FFFFFFFFFFFFFFFull;
-      if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
-    }
-    __syncthreads();
-    __shared__ uint32_t sel_bin, sel_rank;
-    if (threadIdx.x == 0) {
-      uint32_t acc = 0;
-      int bin = 0;
-      for (; bin < nb - 1; ++bin) {
-        if (acc + hist[bin] > rank) break;
-        acc += hist[bin];
-      }
-      sel_bin = (uint32_t)bin;
-      sel_rank = rank - acc;
-    }
-    __syncthreads();
-    prefix |= (unsigned long long)sel_bin << sh;
-    pmask |= (unsigned long long)(nb - 1) << sh;
-    rank = sel_rank;
-    __syncthreads();
-  }
-  return prefix;
+// Exact rank selection over the nonzero |d| of one band, on the IEEE bits (non-negative doubles
+// order like their bit patterns).  Radix passes of <= 11 bits: the first two run over the band,
+// then the keys sharing the selected 22-bit prefix are compacted into a scratch slot and the last
+// four passes run over that (typically a few hundred keys).  The upper middle rank (even counts)
+// costs one more band pass: it equals the lower value while enough keys are <= it, otherwise it
+// is the smallest key above it.
+struct RadixState {
+  unsigned long long prefix, pmask;
+  uint32_t rank;
+};
+
+__device__ __forceinline__ unsigned long long absbits(double v) {
+  return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
 }
 
-__global__ __launch_bounds__(1024) void wl_median(const wreal* __restrict__ ws, size_t img_floats,
+// one histogram pass over keys[0..n) (only keys matching the prefix); narrows the state
+__device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int wd, RadixState& rsx,
+                           uint32_t* hist) {
+  const int nb = 1 << wd;
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
+  __syncthreads();
+  const unsigned long long prefix = rsx.prefix, pmask = rsx.pmask;
+  for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned long long key = absbits(d[k]);
+    if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+  }
+  __syncthreads();
+  __shared__ uint32_t sel_bin, sel_rank;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    int bin = 0;
+    for (; bin < nb - 1; ++bin) {
+      if (acc + hist[bin] > rsx.rank) break;
+      acc += hist[bin];
+    }
+    sel_bin = (uint32_t)bin;
+    sel_rank = rsx.rank - acc;
+  }
+  __syncthreads();
+  rsx.prefix |= (unsigned long long)sel_bin << sh;
+  rsx.pmask |= (unsigned long long)(nb - 1) << sh;
+  rsx.rank = sel_rank;
+  __syncthreads();
+}
+
+__device__ unsigned long long radix_select64(const double* __restrict__ d, size_t n, uint32_t rank,
+                                             uint32_t* hist, double* __restrict__ scratch) {
+  RadixState rsx{0ull, 0ull, rank};
+  radix_pass(d, n, 52, 11, rsx, hist);
+  radix_pass(d, n, 41, 11, rsx, hist);
+  // compact the keys with this 22-bit prefix (their count <= n) into scratch
+  __shared__ uint32_t m_s;
+  if (threadIdx.x == 0) m_s = 0;
+  __syncthreads();
+  for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const double v = d[k];
+    const unsigned long long key = absbits(v);
+    if (key != 0 && (key & rsx.pmask) == rsx.prefix) scratch[atomicAdd(&m_s, 1u)] = v;
+  }
+  __syncthreads();
+  const size_t m = m_s;
+  __syncthreads();
+  radix_pass(scratch, m, 30, 11, rsx, hist);
+  radix_pass(scratch, m, 19, 11, rsx, hist);
+  radix_pass(scratch, m, 8, 11, rsx, hist);
+  radix_pass(scratch, m, 0, 8, rsx, hist);
+  return rsx.prefix;
+}
+
+__global__ __launch_bounds__(1024) void wl_median(wreal* __restrict__ ws, size_t img_floats,
                                                   double* __restrict__ stats, WlLayout Lt) {
   const int img = blockIdx.x / 3, c = blockIdx.x % 3;
   const size_t bsz = (size_t)Lt.H[1] * Lt.W[1];
-  const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
+  wreal* band = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz;
+  const wreal* d = band + 3 * bsz;  // dd
+  // scratch: this channel's input plane (h*w >= band size), consumed by the level-1 analysis
+  double* scratch = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;
   __shared__ uint32_t hist[2048];
-  __shared__ uint32_t cnt_s;
-  if (threadIdx.x == 0) cnt_s = 0;
+  __shared__ uint32_t cnt_s, le_s;
+  __shared__ unsigned long long gt_s;
+  if (threadIdx.x == 0) {
+    cnt_s = 0;
+    le_s = 0;
+    gt_s = ~0ull;
+  }
   __syncthreads();
   uint32_t cnt = 0;
   for (size_t k = threadIdx.x; k < bsz; k += 1024) cnt += d[k] != 0.0;  // -0.0 == 0.0
@@ -405,9 +474,23 @@ __global__ __launch_bounds__(1024) void wl_median(const wreal* __restrict__ ws, 
     med = NAN;  // np.median of an empty selection
   } else {
     const uint32_t klo = (total - 1) / 2, khi = total / 2;
-    const double vlo = __longlong_as_double((long long)radix_select64(d, bsz, klo, hist));
-    const double vhi =
-        (khi == klo) ? vlo : __longlong_as_double((long long)radix_select64(d, bsz, khi, hist));
+    const unsigned long long lo_key = radix_select64(d, bsz, klo, hist, scratch);
+    const double vlo = __longlong_as_double((long long)lo_key);
+    double vhi = vlo;
+    if (khi != klo) {
+      uint32_t le = 0;
+      unsigned long long gt = ~0ull;
+      for (size_t k = threadIdx.x; k < bsz; k += 1024) {
+        const unsigned long long key = absbits(d[k]);
+        if (key == 0) continue;
+        if (key <= lo_key) ++le;
+        else gt = key < gt ? key : gt;
+      }
+      atomicAdd(&le_s, le);
+      atomicMin(&gt_s, gt);
+      __syncthreads();
+      if (le_s <= khi) vhi = __longlong_as_double((long long)gt_s);
+    }
     med = (vlo + vhi) / 2.0;  // np.median: mean of the two middle values
   }
   if (threadIdx.x == 0) {
@@ -584,17 +667,19 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
     const int64_t np = (int64_t)Lt.h * Lt.w;
     int gx = (int)((np + 255) / 256);
     if (gx > 256) gx = 256;
-    hipLaunchKernelGGL(wl_color, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w, row_stride,
-                       wsf, Lt.img_floats, stats);
+    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+                       row_stride, stats);
   }
+  double* part = (double*)((char*)ws + Lt.part_off);
   for (int l = 1; l <= Lt.L; ++l) {
     const size_t in_off = (l == 1) ? 0 : Lt.off_band[l - 1];
-    const int tx = (Lt.W[l] + DT - 1) / DT, ty = (Lt.H[l] + DT - 1) / DT;
-    hipLaunchKernelGGL((wl_dwt<WV>), dim3(tx * ty, 1, n * 3), dim3(256), 0, st, wsf, Lt.img_floats,
-                       stats, l, in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
-                       tx);
+    const int tx = Lt.tiles_x[l];
+    hipLaunchKernelGGL((wl_dwt<WV>), dim3(Lt.tiles[l], 1, n * 3), dim3(256), 0, st, wsf,
+                       Lt.img_floats, stats, l, in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l],
+                       Lt.H[l], Lt.W[l], tx, src, in64, row_stride, part, Lt.part_per_img,
+                       Lt.part_tile0[l], Lt.tiles[l]);
   }
-  hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
+  hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   for (int l = Lt.L; l >= 2; --l) {
