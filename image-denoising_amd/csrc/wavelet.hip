@@ -211,17 +211,17 @@ __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict
   const int img = blockIdx.y;
   const int64_t np = (int64_t)h * w;
   double dmn[3] = {INFINITY, INFINITY, INFINITY}, dmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
-       p += (int64_t)gridDim.x * blockDim.x) {
-    const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
+  // pixel p = y * w + x with 32-bit index math (p < 2^31 per image: checked on the host)
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < (int)np; p += gridDim.x * blockDim.x) {
+    const int y = p / w, x = p - y * w;
     double v[3];
     load_rgb64(src, in64, img, h, w, row_stride, y, x, v);
     double yc[3];
     ycbcr64(v[0], v[1], v[2], yc);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      dmn[c] = fmin(dmn[c], yc[c]);
-      dmx[c] = fmax(dmx[c], yc[c]);
+      dmn[c] = yc[c] < dmn[c] ? yc[c] : dmn[c];  // never NaN: plain selects
+      dmx[c] = yc[c] > dmx[c] ? yc[c] : dmx[c];
     }
   }
 #pragma unroll
@@ -379,11 +379,12 @@ __global__ __launch_bounds__(256) void wl_sumsq(double* __restrict__ stats,
 // the reference: the analysis runs in fp64 with pywt's op order (normalise (Y - min)/(max - min),
 // axis 0 then axis 1, multiply then add), under which equal samples give an exact 0.
 // Exact rank selection over the nonzero |d| of one band, on the IEEE bits (non-negative doubles
-// order like their bit patterns).  Radix passes of <= 11 bits: the first two run over the band,
-// then the keys sharing the selected 22-bit prefix are compacted into a scratch slot and the last
-// four passes run over that (typically a few hundred keys).  The upper middle rank (even counts)
-// costs one more band pass: it equals the lower value while enough keys are <= it, otherwise it
-// is the smallest key above it.
+// order like their bit patterns).  Radix passes of <= 11 bits: the first two run over the band
+// (the first also counts the nonzero keys), then the keys sharing the selected 22-bit prefix are
+// compacted into a scratch slot and the last four passes run over that (typically a few hundred
+// keys).  The upper middle rank (even counts) costs one more band pass: it equals the lower value
+// while enough keys are <= it, otherwise it is the smallest key above it.  Compaction slots are
+// allocated once per wave (ballot + popcount).
 struct RadixState {
   unsigned long long prefix, pmask;
   uint32_t rank;
@@ -393,9 +394,10 @@ __device__ __forceinline__ unsigned long long absbits(double v) {
   return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
 }
 
-// one histogram pass over keys[0..n) (only keys matching the prefix); narrows the state
+// one histogram pass over keys[0..n) (only keys matching the prefix); narrows the state.
+// total (optional) receives the number of nonzero keys seen (first pass only).
 __device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int wd, RadixState& rsx,
-                           uint32_t* hist) {
+                           uint32_t* hist, uint32_t* total) {
   const int nb = 1 << wd;
   for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
   __syncthreads();
@@ -407,6 +409,12 @@ __device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int w
   __syncthreads();
   __shared__ uint32_t sel_bin, sel_rank;
   if (threadIdx.x == 0) {
+    if (total) {
+      uint32_t t = 0;
+      for (int b = 0; b < nb; ++b) t += hist[b];
+      *total = t;
+      rsx.rank = t ? (t - 1) / 2 : 0;  // lower middle rank
+    }
     uint32_t acc = 0;
     int bin = 0;
     for (; bin < nb - 1; ++bin) {
@@ -423,58 +431,53 @@ __device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int w
   __syncthreads();
 }
 
-__device__ unsigned long long radix_select64(const double* __restrict__ d, size_t n, uint32_t rank,
-                                             uint32_t* hist, double* __restrict__ scratch) {
-  RadixState rsx{0ull, 0ull, rank};
-  radix_pass(d, n, 52, 11, rsx, hist);
-  radix_pass(d, n, 41, 11, rsx, hist);
-  // compact the keys with this 22-bit prefix (their count <= n) into scratch
-  __shared__ uint32_t m_s;
-  if (threadIdx.x == 0) m_s = 0;
-  __syncthreads();
-  for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
-    const double v = d[k];
-    const unsigned long long key = absbits(v);
-    if (key != 0 && (key & rsx.pmask) == rsx.prefix) scratch[atomicAdd(&m_s, 1u)] = v;
-  }
-  __syncthreads();
-  const size_t m = m_s;
-  __syncthreads();
-  radix_pass(scratch, m, 30, 11, rsx, hist);
-  radix_pass(scratch, m, 19, 11, rsx, hist);
-  radix_pass(scratch, m, 8, 11, rsx, hist);
-  radix_pass(scratch, m, 0, 8, rsx, hist);
-  return rsx.prefix;
-}
-
 __global__ __launch_bounds__(1024) void wl_median(wreal* __restrict__ ws, size_t img_floats,
                                                   double* __restrict__ stats, WlLayout Lt) {
   const int img = blockIdx.x / 3, c = blockIdx.x % 3;
   const size_t bsz = (size_t)Lt.H[1] * Lt.W[1];
-  wreal* band = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz;
-  const wreal* d = band + 3 * bsz;  // dd
-  // scratch: this channel's input plane (h*w >= band size), consumed by the level-1 analysis
+  const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
+  // scratch: this channel's input-plane slot (h*w >= band size), unused by the transform
   double* scratch = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;
   __shared__ uint32_t hist[2048];
-  __shared__ uint32_t cnt_s, le_s;
+  __shared__ uint32_t total_s, m_s, le_s;
   __shared__ unsigned long long gt_s;
   if (threadIdx.x == 0) {
-    cnt_s = 0;
+    m_s = 0;
     le_s = 0;
     gt_s = ~0ull;
   }
-  __syncthreads();
-  uint32_t cnt = 0;
-  for (size_t k = threadIdx.x; k < bsz; k += 1024) cnt += d[k] != 0.0;  // -0.0 == 0.0
-  atomicAdd(&cnt_s, cnt);
-  __syncthreads();
-  const uint32_t total = cnt_s;
+  RadixState rsx{0ull, 0ull, 0u};
+  radix_pass(d, bsz, 52, 11, rsx, hist, &total_s);  // also counts the nonzero keys
+  const uint32_t total = total_s;
   double med;
   if (total == 0) {
     med = NAN;  // np.median of an empty selection
   } else {
     const uint32_t klo = (total - 1) / 2, khi = total / 2;
-    const unsigned long long lo_key = radix_select64(d, bsz, klo, hist, scratch);
+    radix_pass(d, bsz, 41, 11, rsx, hist, nullptr);
+    // compact the keys with the selected 22-bit prefix (wave-aggregated slot allocation)
+    const int lane = threadIdx.x & 63;
+    const size_t nr = (bsz + 1023) / 1024 * 1024;
+    for (size_t k = threadIdx.x; k < nr; k += 1024) {
+      const double v = k < bsz ? d[k] : 0.0;
+      const unsigned long long key = absbits(v);
+      const bool hit = key != 0 && (key & rsx.pmask) == rsx.prefix;
+      const unsigned long long m = __ballot(hit);
+      if (m) {
+        uint32_t base = 0;
+        const int leader = __ffsll((long long)m) - 1;
+        if (lane == leader) base = atomicAdd(&m_s, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (hit) scratch[base + __popcll(m & ((1ull << lane) - 1))] = v;
+      }
+    }
+    __syncthreads();
+    const size_t mcnt = m_s;
+    radix_pass(scratch, mcnt, 30, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 19, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 8, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 0, 8, rsx, hist, nullptr);
+    const unsigned long long lo_key = rsx.prefix;
     const double vlo = __longlong_as_double((long long)lo_key);
     double vhi = vlo;
     if (khi != klo) {
@@ -486,8 +489,15 @@ __global__ __launch_bounds__(1024) void wl_median(wreal* __restrict__ ws, size_t
         if (key <= lo_key) ++le;
         else gt = key < gt ? key : gt;
       }
-      atomicAdd(&le_s, le);
-      atomicMin(&gt_s, gt);
+      for (int o = 32; o > 0; o >>= 1) {
+        le += __shfl_xor(le, o);
+        const unsigned long long og = (unsigned long long)__shfl_xor((long long)gt, o);
+        gt = og < gt ? og : gt;
+      }
+      if (lane == 0) {
+        atomicAdd(&le_s, le);
+        atomicMin(&gt_s, gt);
+      }
       __syncthreads();
       if (le_s <= khi) vhi = __longlong_as_double((long long)gt_s);
     }
@@ -524,9 +534,11 @@ __global__ void wl_thresh(double* __restrict__ stats, WlLayout Lt) {
   st[WlStats::FLAG] = bad ? 1.0 : 0.0;
 }
 
+// pywt.threshold(d, t, 'soft') = d * max(1 - t/|d|, 0) = sign(d) * max(|d| - t, 0): the same value
+// to a few ulps (t >= 0), without the fp64 division per coefficient
 __device__ __forceinline__ wreal soft(wreal d, wreal t) {
-  const wreal s = 1.0 - t / fabs(d);  // |d| == 0 -> -inf -> 0 (pywt.threshold 'soft')
-  return d * fmax(s, 0.0);
+  const wreal m = fabs(d) - t;
+  return m > 0.0 ? __builtin_copysign(m, d) : 0.0;
 }
 
 // ---- 6: one synthesis level (levels L..2), output = approx of level l-1 -------------------------
@@ -718,6 +730,7 @@ extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, 
   IDN_CHECK_ARG(src || in_f64, "idn_wavelet_denoise_u8: no input");
   IDN_CHECK_ARG(out_u8 || out_f32, "idn_wavelet_denoise_u8: no output");
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0, "idn_wavelet_denoise_u8: bad shape");
+  IDN_CHECK_ARG((int64_t)h * w < ((int64_t)1 << 31), "idn_wavelet_denoise_u8: image too large");
   IDN_CHECK_ARG(row_stride >= (int64_t)w * 3, "idn_wavelet_denoise_u8: row_stride < w*3");
   IDN_CHECK_ARG(wavelet == IDN_WAVELET_DB1 || wavelet == IDN_WAVELET_BIOR15,
                 "idn_wavelet_denoise_u8: unknown wavelet %d", wavelet);
