@@ -7,12 +7,13 @@
 // the L1 distance |db|+|dg|+|dr|, float sums, out = cvRound(sum * (1.f / wsum)), border pixels 0.
 //
 // gfx950 design: a 256-thread workgroup owns a 64 x 16 output tile; the (64+2r) x (16+2r) input
-// tile (BGR0-packed u32 per pixel, zero outside the image) is staged once in LDS.  Each thread
-// walks 4 output rows of one column.  Per tap: v_sad_u8 on the packed pixels gives the colour
-// distance in one instruction; the weight is exp2(fma(dist^2, c2, log2(space_w))) — one FMA + one
-// v_exp_f32 instead of two table loads (the colour LUT of OpenCV is float(exp(double)); the
-// in-register exp differs by <= 1 ulp, inside the <= 1 LSB output tolerance).  Taps are a
-// compile-time table for d = 9 (radius 4, 49 taps); other d use the runtime-tap kernel.
+// tile (BGR0-packed u32 per pixel, zero outside the image) is staged once in LDS, next to
+// OpenCV's colour-weight table color_weight[i] = float(exp(i^2 * -0.5/sc^2)), i = 0..765, which
+// each workgroup builds in LDS.  Each thread walks 4 output rows of one column.  Per tap: v_sad_u8
+// on the packed pixels gives the L1 colour distance in one instruction, the weight is OpenCV's
+// space_weight[k] * color_weight[dist] (space weights are compile-time taps in SGPRs), and
+// (b, g) / (r, wsum) accumulate as packed fp32 pairs.  The weights are then exactly OpenCV's;
+// only the fp32 summation order differs (<= 1 LSB after cvRound).
 #include "idn_common.hpp"
 
 #include <math.h>
@@ -28,9 +29,10 @@ constexpr int BL_RPT = 4;   // output rows per thread
 constexpr int BL_MAXR = 8;  // max radius supported (d <= 17)
 
 struct BilateralTaps {
-  float c2;                                          // -0.5/sc^2 * log2(e)
-  float lsw[(2 * BL_MAXR + 1) * (2 * BL_MAXR + 1)];  // log2(space weight) at (i+R)*(2R+1)+(j+R)
+  double gcc;                                       // -0.5 / sigma_color^2
+  float sw[(2 * BL_MAXR + 1) * (2 * BL_MAXR + 1)];  // space weight at (i+R)*(2R+1)+(j+R)
 };
+constexpr int BL_LUT = 3 * 255 + 1;
 
 template <int C>
 __device__ __forceinline__ uint32_t load_px(const uint8_t* __restrict__ s, int64_t row_stride,
@@ -49,6 +51,7 @@ __global__ __launch_bounds__(256) void bilateral_u8_kernel(const uint8_t* __rest
   constexpr int LW = BL_TW + 2 * R;
   constexpr int LH = BL_TH + 2 * R;
   __shared__ uint32_t tile[LH * LW];
+  __shared__ float cw[BL_LUT];
 
   const int t = blockIdx.x;
   const int tx = t % tiles_x;
@@ -62,6 +65,7 @@ __global__ __launch_bounds__(256) void bilateral_u8_kernel(const uint8_t* __rest
     const int ly = i / LW, lx = i % LW;
     tile[i] = load_px<C>(s, row_stride, h, w, y0 + ly - R, x0 + lx - R);
   }
+  for (int i = threadIdx.x; i < BL_LUT; i += 256) cw[i] = (float)exp((double)(i * i) * taps.gcc);
   __syncthreads();
 
   const int col = threadIdx.x & 63;
@@ -82,9 +86,8 @@ __global__ __launch_bounds__(256) void bilateral_u8_kernel(const uint8_t* __rest
       for (int j = -R; j <= R; ++j) {
         if (i * i + j * j > R * R) continue;  // sqrt(i^2+j^2) > radius: not a tap
         const uint32_t p = tile[(ly + R + i) * LW + col + R + j];
-        const float df = (float)__builtin_amdgcn_sad_u8(p, p0, 0u);
-        const float wt = __builtin_amdgcn_exp2f(
-            __builtin_fmaf(df * df, taps.c2, taps.lsw[(i + R) * (2 * R + 1) + (j + R)]));
+        const uint32_t dist = __builtin_amdgcn_sad_u8(p, p0, 0u);
+        const float wt = taps.sw[(i + R) * (2 * R + 1) + (j + R)] * cw[dist];
         const f32x2 w2 = {wt, wt};
         if constexpr (C == 3) {
           const f32x2 bg = {(float)(p & 0xFFu), (float)((p >> 8) & 0xFFu)};
@@ -145,13 +148,12 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
   memset(&taps, 0, sizeof(taps));
   const double gcc = -0.5 / (sigma_color * sigma_color);
   const double gsc = -0.5 / (sigma_space * sigma_space);
-  taps.c2 = (float)(gcc * 1.4426950408889634);
+  taps.gcc = gcc;
   for (int i = -radius; i <= radius; ++i)
     for (int j = -radius; j <= radius; ++j) {
       const double r = sqrt((double)i * i + (double)j * j);
       if (r > radius) continue;
-      const float sw = (float)exp(r * r * gsc);  // OpenCV's float space weight
-      taps.lsw[(i + radius) * (2 * radius + 1) + (j + radius)] = (float)log2((double)sw);
+      taps.sw[(i + radius) * (2 * radius + 1) + (j + radius)] = (float)exp(r * r * gsc);  // OpenCV's
     }
   hipStream_t st = as_stream(stream);
 #define IDN_BL(CC)                                                          \
