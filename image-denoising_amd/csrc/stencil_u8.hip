@@ -284,6 +284,74 @@ __global__ __launch_bounds__(256) void stencil_u8_vf(const uint8_t* __restrict__
   }
 }
 
+// ---- shared per-row body of the LDS forms ------------------------------------------------------
+// One output row from the register ring of K unpacked input rows whose newest row sits in slot
+// `nw`: vertical taps, DPP halos, tail reflections, horizontal taps, pack, store.
+template <int C, int OP>
+__device__ __forceinline__ v4u ring_row(const uint32_t (&Rg)[Stencil<OP>::K][8], int nw,
+                                        const StripeGeom& g) {
+  constexpr int K = Stencil<OP>::K;
+  constexpr int R = K / 2;
+  uint32_t Vs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if constexpr (K == 5) {
+      Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[(nw + 3) % K][j],
+                       Rg[(nw + 4) % K][j], Rg[nw][j]);
+    } else {
+      Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[nw][j], 0u, 0u);
+    }
+  }
+  VWin V;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    V.SE[2 + j] = Vs[j];
+    V.SO[2 + j] = Vs[4 + j];
+  }
+  if constexpr (R * C > 4) {
+    V.SE[0] = from_prev_lane(Vs[2]);
+    V.SO[0] = from_prev_lane(Vs[6]);
+    V.SE[7] = from_next_lane(Vs[1]);
+    V.SO[7] = from_next_lane(Vs[5]);
+  } else {
+    V.SE[0] = V.SO[0] = V.SE[7] = V.SO[7] = 0u;
+  }
+  V.SE[1] = from_prev_lane(Vs[3]);
+  V.SO[1] = from_prev_lane(Vs[7]);
+  V.SE[6] = from_next_lane(Vs[0]);
+  V.SO[6] = from_next_lane(Vs[4]);
+  if (g.fix_t0) vwin_tail_fix<C>(V, 24);
+  if (g.fix_t8) vwin_tail_fix<C>(V, 16);
+  uint32_t A[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    A[2 * k] = htap<C, OP>(V, 4 * k + 8);
+    A[2 * k + 1] = htap<C, OP>(V, 4 * k + 9);
+  }
+  return finish<OP>(A);
+}
+template <int C, int OP, int NT>
+__device__ __forceinline__ void ring_out_row(const uint32_t (&Rg)[Stencil<OP>::K][8], int nw,
+                                             const StripeGeom& g, rsrc_t rd, const StoreOffs& so,
+                                             uint32_t row_off) {
+  stripe_store_nb<NT>(ring_row<C, OP>(Rg, nw, g), rd, so, row_off);
+}
+
+// the lane's 16-byte chunk of one row staged in LDS at byte `o`, lead lane rebuilt, unpacked
+template <int C>
+__device__ __forceinline__ void lds_take_row(const uint8_t* tile, uint32_t o, bool lead,
+                                             uint32_t (&U)[8]) {
+  const v2u a = *reinterpret_cast<const v2u*>(&tile[o]);
+  const v2u b = *reinterpret_cast<const v2u*>(&tile[o + 8]);
+  v4u Lv = v4u{a.x, a.y, b.x, b.y};
+  if (lead) {
+    const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
+    Lv = v4u{lead_fix<C, BORDER_REFLECT101>(L, -8), lead_fix<C, BORDER_REFLECT101>(L, -4), L[0],
+             L[1]};
+  }
+  unpack_row(Lv, U);
+}
+
 // ---- LDS-tiled form --------------------------------------------------------------------------
 // One workgroup = one band of NB output rows of one image, nseg waves (<= 3: rows <= 3024 bytes).
 // The band's NB + 2R input rows are contiguous in HBM (row_stride == row bytes), so the whole
@@ -349,23 +417,11 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
 
   const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
   const int nin = (y1 - y0) + 2 * R;
-  auto lds_row = [&](int r) -> v4u {
-    const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
-    const uint32_t o = (uint32_t)(y - ys) * (uint32_t)rb + shift + ld_off;
-    const v2u a = *reinterpret_cast<const v2u*>(&tile[o]);
-    const v2u b = *reinterpret_cast<const v2u*>(&tile[o + 8]);
-    return v4u{a.x, a.y, b.x, b.y};
-  };
   const StoreOffs so = store_offs(g);
   uint32_t Rg[K][8];
   auto take_row = [&](int r) {
-    v4u Lv = lds_row(r);
-    if (g.lead) {
-      const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
-      Lv = v4u{lead_fix<C, BORDER_REFLECT101>(L, -8), lead_fix<C, BORDER_REFLECT101>(L, -4),
-               L[0], L[1]};
-    }
-    unpack_row(Lv, Rg[r % K]);
+    const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
+    lds_take_row<C>(tile, (uint32_t)(y - ys) * (uint32_t)rb + shift + ld_off, g.lead, Rg[r % K]);
   };
 #pragma unroll
   for (int r = 0; r < 2 * R; ++r) take_row(r);
@@ -373,47 +429,11 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   for (int u = 0; u < NB; ++u) {
     const int r = 2 * R + u;
     take_row(r);
-    const int nw = r % K;
-    uint32_t Vs[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if constexpr (K == 5) {
-        Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[(nw + 3) % K][j],
-                         Rg[(nw + 4) % K][j], Rg[nw][j]);
-      } else {
-        Vs[j] = vtap<OP>(Rg[(nw + 1) % K][j], Rg[(nw + 2) % K][j], Rg[nw][j], 0u, 0u);
-      }
-    }
-    VWin V;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      V.SE[2 + j] = Vs[j];
-      V.SO[2 + j] = Vs[4 + j];
-    }
-    if constexpr (R * C > 4) {
-      V.SE[0] = from_prev_lane(Vs[2]);
-      V.SO[0] = from_prev_lane(Vs[6]);
-      V.SE[7] = from_next_lane(Vs[1]);
-      V.SO[7] = from_next_lane(Vs[5]);
-    } else {
-      V.SE[0] = V.SO[0] = V.SE[7] = V.SO[7] = 0u;
-    }
-    V.SE[1] = from_prev_lane(Vs[3]);
-    V.SO[1] = from_prev_lane(Vs[7]);
-    V.SE[6] = from_next_lane(Vs[0]);
-    V.SO[6] = from_next_lane(Vs[4]);
-    if (g.fix_t0) vwin_tail_fix<C>(V, 24);
-    if (g.fix_t8) vwin_tail_fix<C>(V, 16);
-    uint32_t A[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      A[2 * k] = htap<C, OP>(V, 4 * k + 8);
-      A[2 * k + 1] = htap<C, OP>(V, 4 * k + 9);
-    }
     const int y = y0 + u;
-    stripe_store_nb<NT>(finish<OP>(A), rd, so, y < y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
+    ring_out_row<C, OP, NT>(Rg, r % K, g, rd, so, y < y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
   }
 }
+
 
 // ---- generic path ------------------------------------------------------------------------
 template <int OP>

@@ -89,7 +89,8 @@ FORMS = [
 
 
 @pytest.mark.parametrize("form", FORMS, ids=lambda f: "-".join(f"{k[12:]}{v}" for k, v in f.items()))
-@pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (2, 13, 104), (1, 601, 1000)])
+@pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (2, 13, 104), (1, 601, 1000),
+                                   (1, 26, 1000), (1, 25, 664)])
 def test_stencil_forms_agree(dev, monkeypatch, form, shape):
     """every memory form of the stencil gives cv2's bytes (band tails, 1-3 segments, odd heights)"""
     import idn
