@@ -7,10 +7,15 @@
 // comparator handles two output bytes.
 //   3x3: sort each 3-row column once (CSE shares it between the three outputs that read it),
 //        then med3(max3(col mins), med3(col medians), min3(col maxes)).
-//   5x5: pruned Batcher selection network over the 25 taps (median_net.hpp, generated and
-//        proven by tools/gen_median_net.py with the 0-1 principle).
+//   5x5: each input row is unpacked once into u16 lanes; per output row every window column is
+//        sorted once (SORT5) and shared by the 5 outputs that read it; the sorted columns'
+//        6-byte halos come from the neighbouring lanes by DPP; two chains of 5 same-channel
+//        outputs (window bytes 8,11,..,20 and 9,12,..,21) each take their medians from 9 sorted
+//        columns with a shared selection network (median_cols.hpp: 276 min/max per chain,
+//        generated and proven by tools/gen_median_cols.py with the 0-1 principle).  ~55 min/max
+//        per output byte pair instead of 202 for the unsorted 25-input network.
 #include "stripe.hpp"
-#include "median_net.hpp"
+#include "median_cols.hpp"
 
 namespace idn {
 
@@ -70,34 +75,59 @@ __device__ __forceinline__ v4u median3_out(const uint32_t (&W0)[8], const uint32
   return r;
 }
 
+// one output row of the 5x5 median from the 5 unpacked rows of its window (oldest first)
 template <int C>
-__device__ __forceinline__ v4u median5_out(const uint32_t (&W0)[8], const uint32_t (&W1)[8],
-                                           const uint32_t (&W2)[8], const uint32_t (&W3)[8],
-                                           const uint32_t (&W4)[8]) {
+__device__ __forceinline__ v4u median5_cols_out(const uint32_t (&U0)[8], const uint32_t (&U1)[8],
+                                                const uint32_t (&U2)[8], const uint32_t (&U3)[8],
+                                                const uint32_t (&U4)[8], bool fix_t0, bool fix_t8) {
   const PkOps op;
-  uint32_t o[4];
+  VWin V[5];  // per rank: u16 window of the sorted columns
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t v[2];
+  for (int j = 0; j < 8; ++j) {
+    uint32_t v[5] = {U0[j], U1[j], U2[j], U3[j], U4[j]};
+    sort5(v, op);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int P = 4 * k + 8 + e;
-      uint32_t x[25];
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const int b = P + (j - 2) * C;
-        x[0 * 5 + j] = lanes16_at(W0, b);
-        x[1 * 5 + j] = lanes16_at(W1, b);
-        x[2 * 5 + j] = lanes16_at(W2, b);
-        x[3 * 5 + j] = lanes16_at(W3, b);
-        x[4 * 5 + j] = lanes16_at(W4, b);
-      }
-      v[e] = median25<uint32_t>(x, op);
+    for (int r = 0; r < 5; ++r) {
+      if (j < 4) V[r].SE[2 + j] = v[r];
+      else V[r].SO[2 + (j - 4)] = v[r];
     }
-    o[k] = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);
   }
-  v4u r = {o[0], o[1], o[2], o[3]};
-  return r;
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {  // 6-byte halos each side (R*C = 6): two dwords per parity
+    V[r].SE[0] = from_prev_lane(V[r].SE[4]);
+    V[r].SO[0] = from_prev_lane(V[r].SO[4]);
+    V[r].SE[1] = from_prev_lane(V[r].SE[5]);
+    V[r].SO[1] = from_prev_lane(V[r].SO[5]);
+    V[r].SE[6] = from_next_lane(V[r].SE[2]);
+    V[r].SO[6] = from_next_lane(V[r].SO[2]);
+    V[r].SE[7] = from_next_lane(V[r].SE[3]);
+    V[r].SO[7] = from_next_lane(V[r].SO[3]);
+    if (fix_t0) vwin_tail_fix<C, BORDER_REPLICATE>(V[r], 24);
+    if (fix_t8) vwin_tail_fix<C, BORDER_REPLICATE>(V[r], 16);
+  }
+  // chain A: output pairs at window bytes 8+3k (bytes 8+3k, 10+3k); chain B: 9+3k (9+3k, 11+3k)
+  uint32_t xa[9][5], xb[9][5];
+#pragma unroll
+  for (int c = 0; c < 9; ++c) {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      xa[c][r] = V[r].at(2 + 3 * c);
+      xb[c][r] = V[r].at(3 + 3 * c);
+    }
+  }
+  uint32_t A[5], B[5];
+  median25_chain5(xa, A, op);
+  median25_chain5(xb, B, op);
+  // each u16 lane holds one output byte in its low byte (b0 = lo lane, b2 = hi lane)
+  //   bytes  8..11 = A0.lo B0.lo A0.hi B0.hi      12..15 = B1.lo A1.hi B1.hi B2.lo
+  //   bytes 16..19 = A2.hi A3.lo B3.lo A3.hi      20..23 = A4.lo B4.lo A4.hi B4.hi
+  const uint32_t o0 = __builtin_amdgcn_perm(B[0], A[0], 0x06020400u);
+  const uint32_t t1 = __builtin_amdgcn_perm(A[1], B[1], 0x0C020600u);  // B1.lo A1.hi B1.hi -
+  const uint32_t o1 = __builtin_amdgcn_perm(B[2], t1, 0x04020100u);
+  const uint32_t t2 = __builtin_amdgcn_perm(A[3], A[2], 0x0C060402u);  // A2.hi A3.lo A3.hi -
+  const uint32_t o2 = __builtin_amdgcn_perm(B[3], t2, 0x02040100u);
+  const uint32_t o3 = __builtin_amdgcn_perm(B[4], A[4], 0x06020400u);
+  return v4u{o0, o1, o2, o3};
 }
 
 template <int C, int K, int NT>
@@ -134,7 +164,7 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
   v4u Lq[PF];
 #pragma unroll
   for (int i = 0; i < PF; ++i) Lq[i] = load_row(i);
-  uint32_t Wr[K][8];
+  uint32_t Wr[K][8];  // K == 3: raw row windows; K == 5: unpacked u16 rows
 
   for (int gi = 0; gi < ngroups; ++gi) {
 #pragma unroll
@@ -142,15 +172,25 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
       const int r = gi * U + u;
       const v4u Lv = Lq[u % PF];
       Lq[u % PF] = load_row(r + PF);
-      build_window<C, BORDER_REPLICATE>(Lv, g.lead, g.fix_t0, g.fix_t8, Wr[u % K]);
+      if constexpr (K == 3) {
+        build_window<C, BORDER_REPLICATE>(Lv, g.lead, g.fix_t0, g.fix_t8, Wr[u % K]);
+      } else {
+        v4u Lx = Lv;
+        if (g.lead) {  // chunk = row bytes -8..7: rebuild the replicated 8 bytes
+          const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
+          Lx = v4u{lead_fix<C, BORDER_REPLICATE>(L, -8), lead_fix<C, BORDER_REPLICATE>(L, -4),
+                   L[0], L[1]};
+        }
+        unpack_row(Lx, Wr[u % K]);
+      }
       const int y = y0 + r - 2 * R;
       if (r >= 2 * R && y < y1) {
         v4u o;
         if constexpr (K == 3) {
           o = median3_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[u % K]);
         } else {
-          o = median5_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[(u + 3) % K],
-                             Wr[(u + 4) % K], Wr[u % K]);
+          o = median5_cols_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[(u + 3) % K],
+                                  Wr[(u + 4) % K], Wr[u % K], g.fix_t0, g.fix_t8);
         }
         stripe_store<NT>(o, rd, (uint32_t)y * row_stride + (uint32_t)g.q, g.kind);
       }

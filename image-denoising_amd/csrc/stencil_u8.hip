@@ -51,64 +51,6 @@ __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t k, uint32_t c) {
   return __umul24(a, k) + c;
 }
 
-// u16 window of vertical sums: SE[m] = window bytes (4m, 4m+2), SO[m] = (4m+1, 4m+3);
-// window byte 0 = chunk byte -8.
-struct VWin {
-  uint32_t SE[8], SO[8];
-  __device__ __forceinline__ uint32_t at(int b) const {  // (b, b+2) as a u16 pair
-    const int m = b >> 2;
-    switch (b & 3) {
-      case 0: return SE[m];
-      case 1: return SO[m];
-      case 2: return __builtin_amdgcn_alignbyte(SE[m + 1], SE[m], 2);
-      default: return __builtin_amdgcn_alignbyte(SO[m + 1], SO[m], 2);
-    }
-  }
-  // register and half holding window byte b
-  __device__ __forceinline__ uint32_t reg(int b) const { return (b & 1) ? SO[b >> 2] : SE[b >> 2]; }
-};
-// (a.half[ha], b.half[hb]) -> one u16 pair, one v_perm_b32
-__device__ __forceinline__ uint32_t pick16(uint32_t a, int ha, uint32_t b, int hb) {
-  const uint32_t sel = (uint32_t)(2 * ha) | (uint32_t)(2 * ha + 1) << 8 |
-                       (uint32_t)(4 + 2 * hb) << 16 | (uint32_t)(5 + 2 * hb) << 24;
-  return __builtin_amdgcn_perm(b, a, sel);
-}
-// rebuild window bytes [base, base+8) past the row end (row end = window byte `base`) by
-// BORDER_REFLECT_101 from the bytes before it
-template <int C>
-__device__ __forceinline__ void vwin_tail_fix(VWin& V, int base) {
-  uint32_t nE[2], nO[2];
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-      int src[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int k = 4 * m + par + 2 * t;  // window byte base + k
-        src[t] = base - 2 * C - (k / C) * C + (k % C);
-      }
-      const uint32_t r = pick16(V.reg(src[0]), (src[0] >> 1) & 1, V.reg(src[1]), (src[1] >> 1) & 1);
-      (par ? nO : nE)[m] = r;
-    }
-  }
-  const int mb = base >> 2;
-  V.SE[mb] = nE[0];
-  V.SO[mb] = nO[0];
-  V.SE[mb + 1] = nE[1];
-  V.SO[mb + 1] = nO[1];
-}
-
-// one input row -> 8 u16x2 dwords: [0..3] even bytes of chunk dwords 0..3, [4..7] odd bytes
-__device__ __forceinline__ void unpack_row(const v4u& x, uint32_t (&U)[8]) {
-  const uint32_t d[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    U[j] = d[j] & 0x00FF00FFu;
-    U[4 + j] = __builtin_amdgcn_perm(0u, d[j], 0x0C030C01u);
-  }
-}
-
 // vertical taps over ring rows r0..r(K-1) (oldest first); raw u16 lanes <= 255
 template <int OP>
 __device__ __forceinline__ uint32_t vtap(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
