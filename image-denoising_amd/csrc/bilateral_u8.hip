@@ -31,6 +31,7 @@ constexpr int BL_MAXR = 8;  // max radius supported (d <= 17)
 struct BilateralTaps {
   double gcc;                                       // -0.5 / sigma_color^2
   float sw[(2 * BL_MAXR + 1) * (2 * BL_MAXR + 1)];  // space weight at (i+R)*(2R+1)+(j+R)
+  float swq[BL_MAXR * BL_MAXR + 1];                 // space weight by r^2 = i^2 + j^2
 };
 constexpr int BL_LUT = 3 * 255 + 1;
 
@@ -117,6 +118,137 @@ __global__ __launch_bounds__(256) void bilateral_u8_kernel(const uint8_t* __rest
   }
 }
 
+// ---- C = 3, radius <= 5: pre-multiplied per-radius weight tables ---------------------------------
+// OpenCV's weight is float(space_weight[k] * color_weight[dist]); the space weight depends only on
+// r^2 = i^2 + j^2, so the workgroup stores one table per distinct r^2 with the products already
+// formed (the same float multiply, so the same bits): a tap is v_sad_u8 + one shift + one LDS read
+// + two packed FMAs.  Each thread owns 4 output rows of one column and walks the (4 + 2R) x (2R+1)
+// input pixels of their union once: every pixel is read from LDS and converted to float once and
+// feeds each of the (up to 4) outputs it is a tap of.
+template <int R>
+struct Rsq {  // the distinct r^2 <= R^2 that are taps: table slot of each r^2, r^2 of each slot
+  int n = 0;
+  int slot[R * R + 1] = {};
+  int q[R * R + 1] = {};
+  constexpr Rsq() {
+    for (int v = 0; v <= R * R; ++v) slot[v] = -1;
+    for (int v = 0; v <= R * R; ++v)
+      for (int i = 0; i <= R; ++i)
+        for (int j = 0; j <= R; ++j)
+          if (i * i + j * j == v && slot[v] < 0) {
+            q[n] = v;
+            slot[v] = n++;
+          }
+  }
+};
+
+template <int R, int RPT>
+__global__ __launch_bounds__(256) void bilateral_u8_pre_kernel(const uint8_t* __restrict__ src,
+                                                               uint8_t* __restrict__ dst, int h,
+                                                               int w, int64_t row_stride,
+                                                               int tiles_x, int tiles_y,
+                                                               int ntiles, BilateralTaps taps) {
+  constexpr int LW = BL_TW + 2 * R;
+  constexpr int TH = 4 * RPT;  // tile height: 4 waves x RPT rows
+  constexpr int LH = TH + 2 * R;
+  constexpr Rsq<R> RS;
+  __shared__ uint32_t tile[LH * LW];
+  __shared__ float cw[BL_LUT];
+  __shared__ float wt[RS.n * BL_LUT];
+
+  // the weight tables, once per (persistent) workgroup
+  for (int i = threadIdx.x; i < BL_LUT; i += 256) cw[i] = (float)exp((double)(i * i) * taps.gcc);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < RS.n; ++k) {
+    const float sw = taps.swq[RS.q[k]];
+    for (int i = threadIdx.x; i < BL_LUT; i += 256)
+      wt[k * BL_LUT + i] = sw * cw[i];  // OpenCV: space_weight[k] * color_weight[dist]
+  }
+
+  const int col = threadIdx.x & 63;
+  const int ly0 = (threadIdx.x >> 6) * RPT;  // first of the thread's RPT output rows
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tx = t % tiles_x;
+    const int ty = (t / tiles_x) % tiles_y;
+    const int img = t / (tiles_x * tiles_y);
+    const uint8_t* s = src + (int64_t)img * h * row_stride;
+    uint8_t* d = dst + (int64_t)img * h * row_stride;
+    const int x0 = tx * BL_TW, y0 = ty * TH;
+    __syncthreads();  // the previous tile is consumed (and the tables are built)
+    for (int i = threadIdx.x; i < LH * LW; i += 256) {
+      const int ly = i / LW, lx = i % LW;
+      tile[i] = load_px<3>(s, row_stride, h, w, y0 + ly - R, x0 + lx - R);
+    }
+    __syncthreads();
+
+    const int x = x0 + col;
+    if (x >= w) continue;
+    uint32_t p0[RPT];
+#pragma unroll
+    for (int o = 0; o < RPT; ++o) p0[o] = tile[(ly0 + o + R) * LW + col + R];
+    f32x2 acc_bg[RPT], acc_rw[RPT];
+#pragma unroll
+    for (int o = 0; o < RPT; ++o) acc_bg[o] = acc_rw[o] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int dy = -R; dy < RPT + R; ++dy) {
+#pragma unroll
+      for (int j = -R; j <= R; ++j) {
+        const uint32_t p = tile[(ly0 + R + dy) * LW + col + R + j];
+        const f32x2 bg = {(float)(p & 0xFFu), (float)((p >> 8) & 0xFFu)};  // v_cvt_f32_ubyte0/1
+        const f32x2 r1 = {(float)((p >> 16) & 0xFFu), 1.f};
+#pragma unroll
+        for (int o = 0; o < RPT; ++o) {
+          const int i = dy - o;
+          if (i < -R || i > R || i * i + j * j > R * R) continue;  // not a tap of output o
+          const uint32_t dist = __builtin_amdgcn_sad_u8(p, p0[o], 0u);
+          const float wv = wt[RS.slot[i * i + j * j] * BL_LUT + dist];
+          const f32x2 w2 = {wv, wv};
+          acc_bg[o] = __builtin_elementwise_fma(bg, w2, acc_bg[o]);
+          acc_rw[o] = __builtin_elementwise_fma(r1, w2, acc_rw[o]);
+        }
+      }
+      // pin the accumulators at every input row: without it LLVM sinks all the FMA pairs below
+      // the walk and keeps every weight and converted pixel live (VGPRs exhausted)
+#pragma unroll
+      for (int o = 0; o < RPT; ++o) asm volatile("" : "+v"(acc_bg[o]), "+v"(acc_rw[o]));
+    }
+    auto cvt = [](float v) -> uint8_t {  // cvRound (half to even) + saturate
+      const float r = __builtin_rintf(v);
+      return (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+    };
+#pragma unroll
+    for (int o = 0; o < RPT; ++o) {
+      const int y = y0 + ly0 + o;
+      if (y >= h) break;
+      const float inv = 1.f / acc_rw[o].y;
+      uint8_t* op = d + (int64_t)y * row_stride + (int64_t)x * 3;
+      op[0] = cvt(acc_bg[o].x * inv);
+      op[1] = cvt(acc_bg[o].y * inv);
+      op[2] = cvt(acc_rw[o].x * inv);
+    }
+  }
+}
+
+template <int R, int RPT>
+static void launch_bl_pre_rpt(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
+                              const BilateralTaps& taps, hipStream_t st) {
+  const int tiles_x = (w + BL_TW - 1) / BL_TW, tiles_y = (h + 4 * RPT - 1) / (4 * RPT);
+  const int64_t ntiles = (int64_t)n * tiles_x * tiles_y;
+  // persistent workgroups: the weight tables are built once per workgroup
+  const int64_t grid = ntiles < 2048 ? ntiles : 2048;
+  hipLaunchKernelGGL((bilateral_u8_pre_kernel<R, RPT>), dim3((unsigned)grid), dim3(256), 0, st, src,
+                     dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
+}
+
+// RPT output rows per thread: each converted pixel feeds up to RPT outputs (RPT = 8 measured
+// worse: the compiler spills the 16 accumulators around the pins)
+template <int R>
+static void launch_bl_pre(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
+                          const BilateralTaps& taps, hipStream_t st) {
+  launch_bl_pre_rpt<R, 4>(src, dst, n, h, w, rs, taps, st);
+}
+
 template <int C, int R>
 static void launch_bl(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
                       const BilateralTaps& taps, hipStream_t st) {
@@ -154,7 +286,9 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
       const double r = sqrt((double)i * i + (double)j * j);
       if (r > radius) continue;
       taps.sw[(i + radius) * (2 * radius + 1) + (j + radius)] = (float)exp(r * r * gsc);  // OpenCV's
+      taps.swq[i * i + j * j] = (float)exp(r * r * gsc);
     }
+  const bool pre = env_int("IDN_BILATERAL_PRE", 1) != 0;
   hipStream_t st = as_stream(stream);
 #define IDN_BL(CC)                                                          \
   switch (radius) {                                                         \
@@ -167,7 +301,15 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
     case 7: launch_bl<CC, 7>(src, dst, n, h, w, row_stride, taps, st); break; \
     default: launch_bl<CC, 8>(src, dst, n, h, w, row_stride, taps, st); break; \
   }
-  if (c == 3) {
+  if (c == 3 && pre && radius <= 5) {
+    switch (radius) {
+      case 1: launch_bl_pre<1>(src, dst, n, h, w, row_stride, taps, st); break;
+      case 2: launch_bl_pre<2>(src, dst, n, h, w, row_stride, taps, st); break;
+      case 3: launch_bl_pre<3>(src, dst, n, h, w, row_stride, taps, st); break;
+      case 4: launch_bl_pre<4>(src, dst, n, h, w, row_stride, taps, st); break;
+      default: launch_bl_pre<5>(src, dst, n, h, w, row_stride, taps, st); break;
+    }
+  } else if (c == 3) {
     IDN_BL(3)
   } else {
     IDN_BL(1)
