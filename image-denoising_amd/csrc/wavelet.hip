@@ -96,7 +96,14 @@ struct WlStats {
   static constexpr int DIAG = 248;  // [248..251) nonzero count of the finest dd per channel
   static constexpr int MN64 = 200;  // [200..203) fp64 channel min (u64 bits), [203..206) max
   static constexpr int MX64 = 203;
+  // fused Haar path (L <= 3): [100..196) the finest dd's exponent histogram, u32[3][64]
+  static constexpr int HIST = 100;
 };
+constexpr int WL_EBINS = 64;  // exponent bins of |dd|: bin = clamp(exponent - (1023 - 61), 0, 63)
+__device__ __forceinline__ int wl_ebin(unsigned long long key) {
+  const int e = (int)(key >> 52) - (1023 - 61);
+  return e < 0 ? 0 : (e > WL_EBINS - 1 ? WL_EBINS - 1 : e);
+}
 
 inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   WlLayout Lt;
@@ -126,6 +133,12 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
     Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + 15) / 16);
     Lt.part_tile0[l] = tiles_tot;
     tiles_tot += (size_t)Lt.tiles[l];
+  }
+  if (wv == IDN_WAVELET_DB1 && Lt.L <= 3 && h % (1 << Lt.L) == 0 && w % (1 << Lt.L) == 0) {
+    // the fused Haar path's partials: one per workgroup of 128 threads and level
+    const size_t ns = Lt.L == 3 ? 4 : 1;
+    const size_t nwg = ((size_t)(h >> Lt.L) * (size_t)(w >> Lt.L) * ns + 127) / 128;
+    tiles_tot = std::max(tiles_tot, (size_t)Lt.L * nwg);
   }
   Lt.part_per_img = 9 * tiles_tot;  // [c][b][tile]
   Lt.part_off = Lt.stats_off + (size_t)n * WL_STATS * sizeof(double);
@@ -402,26 +415,61 @@ __device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int w
   for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
   __syncthreads();
   const unsigned long long prefix = rsx.prefix, pmask = rsx.pmask;
-  for (size_t k = threadIdx.x; k < n; k += blockDim.x) {
-    const unsigned long long key = absbits(d[k]);
-    if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+  // 8 loads in flight per thread (a one-load-per-iteration loop is latency-bound)
+  for (size_t k0 = threadIdx.x; k0 < n; k0 += 8 * (size_t)blockDim.x) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t k = k0 + (size_t)u * blockDim.x;
+      v[u] = k < n ? d[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const unsigned long long key = absbits(v[u]);
+      if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+    }
   }
   __syncthreads();
-  __shared__ uint32_t sel_bin, sel_rank;
+  // block-wide scan of the histogram: thread i owns bins [i*per, (i+1)*per); the thread whose
+  // count range holds the rank finds the bin (a serial scan of 2048 LDS bins by one thread costs
+  // ~100k cycles per pass)
+  __shared__ uint32_t sel_bin, sel_rank, wsum[32], tot_s;
+  const int T = blockDim.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int per = (nb + T - 1) / T, b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
+  uint32_t own = 0;
+  for (int b = b0; b < b1; ++b) own += hist[b];
+  uint32_t inc = own;  // inclusive scan within the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    if (total) {
-      uint32_t t = 0;
-      for (int b = 0; b < nb; ++b) t += hist[b];
-      *total = t;
-      rsx.rank = t ? (t - 1) / 2 : 0;  // lower middle rank
-    }
     uint32_t acc = 0;
-    int bin = 0;
-    for (; bin < nb - 1; ++bin) {
-      if (acc + hist[bin] > rsx.rank) break;
-      acc += hist[bin];
+    for (int k = 0; k < (T + 63) / 64; ++k) {
+      const uint32_t t = wsum[k];
+      wsum[k] = acc;
+      acc += t;
     }
-    sel_bin = (uint32_t)bin;
+    tot_s = acc;
+    sel_bin = (uint32_t)(nb - 1);  // fallback: rank beyond the total
+    sel_rank = 0;
+  }
+  __syncthreads();
+  if (total) {
+    if (threadIdx.x == 0) *total = tot_s;
+    rsx.rank = tot_s ? (tot_s - 1) / 2 : 0;  // lower middle rank
+  }
+  const uint32_t excl = wsum[wv] + inc - own;
+  if (own && rsx.rank >= excl && rsx.rank < excl + own) {
+    uint32_t acc = excl;
+    int b = b0;
+    for (; b < b1 - 1; ++b) {
+      if (acc + hist[b] > rsx.rank) break;
+      acc += hist[b];
+    }
+    sel_bin = (uint32_t)b;
     sel_rank = rsx.rank - acc;
   }
   __syncthreads();
@@ -668,6 +716,485 @@ __global__ __launch_bounds__(256) void wl_idwt_final(const wreal* __restrict__ w
   }
 }
 
+// ---- Haar fast path: every level is local to a 2^L x 2^L block ---------------------------------
+// For db1 with h and w divisible by 2^L, pywt's 'symmetric' extension never triggers and level l's
+// coefficients of a 2^L x 2^L block depend on that block alone.  So the whole denoiser runs as
+//   wl_color_minmax -> wl_haar_analyze -> wl_sumsq -> wl_median -> wl_thresh -> wl_haar_synth
+// where wl_haar_analyze reads the image once and writes only the finest dd band (for sigma) and
+// per-workgroup sums of squares of every detail band, and wl_haar_synth reads the image again,
+// recomputes the analysis of its block, thresholds, synthesises all levels, converts back to
+// RGB and stores the U8 / f32 output: no fp64 band ever makes a round trip through HBM except dd1.
+// The arithmetic is op for op the general path's (multiply then add, axis 0 then axis 1; the
+// synthesis sums A, AD, DA, DD in that order), so the coefficients are bitwise the same.
+constexpr int WLH_WG = 128;  // threads per workgroup (wl_layout sizes the partials for it)
+
+// pywt dwt2 of one 2x2 group, rows 2i / 2i+1 (x0j / x1j), columns 2j / 2j+1
+__device__ __forceinline__ void haar2x2(wreal x00, wreal x01, wreal x10, wreal x11, wreal& aa,
+                                        wreal& ad, wreal& da, wreal& dd) {
+  const wreal lo0 = S2 * x10 + S2 * x00, lo1 = S2 * x11 + S2 * x01;    // axis 0 low
+  const wreal hi0 = -S2 * x10 + S2 * x00, hi1 = -S2 * x11 + S2 * x01;  // axis 0 high
+  aa = S2 * lo1 + S2 * lo0;
+  ad = -S2 * lo1 + S2 * lo0;
+  da = S2 * hi1 + S2 * hi0;
+  dd = -S2 * hi1 + S2 * hi0;
+}
+// pywt idwt2 of one coefficient quadruple to output (r, s) of its 2x2 group (details thresholded)
+__device__ __forceinline__ wreal ihaar(wreal A, wreal AD, wreal DA, wreal DD, int r, int s) {
+  const wreal fd = r ? -S2 : S2, gd = s ? -S2 : S2;
+  wreal acc = 0;
+  acc = acc + S2 * S2 * A;
+  acc = acc + S2 * gd * AD;
+  acc = acc + fd * S2 * DA;
+  acc = acc + fd * gd * DD;
+  return acc;
+}
+
+// one row of 4 pixels (x .. x+3) of image img, normalised YCbCr per channel: v[s][c]
+__device__ __forceinline__ void haar_row4(const uint8_t* __restrict__ src,
+                                          const double* __restrict__ in64, int img, int h, int w,
+                                          int64_t row_stride, int y, int x, const wreal (&mn)[3],
+                                          const wreal (&inv)[3], wreal (&v)[4][3]) {
+  double px[4][3];
+  if (in64) {
+    const double* p = in64 + (((int64_t)img * h + y) * w + x) * 3;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) px[k / 3][k % 3] = p[k];
+  } else {  // 12 bytes, 4-byte aligned (checked on the host): three dword loads
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(src + (int64_t)img * h * row_stride +
+                                                          (int64_t)y * row_stride + (int64_t)x * 3);
+    const uint32_t d[3] = {p[0], p[1], p[2]};
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+      px[k / 3][k % 3] = (double)((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[s][c] = (ycbcr_c(px[s], c) - mn[c]) / inv[c];
+}
+
+// Work split: one thread per 4x4 sub-block (levels 1 and 2 in registers); for L = 3 the four
+// threads of an 8x8 block are consecutive lanes and level 3 runs on their level-2 approximations
+// gathered by shuffles (redundantly in all four; only sub-block 0 counts its squares).
+template <int L>
+struct HaarSplit {
+  static constexpr int B = 1 << L;          // block side
+  static constexpr int SB = B < 4 ? B : 4;  // sub-block side per thread
+  static constexpr int NS = (B / SB) * (B / SB);
+  static constexpr int QS = SB / 2;         // level-1 groups per sub-block side
+};
+
+// level 1 of one thread's sub-block, all channels: a1[c][k] approximations, d1[c][band][k] details
+template <int L>
+__device__ __forceinline__ void haar_sub_analysis(
+    const uint8_t* __restrict__ src, const double* __restrict__ in64, int img, int h, int w,
+    int64_t row_stride, int y0, int x0, const wreal (&mn)[3], const wreal (&inv)[3],
+    wreal (&a1)[3][HaarSplit<L>::QS * HaarSplit<L>::QS],
+    wreal (&d1)[3][3][HaarSplit<L>::QS * HaarSplit<L>::QS]) {
+  using HS = HaarSplit<L>;
+#pragma unroll
+  for (int qy = 0; qy < HS::QS; ++qy) {
+    wreal r0[4][3], r1[4][3];
+    if constexpr (HS::SB == 4) {
+      haar_row4(src, in64, img, h, w, row_stride, y0 + 2 * qy, x0, mn, inv, r0);
+      haar_row4(src, in64, img, h, w, row_stride, y0 + 2 * qy + 1, x0, mn, inv, r1);
+    } else {  // 2x2 sub-block (L = 1): two pixels per row
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        double p0[3], p1[3];
+        load_rgb64(src, in64, img, h, w, row_stride, y0 + 2 * qy, x0 + s, p0);
+        load_rgb64(src, in64, img, h, w, row_stride, y0 + 2 * qy + 1, x0 + s, p1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          r0[s][c] = (ycbcr_c(p0, c) - mn[c]) / inv[c];
+          r1[s][c] = (ycbcr_c(p1, c) - mn[c]) / inv[c];
+        }
+      }
+    }
+#pragma unroll
+    for (int qx = 0; qx < HS::QS; ++qx)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int k = qy * HS::QS + qx;
+        haar2x2(r0[2 * qx][c], r0[2 * qx + 1][c], r1[2 * qx][c], r1[2 * qx + 1][c], a1[c][k],
+                d1[c][0][k], d1[c][1][k], d1[c][2][k]);
+      }
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(WLH_WG) void wl_haar_analyze(
+    const uint8_t* __restrict__ src, const double* __restrict__ in64, int h, int w,
+    int64_t row_stride, wreal* __restrict__ ws, size_t img_floats, size_t dd_off,
+    const double* __restrict__ stats, double* __restrict__ part, size_t part_per_img) {
+  using HS = HaarSplit<L>;
+  constexpr int B = HS::B, QS = HS::QS;
+  const int img = blockIdx.y;
+  const int nbx = w / B, nblk = nbx * (h / B);
+  const int tid = blockIdx.x * WLH_WG + threadIdx.x;
+  const int blk = tid / HS::NS, sub = tid % HS::NS;
+  const bool act = blk < nblk;  // uniform over each block's NS consecutive lanes
+  const double* st = stats + (size_t)img * WL_STATS;
+  wreal mn[3], inv[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    wreal mx;
+    wl_minmax64(st, c, mn[c], mx);
+    inv[c] = mx - mn[c];
+  }
+  double sq[3][L][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) sq[c][l][b] = 0.0;
+  wreal a2[3] = {0, 0, 0};
+  // exponent histogram of the nonzero |dd1| (sigma's first radix digit), per workgroup in LDS,
+  // 8 copies by lane & 7 (|dd| takes few exponents: one copy would serialise the LDS atomics)
+  __shared__ uint32_t ehist[8][3][WL_EBINS];
+  for (int k = threadIdx.x; k < 8 * 3 * WL_EBINS; k += WLH_WG) (&ehist[0][0][0])[k] = 0u;
+  __syncthreads();
+  if (act) {
+    const int by = blk / nbx, bx = blk - by * nbx;
+    const int sy = sub / (B / HS::SB), sx = sub % (B / HS::SB);
+    const int y0 = by * B + sy * HS::SB, x0 = bx * B + sx * HS::SB;
+    wreal a1[3][QS * QS], d1[3][3][QS * QS];
+    haar_sub_analysis<L>(src, in64, img, h, w, row_stride, y0, x0, mn, inv, a1, d1);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int k = 0; k < QS * QS; ++k) {
+        const unsigned long long key = absbits(d1[c][2][k]);
+        if (key) atomicAdd(&ehist[threadIdx.x & 7][c][wl_ebin(key)], 1u);
+      }
+    const size_t W1 = (size_t)(w / 2), bsz = (size_t)(h / 2) * W1;
+    wreal* ddp = ws + img * img_floats + dd_off + 3 * bsz;  // channel c: + c * 4 * bsz
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+      for (int k = 0; k < QS * QS; ++k) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) sq[c][0][b] += d1[c][b][k] * d1[c][b][k];
+        ddp[(size_t)c * 4 * bsz + (size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] = d1[c][2][k];
+      }
+      if constexpr (L >= 2) {  // level 2 on the thread's 2x2 level-1 approximations
+        wreal ad, da, dd;
+        haar2x2(a1[c][0], a1[c][1], a1[c][2], a1[c][3], a2[c], ad, da, dd);
+        sq[c][1][0] += ad * ad;
+        sq[c][1][1] += da * da;
+        sq[c][1][2] += dd * dd;
+      }
+    }
+  }
+  if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
+    const int base = (threadIdx.x & 63) & ~3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const wreal x00 = __shfl(a2[c], base), x01 = __shfl(a2[c], base + 1);
+      const wreal x10 = __shfl(a2[c], base + 2), x11 = __shfl(a2[c], base + 3);
+      wreal aa, ad, da, dd;
+      haar2x2(x00, x01, x10, x11, aa, ad, da, dd);
+      if (act && sub == 0) {
+        sq[c][2][0] += ad * ad;
+        sq[c][2][1] += da * da;
+        sq[c][2][2] += dd * dd;
+      }
+    }
+  }
+  // workgroup sums of squares in a fixed order (wave shuffles, then the two waves)
+  __shared__ double red[3 * L * 3][WLH_WG / 64];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        double v = sq[c][l][b];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0) red[(c * L + l) * 3 + b][threadIdx.x >> 6] = v;
+      }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 3 * WL_EBINS; k += WLH_WG) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int cp = 0; cp < 8; ++cp) v += (&ehist[cp][0][0])[k];
+    if (v) atomicAdd(reinterpret_cast<uint32_t*>(const_cast<double*>(st) + WlStats::HIST) + k, v);
+  }
+  if (threadIdx.x < 3 * L * 3) {
+    const int k = threadIdx.x, b = k % 3, l = (k / 3) % L, c = k / (3 * L);
+    double t = red[k][0];
+#pragma unroll
+    for (int wv = 1; wv < WLH_WG / 64; ++wv) t += red[k][wv];
+    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + (size_t)l * gridDim.x +
+         blockIdx.x] = t;
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
+    const uint8_t* __restrict__ src, const double* __restrict__ in64, int h, int w,
+    int64_t row_stride, const double* __restrict__ stats, uint8_t* __restrict__ out_u8,
+    float* __restrict__ out_f32) {
+  using HS = HaarSplit<L>;
+  constexpr int B = HS::B, QS = HS::QS;
+  const int img = blockIdx.y;
+  const int nbx = w / B, nblk = nbx * (h / B);
+  const int tid = blockIdx.x * WLH_WG + threadIdx.x;
+  const int blk = tid / HS::NS, sub = tid % HS::NS;
+  const bool act = blk < nblk;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const bool bad = st[WlStats::FLAG] != 0.0;
+  wreal mn[3], inv[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    wreal mx;
+    wl_minmax64(st, c, mn[c], mx);
+    inv[c] = mx - mn[c];
+  }
+  auto thr = [&](int c, int l, int b) { return st[WlStats::thr(c, l, b, L)]; };
+  int y0 = 0, x0 = 0;
+  if (act) {
+    const int by = blk / nbx, bx = blk - by * nbx;
+    const int sy = sub / (B / HS::SB), sx = sub % (B / HS::SB);
+    y0 = by * B + sy * HS::SB;
+    x0 = bx * B + sx * HS::SB;
+  }
+  wreal a1[3][QS * QS], d1[3][3][QS * QS];
+  if (act) haar_sub_analysis<L>(src, in64, img, h, w, row_stride, y0, x0, mn, inv, a1, d1);
+  if constexpr (L >= 2) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      wreal a2 = 0, ad2 = 0, da2 = 0, dd2 = 0;
+      if (act) haar2x2(a1[c][0], a1[c][1], a1[c][2], a1[c][3], a2, ad2, da2, dd2);
+      if constexpr (L == 3) {  // level 3 across the block's 4 lanes, synthesised back to a2
+        const int base = (threadIdx.x & 63) & ~3;
+        const wreal x00 = __shfl(a2, base), x01 = __shfl(a2, base + 1);
+        const wreal x10 = __shfl(a2, base + 2), x11 = __shfl(a2, base + 3);
+        wreal aa, ad, da, dd;
+        haar2x2(x00, x01, x10, x11, aa, ad, da, dd);
+        a2 = ihaar(aa, soft(ad, thr(c, 2, 0)), soft(da, thr(c, 2, 1)), soft(dd, thr(c, 2, 2)),
+                   sub >> 1, sub & 1);
+      }
+      const wreal AD = soft(ad2, thr(c, 1, 0)), DA = soft(da2, thr(c, 1, 1));
+      const wreal DD = soft(dd2, thr(c, 1, 2));
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) a1[c][r * 2 + s] = ihaar(a2, AD, DA, DD, r, s);
+    }
+  }
+  if (!act) return;
+  // level 1 per 2x2 group with the pixels' own details, colour, casts
+#pragma unroll
+  for (int k = 0; k < QS * QS; ++k) {
+    const int qy = k / QS, qx = k % QS;
+    wreal o[2][2][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const wreal A = a1[c][k];
+      const wreal AD = soft(d1[c][0][k], thr(c, 0, 0)), DA = soft(d1[c][1][k], thr(c, 0, 1));
+      const wreal DD = soft(d1[c][2][k], thr(c, 0, 2));
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          // inner denoise_wavelet clip (0.14.2), then * (max - min) + min
+          const double vv = fmin(fmax((double)ihaar(A, AD, DA, DD, r, s), 0.0), 1.0);
+          o[r][s][c] = vv * inv[c] + mn[c];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const double Y = o[r][s][0] - 16.0, Cb = o[r][s][1] - 128.0, Cr = o[r][s][2] - 128.0;
+        double o3[3];
+        o3[0] = dot3(Y, Cb, Cr, 0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937);
+        o3[1] = dot3(Y, Cb, Cr, 0.004566210045662101, -0.0015363236860449021, -0.003188110949655707);
+        o3[2] = dot3(Y, Cb, Cr, 0.004566210045662101, 0.007910716233554741, 1.1977497040511743e-08);
+        const int y = y0 + 2 * qy + r, x = x0 + 2 * qx + s;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          double vv = fmin(fmax(o3[c], 0.0), 1.0);
+          if (bad) vv = 0.0;
+          if (out_u8)
+            out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3 + c] =
+                (uint8_t)(int)(255.0 * vv);
+          if (out_f32) out_f32[(((int64_t)img * h + y) * w + x) * 3 + c] = (float)vv;
+        }
+      }
+  }
+}
+
+// sigma for the fused path: the exponent histogram (built by wl_haar_analyze) locates the bin
+// holding the lower middle rank; one pass over the stored dd1 compacts that bin's keys into
+// scratch and takes the smallest key of the next nonempty bin (the upper middle rank may live
+// there); the remaining digits are selected on the compacted keys.
+__global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, size_t img_floats,
+                                                       double* __restrict__ stats, WlLayout Lt) {
+  const int img = blockIdx.x / 3, c = blockIdx.x % 3;
+  const size_t bsz = (size_t)Lt.H[1] * Lt.W[1];
+  const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
+  double* scratch = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;  // unused input-plane slot
+  double* st = stats + (size_t)img * WL_STATS;
+  const uint32_t* eh = reinterpret_cast<const uint32_t*>(st + WlStats::HIST) + c * WL_EBINS;
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t m_s, le_s, total_s, bin_s, rank_s, next_s;
+  __shared__ unsigned long long nmin_s, gt_s;
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int b = 0; b < WL_EBINS; ++b) t += eh[b];
+    total_s = t;
+    const uint32_t klo = t ? (t - 1) / 2 : 0;
+    uint32_t acc = 0;
+    int b = 0;
+    for (; b < WL_EBINS - 1; ++b) {
+      if (acc + eh[b] > klo) break;
+      acc += eh[b];
+    }
+    bin_s = (uint32_t)b;
+    rank_s = klo - acc;
+    int nb = b + 1;
+    while (nb < WL_EBINS && eh[nb] == 0) ++nb;
+    next_s = (uint32_t)nb;  // WL_EBINS: none
+    m_s = 0;
+    le_s = 0;
+    nmin_s = ~0ull;
+    gt_s = ~0ull;
+  }
+  __syncthreads();
+  const uint32_t total = total_s;
+  double med;
+  if (total == 0) {
+    med = NAN;  // np.median of an empty selection
+  } else {
+    const uint32_t klo = (total - 1) / 2, khi = total / 2;
+    const int bsel = (int)bin_s, bnext = (int)next_s;
+    const int lane = threadIdx.x & 63;
+    unsigned long long nmin = ~0ull;
+    for (size_t k0 = threadIdx.x; k0 < bsz; k0 += 8 * 1024) {
+      double vv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // 8 loads in flight per thread
+        const size_t k = k0 + (size_t)u * 1024;
+        vv[u] = k < bsz ? d[k] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double v = vv[u];
+        const unsigned long long key = absbits(v);
+        const int b = key ? wl_ebin(key) : -1;
+        if (b == bnext) nmin = key < nmin ? key : nmin;
+        const bool hit = b == bsel;
+        const unsigned long long m = __ballot(hit);
+        if (m) {
+          uint32_t base = 0;
+          const int leader = __ffsll((long long)m) - 1;
+          if (lane == leader) base = atomicAdd(&m_s, (uint32_t)__popcll(m));
+          base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+          if (hit) scratch[base + __popcll(m & ((1ull << lane) - 1))] = fabs(v);
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long on = (unsigned long long)__shfl_xor((long long)nmin, o);
+      nmin = on < nmin ? on : nmin;
+    }
+    if (lane == 0) atomicMin(&nmin_s, nmin);
+    __syncthreads();
+    const size_t mcnt = m_s;
+    RadixState rsx{0ull, 0ull, rank_s};
+    if (bsel > 0 && bsel < WL_EBINS - 1) {  // an unclamped bin is one exponent: digit known
+      rsx.prefix = (unsigned long long)(bsel + (1023 - 61)) << 52;
+      rsx.pmask = 0x7FFull << 52;
+    } else {
+      radix_pass(scratch, mcnt, 52, 11, rsx, hist, nullptr);
+    }
+    radix_pass(scratch, mcnt, 41, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 30, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 19, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 8, 11, rsx, hist, nullptr);
+    radix_pass(scratch, mcnt, 0, 8, rsx, hist, nullptr);
+    const unsigned long long lo_key = rsx.prefix;
+    const double vlo = __longlong_as_double((long long)lo_key);
+    double vhi = vlo;
+    if (khi != klo) {
+      if (rank_s + 1 < mcnt) {  // the upper middle rank is in the same bin
+        uint32_t le = 0;
+        unsigned long long gt = ~0ull;
+        for (size_t k = threadIdx.x; k < mcnt; k += 1024) {
+          const unsigned long long key = absbits(scratch[k]);
+          if (key <= lo_key) ++le;
+          else gt = key < gt ? key : gt;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          le += __shfl_xor(le, o);
+          const unsigned long long og = (unsigned long long)__shfl_xor((long long)gt, o);
+          gt = og < gt ? og : gt;
+        }
+        if (lane == 0) {
+          atomicAdd(&le_s, le);
+          atomicMin(&gt_s, gt);
+        }
+        __syncthreads();
+        if (le_s <= rank_s + 1) vhi = __longlong_as_double((long long)gt_s);
+      } else {  // it is the smallest key of the next nonempty bin
+        vhi = __longlong_as_double((long long)nmin_s);
+      }
+    }
+    med = (vlo + vhi) / 2.0;  // np.median: mean of the two middle values
+  }
+  if (threadIdx.x == 0) {
+    st[WlStats::median(c, Lt.L)] = med;
+    st[WlStats::DIAG + c] = (double)total;  // diagnostics
+  }
+}
+
+template <int L>
+static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8, float* out_f32,
+                        const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st) {
+  wreal* wsf = (wreal*)ws;
+  double* stats = (double*)((char*)ws + Lt.stats_off);
+  double* part = (double*)((char*)ws + Lt.part_off);
+  const int n = Lt.n;
+  const int nthr = (Lt.h >> L) * (Lt.w >> L) * HaarSplit<L>::NS;
+  const int nwg = (nthr + WLH_WG - 1) / WLH_WG;
+  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n);
+  {
+    const int64_t np = (int64_t)Lt.h * Lt.w;
+    int gx = (int)((np + 255) / 256);
+    if (gx > 256) gx = 256;
+    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+                       row_stride, stats);
+  }
+  hipLaunchKernelGGL((wl_haar_analyze<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
+                     Lt.w, row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
+                     Lt.part_per_img);
+  WlLayout Ls = Lt;  // wl_sumsq view of the fused partials: nwg per level, levels back to back
+  for (int l = 1; l <= L; ++l) {
+    Ls.tiles[l] = nwg;
+    Ls.part_tile0[l] = (size_t)(l - 1) * nwg;
+  }
+  hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * L * 3), dim3(256), 0, st, stats, part, Ls);
+  hipLaunchKernelGGL(wl_haar_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
+  hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  hipLaunchKernelGGL((wl_haar_synth<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
+                     Lt.w, row_stride, stats, out_u8, out_f32);
+}
+
+// the fused path applies: db1, 1 <= L <= 3, both sides divisible by 2^L, room for its partials
+static bool wl_haar_ok(int wavelet, const WlLayout& Lt, const uint8_t* src, int64_t row_stride) {
+  if (wavelet != IDN_WAVELET_DB1 || Lt.L < 1 || Lt.L > 3 || env_int("IDN_WAVELET_FUSED", 1) == 0)
+    return false;
+  const int B = 1 << Lt.L;
+  if (Lt.h % B || Lt.w % B) return false;
+  if (src && (((uintptr_t)src & 3) || (row_stride & 3))) return false;  // dword row loads
+  const int64_t ns = Lt.L == 3 ? 4 : 1;
+  const int64_t nwg = ((int64_t)(Lt.h / B) * (Lt.w / B) * ns + WLH_WG - 1) / WLH_WG;
+  return (int64_t)Lt.L * nwg <= (int64_t)(Lt.part_per_img / 9);
+}
+
 template <int WV>
 static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float* out_f32,
                   const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st) {
@@ -744,8 +1271,15 @@ extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, 
     return set_error(IDN_EWORKSPACE, "idn_wavelet_denoise_u8: needs %zu workspace bytes (got %zu)",
                      Lt.bytes, ws_bytes);
   hipStream_t st = as_stream(stream);
-  if (wavelet == IDN_WAVELET_DB1) wl_run<IDN_WAVELET_DB1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
-  else wl_run<IDN_WAVELET_BIOR15>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+  if (wl_haar_ok(wavelet, Lt, src, row_stride)) {
+    if (Lt.L == 1) wl_run_haar<1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+    else if (Lt.L == 2) wl_run_haar<2>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+    else wl_run_haar<3>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+  } else if (wavelet == IDN_WAVELET_DB1) {
+    wl_run<IDN_WAVELET_DB1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+  } else {
+    wl_run<IDN_WAVELET_BIOR15>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+  }
   IDN_CHECK_LAUNCH("idn_wavelet_denoise_u8");
   return IDN_OK;
 }

@@ -93,3 +93,24 @@ def test_wavelet_odd_shapes(dev, shape):
         ref = oracle.wavelet.denoise_wavelet(img, wavelet, levels)
         assert np.abs(f - ref).max() <= TOL
         check_u8(u8, ref, oracle.sk.to_u8(255 * ref))
+
+
+@pytest.mark.parametrize("shape,levels", [((120, 200), 3), ((64, 96), 2), ((30, 50), 1),
+                                          ((600, 1000), 3), ((48, 40), None)])
+@pytest.mark.parametrize("f64", [False, True])
+def test_wavelet_haar_fused_matches_general(dev, monkeypatch, shape, levels, f64):
+    """the block-local Haar path (2^L-divisible sizes) agrees with the general multi-pass path:
+    identical coefficients, only the sum-of-squares order differs (thresholds to a few ulps)"""
+    import oracle
+    img = make_img(*shape, 11)
+    if f64:
+        img = np.clip(img / 255.0 + np.random.RandomState(1).normal(0, 0.1, img.shape), 0, 1)
+    u8a, fa = run(img, "db1", levels)
+    monkeypatch.setenv("IDN_WAVELET_FUSED", "0")
+    u8b, fb = run(img, "db1", levels)
+    assert np.abs(fa - fb).max() <= 1e-6
+    d = u8a.astype(int) - u8b.astype(int)
+    assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-4
+    if shape[0] * shape[1] <= 24000:
+        ref = oracle.wavelet.denoise_wavelet(img, "db1", levels)
+        assert np.abs(fa - ref).max() <= TOL
