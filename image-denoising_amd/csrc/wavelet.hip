@@ -96,8 +96,6 @@ struct WlStats {
   static constexpr int DIAG = 248;  // [248..251) nonzero count of the finest dd per channel
   static constexpr int MN64 = 200;  // [200..203) fp64 channel min (u64 bits), [203..206) max
   static constexpr int MX64 = 203;
-  // fused Haar path (L <= 3): [100..196) the finest dd's exponent histogram, u32[3][64]
-  static constexpr int HIST = 100;
 };
 constexpr int WL_EBINS = 64;  // exponent bins of |dd|: bin = clamp(exponent - (1023 - 61), 0, 63)
 __device__ __forceinline__ int wl_ebin(unsigned long long key) {
@@ -216,25 +214,60 @@ __device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn,
   mx = dkey_inv(u64[WlStats::MX64 + c]);
 }
 
-// per-channel min / max of the YCbCr image (fp64 exact, and fp32 bits for diagnostics); the
-// planes themselves are never stored: the level-1 analysis recomputes Y/Cb/Cr while staging
+// per-channel min / max of the YCbCr image (fp64 exact); the planes themselves are never
+// stored: the analysis recomputes Y/Cb/Cr while staging.  Compact u8 rows (row_stride == 3w,
+// dword-aligned) take 4 pixels per thread with three dword loads and no index division.
 __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict__ src,
                                                        const double* __restrict__ in64, int h, int w,
                                                        int64_t row_stride, double* __restrict__ stats) {
   const int img = blockIdx.y;
   const int64_t np = (int64_t)h * w;
   double dmn[3] = {INFINITY, INFINITY, INFINITY}, dmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  // pixel p = y * w + x with 32-bit index math (p < 2^31 per image: checked on the host)
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < (int)np; p += gridDim.x * blockDim.x) {
-    const int y = p / w, x = p - y * w;
-    double v[3];
-    load_rgb64(src, in64, img, h, w, row_stride, y, x, v);
+  auto acc = [&](double v0, double v1, double v2) {
     double yc[3];
-    ycbcr64(v[0], v[1], v[2], yc);
+    ycbcr64(v0, v1, v2, yc);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      dmn[c] = yc[c] < dmn[c] ? yc[c] : dmn[c];  // never NaN: plain selects
-      dmx[c] = yc[c] > dmx[c] ? yc[c] : dmx[c];
+    for (int c = 0; c < 3; ++c) {  // inputs are finite: fmin / fmax are plain selects
+      dmn[c] = fmin(dmn[c], yc[c]);
+      dmx[c] = fmax(dmx[c], yc[c]);
+    }
+  };
+  const bool flat = !in64 && row_stride == (int64_t)w * 3 && (np & 3) == 0 &&
+                    (((uintptr_t)src & 3) == 0);
+  if (flat) {
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src + (int64_t)img * h * row_stride);
+    const int nq = (int)(np >> 2);  // groups of 4 pixels = 3 dwords
+    const int stride = gridDim.x * blockDim.x;
+    for (int q0 = blockIdx.x * blockDim.x + threadIdx.x; q0 < nq; q0 += 4 * stride) {
+      uint32_t d[4][3];  // 4 groups in flight per thread
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * stride;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) d[u][j] = q < nq ? s4[3 * q + j] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (q0 + u * stride >= nq) break;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          double v[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int k = 3 * p + c;
+            v[c] = (double)((d[u][k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
+          }
+          acc(v[0], v[1], v[2]);
+        }
+      }
+    }
+  } else {
+    // pixel p = y * w + x with 32-bit index math (p < 2^31 per image: checked on the host)
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < (int)np; p += gridDim.x * blockDim.x) {
+      const int y = p / w, x = p - y * w;
+      double v[3];
+      load_rgb64(src, in64, img, h, w, row_stride, y, x, v);
+      acc(v[0], v[1], v[2]);
     }
   }
 #pragma unroll
@@ -784,6 +817,47 @@ struct HaarSplit {
   static constexpr int QS = SB / 2;         // level-1 groups per sub-block side
 };
 
+// channel c of one row of 4 pixels (x .. x+3), normalised: v[s]
+__device__ __forceinline__ void haar_row4_c(const uint8_t* __restrict__ src,
+                                            const double* __restrict__ in64, int img, int h, int w,
+                                            int64_t row_stride, int y, int x, int c, wreal mn,
+                                            wreal inv, wreal (&v)[4]) {
+  double px[4][3];
+  if (in64) {
+    const double* p = in64 + (((int64_t)img * h + y) * w + x) * 3;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) px[k / 3][k % 3] = p[k];
+  } else {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(src + (int64_t)img * h * row_stride +
+                                                          (int64_t)y * row_stride + (int64_t)x * 3);
+    const uint32_t d[3] = {p[0], p[1], p[2]};
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+      px[k / 3][k % 3] = (double)((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) v[s] = (ycbcr_c(px[s], c) - mn) / inv;
+}
+
+// level 1 of channel c of one thread's 4x4 sub-block (L >= 2)
+__device__ __forceinline__ void haar_sub4_c(const uint8_t* __restrict__ src,
+                                            const double* __restrict__ in64, int img, int h, int w,
+                                            int64_t row_stride, int y0, int x0, int c, wreal mn,
+                                            wreal inv, wreal (&a1)[4], wreal (&d1)[3][4]) {
+#pragma unroll
+  for (int qy = 0; qy < 2; ++qy) {
+    wreal r0[4], r1[4];
+    haar_row4_c(src, in64, img, h, w, row_stride, y0 + 2 * qy, x0, c, mn, inv, r0);
+    haar_row4_c(src, in64, img, h, w, row_stride, y0 + 2 * qy + 1, x0, c, mn, inv, r1);
+#pragma unroll
+    for (int qx = 0; qx < 2; ++qx) {
+      const int k = qy * 2 + qx;
+      haar2x2(r0[2 * qx], r0[2 * qx + 1], r1[2 * qx], r1[2 * qx + 1], a1[k], d1[0][k], d1[1][k],
+              d1[2][k]);
+    }
+  }
+}
+
 // level 1 of one thread's sub-block, all channels: a1[c][k] approximations, d1[c][band][k] details
 template <int L>
 __device__ __forceinline__ void haar_sub_analysis(
@@ -835,92 +909,81 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_analyze(
   const int blk = tid / HS::NS, sub = tid % HS::NS;
   const bool act = blk < nblk;  // uniform over each block's NS consecutive lanes
   const double* st = stats + (size_t)img * WL_STATS;
-  wreal mn[3], inv[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    wreal mx;
-    wl_minmax64(st, c, mn[c], mx);
-    inv[c] = mx - mn[c];
-  }
-  double sq[3][L][3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) sq[c][l][b] = 0.0;
-  wreal a2[3] = {0, 0, 0};
-  // exponent histogram of the nonzero |dd1| (sigma's first radix digit), per workgroup in LDS,
-  // 8 copies by lane & 7 (|dd| takes few exponents: one copy would serialise the LDS atomics)
-  __shared__ uint32_t ehist[8][3][WL_EBINS];
-  for (int k = threadIdx.x; k < 8 * 3 * WL_EBINS; k += WLH_WG) (&ehist[0][0][0])[k] = 0u;
-  __syncthreads();
+  __shared__ double red[3 * L * 3][WLH_WG / 64];
+  int y0 = 0, x0 = 0;
   if (act) {
     const int by = blk / nbx, bx = blk - by * nbx;
     const int sy = sub / (B / HS::SB), sx = sub % (B / HS::SB);
-    const int y0 = by * B + sy * HS::SB, x0 = bx * B + sx * HS::SB;
-    wreal a1[3][QS * QS], d1[3][3][QS * QS];
-    haar_sub_analysis<L>(src, in64, img, h, w, row_stride, y0, x0, mn, inv, a1, d1);
+    y0 = by * B + sy * HS::SB;
+    x0 = bx * B + sx * HS::SB;
+  }
+  const size_t W1 = (size_t)(w / 2), bsz = (size_t)(h / 2) * W1;
+  // one channel at a time (keeps the live state to one channel's coefficients and sums)
+#pragma unroll 1
+  for (int c = 0; c < 3; ++c) {
+    wreal mn, mx;
+    wl_minmax64(st, c, mn, mx);
+    const wreal inv = mx - mn;
+    double sq[L][3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int l = 0; l < L; ++l)
 #pragma unroll
-      for (int k = 0; k < QS * QS; ++k) {
-        const unsigned long long key = absbits(d1[c][2][k]);
-        if (key) atomicAdd(&ehist[threadIdx.x & 7][c][wl_ebin(key)], 1u);
+      for (int b = 0; b < 3; ++b) sq[l][b] = 0.0;
+    wreal a2 = 0;
+    if (act) {
+      wreal a1[QS * QS], d1[3][QS * QS];
+      if constexpr (QS == 2) {
+        haar_sub4_c(src, in64, img, h, w, row_stride, y0, x0, c, mn, inv, a1, d1);
+      } else {  // L = 1: a 2x2 block per thread
+        wreal r[2][2];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) {
+            double px[3];
+            load_rgb64(src, in64, img, h, w, row_stride, y0 + rr, x0 + ss, px);
+            r[rr][ss] = (ycbcr_c(px, c) - mn) / inv;
+          }
+        haar2x2(r[0][0], r[0][1], r[1][0], r[1][1], a1[0], d1[0][0], d1[1][0], d1[2][0]);
       }
-    const size_t W1 = (size_t)(w / 2), bsz = (size_t)(h / 2) * W1;
-    wreal* ddp = ws + img * img_floats + dd_off + 3 * bsz;  // channel c: + c * 4 * bsz
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
+      wreal* ddp = ws + img * img_floats + dd_off + (size_t)c * 4 * bsz + 3 * bsz;
 #pragma unroll
       for (int k = 0; k < QS * QS; ++k) {
 #pragma unroll
-        for (int b = 0; b < 3; ++b) sq[c][0][b] += d1[c][b][k] * d1[c][b][k];
-        ddp[(size_t)c * 4 * bsz + (size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] = d1[c][2][k];
+        for (int b = 0; b < 3; ++b) sq[0][b] += d1[b][k] * d1[b][k];
+        ddp[(size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] = d1[2][k];
       }
       if constexpr (L >= 2) {  // level 2 on the thread's 2x2 level-1 approximations
         wreal ad, da, dd;
-        haar2x2(a1[c][0], a1[c][1], a1[c][2], a1[c][3], a2[c], ad, da, dd);
-        sq[c][1][0] += ad * ad;
-        sq[c][1][1] += da * da;
-        sq[c][1][2] += dd * dd;
+        haar2x2(a1[0], a1[1], a1[2], a1[3], a2, ad, da, dd);
+        sq[1][0] += ad * ad;
+        sq[1][1] += da * da;
+        sq[1][2] += dd * dd;
       }
     }
-  }
-  if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
-    const int base = (threadIdx.x & 63) & ~3;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const wreal x00 = __shfl(a2[c], base), x01 = __shfl(a2[c], base + 1);
-      const wreal x10 = __shfl(a2[c], base + 2), x11 = __shfl(a2[c], base + 3);
+    if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
+      const int base = (threadIdx.x & 63) & ~3;
+      const wreal x00 = __shfl(a2, base), x01 = __shfl(a2, base + 1);
+      const wreal x10 = __shfl(a2, base + 2), x11 = __shfl(a2, base + 3);
       wreal aa, ad, da, dd;
       haar2x2(x00, x01, x10, x11, aa, ad, da, dd);
       if (act && sub == 0) {
-        sq[c][2][0] += ad * ad;
-        sq[c][2][1] += da * da;
-        sq[c][2][2] += dd * dd;
+        sq[2][0] += ad * ad;
+        sq[2][1] += da * da;
+        sq[2][2] += dd * dd;
       }
     }
-  }
-  // workgroup sums of squares in a fixed order (wave shuffles, then the two waves)
-  __shared__ double red[3 * L * 3][WLH_WG / 64];
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
 #pragma unroll
     for (int l = 0; l < L; ++l)
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
-        double v = sq[c][l][b];
+        double v = sq[l][b];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if ((threadIdx.x & 63) == 0) red[(c * L + l) * 3 + b][threadIdx.x >> 6] = v;
       }
-  __syncthreads();
-  for (int k = threadIdx.x; k < 3 * WL_EBINS; k += WLH_WG) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int cp = 0; cp < 8; ++cp) v += (&ehist[cp][0][0])[k];
-    if (v) atomicAdd(reinterpret_cast<uint32_t*>(const_cast<double*>(st) + WlStats::HIST) + k, v);
   }
+  __syncthreads();
+  // workgroup sums of squares in a fixed order (wave shuffles, then the two waves)
   if (threadIdx.x < 3 * L * 3) {
     const int k = threadIdx.x, b = k % 3, l = (k / 3) % L, c = k / (3 * L);
     double t = red[k][0];
@@ -1027,8 +1090,8 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
   }
 }
 
-// sigma for the fused path: the exponent histogram (built by wl_haar_analyze) locates the bin
-// holding the lower middle rank; one pass over the stored dd1 compacts that bin's keys into
+// sigma for the fused path: an exponent histogram of the stored dd1 locates the bin holding the
+// lower middle rank; one pass over the stored dd1 compacts that bin's keys into
 // scratch and takes the smallest key of the next nonempty bin (the upper middle rank may live
 // there); the remaining digits are selected on the compacted keys.
 __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, size_t img_floats,
@@ -1038,10 +1101,34 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
   const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
   double* scratch = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;  // unused input-plane slot
   double* st = stats + (size_t)img * WL_STATS;
-  const uint32_t* eh = reinterpret_cast<const uint32_t*>(st + WlStats::HIST) + c * WL_EBINS;
   __shared__ uint32_t hist[2048];
   __shared__ uint32_t m_s, le_s, total_s, bin_s, rank_s, next_s;
   __shared__ unsigned long long nmin_s, gt_s;
+  // pass 1: exponent histogram of the nonzero |dd| (16 copies by lane & 15: |dd| takes few
+  // exponents, one copy would serialise the LDS atomics); copy k lives at hist[k * 64 ..]
+  for (int k = threadIdx.x; k < 16 * WL_EBINS; k += 1024) hist[k] = 0u;
+  __syncthreads();
+  for (size_t k0 = threadIdx.x; k0 < bsz; k0 += 8 * 1024) {
+    double vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t k = k0 + (size_t)u * 1024;
+      vv[u] = k < bsz ? d[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const unsigned long long key = absbits(vv[u]);
+      if (key) atomicAdd(&hist[(threadIdx.x & 15) * WL_EBINS + wl_ebin(key)], 1u);
+    }
+  }
+  __syncthreads();
+  __shared__ uint32_t eh[WL_EBINS];
+  if (threadIdx.x < WL_EBINS) {
+    uint32_t v = 0;
+    for (int cp = 0; cp < 16; ++cp) v += hist[cp * WL_EBINS + threadIdx.x];
+    eh[threadIdx.x] = v;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
     for (int b = 0; b < WL_EBINS; ++b) t += eh[b];
@@ -1163,8 +1250,9 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
   hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n);
   {
     const int64_t np = (int64_t)Lt.h * Lt.w;
-    int gx = (int)((np + 255) / 256);
-    if (gx > 256) gx = 256;
+    // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
+    int gx = (int)((np / 4 + 255) / 256);
+    if (gx > 24) gx = 24;
     hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
@@ -1204,8 +1292,9 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n);
   {
     const int64_t np = (int64_t)Lt.h * Lt.w;
-    int gx = (int)((np + 255) / 256);
-    if (gx > 256) gx = 256;
+    // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
+    int gx = (int)((np / 4 + 255) / 256);
+    if (gx > 24) gx = 24;
     hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
