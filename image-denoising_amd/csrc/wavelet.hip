@@ -800,10 +800,14 @@ __device__ __forceinline__ void haar_row4(const uint8_t* __restrict__ src,
     for (int k = 0; k < 12; ++k)
       px[k / 3][k % 3] = (double)((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
   }
+  // the synthesis is continuous in the coefficients: a reciprocal multiply (<= 1 ulp from the
+  // quotient) is enough here; sigma's exact zeros come from wl_haar_analyze's exact quotients
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int c = 0; c < 3; ++c) {
+    const wreal rcp = 1.0 / inv[c];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) v[s][c] = (ycbcr_c(px[s], c) - mn[c]) / inv[c];
+    for (int s = 0; s < 4; ++s) v[s][c] = (ycbcr_c(px[s], c) - mn[c]) * rcp;
+  }
 }
 
 // Work split: one thread per 4x4 sub-block (levels 1 and 2 in registers); for L = 3 the four
@@ -835,8 +839,16 @@ __device__ __forceinline__ void haar_row4_c(const uint8_t* __restrict__ src,
     for (int k = 0; k < 12; ++k)
       px[k / 3][k % 3] = (double)((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
   }
+  // (Y - min) / (max - min) correctly rounded without a division per value: q0 = a * (1/b),
+  // q1 = q0 + (a - q0 b)(1/b) with exact fma residuals (Markstein) -- bitwise the IEEE quotient
+  // (also checked over every u8 triple for 24 channel ranges: tools/check_div.c)
+  const wreal rcp = 1.0 / inv;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) v[s] = (ycbcr_c(px[s], c) - mn) / inv;
+  for (int s = 0; s < 4; ++s) {
+    const wreal a = ycbcr_c(px[s], c) - mn;
+    const wreal q0 = a * rcp;
+    v[s] = __fma_rn(__fma_rn(-q0, inv, a), rcp, q0);
+  }
 }
 
 // level 1 of channel c of one thread's 4x4 sub-block (L >= 2)
