@@ -17,6 +17,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace idn {
 
 __device__ __forceinline__ double img_as_float(uint32_t v) { return __dmul_rn((double)v, 1.0 / 255.0); }
@@ -224,7 +226,8 @@ __global__ void vals_from_mask_kernel(uint32_t* mask, int n) {
   mask[8 * n + img] = v;
 }
 
-// numpy legacy Poisson: multiplication method for lam < 10, PTRS (Hormann 1993) otherwise
+// numpy legacy Poisson: multiplication method for lam < 10, PTRS (Hormann 1993) otherwise, with
+// numpy's own loggam in the acceptance test
 struct PhiloxStream {
   uint64_t key;
   uint32_t e_lo, e_hi, g_lo, g_hi;
@@ -243,32 +246,78 @@ struct PhiloxStream {
   }
 };
 
-__device__ double poisson_sample(double lam, PhiloxStream& rs) {
+// the per-lambda constants of numpy's samplers (lambda depends only on the u8 value and the
+// image's vals: the flat kernel tabulates them once per workgroup)
+struct PoisConst {
+  double lam, enlam, slam, loglam, b, a, invalpha, vr, loginvalpha;
+};
+__device__ __forceinline__ PoisConst pois_const(double lam) {
+  PoisConst p{};
+  p.lam = lam;
+  if (lam < 10.0) {
+    p.enlam = exp(-lam);
+  } else {
+    p.slam = sqrt(lam);
+    p.loglam = log(lam);
+    p.b = 0.931 + 2.53 * p.slam;
+    p.a = -0.059 + 0.02483 * p.b;
+    p.invalpha = 1.1239 + 1.1328 / (p.b - 3.4);
+    p.vr = 0.9277 - 3.6224 / (p.b - 2);
+    p.loginvalpha = log(p.invalpha);
+  }
+  return p;
+}
+
+// numpy's legacy random_loggam (log Gamma(x), Stirling series with the recursion below 7): the
+// function numpy's PTRS acceptance test evaluates at k + 1
+__device__ double np_loggam(double x) {
+  constexpr double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
+                            -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
+                            6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
+                            -1.39243221690590e+00};
+  if (x == 1.0 || x == 2.0) return 0.0;
+  const int n = x < 7.0 ? (int)(7 - x) : 0;
+  double x0 = x + n;
+  const double x2 = (1.0 / x0) * (1.0 / x0);
+  double gl0 = a[9];
+#pragma unroll
+  for (int k = 8; k >= 0; --k) {
+    gl0 *= x2;
+    gl0 += a[k];
+  }
+  double gl = gl0 / x0 + 0.5 * 1.8378770664093453e+00 + (x0 - 0.5) * log(x0) - x0;
+  for (int k = 1; k <= n; ++k) {
+    gl -= log(x0 - 1.0);
+    x0 -= 1.0;
+  }
+  return gl;
+}
+
+constexpr int LOGGAM_TAB = 1024;  // loggam(k + 1) for k < 1024 (a workgroup table in LDS)
+
+__device__ double poisson_sample(const PoisConst& p, PhiloxStream& rs,
+                                 const double* loggam_tab = nullptr) {
+  const double lam = p.lam;
   if (lam == 0.0) return 0.0;
   if (lam < 10.0) {
-    const double enlam = exp(-lam);
     double prod = 1.0;
     int x = 0;
     for (int it = 0; it < 1000; ++it) {
       prod *= rs.next();
-      if (prod > enlam) ++x;
+      if (prod > p.enlam) ++x;
       else return (double)x;
     }
     return (double)x;
   }
-  const double slam = sqrt(lam), loglam = log(lam);
-  const double b = 0.931 + 2.53 * slam;
-  const double a = -0.059 + 0.02483 * b;
-  const double invalpha = 1.1239 + 1.1328 / (b - 3.4);
-  const double vr = 0.9277 - 3.6224 / (b - 2);
   for (int it = 0; it < 1000; ++it) {
     const double U = rs.next() - 0.5;
     const double V = rs.next();
     const double us = 0.5 - fabs(U);
-    const double k = floor((2 * a / us + b) * U + lam + 0.43);
-    if (us >= 0.07 && V <= vr) return k;
+    const double k = floor((2 * p.a / us + p.b) * U + lam + 0.43);
+    if (us >= 0.07 && V <= p.vr) return k;
     if (k < 0 || (us < 0.013 && V > us)) continue;
-    if (log(V) + log(invalpha) - log(a / (us * us) + b) <= -lam + k * loglam - lgamma(k + 1))
+    const double lg = (loggam_tab && k < LOGGAM_TAB) ? loggam_tab[(int)k] : np_loggam(k + 1);
+    if (log(V) + p.loginvalpha - log(p.a / (us * us) + p.b) <= -lam + k * p.loglam - lg)
       return k;
   }
   return floor(lam);  // unreachable in practice (bounded loop)
@@ -293,9 +342,152 @@ __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a) {
       const uint64_t gimg = a.offset + (uint64_t)img;
       PhiloxStream rs{a.key, (uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg,
                       (uint32_t)(gimg >> 32)};
-      k = poisson_sample(__dmul_rn(img_as_float(a.src[boff]), vals), rs);
+      k = poisson_sample(pois_const(__dmul_rn(img_as_float(a.src[boff]), vals)), rs);
     }
     store_out(a, img, e, boff, clip01(k / vals));
+  }
+}
+
+// flat Poisson (compact rows, Philox stream): 16 consecutive elements per thread, image =
+// blockIdx.y, the 256 per-value lambda constants tabulated in LDS; same streams and arithmetic
+// as noise_poisson_kernel, so the two forms agree bit for bit
+__global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a) {
+  __shared__ PoisConst tab[256];
+  __shared__ double lgt[LOGGAM_TAB];
+  const int img = blockIdx.y;
+  const double vals = (double)a.vals[img];
+  tab[threadIdx.x] = pois_const(__dmul_rn(img_as_float(threadIdx.x), vals));
+  for (int k = threadIdx.x; k < LOGGAM_TAB; k += 256) lgt[k] = np_loggam((double)k + 1.0);
+  __syncthreads();
+  const uint32_t chunk = blockIdx.x * 256u + threadIdx.x;
+  const int64_t e0 = (int64_t)chunk * 16;
+  if (e0 >= a.elems) return;
+  const uint64_t gimg = a.offset + (uint64_t)img;
+  const v4u raw = *reinterpret_cast<const v4u*>(a.src + (int64_t)img * a.elems + e0);
+  const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
+  double* of = a.out_f64 ? a.out_f64 + (int64_t)img * a.elems + e0 : nullptr;
+  uint32_t* o8 = a.out_u8 ? reinterpret_cast<uint32_t*>(a.out_u8 + (int64_t)img * a.elems + e0) : nullptr;
+  // Each lane walks its 16 elements with its own rejection state: one loop iteration is one
+  // attempt (PTRS) or one factor (multiplication method) of the lane's current element, and a
+  // lane moves on as soon as its element is accepted -- the wave never waits for the unluckiest
+  // lane of every element (the element kernel's max over 64 geometric attempt counts).
+  // Per element the draws and arithmetic are exactly poisson_sample's.
+  auto byte_of = [&](int j) -> uint32_t {
+    const uint32_t dw = (j >> 2) == 0 ? in[0] : (j >> 2) == 1 ? in[1] : (j >> 2) == 2 ? in[2] : in[3];
+    return (dw >> (8 * (j & 3))) & 0xFFu;
+  };
+  int j = 0, it = 0, x = 0;
+  double prod = 1.0;
+  PoisConst pc = tab[byte_of(0)];
+  PhiloxStream rs{a.key, (uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)gimg, (uint32_t)(gimg >> 32)};
+  uint32_t o = 0u;
+  while (j < 16) {
+    bool done = false;
+    double k = 0.0;
+    if (pc.lam == 0.0) {
+      done = true;
+    } else if (pc.lam < 10.0) {
+      prod *= rs.next();
+      if (prod > pc.enlam) {
+        ++x;
+        if (++it >= 1000) done = true;
+      } else {
+        done = true;
+      }
+      k = (double)x;
+    } else {
+      const double U = rs.next() - 0.5;
+      const double V = rs.next();
+      const double us = 0.5 - fabs(U);
+      k = floor((2 * pc.a / us + pc.b) * U + pc.lam + 0.43);
+      if (us >= 0.07 && V <= pc.vr) {
+        done = true;
+      } else if (!(k < 0 || (us < 0.013 && V > us))) {
+        const double lg = k < LOGGAM_TAB ? lgt[(int)k] : np_loggam(k + 1);
+        done = log(V) + pc.loginvalpha - log(pc.a / (us * us) + pc.b) <= -pc.lam + k * pc.loglam - lg;
+      }
+      if (!done && ++it >= 1000) {
+        done = true;
+        k = floor(pc.lam);
+      }
+    }
+    if (done) {
+      const double out = clip01(k / vals);
+      o |= (uint32_t)u8_of(out) << (8 * (j & 3));
+      if (of) of[j] = out;
+      if ((j & 3) == 3) {
+        if (o8) o8[j >> 2] = o;
+        o = 0u;
+      }
+      ++j;
+      if (j < 16) {
+        const int64_t e = e0 + j;
+        pc = tab[byte_of(j)];
+        rs = PhiloxStream{a.key, (uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg,
+                          (uint32_t)(gimg >> 32)};
+        it = 0;
+        x = 0;
+        prod = 1.0;
+      }
+    }
+  }
+}
+
+// flat per-image distinct-value mask: 16 bytes per thread per step, a private 256-bit mask per
+// thread, OR-reduced over the wave before one LDS atomic per word
+__global__ __launch_bounds__(256) void unique_mask_flat_kernel(const uint8_t* __restrict__ src,
+                                                               int64_t per_img,
+                                                               uint32_t* __restrict__ mask) {
+  __shared__ uint32_t m[8];
+  if (threadIdx.x < 8) m[threadIdx.x] = 0;
+  __syncthreads();
+  const int img = blockIdx.y;
+  const v4u* s = reinterpret_cast<const v4u*>(src + (int64_t)img * per_img);
+  const int64_t nq = per_img / 16;
+  uint32_t mk[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const v4u v = s[q];
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const uint32_t x = (d[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+      const uint32_t bit = 1u << (x & 31u), word = x >> 5;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mk[k] |= word == (uint32_t)k ? bit : 0u;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t v = mk[k];
+    for (int off = 32; off > 0; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off);
+    if ((threadIdx.x & 63) == 0 && v) atomicOr(&m[k], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && m[threadIdx.x]) atomicOr(&mask[img * 8 + threadIdx.x], m[threadIdx.x]);
+}
+
+// cv2.add(u8, u8) on compact rows, 16 bytes per thread: SWAR saturating byte add
+__device__ __forceinline__ uint32_t addsat_u8x4(uint32_t a, uint32_t b) {
+  const uint32_t low7 = (a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu);  // no carry out of any byte
+  const uint32_t sum = low7 ^ ((a ^ b) & 0x80808080u);          // byte sums mod 256
+  const uint32_t carry = ((a & b) | ((a | b) & ~sum)) & 0x80808080u;
+  return sum | ((carry >> 7) * 0xFFu);
+}
+__global__ __launch_bounds__(256) void add_pattern_flat_kernel(const uint8_t* __restrict__ src,
+                                                               const uint8_t* __restrict__ pat,
+                                                               uint8_t* __restrict__ dst,
+                                                               int64_t per_img) {
+  const int img = blockIdx.y;
+  const int64_t nq = per_img / 16;
+  const v4u* s = reinterpret_cast<const v4u*>(src + (int64_t)img * per_img);
+  const v4u* p = reinterpret_cast<const v4u*>(pat);
+  v4u* d = reinterpret_cast<v4u*>(dst + (int64_t)img * per_img);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const v4u a = s[q], b = p[q];
+    d[q] = v4u{addsat_u8x4(a.x, b.x), addsat_u8x4(a.y, b.y), addsat_u8x4(a.z, b.z),
+               addsat_u8x4(a.w, b.w)};
   }
 }
 
@@ -422,12 +614,24 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
       if (hipMemsetAsync(mask, 0, (size_t)n * 8 * sizeof(uint32_t), st) != hipSuccess)
         return set_error(IDN_EHIP, "idn_noise_u8: memset failed");
       const int64_t per_img = (int64_t)h * w * c;
-      unsigned gx = grid_for(per_img, 64);
-      hipLaunchKernelGGL(unique_mask_kernel, dim3(gx, (unsigned)n), dim3(256), 0, st, src, h, w * c,
-                         row_stride, mask);
+      const bool compact = row_stride == (int64_t)w * c && per_img % 16 == 0 &&
+                           ((uintptr_t)src & 15) == 0;
+      if (compact) {
+        hipLaunchKernelGGL(unique_mask_flat_kernel, dim3(16, (unsigned)n), dim3(256), 0, st, src,
+                           per_img, mask);
+      } else {
+        unsigned gx = grid_for(per_img, 64);
+        hipLaunchKernelGGL(unique_mask_kernel, dim3(gx, (unsigned)n), dim3(256), 0, st, src, h,
+                           w * c, row_stride, mask);
+      }
       hipLaunchKernelGGL(vals_from_mask_kernel, dim3((n + 255) / 256), dim3(256), 0, st, mask, n);
       a.vals = mask + 8 * n;
-      hipLaunchKernelGGL(noise_poisson_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      if (flat) {
+        const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
+        hipLaunchKernelGGL(noise_poisson_flat_kernel, grid, dim3(256), 0, st, a);
+      } else {
+        hipLaunchKernelGGL(noise_poisson_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      }
       break;
     }
   }
@@ -456,8 +660,17 @@ extern "C" int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, ui
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c > 0, "idn_add_pattern_u8: bad shape");
   IDN_CHECK_ARG(row_stride >= (int64_t)w * c, "idn_add_pattern_u8: row_stride < w*c");
   if (n == 0) return IDN_OK;
-  hipLaunchKernelGGL(add_pattern_kernel, dim3(grid_for((int64_t)n * h * w * c)), dim3(256), 0,
-                     as_stream(stream), src, pattern, dst, n, h, w * c, row_stride);
+  const int64_t per_img = (int64_t)h * w * c;
+  if (row_stride == (int64_t)w * c && per_img % 16 == 0 && n <= 65535 &&
+      (((uintptr_t)src | (uintptr_t)pattern | (uintptr_t)dst) & 15) == 0) {
+    const int64_t nq = per_img / 16;
+    const unsigned gx = (unsigned)std::min<int64_t>((nq + 255) / 256, 1024);
+    hipLaunchKernelGGL(add_pattern_flat_kernel, dim3(gx, (unsigned)n), dim3(256), 0,
+                       as_stream(stream), src, pattern, dst, per_img);
+  } else {
+    hipLaunchKernelGGL(add_pattern_kernel, dim3(grid_for((int64_t)n * h * w * c)), dim3(256), 0,
+                       as_stream(stream), src, pattern, dst, n, h, w * c, row_stride);
+  }
   IDN_CHECK_LAUNCH("idn_add_pattern_u8");
   return IDN_OK;
 }

@@ -253,3 +253,20 @@ def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
     assert abs(ref["0"].mean() - ref["1"].mean()) < 4e-3
     assert abs(ref["0"].std() - ref["1"].std()) < 4e-3
     assert abs(d.mean() - ref["1"].mean()) < 4e-3
+
+
+def test_poisson_flat_matches_element_kernel(dev, monkeypatch):
+    """the flat Poisson kernel (per-value constants and loggam tabulated in LDS) draws the same
+    per-element streams with the same arithmetic as the element kernel: identical outputs"""
+    import torch
+    import idn
+    imgs = np.stack([make_img(48, 64, s) for s in (1, 2)])
+    imgs[0, :8] //= 16  # dark rows: lambda < 10 takes the multiplication method
+    x = torch.from_numpy(imgs).cuda()
+    res = {}
+    for flat in ("0", "1"):
+        monkeypatch.setenv("IDN_NOISE_FLAT", flat)
+        u8, f64 = idn.ops.random_noise(x, "poisson", seed=5, offset=3, out="both")
+        res[flat] = (u8.cpu().numpy(), f64.cpu().numpy())
+    assert np.array_equal(res["0"][0], res["1"][0])
+    assert np.array_equal(res["0"][1], res["1"][1])
