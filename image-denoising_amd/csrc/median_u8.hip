@@ -2,11 +2,12 @@
 // Reference call sites: lib/model/test.py:259, lib/roi_data_layer/minibatch.py:153,1644-1648.
 //
 // Same wave-stripe streaming as the stencils (stripe.hpp): one wave = one segment of a band of
-// rows, 16 bytes per lane, DPP halos, replicated borders rebuilt in registers, a K-row ring of raw
-// window dwords.  Selection runs on packed u16 pairs (v_pk_min_u16 / v_pk_max_u16): every
+// rows, 16 bytes per lane, DPP halos, replicated borders rebuilt in registers, a K-row ring of
+// unpacked rows.  Selection runs on packed u16 pairs (v_pk_min_u16 / v_pk_max_u16): every
 // comparator handles two output bytes.
-//   3x3: sort each 3-row column once (CSE shares it between the three outputs that read it),
-//        then med3(max3(col mins), med3(col medians), min3(col maxes)).
+//   3x3: each input row is unpacked once into u16 lanes; per output row every window column is
+//        sorted once and shared by the 3 outputs that read it (halos by DPP on the sorted
+//        columns), then med3(max3(col mins), med3(col medians), min3(col maxes)).
 //   5x5: each input row is unpacked once into u16 lanes; per output row every window column is
 //        sorted once (SORT5) and shared by the 5 outputs that read it; the sorted columns'
 //        6-byte halos come from the neighbouring lanes by DPP; two chains of 5 same-channel
@@ -35,44 +36,51 @@ struct PkOps {
   }
 };
 
-// 3-row column at window u16 position b: (min, median, max) of rows r0, r1, r2
-__device__ __forceinline__ void col3(const uint32_t (&W0)[8], const uint32_t (&W1)[8],
-                                     const uint32_t (&W2)[8], int b, uint32_t& lo, uint32_t& md,
-                                     uint32_t& hi) {
-  const PkOps op;
-  const uint32_t a = lanes16_at(W0, b), c = lanes16_at(W1, b), d = lanes16_at(W2, b);
-  const uint32_t l1 = op.mn(a, c), h1 = op.mx(a, c);
-  lo = op.mn(l1, d);
-  const uint32_t h2 = op.mx(l1, d);
-  hi = op.mx(h1, h2);
-  md = op.mn(h1, h2);
-}
-
+// one output row of the 3x3 median from the 3 unpacked rows of its window (oldest first): every
+// window column is sorted once (shared by the 3 outputs that read it), the sorted columns' 3-byte
+// halos come by DPP, then med3(max of the 3 column minima, med3 of the medians, min of the maxima)
 template <int C>
-__device__ __forceinline__ v4u median3_out(const uint32_t (&W0)[8], const uint32_t (&W1)[8],
-                                           const uint32_t (&W2)[8]) {
+__device__ __forceinline__ v4u median3_cols_out(const uint32_t (&U0)[8], const uint32_t (&U1)[8],
+                                                const uint32_t (&U2)[8], bool fix_t0, bool fix_t8) {
   const PkOps op;
+  VWin V[3];  // per rank (min, median, max): u16 window of the sorted columns
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t a = U0[j], b = U1[j], c = U2[j];
+    const uint32_t l1 = op.mn(a, b), h1 = op.mx(a, b);
+    const uint32_t lo = op.mn(l1, c), h2 = op.mx(l1, c);
+    const uint32_t r[3] = {lo, op.mn(h1, h2), op.mx(h1, h2)};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (j < 4) V[k].SE[2 + j] = r[k];
+      else V[k].SO[2 + (j - 4)] = r[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {  // 3-byte halos each side (R*C = 3): one dword per parity
+    V[k].SE[0] = V[k].SO[0] = V[k].SE[7] = V[k].SO[7] = 0u;
+    V[k].SE[1] = from_prev_lane(V[k].SE[5]);
+    V[k].SO[1] = from_prev_lane(V[k].SO[5]);
+    V[k].SE[6] = from_next_lane(V[k].SE[2]);
+    V[k].SO[6] = from_next_lane(V[k].SO[2]);
+    if (fix_t0) vwin_tail_fix<C, BORDER_REPLICATE>(V[k], 24);
+    if (fix_t8) vwin_tail_fix<C, BORDER_REPLICATE>(V[k], 16);
+  }
   uint32_t o[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int q = 0; q < 4; ++q) {
     uint32_t v[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int P = 4 * k + 8 + e;
-      uint32_t l0, m0, h0, l1, m1, h1, l2, m2, h2;
-      col3(W0, W1, W2, P - C, l0, m0, h0);
-      col3(W0, W1, W2, P, l1, m1, h1);
-      col3(W0, W1, W2, P + C, l2, m2, h2);
-      const uint32_t lmax = op.mx(op.mx(l0, l1), l2);
-      const uint32_t mmed = op.med3(m0, m1, m2);
-      const uint32_t hmin = op.mn(op.mn(h0, h1), h2);
+      const int P = 4 * q + 8 + e;
+      const uint32_t lmax = op.mx(op.mx(V[0].at(P - C), V[0].at(P)), V[0].at(P + C));
+      const uint32_t mmed = op.med3(V[1].at(P - C), V[1].at(P), V[1].at(P + C));
+      const uint32_t hmin = op.mn(op.mn(V[2].at(P - C), V[2].at(P)), V[2].at(P + C));
       v[e] = op.med3(lmax, mmed, hmin);
     }
-    // each u16 lane holds one output byte in its low byte
-    o[k] = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);
+    o[q] = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);  // low byte of each u16 lane
   }
-  v4u r = {o[0], o[1], o[2], o[3]};
-  return r;
+  return v4u{o[0], o[1], o[2], o[3]};
 }
 
 // one output row of the 5x5 median from the 5 unpacked rows of its window (oldest first)
@@ -164,7 +172,7 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
   v4u Lq[PF];
 #pragma unroll
   for (int i = 0; i < PF; ++i) Lq[i] = load_row(i);
-  uint32_t Wr[K][8];  // K == 3: raw row windows; K == 5: unpacked u16 rows
+  uint32_t Wr[K][8];  // unpacked u16 rows (even / odd bytes)
 
   for (int gi = 0; gi < ngroups; ++gi) {
 #pragma unroll
@@ -172,9 +180,7 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
       const int r = gi * U + u;
       const v4u Lv = Lq[u % PF];
       Lq[u % PF] = load_row(r + PF);
-      if constexpr (K == 3) {
-        build_window<C, BORDER_REPLICATE>(Lv, g.lead, g.fix_t0, g.fix_t8, Wr[u % K]);
-      } else {
+      {
         v4u Lx = Lv;
         if (g.lead) {  // chunk = row bytes -8..7: rebuild the replicated 8 bytes
           const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
@@ -187,7 +193,7 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
       if (r >= 2 * R && y < y1) {
         v4u o;
         if constexpr (K == 3) {
-          o = median3_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[u % K]);
+          o = median3_cols_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[u % K], g.fix_t0, g.fix_t8);
         } else {
           o = median5_cols_out<C>(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[(u + 3) % K],
                                   Wr[(u + 4) % K], Wr[u % K], g.fix_t0, g.fix_t8);
@@ -243,8 +249,10 @@ static int launch_median(const uint8_t* src, uint8_t* dst, int n, int h, int w, 
                          int64_t row_stride, hipStream_t st) {
   const int64_t rb = (int64_t)w * c;
   if (stripe_ok(c, rb, row_stride, h, src, dst)) {
-    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096, env_int("IDN_MEDIAN_MAP", 0),
-                                     env_int("IDN_MEDIAN_ROWS", 32));
+    // measured (tools/sweep_stencil.py): 3x3 is near the memory side -> whole-row workgroups over
+    // 16-row bands with XCD-contiguous band order; 5x5 is VALU-bound -> independent waves
+    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096, env_int("IDN_MEDIAN_MAP", K == 3 ? 1 : 0),
+                                     env_int("IDN_MEDIAN_ROWS", K == 3 ? 16 : 32));
     IDN_CHECK_ARG(p.total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
     hipLaunchKernelGGL((median_u8_fast<3, K, 0>), dim3(p.grid), dim3(p.block), 0, st, src, dst, h,
                        (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len, p.bands, p.band_rows,

@@ -197,3 +197,19 @@ def test_bilateral_gray(dev):
     got = _run(idn.bilateral_filter, img, 9, 20.0, 100.0)
     ref = oracle.cv.bilateral_filter(img, 9, 20.0, 100.0)
     assert np.abs(got.astype(int) - ref.astype(int)).max() <= 1
+
+
+@pytest.mark.parametrize("form", [{"IDN_MEDIAN_MAP": "0", "IDN_MEDIAN_ROWS": "32"},
+                                  {"IDN_MEDIAN_MAP": "1", "IDN_MEDIAN_ROWS": "16"},
+                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"}],
+                         ids=lambda f: "-".join(f"{k[11:]}{v}" for k, v in f.items()))
+@pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (1, 601, 1000), (2, 13, 104)])
+def test_median_forms_agree(dev, monkeypatch, form, shape):
+    """every band / workgroup mapping of the median gives cv2's bytes (band tails, 1-3 segments)"""
+    import idn
+    import oracle
+    for k, v in form.items():
+        monkeypatch.setenv(k, v)
+    img = textured(*shape, seed=sum(shape) + 1)
+    for k in (3, 5):
+        assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k)), k
