@@ -52,7 +52,11 @@ struct NoiseArgs {
   int64_t elems;  // h*w*c
   double p0, p1;  // mean/sd (gaussian, speckle), sap thresholds
   uint64_t key, offset;
+  const uint64_t* ids;  // optional per-image ids (device); else id = offset + image index
 };
+__device__ __forceinline__ uint64_t image_id(const NoiseArgs& a, int img) {
+  return a.ids ? a.ids[img] : a.offset + (uint64_t)img;
+}
 
 __device__ __forceinline__ void store_out(const NoiseArgs& a, int img, int64_t e, int64_t boff,
                                           double out) {
@@ -75,7 +79,7 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
       nz[0] = a.replay[(int64_t)img * a.elems + e0];
       nz[1] = (e0 + 1 < a.elems) ? a.replay[(int64_t)img * a.elems + e0 + 1] : 0.0;
     } else {
-      const uint64_t gimg = a.offset + (uint64_t)img;
+      const uint64_t gimg = image_id(a, img);
       const u32x4 r = philox4x32(u32x4{(uint32_t)pr, (uint32_t)(pr >> 32), (uint32_t)gimg,
                                        (uint32_t)(gimg >> 32)},
                                  a.key);
@@ -122,7 +126,7 @@ __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t
   const uint32_t chunk = blockIdx.x * 256u + threadIdx.x;
   const int64_t e0 = (int64_t)chunk * 16;
   if (e0 >= a.elems) return;
-  const uint64_t gimg = a.offset + (uint64_t)img;
+  const uint64_t gimg = image_id(a, img);
   const uint8_t* src = a.src + (int64_t)img * a.elems + e0;
   const v4u raw = *reinterpret_cast<const v4u*>(src);
   const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(256) void noise_sap_kernel(NoiseArgs a) {
       u1 = a.replay[t];
       u2 = a.replay[total + t];
     } else {
-      const uint64_t gimg = a.offset + (uint64_t)img;
+      const uint64_t gimg = image_id(a, img);
       const u32x4 r = philox4x32(
           u32x4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
       u1 = u01_closed_open(r.x, r.y);
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a) {
     if (a.replay) {
       k = a.replay[t];
     } else {
-      const uint64_t gimg = a.offset + (uint64_t)img;
+      const uint64_t gimg = image_id(a, img);
       PhiloxStream rs{a.key, (uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg,
                       (uint32_t)(gimg >> 32)};
       k = poisson_sample(pois_const(__dmul_rn(img_as_float(a.src[boff]), vals)), rs);
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a) {
   const uint32_t chunk = blockIdx.x * 256u + threadIdx.x;
   const int64_t e0 = (int64_t)chunk * 16;
   if (e0 >= a.elems) return;
-  const uint64_t gimg = a.offset + (uint64_t)img;
+  const uint64_t gimg = image_id(a, img);
   const v4u raw = *reinterpret_cast<const v4u*>(a.src + (int64_t)img * a.elems + e0);
   const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
   double* of = a.out_f64 ? a.out_f64 + (int64_t)img * a.elems + e0 : nullptr;
@@ -534,11 +538,11 @@ extern "C" size_t idn_noise_workspace_size(int kind, int n) {
   return (size_t)n * 9 * sizeof(uint32_t);
 }
 
-extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
-                            int w, int c, int64_t row_stride, int kind, double p0, double p1,
-                            uint64_t seed, uint64_t offset, const double* replay, void* workspace,
-                            size_t ws_bytes, void* stream) {
-  using namespace idn;
+namespace idn {
+static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
+                         int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
+                         uint64_t offset, const uint64_t* ids, const double* replay,
+                         void* workspace, size_t ws_bytes, void* stream) {
   IDN_CHECK_ARG(src, "idn_noise_u8: null src");
   IDN_CHECK_ARG(out_u8 || out_f64, "idn_noise_u8: at least one of out_u8 / out_f64 is required");
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c >= 1 && c <= 4, "idn_noise_u8: bad shape");
@@ -562,6 +566,7 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
   a.elems = (int64_t)h * w * c;
   a.key = seed ^ (KIND_TAG * (uint64_t)(kind + 1));
   a.offset = offset;
+  a.ids = ids;
   // flat form: Philox stream, compact rows, 16-element chunks that never straddle images
   const bool flat = !replay && row_stride == (int64_t)w * c && a.elems % 16 == 0 &&
                     ((uintptr_t)src & 15) == 0 && ((uintptr_t)out_u8 & 15) == 0 &&
@@ -637,6 +642,25 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
   }
   IDN_CHECK_LAUNCH("idn_noise_u8");
   return IDN_OK;
+}
+}  // namespace idn
+
+extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
+                            int w, int c, int64_t row_stride, int kind, double p0, double p1,
+                            uint64_t seed, uint64_t offset, const double* replay, void* workspace,
+                            size_t ws_bytes, void* stream) {
+  return idn::noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed,
+                            offset, nullptr, replay, workspace, ws_bytes, stream);
+}
+
+extern "C" int idn_noise_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n,
+                                int h, int w, int c, int64_t row_stride, int kind, double p0,
+                                double p1, uint64_t seed, const uint64_t* image_ids,
+                                void* workspace, size_t ws_bytes, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(image_ids || n == 0, "idn_noise_ids_u8: null image_ids");
+  return noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed, 0,
+                       image_ids, nullptr, workspace, ws_bytes, stream);
 }
 
 extern "C" int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, double amplitude,

@@ -35,8 +35,12 @@ struct AddArgs {
   int64_t elems;
   double p0, p1;
   uint64_t key, offset;
+  const uint64_t* ids;  // optional per-image ids (device); else id = offset + image index
   int nblk;  // brownian blocks per image
 };
+__device__ __forceinline__ uint64_t image_id(const AddArgs& a, int img) {
+  return a.ids ? a.ids[img] : a.offset + (uint64_t)img;
+}
 
 __device__ __forceinline__ double img_as_float_(uint32_t v) { return __dmul_rn((double)v, 1.0 / 255.0); }
 
@@ -90,7 +94,7 @@ __device__ float std_gamma(double a_d, uint64_t key, uint32_t e_lo, uint32_t e_h
 template <int KIND>
 __device__ __forceinline__ double unit_draw(const AddArgs& a, int img, int64_t e, int64_t flat) {
   if (a.replay) return a.replay[flat];
-  const uint64_t gimg = a.offset + (uint64_t)img;
+  const uint64_t gimg = image_id(a, img);
   if constexpr (KIND == IDN_NOISE_GAMMA) {
     return (double)std_gamma(a.p0, a.key, (uint32_t)e, (uint32_t)(e >> 32), gimg);
   } else {
@@ -135,7 +139,7 @@ constexpr int BR_THREADS = 256, BR_PER_THREAD = 16, BR_BLOCK = BR_THREADS * BR_P
 
 __device__ __forceinline__ void brownian_incs(const AddArgs& a, int img, int64_t e0, double sdt,
                                               double (&inc)[BR_PER_THREAD]) {
-  const uint64_t gimg = a.offset + (uint64_t)img;
+  const uint64_t gimg = image_id(a, img);
 #pragma unroll
   for (int q = 0; q < BR_PER_THREAD / 4; ++q) {
     float z[4] = {0.f, 0.f, 0.f, 0.f};
@@ -253,11 +257,11 @@ extern "C" size_t idn_noise_add_workspace_size(int kind, int n, int h, int w, in
   return (size_t)(nblk * n) * sizeof(double);
 }
 
-extern "C" int idn_noise_add_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
-                                int w, int c, int64_t row_stride, int kind, double p0, double p1,
-                                uint64_t seed, uint64_t offset, const double* replay,
-                                void* workspace, size_t ws_bytes, void* stream) {
-  using namespace idn;
+namespace idn {
+static int noise_add_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
+                          int w, int c, int64_t row_stride, int kind, double p0, double p1,
+                          uint64_t seed, uint64_t offset, const uint64_t* ids,
+                          const double* replay, void* workspace, size_t ws_bytes, void* stream) {
   IDN_CHECK_ARG(src, "idn_noise_add_u8: null src");
   IDN_CHECK_ARG(out_u8 || out_f64, "idn_noise_add_u8: at least one of out_u8 / out_f64 is required");
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c >= 1 && c <= 4, "idn_noise_add_u8: bad shape");
@@ -283,6 +287,7 @@ extern "C" int idn_noise_add_u8(const uint8_t* src, uint8_t* out_u8, double* out
   a.p1 = p1;
   a.key = seed ^ (ADD_TAG * (uint64_t)(kind + 1));
   a.offset = offset;
+  a.ids = ids;
   a.nblk = 0;
   const unsigned gx = (unsigned)std::min<int64_t>((a.elems + 255) / 256, 65535);
   switch (kind) {
@@ -314,4 +319,23 @@ extern "C" int idn_noise_add_u8(const uint8_t* src, uint8_t* out_u8, double* out
   }
   IDN_CHECK_LAUNCH("idn_noise_add_u8");
   return IDN_OK;
+}
+}  // namespace idn
+
+extern "C" int idn_noise_add_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
+                                int w, int c, int64_t row_stride, int kind, double p0, double p1,
+                                uint64_t seed, uint64_t offset, const double* replay,
+                                void* workspace, size_t ws_bytes, void* stream) {
+  return idn::noise_add_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed,
+                             offset, nullptr, replay, workspace, ws_bytes, stream);
+}
+
+extern "C" int idn_noise_add_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n,
+                                    int h, int w, int c, int64_t row_stride, int kind, double p0,
+                                    double p1, uint64_t seed, const uint64_t* image_ids,
+                                    void* workspace, size_t ws_bytes, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(image_ids || n == 0, "idn_noise_add_ids_u8: null image_ids");
+  return noise_add_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed, 0,
+                        image_ids, nullptr, workspace, ws_bytes, stream);
 }

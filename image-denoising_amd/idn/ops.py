@@ -100,10 +100,20 @@ def _empty_like_img(xb: torch.Tensor, dtype) -> torch.Tensor:
     return torch.empty(xb.shape, dtype=dtype, device=xb.device)
 
 
+def _ids_tensor(image_ids, n: int, device) -> torch.Tensor:
+    """device uint64 (int64 storage) array of n image ids for the *_ids_u8 entry points"""
+    t = torch.as_tensor(image_ids, dtype=torch.int64).reshape(-1)
+    if t.numel() != n:
+        raise ValueError(f"image_ids has {t.numel()} entries for a batch of {n}")
+    if bool((t < 0).any()):
+        raise ValueError("image_ids must be non-negative")
+    return t.to(device).contiguous()
+
+
 def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, var: float = 0.01,
                  amount: float = 0.05, salt_vs_pepper: float = 0.5, seed: int = 0,
                  offset: int = 0, replay: Optional[torch.Tensor] = None, out: str = "u8",
-                 out_u8: Optional[torch.Tensor] = None):
+                 out_u8: Optional[torch.Tensor] = None, image_ids=None):
     """skimage.util.random_noise(x, mode, ...) on a uint8 batch, plus the caller's U8 cast.
 
     out="u8"   -> (255 * random_noise(...)).astype(np.uint8)   (denoise-branch input)
@@ -113,6 +123,8 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
     random field numpy would have drawn (gaussian/speckle: N(mean, sqrt(var)) field of x.shape;
     s&p: float64 [2, *x.shape] random_sample fields for `flipped` then `salted`; poisson: the
     Poisson draws), which makes the result bit-exact with the reference.
+    image_ids: optional per-image ids (Philox stream only) instead of offset + index -- one launch
+    for any subset of a batch, drawing what per-image calls with offset = id would.
     """
     kind = NOISE_KINDS.get(mode.lower())
     if kind is None:
@@ -145,12 +157,22 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
     ws_bytes = lib.idn_noise_workspace_size(kind, n)
     if ws_bytes:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=xb.device)
-    rc = lib.idn_noise_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
-                          y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c, kind,
-                          p0, p1, int(seed) & (2 ** 64 - 1), int(offset),
-                          rp.data_ptr() if rp is not None else None,
-                          ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
-    _lib.check(rc, "idn_noise_u8")
+    if image_ids is not None:
+        if rp is not None:
+            raise ValueError("random_noise: image_ids applies to the Philox stream, not to replay")
+        ids = _ids_tensor(image_ids, n, xb.device)
+        rc = lib.idn_noise_ids_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
+                                  y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c,
+                                  kind, p0, p1, int(seed) & (2 ** 64 - 1), ids.data_ptr(),
+                                  ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+        _lib.check(rc, "idn_noise_ids_u8")
+    else:
+        rc = lib.idn_noise_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
+                              y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c,
+                              kind, p0, p1, int(seed) & (2 ** 64 - 1), int(offset),
+                              rp.data_ptr() if rp is not None else None,
+                              ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+        _lib.check(rc, "idn_noise_u8")
     if out == "u8":
         return _finish(y8, sq)
     if out == "f64":
@@ -164,7 +186,7 @@ GAMMA_SHAPE = 1.99  # a = 1.99 in every gamma closure (lib/model/test.py:1303)
 
 def noise_add(x: torch.Tensor, mode: str, level: float, *, seed: int = 0, offset: int = 0,
               replay: Optional[torch.Tensor] = None, out: str = "u8",
-              out_u8: Optional[torch.Tensor] = None, shape: float = GAMMA_SHAPE):
+              out_u8: Optional[torch.Tensor] = None, shape: float = GAMMA_SHAPE, image_ids=None):
     """The reference's own additive noises (lib/model/test.py:767-1572), u8 batch in:
       uniform  level = high:  out = img_as_float(x) + np.random.uniform(0, high)
       gamma    level = scale: out = x + scipy.stats.gamma.rvs(1.99, scale=level)
@@ -173,7 +195,8 @@ def noise_add(x: torch.Tensor, mode: str, level: float, *, seed: int = 0, offset
     cv2.add(float64, float64) does not clip: out="f64" is the unclipped sum (what train_v0's plain
     branches return), out="u8" is (255 * out).astype(np.uint8) with its modulo-256 wrap.
     replay: numpy's unit draws (random_sample / standard_gamma(1.99) / sqrt(chisquare(2)) /
-    for brownian the normals with element e holding z[e-1]), float64 of x's shape."""
+    for brownian the normals with element e holding z[e-1]), float64 of x's shape.
+    image_ids: optional per-image ids (Philox stream only), as in random_noise."""
     kind = ADD_NOISE_KINDS.get(mode.lower())
     if kind is None:
         raise ValueError(f"noise_add: unsupported mode {mode!r}; supported: {sorted(ADD_NOISE_KINDS)}")
@@ -194,12 +217,23 @@ def noise_add(x: torch.Tensor, mode: str, level: float, *, seed: int = 0, offset
     lib = _lib.load()
     ws_bytes = lib.idn_noise_add_workspace_size(kind, n, h, w, c)
     ws = _workspace(ws_bytes, xb.device) if ws_bytes else None
-    rc = lib.idn_noise_add_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
-                              y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c, kind,
-                              p0, p1, int(seed) & (2 ** 64 - 1), int(offset),
-                              rp.data_ptr() if rp is not None else None,
-                              ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
-    _lib.check(rc, "idn_noise_add_u8")
+    if image_ids is not None:
+        if rp is not None:
+            raise ValueError("noise_add: image_ids applies to the Philox stream, not to replay")
+        ids = _ids_tensor(image_ids, n, xb.device)
+        rc = lib.idn_noise_add_ids_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
+                                      y64.data_ptr() if y64 is not None else None, n, h, w, c,
+                                      w * c, kind, p0, p1, int(seed) & (2 ** 64 - 1),
+                                      ids.data_ptr(), ws.data_ptr() if ws is not None else None,
+                                      ws_bytes, _stream())
+        _lib.check(rc, "idn_noise_add_ids_u8")
+    else:
+        rc = lib.idn_noise_add_u8(xb.data_ptr(), y8.data_ptr() if y8 is not None else None,
+                                  y64.data_ptr() if y64 is not None else None, n, h, w, c, w * c,
+                                  kind, p0, p1, int(seed) & (2 ** 64 - 1), int(offset),
+                                  rp.data_ptr() if rp is not None else None,
+                                  ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+        _lib.check(rc, "idn_noise_add_u8")
     if out == "u8":
         return _finish(y8, sq)
     if out == "f64":

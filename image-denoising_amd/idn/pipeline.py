@@ -94,9 +94,8 @@ class Preprocessor:
             if self.noise_rng == "numpy":
                 return ops.noise_add(x, op, level, replay=self._numpy_add_field(x, op), out=out)
             if ids != list(range(ids[0], ids[0] + len(ids))):
-                return torch.cat([ops.noise_add(x[k:k + 1], op, level, seed=self.seed,
-                                                offset=int(i), out=out)
-                                  for k, i in enumerate(ids)])
+                # non-contiguous image ids (a mixed batch): one launch with the id array
+                return ops.noise_add(x, op, level, seed=self.seed, image_ids=ids, out=out)
             return ops.noise_add(x, op, level, seed=self.seed, offset=int(ids[0]), out=out)
         mode = {"gaussian": "gaussian", "speckle": "speckle", "sap": "s&p", "poisson": "poisson"}[op]
         kw = {}
@@ -108,9 +107,9 @@ class Preprocessor:
         replay = self._numpy_field(x, mode, kw) if self.noise_rng == "numpy" else None
         offsets = ids
         if replay is None and offsets != list(range(offsets[0], offsets[0] + len(offsets))):
-            # non-contiguous image ids: one launch per image keeps the (seed, id) stream
-            return torch.cat([ops.random_noise(x[k:k + 1], mode, seed=self.seed, offset=int(i),
-                                               out=out, **kw) for k, i in enumerate(offsets)])
+            # non-contiguous image ids (a mixed batch): one launch with the id array keeps the
+            # (seed, id) stream of every image
+            return ops.random_noise(x, mode, seed=self.seed, image_ids=offsets, out=out, **kw)
         return ops.random_noise(x, mode, seed=self.seed, offset=int(offsets[0]), replay=replay,
                                 out=out, **kw)
 

@@ -101,6 +101,13 @@ int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, in
                  uint64_t offset, const double* replay, void* workspace, size_t ws_bytes,
                  void* stream);
 size_t idn_noise_workspace_size(int kind, int n);
+/* As idn_noise_u8 (Philox stream only) with an explicit device array of n image ids instead of
+ * offset + i: a mixed batch's images of one noise type (any ids) run as one launch and draw
+ * exactly what per-image calls with offset = id would.  Replaces the per-image dispatch of the
+ * mix lists (test.py:1611-1677, minibatch.py:1518-1574). */
+int idn_noise_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
+                     int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
+                     const uint64_t* image_ids, void* workspace, size_t ws_bytes, void* stream);
 
 /* The reference's own additive noises (not skimage), SURVEY §8f:
  *   IDN_NOISE_UNIFORM   p0 = high   out = img_as_float(x) + U(0, high)         (test.py:767-903)
@@ -124,6 +131,12 @@ int idn_noise_add_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n
                      uint64_t offset, const double* replay, void* workspace, size_t ws_bytes,
                      void* stream);
 size_t idn_noise_add_workspace_size(int kind, int n, int h, int w, int c);
+/* As idn_noise_add_u8 (Philox stream only) with a device array of n image ids (see
+ * idn_noise_ids_u8). */
+int idn_noise_add_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h,
+                         int w, int c, int64_t row_stride, int kind, double p0, double p1,
+                         uint64_t seed, const uint64_t* image_ids, void* workspace,
+                         size_t ws_bytes, void* stream);
 
 /* Periodic noise pattern of add_periodic_noise (lib/model/test.py:1128-1298):
  * pattern[i] = U8(255*sin(t_i)), t = np.linspace(-A, A, h*w*c), written as u8 HxWxC (pitch w*c).

@@ -102,3 +102,19 @@ def test_additive_offset_is_image_id(dev, mode):
     for i in range(3):
         one = idn.ops.noise_add(x[i:i + 1], mode, 0.2, seed=5, offset=10 + i).cpu().numpy()
         assert np.array_equal(full[i], one[0])
+
+
+@pytest.mark.parametrize("mode", ["uniform", "gamma", "rayleigh", "brownian"])
+def test_additive_image_ids_match_offsets(dev, mode):
+    """one launch over arbitrary image ids == per-image offset launches"""
+    import torch
+    import idn
+    from test_oracle import make_img
+    imgs = np.stack([make_img(24, 40, s) for s in range(3)])
+    x = torch.from_numpy(imgs).cuda()
+    ids = [9, 2, 40]
+    level = {"uniform": 0.2, "gamma": 0.05, "rayleigh": 0.1, "brownian": 1e-6}[mode]
+    u8 = idn.ops.noise_add(x, mode, level, seed=2, image_ids=ids).cpu().numpy()
+    for k, i in enumerate(ids):
+        one = idn.ops.noise_add(x[k:k + 1], mode, level, seed=2, offset=i).cpu().numpy()
+        assert np.array_equal(u8[k], one[0])

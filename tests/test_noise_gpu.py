@@ -270,3 +270,19 @@ def test_poisson_flat_matches_element_kernel(dev, monkeypatch):
         res[flat] = (u8.cpu().numpy(), f64.cpu().numpy())
     assert np.array_equal(res["0"][0], res["1"][0])
     assert np.array_equal(res["0"][1], res["1"][1])
+
+
+@pytest.mark.parametrize("mode,kw", [("gaussian", {"var": 0.1}), ("s&p", {"amount": 0.4}),
+                                     ("poisson", {}), ("speckle", {"var": 1.0})])
+def test_image_ids_match_per_image_offsets(dev, mode, kw):
+    """one launch over arbitrary image ids draws exactly what per-image offset launches draw"""
+    import torch
+    import idn
+    imgs = np.stack([make_img(40, 64, s) for s in range(4)])
+    x = torch.from_numpy(imgs).cuda()
+    ids = [17, 3, 250, 4]
+    u8, f64 = idn.ops.random_noise(x, mode, seed=6, image_ids=ids, out="both", **kw)
+    for k, i in enumerate(ids):
+        one8, one64 = idn.ops.random_noise(x[k:k + 1], mode, seed=6, offset=i, out="both", **kw)
+        assert np.array_equal(u8[k].cpu().numpy(), one8[0].cpu().numpy())
+        assert np.array_equal(f64[k].cpu().numpy(), one64[0].cpu().numpy())
