@@ -61,6 +61,7 @@ def _pipeline(kind):
     state = {}
 
     def step(idn, x, y):
+        import torch
         t = state.get("t")
         if t is None or t.shape != x.shape:
             t = state["t"] = x.new_empty(x.shape)
@@ -84,32 +85,26 @@ def _pipeline(kind):
                 groups = {}
                 for i, k in enumerate(kinds):
                     groups.setdefault(k, []).append(i)
-                state["groups"] = groups = {k: (v[0], len(v)) for k, v in
-                                            _contiguous(groups).items()}
-            for k, (lo, cnt) in groups.items():
-                xs, ts = x[lo:lo + cnt], t[lo:lo + cnt]
+                # images of a type are scattered through the batch, as a mixed loader yields them:
+                # each type is gathered, noised with its image ids in one launch, scattered back
+                state["groups"] = groups = {
+                    k: (v, torch.as_tensor(v, device=x.device)) for k, v in groups.items()}
+            for k, (ids, idx) in groups.items():
                 if k == "original":
-                    ts.copy_(xs)
-                elif k == "periodic":
-                    ops.periodic_noise(xs, 100.0, out=ts)
+                    t.index_copy_(0, idx, x.index_select(0, idx))
+                    continue
+                xs = x.index_select(0, idx)
+                if k == "periodic":
+                    ys = ops.periodic_noise(xs, 100.0)
                 elif k == "s&p":
-                    ops.random_noise(xs, "s&p", amount=0.4, seed=3, offset=lo, out="u8", out_u8=ts)
+                    ys = ops.random_noise(xs, "s&p", amount=0.4, seed=3, image_ids=ids, out="u8")
                 elif k == "poisson":
-                    ops.random_noise(xs, "poisson", seed=3, offset=lo, out="u8", out_u8=ts)
+                    ys = ops.random_noise(xs, "poisson", seed=3, image_ids=ids, out="u8")
                 else:
-                    ops.random_noise(xs, k, var=1.0, seed=3, offset=lo, out="u8", out_u8=ts)
+                    ys = ops.random_noise(xs, k, var=1.0, seed=3, image_ids=ids, out="u8")
+                t.index_copy_(0, idx, ys)
             ops.denoise_wavelet(t, "db1", 3, out_u8=y)
     return step
-
-
-def _contiguous(groups):
-    """mixed batch: images of one noise type are made contiguous (the bench's synthetic batch
-    is laid out by type, as a type-grouped loader would do)"""
-    out, lo = {}, 0
-    for k in sorted(groups):
-        out[k] = [lo + i for i in range(len(groups[k]))]
-        lo += len(groups[k])
-    return out
 
 
 PIPELINES = {
