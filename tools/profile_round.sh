@@ -27,7 +27,7 @@ for op in $OPS; do
 done
 step 400 prof_stats rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o stats --output-format csv -- python3 bench.py --no-cpu --steps 20 --warmup 5
 if [ "$MODE" = full ]; then
-  for op in median5 bilateral box3 noise_gaussian wavelet_haar3; do
+  for op in median3 median5 bilateral box3 noise_gaussian wavelet_haar3 cfg3 cfg4 cfg5; do
     step 300 prof_stats_$op rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof_$op" -o stats --output-format csv -- python3 bench.py --op $op --no-cpu --steps 10 --warmup 3
   done
 fi
