@@ -69,13 +69,22 @@ __host__ __device__ __forceinline__ int clampi(int i, int lo, int hi) {
 // ---- Philox4x32-10 (Salmon et al., SC'11) --------------------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 
+// a ^ b ^ c: one v_bitop3_b32 (truth table 0x96) on gfx950
+__host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 __host__ __device__ __forceinline__ void philox_round(u32x4& c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
   // one 32x32->64 product per word (v_mad_u64_u32 on the device instead of mul_hi + mul_lo)
   const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
   const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
   const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-  c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+  c = u32x4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
 }
 
 __host__ __device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint64_t key) {

@@ -29,12 +29,14 @@ __device__ __forceinline__ double clip01(double v) { return __builtin_fmin(__bui
 // (255 * out).astype(np.uint8) for out in [0, 1]: truncation (out is never negative here)
 __device__ __forceinline__ uint8_t u8_of(double out) { return (uint8_t)(int)__dmul_rn(out, 255.0); }
 
-// two standard normals from one Philox block (Box-Muller, fp32 transcendental: v_log/v_sin/v_cos
-// take revolutions, so theta = u2 needs no 2*pi multiply)
+// two standard normals from one Philox block (Box-Muller, fp32 hardware transcendentals:
+// v_log/v_sqrt/v_sin/v_cos; sin/cos take revolutions, so theta = u2 needs no 2*pi multiply, and
+// the raw v_sqrt_f32 (1 ulp) replaces the 13-instruction correctly rounded sqrtf sequence)
 __device__ __forceinline__ void normal2(const u32x4& r, float& z0, float& z1) {
   const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
   const float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);           // [0, 1)
-  const float rad = __builtin_sqrtf(-2.0f * 0.6931471805599453f * __builtin_amdgcn_logf(u1));
+  const float rad =
+      __builtin_amdgcn_sqrtf(-2.0f * 0.6931471805599453f * __builtin_amdgcn_logf(u1));
   z0 = rad * __builtin_amdgcn_cosf(u2);
   z1 = rad * __builtin_amdgcn_sinf(u2);
 }
@@ -119,7 +121,9 @@ __device__ __forceinline__ void normal4(const u32x4& r, float (&z)[4]) {
   normal2(r2, z[2], z[3]);
 }
 
-template <int KIND>
+// MEAN0: mean == 0.0, so mean + sd*z is sd*z exactly up to the sign of a zero, which the
+// following x + n / x + x*n (x >= 0) cannot see: one float64 add per element less
+template <int KIND, bool MEAN0 = false>
 __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t t_flip,
                                                            uint32_t t_salt) {
   const int img = blockIdx.y;
@@ -155,7 +159,8 @@ __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t
       normal4(r, z);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const double nz = __dadd_rn(a.p0, __dmul_rn(a.p1, (double)z[b]));
+        const double sz = __dmul_rn(a.p1, (double)z[b]);
+        const double nz = MEAN0 ? sz : __dadd_rn(a.p0, sz);
         const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
         if (KIND == IDN_NOISE_GAUSSIAN) outv[b] = clip01(__dadd_rn(xv, nz));
         else outv[b] = clip01(__dadd_rn(xv, __dmul_rn(xv, nz)));
@@ -581,8 +586,13 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       const int64_t work = (a.elems + 1) / 2 * n;
       if (flat) {
         const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
-        if (kind == IDN_NOISE_GAUSSIAN)
+        const bool m0 = a.p0 == 0.0;
+        if (kind == IDN_NOISE_GAUSSIAN && m0)
+          hipLaunchKernelGGL((noise_flat16_kernel<IDN_NOISE_GAUSSIAN, true>), grid, dim3(256), 0, st, a, 0u, 0u);
+        else if (kind == IDN_NOISE_GAUSSIAN)
           hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_GAUSSIAN>, grid, dim3(256), 0, st, a, 0u, 0u);
+        else if (m0)
+          hipLaunchKernelGGL((noise_flat16_kernel<IDN_NOISE_SPECKLE, true>), grid, dim3(256), 0, st, a, 0u, 0u);
         else
           hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SPECKLE>, grid, dim3(256), 0, st, a, 0u, 0u);
       } else if (kind == IDN_NOISE_GAUSSIAN)
