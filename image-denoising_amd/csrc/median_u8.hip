@@ -21,7 +21,10 @@
 namespace idn {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+// Lanes hold float16 1024 + v (unpack_row_f16): 2-input min/max as packed u16, 3-input as the
+// packed float16 v_pk_minimum3_f16 / v_pk_maximum3_f16 (exact: they return one of the inputs)
 struct PkOps {
   __device__ __forceinline__ uint32_t mn(uint32_t a, uint32_t b) const {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
@@ -30,6 +33,20 @@ struct PkOps {
   __device__ __forceinline__ uint32_t mx(uint32_t a, uint32_t b) const {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
                                                                   __builtin_bit_cast(u16x2, b)));
+  }
+  __device__ __forceinline__ uint32_t mn3(uint32_t a, uint32_t b, uint32_t c) const {
+    return __builtin_bit_cast(
+        uint32_t, __builtin_elementwise_minimum(
+                      __builtin_bit_cast(f16x2, a),
+                      __builtin_elementwise_minimum(__builtin_bit_cast(f16x2, b),
+                                                    __builtin_bit_cast(f16x2, c))));
+  }
+  __device__ __forceinline__ uint32_t mx3(uint32_t a, uint32_t b, uint32_t c) const {
+    return __builtin_bit_cast(
+        uint32_t, __builtin_elementwise_maximum(
+                      __builtin_bit_cast(f16x2, a),
+                      __builtin_elementwise_maximum(__builtin_bit_cast(f16x2, b),
+                                                    __builtin_bit_cast(f16x2, c))));
   }
   __device__ __forceinline__ uint32_t med3(uint32_t a, uint32_t b, uint32_t c) const {
     return mx(mn(a, b), mn(mx(a, b), c));
@@ -73,9 +90,9 @@ __device__ __forceinline__ v4u median3_cols_out(const uint32_t (&U0)[8], const u
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int P = 4 * q + 8 + e;
-      const uint32_t lmax = op.mx(op.mx(V[0].at(P - C), V[0].at(P)), V[0].at(P + C));
+      const uint32_t lmax = op.mx3(V[0].at(P - C), V[0].at(P), V[0].at(P + C));
       const uint32_t mmed = op.med3(V[1].at(P - C), V[1].at(P), V[1].at(P + C));
-      const uint32_t hmin = op.mn(op.mn(V[2].at(P - C), V[2].at(P)), V[2].at(P + C));
+      const uint32_t hmin = op.mn3(V[2].at(P - C), V[2].at(P), V[2].at(P + C));
       v[e] = op.med3(lmax, mmed, hmin);
     }
     o[q] = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);  // low byte of each u16 lane
@@ -187,7 +204,7 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
           Lx = v4u{lead_fix<C, BORDER_REPLICATE>(L, -8), lead_fix<C, BORDER_REPLICATE>(L, -4),
                    L[0], L[1]};
         }
-        unpack_row(Lx, Wr[u % K]);
+        unpack_row_f16(Lx, Wr[u % K]);
       }
       const int y = y0 + r - 2 * R;
       if (r >= 2 * R && y < y1) {

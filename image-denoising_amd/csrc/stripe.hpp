@@ -174,6 +174,19 @@ __device__ __forceinline__ void vwin_tail_fix(VWin& V, int base) {
   V.SO[mb + 1] = nO[1];
 }
 
+// as unpack_row with 0x64 in the high byte of every u16 lane: each lane is the float16 value
+// 1024 + v (a normal number, exact), whose bit pattern orders as v does, so the u16 and the
+// float16 min/max instructions (v_pk_minimum3_f16 / v_pk_maximum3_f16) agree on it; the low byte
+// is still v
+__device__ __forceinline__ void unpack_row_f16(const v4u& x, uint32_t (&U)[8]) {
+  const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    U[j] = (d[j] & 0x00FF00FFu) | 0x64006400u;
+    U[4 + j] = __builtin_amdgcn_perm(0x64646464u, d[j], 0x04030401u);
+  }
+}
+
 // one input row -> 8 u16x2 dwords: [0..3] even bytes of chunk dwords 0..3, [4..7] odd bytes
 __device__ __forceinline__ void unpack_row(const v4u& x, uint32_t (&U)[8]) {
   const uint32_t d[4] = {x.x, x.y, x.z, x.w};

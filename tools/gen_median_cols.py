@@ -184,7 +184,7 @@ def emit(net, outs, nout):
     lines = [
         "// GENERATED by tools/gen_median_cols.py -- do not edit.",
         "// 5x5 median over pre-sorted window columns (proven by the 0-1 principle under the",
-        "// sorted-column premise; see the generator).  F must provide mn / mx.",
+        "// sorted-column premise; see the generator).  F must provide mn / mx / mn3 / mx3.",
         "#pragma once",
         "",
         "namespace idn {",
@@ -202,25 +202,67 @@ def emit(net, outs, nout):
               "template <typename T, typename F>",
               f"__device__ __forceinline__ void median25_chain{nout}(const T (&x)[{nout + 4}][5], "
               f"T (&o)[{nout}], F ops) {{"]
-    for k, v in enumerate(ops):
-        kind, a, b = net.vals[v]
+    prog = fuse3(net, ops, outs)
+    verify_program(net, prog, outs)
+    for k, (v, kind, args) in enumerate(prog):
         name[v] = f"t{k}"
-        fn = "ops.mn" if kind == "min" else "ops.mx"
-        lines.append(f"  const T t{k} = {fn}({name[a]}, {name[b]});")
+        fn = ("ops.mn" if kind == "min" else "ops.mx") + ("3" if len(args) == 3 else "")
+        lines.append(f"  const T t{k} = {fn}({', '.join(name[a] for a in args)});")
     for k, o in enumerate(outs):
         lines.append(f"  o[{k}] = {name[o]};")
     lines += ["}", "", "}  // namespace idn", ""]
     OUT.write_text("\n".join(lines))
-    return len(ops)
+    return len(ops), len(prog)
+
+
+def fuse3(net, ops, outs):
+    """3-input min/max (v_pk_minimum3_f16 / v_pk_maximum3_f16): a node z = op(x, y) absorbs a
+    2-input child x of the same op that nothing else reads.  Greedy from the outputs down."""
+    fan = {}
+    for v in ops:
+        for a in net.vals[v][1:]:
+            fan[a] = fan.get(a, 0) + 1
+    for o in outs:
+        fan[o] = fan.get(o, 0) + 1
+    args = {v: list(net.vals[v][1:]) for v in ops}
+    kind = {v: net.vals[v][0] for v in ops}
+    gone = set()
+    for z in reversed(ops):
+        if z in gone or len(args[z]) == 3:
+            continue
+        for i, x in enumerate(args[z]):
+            if x in kind and x not in gone and kind[x] == kind[z] and fan[x] == 1 \
+                    and len(args[x]) == 2:
+                args[z] = args[z][:i] + args[x] + args[z][i + 1:]
+                gone.add(x)
+                break
+    return [(v, kind[v], args[v]) for v in ops if v not in gone]
+
+
+def verify_program(net, prog, outs):
+    """re-simulate the emitted (fused) program over the premise set: same truth tables"""
+    tt = {idx: net.tt[idx] for idx in net.leaf.values()}
+    for key, idx in net.by_tt.items():
+        if net.vals[idx][0] == "const":
+            tt[idx] = net.tt[idx]
+    for v, kind, args in prog:
+        acc = tt[args[0]]
+        for a in args[1:]:
+            acc = (acc & tt[a]) if kind == "min" else (acc | tt[a])
+        tt[v] = acc
+    for o in outs:
+        if not np.array_equal(tt[o], net.tt[o]):
+            raise SystemExit("fused program FAILED")
 
 
 def main():
     verify_sort5()
     nout = 5
     net, outs = chain_net(nout)
-    n = emit(net, outs, nout)
-    print(f"sort5: 9 comparators PROVEN; chain of {nout}: {n} ops ({n / nout:.1f} per output), "
-          f"0-1 principle PROVEN over {net.n} premise vectors; wrote {OUT}")
+    n, nf = emit(net, outs, nout)
+    print(f"sort5: 9 comparators PROVEN; chain of {nout}: {n} 2-input ops ({n / nout:.1f} per "
+          f"output), {nf} after 3-input fusion; 0-1 principle PROVEN over {net.n} premise "
+          f"vectors; wrote {OUT}")
 
 
 if __name__ == "__main__":
