@@ -440,32 +440,15 @@ __device__ __forceinline__ unsigned long long absbits(double v) {
   return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
 }
 
-// one histogram pass over keys[0..n) (only keys matching the prefix); narrows the state.
-// total (optional) receives the number of nonzero keys seen (first pass only).
-__device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int wd, RadixState& rsx,
-                           uint32_t* hist, uint32_t* total) {
-  const int nb = 1 << wd;
-  for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
-  __syncthreads();
-  const unsigned long long prefix = rsx.prefix, pmask = rsx.pmask;
-  // 8 loads in flight per thread (a one-load-per-iteration loop is latency-bound)
-  for (size_t k0 = threadIdx.x; k0 < n; k0 += 8 * (size_t)blockDim.x) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const size_t k = k0 + (size_t)u * blockDim.x;
-      v[u] = k < n ? d[k] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const unsigned long long key = absbits(v[u]);
-      if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
-    }
-  }
-  __syncthreads();
-  // block-wide scan of the histogram: thread i owns bins [i*per, (i+1)*per); the thread whose
-  // count range holds the rank finds the bin (a serial scan of 2048 LDS bins by one thread costs
-  // ~100k cycles per pass)
+// block-wide selection over an LDS histogram: the bin holding rank `rank` and the rank within
+// it.  Thread i owns bins [i*per, (i+1)*per); the thread whose count range holds the rank finds
+// the bin (a serial scan of 2048 LDS bins by one thread costs ~100k cycles).  lower_mid: select
+// the lower middle rank (total-1)/2 instead, and return the total through *total.
+struct BinSel {
+  uint32_t bin, rank;
+};
+__device__ BinSel select_bin(const uint32_t* hist, int nb, uint32_t rank, uint32_t* total,
+                             bool lower_mid) {
   __shared__ uint32_t sel_bin, sel_rank, wsum[32], tot_s;
   const int T = blockDim.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int per = (nb + T - 1) / T, b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
@@ -490,25 +473,54 @@ __device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int w
     sel_rank = 0;
   }
   __syncthreads();
-  if (total) {
-    if (threadIdx.x == 0) *total = tot_s;
-    rsx.rank = tot_s ? (tot_s - 1) / 2 : 0;  // lower middle rank
+  if (lower_mid) {
+    if (total) *total = tot_s;
+    rank = tot_s ? (tot_s - 1) / 2 : 0;
   }
   const uint32_t excl = wsum[wv] + inc - own;
-  if (own && rsx.rank >= excl && rsx.rank < excl + own) {
+  if (own && rank >= excl && rank < excl + own) {
     uint32_t acc = excl;
     int b = b0;
     for (; b < b1 - 1; ++b) {
-      if (acc + hist[b] > rsx.rank) break;
+      if (acc + hist[b] > rank) break;
       acc += hist[b];
     }
     sel_bin = (uint32_t)b;
-    sel_rank = rsx.rank - acc;
+    sel_rank = rank - acc;
   }
   __syncthreads();
-  rsx.prefix |= (unsigned long long)sel_bin << sh;
+  const BinSel r{sel_bin, sel_rank};
+  __syncthreads();
+  return r;
+}
+
+// one histogram pass over keys[0..n) (only keys matching the prefix); narrows the state.
+// total (optional) receives the number of nonzero keys seen (first pass only).
+__device__ void radix_pass(const double* __restrict__ d, size_t n, int sh, int wd, RadixState& rsx,
+                           uint32_t* hist, uint32_t* total) {
+  const int nb = 1 << wd;
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
+  __syncthreads();
+  const unsigned long long prefix = rsx.prefix, pmask = rsx.pmask;
+  // 8 loads in flight per thread (a one-load-per-iteration loop is latency-bound)
+  for (size_t k0 = threadIdx.x; k0 < n; k0 += 8 * (size_t)blockDim.x) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t k = k0 + (size_t)u * blockDim.x;
+      v[u] = k < n ? d[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const unsigned long long key = absbits(v[u]);
+      if (key != 0 && (key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  const BinSel bs = select_bin(hist, nb, rsx.rank, total, total != nullptr);
+  rsx.prefix |= (unsigned long long)bs.bin << sh;
   rsx.pmask |= (unsigned long long)(nb - 1) << sh;
-  rsx.rank = sel_rank;
+  rsx.rank = bs.rank;
   __syncthreads();
 }
 
@@ -1102,10 +1114,20 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
   }
 }
 
-// sigma for the fused path: an exponent histogram of the stored dd1 locates the bin holding the
-// lower middle rank; one pass over the stored dd1 compacts that bin's keys into
-// scratch and takes the smallest key of the next nonempty bin (the upper middle rank may live
-// there); the remaining digits are selected on the compacted keys.
+// sigma for the fused path.  Pass 1: a 1024-bin histogram of the nonzero |dd1| keys by exponent
+// and the top 4 mantissa bits (monotone in the key; the clamped exponent bins keep one sub-bin)
+// locates the fine bin holding the lower middle rank (block-wide scan).  Pass 2 compacts that
+// bin's keys into scratch (about 1/16 of a binade) and takes the smallest key of the next
+// nonempty bin (the upper middle rank may live there); the remaining digits are selected on the
+// compacted keys.
+constexpr int WL_FBINS = WL_EBINS * 16;
+__device__ __forceinline__ int wl_fbin(unsigned long long key) {
+  const int e = (int)(key >> 52) - (1023 - 61);
+  if (e < 0) return 0;
+  if (e > WL_EBINS - 1) return WL_FBINS - 1;
+  return e * 16 + (int)((key >> 48) & 15u);
+}
+
 __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, size_t img_floats,
                                                        double* __restrict__ stats, WlLayout Lt) {
   const int img = blockIdx.x / 3, c = blockIdx.x % 3;
@@ -1113,12 +1135,19 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
   const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
   double* scratch = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;  // unused input-plane slot
   double* st = stats + (size_t)img * WL_STATS;
-  __shared__ uint32_t hist[2048];
-  __shared__ uint32_t m_s, le_s, total_s, bin_s, rank_s, next_s;
+  // 8 copies of the fine histogram (by lane & 7: |dd| crowds into few bins, one copy would
+  // serialise the LDS atomics); copy k lives at hist[k * WL_FBINS ..]
+  __shared__ uint32_t hist[8 * WL_FBINS];
+  __shared__ uint32_t m_s, le_s, next_s;
   __shared__ unsigned long long nmin_s, gt_s;
-  // pass 1: exponent histogram of the nonzero |dd| (16 copies by lane & 15: |dd| takes few
-  // exponents, one copy would serialise the LDS atomics); copy k lives at hist[k * 64 ..]
-  for (int k = threadIdx.x; k < 16 * WL_EBINS; k += 1024) hist[k] = 0u;
+  for (int k = threadIdx.x; k < 8 * WL_FBINS; k += 1024) hist[k] = 0u;
+  if (threadIdx.x == 0) {
+    m_s = 0;
+    le_s = 0;
+    next_s = WL_FBINS;
+    nmin_s = ~0ull;
+    gt_s = ~0ull;
+  }
   __syncthreads();
   for (size_t k0 = threadIdx.x; k0 < bsz; k0 += 8 * 1024) {
     double vv[8];
@@ -1130,46 +1159,29 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const unsigned long long key = absbits(vv[u]);
-      if (key) atomicAdd(&hist[(threadIdx.x & 15) * WL_EBINS + wl_ebin(key)], 1u);
+      if (key) atomicAdd(&hist[(threadIdx.x & 7) * WL_FBINS + wl_fbin(key)], 1u);
     }
   }
   __syncthreads();
-  __shared__ uint32_t eh[WL_EBINS];
-  if (threadIdx.x < WL_EBINS) {
+  {  // fold the copies into copy 0 (one bin per thread)
+    const int b = threadIdx.x;
     uint32_t v = 0;
-    for (int cp = 0; cp < 16; ++cp) v += hist[cp * WL_EBINS + threadIdx.x];
-    eh[threadIdx.x] = v;
+#pragma unroll
+    for (int cp = 0; cp < 8; ++cp) v += hist[cp * WL_FBINS + b];
+    hist[b] = v;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int b = 0; b < WL_EBINS; ++b) t += eh[b];
-    total_s = t;
-    const uint32_t klo = t ? (t - 1) / 2 : 0;
-    uint32_t acc = 0;
-    int b = 0;
-    for (; b < WL_EBINS - 1; ++b) {
-      if (acc + eh[b] > klo) break;
-      acc += eh[b];
-    }
-    bin_s = (uint32_t)b;
-    rank_s = klo - acc;
-    int nb = b + 1;
-    while (nb < WL_EBINS && eh[nb] == 0) ++nb;
-    next_s = (uint32_t)nb;  // WL_EBINS: none
-    m_s = 0;
-    le_s = 0;
-    nmin_s = ~0ull;
-    gt_s = ~0ull;
-  }
+  uint32_t total = 0;
+  const BinSel bs = select_bin(hist, WL_FBINS, 0u, &total, true);
+  const int bsel = (int)bs.bin;
+  if ((int)threadIdx.x > bsel && hist[threadIdx.x]) atomicMin(&next_s, threadIdx.x);
   __syncthreads();
-  const uint32_t total = total_s;
   double med;
   if (total == 0) {
     med = NAN;  // np.median of an empty selection
   } else {
     const uint32_t klo = (total - 1) / 2, khi = total / 2;
-    const int bsel = (int)bin_s, bnext = (int)next_s;
+    const int bnext = (int)next_s;
     const int lane = threadIdx.x & 63;
     unsigned long long nmin = ~0ull;
     for (size_t k0 = threadIdx.x; k0 < bsz; k0 += 8 * 1024) {
@@ -1183,7 +1195,7 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
       for (int u = 0; u < 8; ++u) {
         const double v = vv[u];
         const unsigned long long key = absbits(v);
-        const int b = key ? wl_ebin(key) : -1;
+        const int b = key ? wl_fbin(key) : -1;
         if (b == bnext) nmin = key < nmin ? key : nmin;
         const bool hit = b == bsel;
         const unsigned long long m = __ballot(hit);
@@ -1203,23 +1215,30 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
     if (lane == 0) atomicMin(&nmin_s, nmin);
     __syncthreads();
     const size_t mcnt = m_s;
-    RadixState rsx{0ull, 0ull, rank_s};
-    if (bsel > 0 && bsel < WL_EBINS - 1) {  // an unclamped bin is one exponent: digit known
-      rsx.prefix = (unsigned long long)(bsel + (1023 - 61)) << 52;
-      rsx.pmask = 0x7FFull << 52;
+    const uint32_t rank_in = bs.rank;
+    RadixState rsx{0ull, 0ull, rank_in};
+    if (bsel > 0 && bsel < WL_FBINS - 1) {  // an unclamped bin: exponent and 4 mantissa bits known
+      rsx.prefix = ((unsigned long long)(bsel / 16 + (1023 - 61)) << 52) |
+                   ((unsigned long long)(bsel % 16) << 48);
+      rsx.pmask = 0x7FFFull << 48;
+      radix_pass(scratch, mcnt, 37, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 26, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 15, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 4, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 0, 4, rsx, hist, nullptr);
     } else {
       radix_pass(scratch, mcnt, 52, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 41, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 30, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 19, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 8, 11, rsx, hist, nullptr);
+      radix_pass(scratch, mcnt, 0, 8, rsx, hist, nullptr);
     }
-    radix_pass(scratch, mcnt, 41, 11, rsx, hist, nullptr);
-    radix_pass(scratch, mcnt, 30, 11, rsx, hist, nullptr);
-    radix_pass(scratch, mcnt, 19, 11, rsx, hist, nullptr);
-    radix_pass(scratch, mcnt, 8, 11, rsx, hist, nullptr);
-    radix_pass(scratch, mcnt, 0, 8, rsx, hist, nullptr);
     const unsigned long long lo_key = rsx.prefix;
     const double vlo = __longlong_as_double((long long)lo_key);
     double vhi = vlo;
     if (khi != klo) {
-      if (rank_s + 1 < mcnt) {  // the upper middle rank is in the same bin
+      if (rank_in + 1 < mcnt) {  // the upper middle rank is in the same bin
         uint32_t le = 0;
         unsigned long long gt = ~0ull;
         for (size_t k = threadIdx.x; k < mcnt; k += 1024) {
@@ -1237,7 +1256,7 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
           atomicMin(&gt_s, gt);
         }
         __syncthreads();
-        if (le_s <= rank_s + 1) vhi = __longlong_as_double((long long)gt_s);
+        if (le_s <= rank_in + 1) vhi = __longlong_as_double((long long)gt_s);
       } else {  // it is the smallest key of the next nonempty bin
         vhi = __longlong_as_double((long long)nmin_s);
       }
