@@ -103,6 +103,16 @@ __device__ __forceinline__ int wl_ebin(unsigned long long key) {
   return e < 0 ? 0 : (e > WL_EBINS - 1 ? WL_EBINS - 1 : e);
 }
 
+// fine bins of |dd| keys: exponent (clamped as wl_ebin) and the top 4 mantissa bits, monotone in
+// the key; the clamped exponent bins keep one sub-bin
+constexpr int WL_FBINS = WL_EBINS * 16;
+__device__ __forceinline__ int wl_fbin(unsigned long long key) {
+  const int e = (int)(key >> 52) - (1023 - 61);
+  if (e < 0) return 0;
+  if (e > WL_EBINS - 1) return WL_FBINS - 1;
+  return e * 16 + (int)((key >> 48) & 15u);
+}
+
 inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   WlLayout Lt;
   Lt.n = n;
@@ -970,12 +980,17 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_analyze(
           }
         haar2x2(r[0][0], r[0][1], r[1][0], r[1][1], a1[0], d1[0][0], d1[1][0], d1[2][0]);
       }
-      wreal* ddp = ws + img * img_floats + dd_off + (size_t)c * 4 * bsz + 3 * bsz;
+      // the finest dd is kept only as its fine-bin code (0: exact zero, else wl_fbin + 1): the
+      // sigma median recomputes the exact values of the one or two bins it needs
+      uint16_t* cdp = reinterpret_cast<uint16_t*>(ws + img * img_floats + dd_off +
+                                                  (size_t)c * 4 * bsz + 3 * bsz);
 #pragma unroll
       for (int k = 0; k < QS * QS; ++k) {
 #pragma unroll
         for (int b = 0; b < 3; ++b) sq[0][b] += d1[b][k] * d1[b][k];
-        ddp[(size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] = d1[2][k];
+        const unsigned long long key = absbits(d1[2][k]);
+        cdp[(size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] =
+            (uint16_t)(key ? wl_fbin(key) + 1 : 0);
       }
       if constexpr (L >= 2) {  // level 2 on the thread's 2x2 level-1 approximations
         wreal ad, da, dd;
@@ -1114,125 +1129,278 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
   }
 }
 
-// sigma for the fused path.  Pass 1: a 1024-bin histogram of the nonzero |dd1| keys by exponent
-// and the top 4 mantissa bits (monotone in the key; the clamped exponent bins keep one sub-bin)
-// locates the fine bin holding the lower middle rank (block-wide scan).  Pass 2 compacts that
-// bin's keys into scratch (about 1/16 of a binade) and takes the smallest key of the next
-// nonempty bin (the upper middle rank may live there); the remaining digits are selected on the
-// compacted keys.
-constexpr int WL_FBINS = WL_EBINS * 16;
-__device__ __forceinline__ int wl_fbin(unsigned long long key) {
-  const int e = (int)(key >> 52) - (1023 - 61);
-  if (e < 0) return 0;
-  if (e > WL_EBINS - 1) return WL_FBINS - 1;
-  return e * 16 + (int)((key >> 48) & 15u);
+// sigma for the fused path.  wl_haar_analyze left one fine-bin code per finest dd (u16: 0 for an
+// exact zero, else wl_fbin(|dd|) + 1).  Pass 1: histogram of the codes, block-wide selection of
+// the fine bin holding the lower middle rank.  Pass 2: the positions of that bin's codes (and of
+// the next nonempty bin's, where the upper middle rank may live) are compacted; the exact |dd| of
+// just those positions are recomputed from the input (wl_dd1_key: the analysis' loads and op
+// order), and the remaining digits are selected on them.  The fp64 band never goes through HBM.
+template <bool MARK>
+__device__ unsigned long long wl_dd1_key(const uint8_t* __restrict__ src,
+                                         const double* __restrict__ in64, int img, int h, int w,
+                                         int64_t row_stride, uint32_t pos, int W1, int c, wreal mn,
+                                         wreal inv, wreal rcp) {
+  const int i = (int)(pos / (uint32_t)W1), j = (int)(pos - (uint32_t)i * (uint32_t)W1);
+  wreal r[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      double px[3];
+      load_rgb64(src, in64, img, h, w, row_stride, 2 * i + rr, 2 * j + ss, px);
+      const wreal a = ycbcr_c(px, c) - mn;
+      if (MARK) {  // haar_row4_c
+        const wreal q0 = a * rcp;
+        r[rr][ss] = __fma_rn(__fma_rn(-q0, inv, a), rcp, q0);
+      } else {  // L = 1: the plain quotient
+        r[rr][ss] = a / inv;
+      }
+    }
+  wreal aa, ad, da, dd;
+  haar2x2(r[0][0], r[0][1], r[1][0], r[1][1], aa, ad, da, dd);
+  return absbits(dd);
 }
 
-__global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, size_t img_floats,
+// the same for u8 input, split into the loads (two rows of 6 bytes as 3 half-words each: row
+// starts are 4-byte aligned on this path, 6 j is even) and the arithmetic, so that a thread can
+// keep several positions' loads in flight
+struct Dd1Raw {
+  uint32_t r[2][3];
+};
+__device__ __forceinline__ Dd1Raw wl_dd1_load(const uint8_t* __restrict__ src, int img, int h,
+                                              int64_t row_stride, uint32_t pos, int W1) {
+  const int i = (int)(pos / (uint32_t)W1), j = (int)(pos - (uint32_t)i * (uint32_t)W1);
+  Dd1Raw q;
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const uint16_t* p = reinterpret_cast<const uint16_t*>(
+        src + ((int64_t)img * h + 2 * i + rr) * row_stride + (int64_t)6 * j);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) q.r[rr][k] = p[k];
+  }
+  return q;
+}
+template <bool MARK>
+__device__ __forceinline__ unsigned long long wl_dd1_eval(const Dd1Raw& q, int c, wreal mn,
+                                                          wreal inv, wreal rcp) {
+  wreal r[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      double px[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const int b = ss * 3 + ch;
+        px[ch] = (double)((q.r[rr][b >> 1] >> (8 * (b & 1))) & 0xFFu) * (1.0 / 255.0);
+      }
+      const wreal a = ycbcr_c(px, c) - mn;
+      if (MARK) {
+        const wreal q0 = a * rcp;
+        r[rr][ss] = __fma_rn(__fma_rn(-q0, inv, a), rcp, q0);
+      } else {
+        r[rr][ss] = a / inv;
+      }
+    }
+  wreal aa, ad, da, dd;
+  haar2x2(r[0][0], r[0][1], r[1][0], r[1][1], aa, ad, da, dd);
+  return absbits(dd);
+}
+
+constexpr int WLM_WG = 256;  // threads per (image, channel): several workgroups per CU overlap phases
+constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slower: fewer workgroups per CU)
+template <int L>
+__global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restrict__ src,
+                                                       const double* __restrict__ in64,
+                                                       int64_t row_stride,
+                                                       wreal* __restrict__ ws, size_t img_floats,
                                                        double* __restrict__ stats, WlLayout Lt) {
+  constexpr bool MARK = L >= 2;
   const int img = blockIdx.x / 3, c = blockIdx.x % 3;
-  const size_t bsz = (size_t)Lt.H[1] * Lt.W[1];
-  const wreal* d = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;  // dd
-  double* scratch = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;  // unused input-plane slot
+  const int W1 = Lt.W[1];
+  const uint32_t bsz = (uint32_t)Lt.H[1] * (uint32_t)W1;
+  const uint16_t* codes = reinterpret_cast<const uint16_t*>(
+      ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz);
+  // scratch (the unused input-plane slot of this channel, h*w doubles): [0, bsz) keys of the
+  // selected bin, then positions of the selected bin and of the next bin
+  double* keys = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;
+  uint32_t* pos_sel = reinterpret_cast<uint32_t*>(keys + bsz);
+  uint32_t* pos_next = pos_sel + bsz;
   double* st = stats + (size_t)img * WL_STATS;
-  // 8 copies of the fine histogram (by lane & 7: |dd| crowds into few bins, one copy would
+  wreal mn, mx;
+  wl_minmax64(st, c, mn, mx);
+  const wreal inv = mx - mn, rcp = 1.0 / inv;
+  // WLM_NH copies of the histogram (by lane: the codes crowd into few bins, one copy would
   // serialise the LDS atomics); copy k lives at hist[k * WL_FBINS ..]
-  __shared__ uint32_t hist[8 * WL_FBINS];
-  __shared__ uint32_t m_s, le_s, next_s;
+  __shared__ uint32_t hist[WLM_NH * WL_FBINS];
+  __shared__ uint32_t m_s, mn_s, le_s, next_s;
   __shared__ unsigned long long nmin_s, gt_s;
-  for (int k = threadIdx.x; k < 8 * WL_FBINS; k += 1024) hist[k] = 0u;
+  for (int k = threadIdx.x; k < WLM_NH * WL_FBINS; k += WLM_WG) hist[k] = 0u;
   if (threadIdx.x == 0) {
     m_s = 0;
+    mn_s = 0;
     le_s = 0;
     next_s = WL_FBINS;
     nmin_s = ~0ull;
     gt_s = ~0ull;
   }
   __syncthreads();
-  for (size_t k0 = threadIdx.x; k0 < bsz; k0 += 8 * 1024) {
-    double vv[8];
+  // codes in 8-byte groups of 4 (the code array is 8-byte aligned), 8 groups in flight per lane:
+  // every workgroup of the grid is resident at once, so each phase costs its latency chain
+  const uint32_t ngrp = bsz / 4;
+  const uint2* cg = reinterpret_cast<const uint2*>(codes);
+  auto code_at = [](const uint2& g, int q) -> uint32_t {
+    return ((q < 2 ? g.x : g.y) >> (16 * (q & 1))) & 0xFFFFu;
+  };
+  for (uint32_t g0 = threadIdx.x; g0 < ngrp; g0 += 8 * WLM_WG) {
+    uint2 gv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const size_t k = k0 + (size_t)u * 1024;
-      vv[u] = k < bsz ? d[k] : 0.0;
+      const uint32_t g = g0 + (uint32_t)u * WLM_WG;
+      gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const unsigned long long key = absbits(vv[u]);
-      if (key) atomicAdd(&hist[(threadIdx.x & 7) * WL_FBINS + wl_fbin(key)], 1u);
-    }
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t cd = code_at(gv[u], q);
+        if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
+      }
+  }
+  for (uint32_t k = ngrp * 4 + threadIdx.x; k < bsz; k += WLM_WG) {  // tail codes
+    const uint32_t cd = codes[k];
+    if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
   }
   __syncthreads();
-  {  // fold the copies into copy 0 (one bin per thread)
-    const int b = threadIdx.x;
+  for (int b = threadIdx.x; b < WL_FBINS; b += WLM_WG) {  // fold the copies into copy 0
     uint32_t v = 0;
 #pragma unroll
-    for (int cp = 0; cp < 8; ++cp) v += hist[cp * WL_FBINS + b];
+    for (int cp = 0; cp < WLM_NH; ++cp) v += hist[cp * WL_FBINS + b];
     hist[b] = v;
   }
   __syncthreads();
   uint32_t total = 0;
   const BinSel bs = select_bin(hist, WL_FBINS, 0u, &total, true);
   const int bsel = (int)bs.bin;
-  if ((int)threadIdx.x > bsel && hist[threadIdx.x]) atomicMin(&next_s, threadIdx.x);
+  for (int b = threadIdx.x; b < WL_FBINS; b += WLM_WG)
+    if (b > bsel && hist[b]) atomicMin(&next_s, (uint32_t)b);
   __syncthreads();
   double med;
   if (total == 0) {
     med = NAN;  // np.median of an empty selection
   } else {
     const uint32_t klo = (total - 1) / 2, khi = total / 2;
-    const int bnext = (int)next_s;
+    const uint32_t csel = (uint32_t)bsel + 1, cnext = next_s + 1;
     const int lane = threadIdx.x & 63;
-    unsigned long long nmin = ~0ull;
-    for (size_t k0 = threadIdx.x; k0 < bsz; k0 += 8 * 1024) {
-      double vv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {  // 8 loads in flight per thread
-        const size_t k = k0 + (size_t)u * 1024;
-        vv[u] = k < bsz ? d[k] : 0.0;
+    // pass 2: positions of the selected and the next bin.  Each lane counts its hits (selected
+    // bin in the low half-word, next bin in the high one), one wave scan places them and one
+    // LDS atomic per wave and iteration allocates the slots (per-hit ballots with an atomic each
+    // serialise: a 3 % bin hits nearly every wave-wide ballot).
+    auto place = [&](uint32_t cnt2, uint32_t& off_sel, uint32_t& off_next) {
+      uint32_t inc = cnt2;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += t;
       }
+      const uint32_t tot = (uint32_t)__shfl((int)inc, 63);
+      uint32_t base_sel = 0, base_next = 0;
+      if (lane == 63) {
+        if (tot & 0xFFFFu) base_sel = atomicAdd(&m_s, tot & 0xFFFFu);
+        if (tot >> 16) base_next = atomicAdd(&mn_s, tot >> 16);
+      }
+      base_sel = (uint32_t)__shfl((int)base_sel, 63);
+      base_next = (uint32_t)__shfl((int)base_next, 63);
+      const uint32_t excl = inc - cnt2;
+      off_sel = base_sel + (excl & 0xFFFFu);
+      off_next = base_next + (excl >> 16);
+    };
+    for (uint32_t gb = 0; gb < ngrp; gb += 8 * WLM_WG) {  // uniform trip count: the scan needs
+      const uint32_t g0 = gb + threadIdx.x;                // every lane of the wave
+      uint2 gv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const double v = vv[u];
-        const unsigned long long key = absbits(v);
-        const int b = key ? wl_fbin(key) : -1;
-        if (b == bnext) nmin = key < nmin ? key : nmin;
-        const bool hit = b == bsel;
-        const unsigned long long m = __ballot(hit);
-        if (m) {
-          uint32_t base = 0;
-          const int leader = __ffsll((long long)m) - 1;
-          if (lane == leader) base = atomicAdd(&m_s, (uint32_t)__popcll(m));
-          base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-          if (hit) scratch[base + __popcll(m & ((1ull << lane) - 1))] = fabs(v);
+        const uint32_t g = g0 + (uint32_t)u * WLM_WG;
+        gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
+      }
+      uint32_t cnt2 = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t cd = code_at(gv[u], q);
+          cnt2 += (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
+        }
+      if (__ballot(cnt2 != 0) == 0) continue;  // wave-uniform
+      uint32_t os, on;
+      place(cnt2, os, on);
+      if (cnt2) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t cd = code_at(gv[u], q);
+            const uint32_t p = 4 * (g0 + (uint32_t)u * WLM_WG) + (uint32_t)q;
+            if (cd == csel) pos_sel[os++] = p;
+            if (cd == cnext) pos_next[on++] = p;
+          }
+      }
+    }
+    for (uint32_t k0 = ngrp * 4; k0 < bsz; k0 += WLM_WG) {  // tail codes (every lane takes part)
+      const uint32_t k = k0 + threadIdx.x;
+      const uint32_t cd = k < bsz ? codes[k] : 0u;
+      const uint32_t cnt2 = (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
+      uint32_t os, on;
+      place(cnt2, os, on);
+      if (cd == csel) pos_sel[os] = k;
+      if (cd == cnext) pos_next[on] = k;
+    }
+    __syncthreads();
+    const uint32_t mcnt = m_s, ncnt = mn_s;
+    // the selected bin's keys live in LDS when they fit: the level-1 histogram is dead now and
+    // the radix passes use only its first 2048 words
+    constexpr uint32_t LDS_KEYS = (WLM_NH * WL_FBINS - 2048) / 2;
+    double* kb = mcnt <= LDS_KEYS ? reinterpret_cast<double*>(hist + 2048) : keys;
+    // the exact keys of the selected bin, recomputed from the input (u8: 8 positions' loads in
+    // flight per thread; the recompute is latency-bound otherwise)
+    if (in64) {
+      for (uint32_t t = threadIdx.x; t < mcnt; t += WLM_WG)
+        kb[t] = __longlong_as_double((long long)wl_dd1_key<MARK>(
+            src, in64, img, Lt.h, Lt.w, row_stride, pos_sel[t], W1, c, mn, inv, rcp));
+    } else {
+      for (uint32_t t0 = threadIdx.x; t0 < mcnt; t0 += 8 * WLM_WG) {
+        Dd1Raw q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint32_t t = t0 + (uint32_t)u * WLM_WG;
+          q[u] = wl_dd1_load(src, img, Lt.h, row_stride, t < mcnt ? pos_sel[t] : 0u, W1);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint32_t t = t0 + (uint32_t)u * WLM_WG;
+          if (t < mcnt)
+            kb[t] = __longlong_as_double((long long)wl_dd1_eval<MARK>(q[u], c, mn, inv, rcp));
         }
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long on = (unsigned long long)__shfl_xor((long long)nmin, o);
-      nmin = on < nmin ? on : nmin;
-    }
-    if (lane == 0) atomicMin(&nmin_s, nmin);
     __syncthreads();
-    const size_t mcnt = m_s;
     const uint32_t rank_in = bs.rank;
     RadixState rsx{0ull, 0ull, rank_in};
     if (bsel > 0 && bsel < WL_FBINS - 1) {  // an unclamped bin: exponent and 4 mantissa bits known
       rsx.prefix = ((unsigned long long)(bsel / 16 + (1023 - 61)) << 52) |
                    ((unsigned long long)(bsel % 16) << 48);
       rsx.pmask = 0x7FFFull << 48;
-      radix_pass(scratch, mcnt, 37, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 26, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 15, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 4, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 0, 4, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 37, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 26, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 15, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 4, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 0, 4, rsx, hist, nullptr);
     } else {
-      radix_pass(scratch, mcnt, 52, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 41, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 30, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 19, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 8, 11, rsx, hist, nullptr);
-      radix_pass(scratch, mcnt, 0, 8, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 52, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 41, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 30, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 19, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 8, 11, rsx, hist, nullptr);
+      radix_pass(kb, mcnt, 0, 8, rsx, hist, nullptr);
     }
     const unsigned long long lo_key = rsx.prefix;
     const double vlo = __longlong_as_double((long long)lo_key);
@@ -1241,8 +1409,8 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
       if (rank_in + 1 < mcnt) {  // the upper middle rank is in the same bin
         uint32_t le = 0;
         unsigned long long gt = ~0ull;
-        for (size_t k = threadIdx.x; k < mcnt; k += 1024) {
-          const unsigned long long key = absbits(scratch[k]);
+        for (uint32_t k = threadIdx.x; k < mcnt; k += WLM_WG) {
+          const unsigned long long key = absbits(kb[k]);
           if (key <= lo_key) ++le;
           else gt = key < gt ? key : gt;
         }
@@ -1258,6 +1426,18 @@ __global__ __launch_bounds__(1024) void wl_haar_median(wreal* __restrict__ ws, s
         __syncthreads();
         if (le_s <= rank_in + 1) vhi = __longlong_as_double((long long)gt_s);
       } else {  // it is the smallest key of the next nonempty bin
+        unsigned long long nmin = ~0ull;
+        for (uint32_t t = threadIdx.x; t < ncnt; t += WLM_WG) {
+          const unsigned long long key = wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride,
+                                                          pos_next[t], W1, c, mn, inv, rcp);
+          nmin = key < nmin ? key : nmin;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const unsigned long long on = (unsigned long long)__shfl_xor((long long)nmin, o);
+          nmin = on < nmin ? on : nmin;
+        }
+        if (lane == 0) atomicMin(&nmin_s, nmin);
+        __syncthreads();
         vhi = __longlong_as_double((long long)nmin_s);
       }
     }
@@ -1296,7 +1476,8 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     Ls.part_tile0[l] = (size_t)(l - 1) * nwg;
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * L * 3), dim3(256), 0, st, stats, part, Ls);
-  hipLaunchKernelGGL(wl_haar_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
+  hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
+                     wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   hipLaunchKernelGGL((wl_haar_synth<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
                      Lt.w, row_stride, stats, out_u8, out_f32);
