@@ -782,6 +782,7 @@ __global__ __launch_bounds__(256) void wl_idwt_final(const wreal* __restrict__ w
 // The arithmetic is op for op the general path's (multiply then add, axis 0 then axis 1; the
 // synthesis sums A, AD, DA, DD in that order), so the coefficients are bitwise the same.
 constexpr int WLH_WG = 128;  // threads per workgroup (wl_layout sizes the partials for it)
+constexpr int WLH_IT = 4;    // wl_haar_analyze: chunks of WLH_WG sub-blocks per thread
 
 // pywt dwt2 of one 2x2 group, rows 2i / 2i+1 (x0j / x1j), columns 2j / 2j+1
 __device__ __forceinline__ void haar2x2(wreal x00, wreal x01, wreal x10, wreal x11, wreal& aa,
@@ -939,18 +940,8 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_analyze(
   constexpr int B = HS::B, QS = HS::QS;
   const int img = blockIdx.y;
   const int nbx = w / B, nblk = nbx * (h / B);
-  const int tid = blockIdx.x * WLH_WG + threadIdx.x;
-  const int blk = tid / HS::NS, sub = tid % HS::NS;
-  const bool act = blk < nblk;  // uniform over each block's NS consecutive lanes
   const double* st = stats + (size_t)img * WL_STATS;
   __shared__ double red[3 * L * 3][WLH_WG / 64];
-  int y0 = 0, x0 = 0;
-  if (act) {
-    const int by = blk / nbx, bx = blk - by * nbx;
-    const int sy = sub / (B / HS::SB), sx = sub % (B / HS::SB);
-    y0 = by * B + sy * HS::SB;
-    x0 = bx * B + sx * HS::SB;
-  }
   const size_t W1 = (size_t)(w / 2), bsz = (size_t)(h / 2) * W1;
   // one channel at a time (keeps the live state to one channel's coefficients and sums)
 #pragma unroll 1
@@ -963,53 +954,68 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_analyze(
     for (int l = 0; l < L; ++l)
 #pragma unroll
       for (int b = 0; b < 3; ++b) sq[l][b] = 0.0;
-    wreal a2 = 0;
-    if (act) {
-      wreal a1[QS * QS], d1[3][QS * QS];
-      if constexpr (QS == 2) {
-        haar_sub4_c(src, in64, img, h, w, row_stride, y0, x0, c, mn, inv, a1, d1);
-      } else {  // L = 1: a 2x2 block per thread
-        wreal r[2][2];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-          for (int ss = 0; ss < 2; ++ss) {
-            double px[3];
-            load_rgb64(src, in64, img, h, w, row_stride, y0 + rr, x0 + ss, px);
-            r[rr][ss] = (ycbcr_c(px, c) - mn) / inv;
-          }
-        haar2x2(r[0][0], r[0][1], r[1][0], r[1][1], a1[0], d1[0][0], d1[1][0], d1[2][0]);
+    // WLH_IT chunks of WLH_WG sub-blocks per thread, summed in registers before the one wave
+    // reduction per channel (the reductions, not the arithmetic, dominated at one chunk)
+#pragma unroll 1
+    for (int it = 0; it < WLH_IT; ++it) {
+      const int tid = (blockIdx.x * WLH_IT + it) * WLH_WG + threadIdx.x;
+      const int blk = tid / HS::NS, sub = tid % HS::NS;
+      const bool act = blk < nblk;  // uniform over each block's NS consecutive lanes
+      int y0 = 0, x0 = 0;
+      if (act) {
+        const int by = blk / nbx, bx = blk - by * nbx;
+        const int sy = sub / (B / HS::SB), sx = sub % (B / HS::SB);
+        y0 = by * B + sy * HS::SB;
+        x0 = bx * B + sx * HS::SB;
       }
-      // the finest dd is kept only as its fine-bin code (0: exact zero, else wl_fbin + 1): the
-      // sigma median recomputes the exact values of the one or two bins it needs
-      uint16_t* cdp = reinterpret_cast<uint16_t*>(ws + img * img_floats + dd_off +
-                                                  (size_t)c * 4 * bsz + 3 * bsz);
+      wreal a2 = 0;
+      if (act) {
+        wreal a1[QS * QS], d1[3][QS * QS];
+        if constexpr (QS == 2) {
+          haar_sub4_c(src, in64, img, h, w, row_stride, y0, x0, c, mn, inv, a1, d1);
+        } else {  // L = 1: a 2x2 block per thread
+          wreal r[2][2];
 #pragma unroll
-      for (int k = 0; k < QS * QS; ++k) {
+          for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) sq[0][b] += d1[b][k] * d1[b][k];
-        const unsigned long long key = absbits(d1[2][k]);
-        cdp[(size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] =
-            (uint16_t)(key ? wl_fbin(key) + 1 : 0);
+            for (int ss = 0; ss < 2; ++ss) {
+              double px[3];
+              load_rgb64(src, in64, img, h, w, row_stride, y0 + rr, x0 + ss, px);
+              r[rr][ss] = (ycbcr_c(px, c) - mn) / inv;
+            }
+          haar2x2(r[0][0], r[0][1], r[1][0], r[1][1], a1[0], d1[0][0], d1[1][0], d1[2][0]);
+        }
+        // the finest dd is kept only as its fine-bin code (0: exact zero, else wl_fbin + 1): the
+        // sigma median recomputes the exact values of the one or two bins it needs
+        uint16_t* cdp = reinterpret_cast<uint16_t*>(ws + img * img_floats + dd_off +
+                                                    (size_t)c * 4 * bsz + 3 * bsz);
+#pragma unroll
+        for (int k = 0; k < QS * QS; ++k) {
+#pragma unroll
+          for (int b = 0; b < 3; ++b) sq[0][b] += d1[b][k] * d1[b][k];
+          const unsigned long long key = absbits(d1[2][k]);
+          cdp[(size_t)(y0 / 2 + k / QS) * W1 + x0 / 2 + k % QS] =
+              (uint16_t)(key ? wl_fbin(key) + 1 : 0);
+        }
+        if constexpr (L >= 2) {  // level 2 on the thread's 2x2 level-1 approximations
+          wreal ad, da, dd;
+          haar2x2(a1[0], a1[1], a1[2], a1[3], a2, ad, da, dd);
+          sq[1][0] += ad * ad;
+          sq[1][1] += da * da;
+          sq[1][2] += dd * dd;
+        }
       }
-      if constexpr (L >= 2) {  // level 2 on the thread's 2x2 level-1 approximations
-        wreal ad, da, dd;
-        haar2x2(a1[0], a1[1], a1[2], a1[3], a2, ad, da, dd);
-        sq[1][0] += ad * ad;
-        sq[1][1] += da * da;
-        sq[1][2] += dd * dd;
-      }
-    }
-    if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
-      const int base = (threadIdx.x & 63) & ~3;
-      const wreal x00 = __shfl(a2, base), x01 = __shfl(a2, base + 1);
-      const wreal x10 = __shfl(a2, base + 2), x11 = __shfl(a2, base + 3);
-      wreal aa, ad, da, dd;
-      haar2x2(x00, x01, x10, x11, aa, ad, da, dd);
-      if (act && sub == 0) {
-        sq[2][0] += ad * ad;
-        sq[2][1] += da * da;
-        sq[2][2] += dd * dd;
+      if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
+        const int base = (threadIdx.x & 63) & ~3;
+        const wreal x00 = __shfl(a2, base), x01 = __shfl(a2, base + 1);
+        const wreal x10 = __shfl(a2, base + 2), x11 = __shfl(a2, base + 3);
+        wreal aa, ad, da, dd;
+        haar2x2(x00, x01, x10, x11, aa, ad, da, dd);
+        if (act && sub == 0) {
+          sq[2][0] += ad * ad;
+          sq[2][1] += da * da;
+          sq[2][2] += dd * dd;
+        }
       }
     }
 #pragma unroll
@@ -1467,13 +1473,14 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
-  hipLaunchKernelGGL((wl_haar_analyze<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
+  const int nwg_a = (nthr + WLH_WG * WLH_IT - 1) / (WLH_WG * WLH_IT);
+  hipLaunchKernelGGL((wl_haar_analyze<L>), dim3(nwg_a, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
                      Lt.w, row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
                      Lt.part_per_img);
   WlLayout Ls = Lt;  // wl_sumsq view of the fused partials: nwg per level, levels back to back
   for (int l = 1; l <= L; ++l) {
-    Ls.tiles[l] = nwg;
-    Ls.part_tile0[l] = (size_t)(l - 1) * nwg;
+    Ls.tiles[l] = nwg_a;
+    Ls.part_tile0[l] = (size_t)(l - 1) * nwg_a;
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * L * 3), dim3(256), 0, st, stats, part, Ls);
   hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
