@@ -88,8 +88,9 @@ def _pipeline(kind):
                 # images of a type are scattered through the batch, as a mixed loader yields them:
                 # each type is gathered, noised with its image ids in one launch, scattered back
                 state["groups"] = groups = {
-                    k: (v, torch.as_tensor(v, device=x.device)) for k, v in groups.items()}
-            for k, (ids, idx) in groups.items():
+                    k: (v, torch.as_tensor(v, dtype=torch.int64, device=x.device))
+                    for k, v in groups.items()}
+            for k, (_, idx) in groups.items():
                 if k == "original":
                     t.index_copy_(0, idx, x.index_select(0, idx))
                     continue
@@ -97,13 +98,14 @@ def _pipeline(kind):
                 if k == "periodic":
                     ys = ops.periodic_noise(xs, 100.0)
                 elif k == "s&p":
-                    ys = ops.random_noise(xs, "s&p", amount=0.4, seed=3, image_ids=ids, out="u8")
+                    ys = ops.random_noise(xs, "s&p", amount=0.4, seed=3, image_ids=idx, out="u8")
                 elif k == "poisson":
-                    ys = ops.random_noise(xs, "poisson", seed=3, image_ids=ids, out="u8")
+                    ys = ops.random_noise(xs, "poisson", seed=3, image_ids=idx, out="u8")
                 else:
-                    ys = ops.random_noise(xs, k, var=1.0, seed=3, image_ids=ids, out="u8")
+                    ys = ops.random_noise(xs, k, var=1.0, seed=3, image_ids=idx, out="u8")
                 t.index_copy_(0, idx, ys)
             ops.denoise_wavelet(t, "db1", 3, out_u8=y)
+    step.state = state
     return step
 
 
@@ -324,6 +326,8 @@ def main():
             },
             "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(args.op),
         }
+        if args.op == "cfg5":  # the drawn noise mix (record it in the output)
+            rec["config"]["mix"] = {k: len(v[0]) for k, v in call.state["groups"].items()}
         if gather is not None:
             step_ms = wall / args.steps * 1e3
             gather["e2e_value"] = round(pix_step / ((step_ms + gather["ms_per_step"]) * 1e-3) / 1e6, 1)

@@ -101,7 +101,15 @@ def _empty_like_img(xb: torch.Tensor, dtype) -> torch.Tensor:
 
 
 def _ids_tensor(image_ids, n: int, device) -> torch.Tensor:
-    """device uint64 (int64 storage) array of n image ids for the *_ids_u8 entry points"""
+    """device uint64 (int64 storage) array of n image ids for the *_ids_u8 entry points.  An
+    int64 tensor already on the device is used as is (no host copy, no sync; the caller owns its
+    validity); anything else is checked on the host and copied over."""
+    if isinstance(image_ids, torch.Tensor) and image_ids.device == device \
+            and image_ids.dtype == torch.int64:
+        t = image_ids.reshape(-1)
+        if t.numel() != n:
+            raise ValueError(f"image_ids has {t.numel()} entries for a batch of {n}")
+        return t.contiguous()
     t = torch.as_tensor(image_ids, dtype=torch.int64).reshape(-1)
     if t.numel() != n:
         raise ValueError(f"image_ids has {t.numel()} entries for a batch of {n}")
