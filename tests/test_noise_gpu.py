@@ -286,3 +286,9 @@ def test_image_ids_match_per_image_offsets(dev, mode, kw):
         one8, one64 = idn.ops.random_noise(x[k:k + 1], mode, seed=6, offset=i, out="both", **kw)
         assert np.array_equal(u8[k].cpu().numpy(), one8[0].cpu().numpy())
         assert np.array_equal(f64[k].cpu().numpy(), one64[0].cpu().numpy())
+    # the same ids as an int64 tensor already on the device (used as is, no host round trip)
+    dev8 = idn.ops.random_noise(x, mode, seed=6, image_ids=torch.tensor(ids, device="cuda"),
+                                out="u8", **kw)
+    assert torch.equal(dev8, u8)
+    with pytest.raises(ValueError):
+        idn.ops.random_noise(x, mode, seed=6, image_ids=torch.tensor(ids[:3], device="cuda"), **kw)
