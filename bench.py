@@ -86,24 +86,23 @@ def _pipeline(kind):
                 for i, k in enumerate(kinds):
                     groups.setdefault(k, []).append(i)
                 # images of a type are scattered through the batch, as a mixed loader yields them:
-                # each type is gathered, noised with its image ids in one launch, scattered back
+                # each type is noised in place in the full batch (its batch positions as slots,
+                # its image ids for the streams) in one launch -- no gather / scatter
                 state["groups"] = groups = {
                     k: (v, torch.as_tensor(v, dtype=torch.int64, device=x.device))
                     for k, v in groups.items()}
             for k, (_, idx) in groups.items():
                 if k == "original":
-                    t.index_copy_(0, idx, x.index_select(0, idx))
-                    continue
-                xs = x.index_select(0, idx)
-                if k == "periodic":
-                    ys = ops.periodic_noise(xs, 100.0)
+                    ops.copy_slots(x, t, idx)
+                elif k == "periodic":
+                    ops.periodic_noise(x, 100.0, out=t, slots=idx)
                 elif k == "s&p":
-                    ys = ops.random_noise(xs, "s&p", amount=0.4, seed=3, image_ids=idx, out="u8")
+                    ops.random_noise(x, "s&p", amount=0.4, seed=3, image_ids=idx, slots=idx,
+                                     out_u8=t)
                 elif k == "poisson":
-                    ys = ops.random_noise(xs, "poisson", seed=3, image_ids=idx, out="u8")
+                    ops.random_noise(x, "poisson", seed=3, image_ids=idx, slots=idx, out_u8=t)
                 else:
-                    ys = ops.random_noise(xs, k, var=1.0, seed=3, image_ids=idx, out="u8")
-                t.index_copy_(0, idx, ys)
+                    ops.random_noise(x, k, var=1.0, seed=3, image_ids=idx, slots=idx, out_u8=t)
             ops.denoise_wavelet(t, "db1", 3, out_u8=y)
     step.state = state
     return step

@@ -55,14 +55,19 @@ struct NoiseArgs {
   double p0, p1;  // mean/sd (gaussian, speckle), sap thresholds
   uint64_t key, offset;
   const uint64_t* ids;  // optional per-image ids (device); else id = offset + image index
+  const int64_t* slots;  // optional batch positions (device): image i of the launch reads and
+                         // writes image slots[i] of src / out_u8 / out_f64; else slot = i
 };
 __device__ __forceinline__ uint64_t image_id(const NoiseArgs& a, int img) {
   return a.ids ? a.ids[img] : a.offset + (uint64_t)img;
 }
+__device__ __forceinline__ int64_t slot_of(const NoiseArgs& a, int img) {
+  return a.slots ? a.slots[img] : (int64_t)img;
+}
 
 __device__ __forceinline__ void store_out(const NoiseArgs& a, int img, int64_t e, int64_t boff,
                                           double out) {
-  if (a.out_f64) a.out_f64[(int64_t)img * a.elems + e] = out;
+  if (a.out_f64) a.out_f64[slot_of(a, img) * a.elems + e] = out;
   if (a.out_u8) a.out_u8[boff] = u8_of(out);
 }
 
@@ -97,7 +102,7 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
       const int64_t pix = e / a.c;
       const int ch = (int)(e - pix * a.c);
       const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
-      const int64_t boff = (int64_t)img * a.h * a.row_stride + (int64_t)y * a.row_stride +
+      const int64_t boff = slot_of(a, img) * a.h * a.row_stride + (int64_t)y * a.row_stride +
                            (int64_t)x * a.c + ch;
       const double xv = img_as_float(a.src[boff]);
       double out;
@@ -131,11 +136,12 @@ __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t
   const int64_t e0 = (int64_t)chunk * 16;
   if (e0 >= a.elems) return;
   const uint64_t gimg = image_id(a, img);
-  const uint8_t* src = a.src + (int64_t)img * a.elems + e0;
+  const int64_t base = slot_of(a, img) * a.elems + e0;
+  const uint8_t* src = a.src + base;
   const v4u raw = *reinterpret_cast<const v4u*>(src);
   const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
   uint32_t o[4] = {0u, 0u, 0u, 0u};
-  double* of = a.out_f64 ? a.out_f64 + (int64_t)img * a.elems + e0 : nullptr;
+  double* of = a.out_f64 ? a.out_f64 + base : nullptr;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {  // elements 4k .. 4k+3
     double outv[4];
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t
     }
   }
   if (a.out_u8)
-    *reinterpret_cast<v4u*>(a.out_u8 + (int64_t)img * a.elems + e0) = v4u{o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<v4u*>(a.out_u8 + base) = v4u{o[0], o[1], o[2], o[3]};
 }
 
 // salt & pepper: flipped = U1 < cdf0(amount), salted = U2 < cdf0(salt_vs_pepper)
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(256) void noise_sap_kernel(NoiseArgs a) {
     const int ch = (int)(e - pix * a.c);
     const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
     const int64_t boff =
-        (int64_t)img * a.h * a.row_stride + (int64_t)y * a.row_stride + (int64_t)x * a.c + ch;
+        slot_of(a, img) * a.h * a.row_stride + (int64_t)y * a.row_stride + (int64_t)x * a.c + ch;
     double out = img_as_float(a.src[boff]);
     if (u1 < a.p0) out = (u2 < a.p1) ? 1.0 : 0.0;
     store_out(a, img, e, boff, out);
@@ -208,12 +214,13 @@ __global__ __launch_bounds__(256) void noise_sap_kernel(NoiseArgs a) {
 // per-image distinct-value mask (256 bits) -> vals = 2^ceil(log2(#distinct))
 __global__ __launch_bounds__(256) void unique_mask_kernel(const uint8_t* __restrict__ src, int h,
                                                           int rowbytes, int64_t row_stride,
+                                                          const int64_t* __restrict__ slots,
                                                           uint32_t* __restrict__ mask) {
   __shared__ uint32_t m[8];
   if (threadIdx.x < 8) m[threadIdx.x] = 0;
   __syncthreads();
   const int img = blockIdx.y;
-  const uint8_t* s = src + (int64_t)img * h * row_stride;
+  const uint8_t* s = src + (slots ? slots[img] : (int64_t)img) * h * row_stride;
   const int64_t total = (int64_t)h * rowbytes;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -235,104 +242,90 @@ __global__ void vals_from_mask_kernel(uint32_t* mask, int n) {
   mask[8 * n + img] = v;
 }
 
-// numpy legacy Poisson: multiplication method for lam < 10, PTRS (Hormann 1993) otherwise, with
-// numpy's own loggam in the acceptance test
-struct PhiloxStream {
-  uint64_t key;
-  uint32_t e_lo, e_hi, g_lo, g_hi;
-  uint32_t blk = 0;
-  u32x4 cur;
-  int used = 2;
-  __device__ __forceinline__ double next() {
-    if (used == 2) {
-      cur = philox4x32(u32x4{e_lo, e_hi ^ (blk << 20), g_lo, g_hi}, key);
-      ++blk;
-      used = 0;
-    }
-    const double u = (used == 0) ? u01_closed_open(cur.x, cur.y) : u01_closed_open(cur.z, cur.w);
-    ++used;
-    return u;
-  }
+// Philox-stream Poisson by inversion of the exact CDF.  lambda = img_as_float(v) * vals takes one
+// of 256 values per power-of-two vals (vals <= 256), so the CDF of every
+// (vals, v) pair is tabulated once per call (POIS_KMAX entries; P(X >= 512) < 1e-25 at
+// lambda = 256) with a 1024-entry guide table.  A draw is one 53-bit uniform; the guide entries
+// of its quantile interval bracket the answer (usually to one or two candidates) and a bisection
+// of the bracket finishes it.  The same law as numpy's multiplication / PTRS samplers (the replay
+// mode takes numpy's own draws), without their rejection loops.
+constexpr int POIS_NV = 9;       // vals = 1, 2, 4, ..., 256
+constexpr int POIS_KMAX = 512;   // CDF entries per lambda
+constexpr int POIS_G = 1024;     // guide entries per lambda
+struct PoisTables {
+  double* cdf;      // [POIS_NV][256][POIS_KMAX]
+  uint16_t* guide;  // [POIS_NV][256][POIS_G]: smallest k with cdf[k] > j / POIS_G
 };
-
-// the per-lambda constants of numpy's samplers (lambda depends only on the u8 value and the
-// image's vals: the flat kernel tabulates them once per workgroup)
-struct PoisConst {
-  double lam, enlam, slam, loglam, b, a, invalpha, vr, loginvalpha;
-};
-__device__ __forceinline__ PoisConst pois_const(double lam) {
-  PoisConst p{};
-  p.lam = lam;
-  if (lam < 10.0) {
-    p.enlam = exp(-lam);
-  } else {
-    p.slam = sqrt(lam);
-    p.loglam = log(lam);
-    p.b = 0.931 + 2.53 * p.slam;
-    p.a = -0.059 + 0.02483 * p.b;
-    p.invalpha = 1.1239 + 1.1328 / (p.b - 3.4);
-    p.vr = 0.9277 - 3.6224 / (p.b - 2);
-    p.loginvalpha = log(p.invalpha);
+// one thread per (vals, v): the CDF by the recurrence p(k+1) = p(k) * lambda / (k+1)
+__global__ __launch_bounds__(64) void pois_cdf_kernel(PoisTables t) {
+  const int id = blockIdx.x * 64 + threadIdx.x;  // vi * 256 + v
+  if (id >= POIS_NV * 256) return;
+  const int vi = id >> 8, v = id & 255;
+  const double lam = __dmul_rn(img_as_float((uint32_t)v), (double)(1u << vi));
+  double* cdf = t.cdf + (size_t)id * POIS_KMAX;
+  double p = exp(-lam), acc = 0.0;
+  for (int k = 0; k < POIS_KMAX; ++k) {
+    acc += p;
+    cdf[k] = k == POIS_KMAX - 1 ? 1.0 : fmin(acc, 1.0);
+    p = p * lam / (double)(k + 1);
   }
-  return p;
 }
+// one thread per guide entry: the smallest k with cdf[k] > j / POIS_G (bisection)
+__global__ __launch_bounds__(256) void pois_guide_kernel(PoisTables t) {
+  const int id = blockIdx.x * 256 + threadIdx.x;  // (vi * 256 + v) * POIS_G + j
+  if (id >= POIS_NV * 256 * POIS_G) return;
+  const int row = id / POIS_G, j = id % POIS_G;
+  const double* cdf = t.cdf + (size_t)row * POIS_KMAX;
+  const double q = (double)j / POIS_G;
+  int lo = 0, hi = POIS_KMAX - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cdf[mid] > q) hi = mid;
+    else lo = mid + 1;
+  }
+  t.guide[id] = (uint16_t)lo;
+}
+// element e's uniform: element pairs share one Philox block (counter (e/2, tag, image id)),
+// element 2q takes words (x, y), element 2q+1 words (z, w)
+__device__ __forceinline__ u32x4 pois_block(uint64_t key, uint64_t q, uint64_t gimg) {
+  return philox4x32(u32x4{(uint32_t)q, (uint32_t)(q >> 32) ^ 0x80000000u, (uint32_t)gimg,
+                          (uint32_t)(gimg >> 32)}, key);
+}
+__device__ __forceinline__ int vals_index(uint32_t vals) { return __ffs((int)vals) - 1; }
 
-// numpy's legacy random_loggam (log Gamma(x), Stirling series with the recursion below 7): the
-// function numpy's PTRS acceptance test evaluates at k + 1
-__device__ double np_loggam(double x) {
-  constexpr double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
-                            -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
-                            6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
-                            -1.39243221690590e+00};
-  if (x == 1.0 || x == 2.0) return 0.0;
-  const int n = x < 7.0 ? (int)(7 - x) : 0;
-  double x0 = x + n;
-  const double x2 = (1.0 / x0) * (1.0 / x0);
-  double gl0 = a[9];
+// NE elements of one thread: bracket from the guide (all reads issued together), then bisection
+// rounds in lockstep, each round issuing the probes of every unfinished element at once
+template <int NE>
+__device__ __forceinline__ void pois_invert_n(const PoisTables& pt, const size_t (&row)[NE],
+                                              const double (&u)[NE], int (&lo)[NE]) {
+  int hi[NE];
 #pragma unroll
-  for (int k = 8; k >= 0; --k) {
-    gl0 *= x2;
-    gl0 += a[k];
+  for (int jj = 0; jj < NE; ++jj) {
+    const int gj = (int)(u[jj] * POIS_G);
+    const uint16_t* g = pt.guide + row[jj] * POIS_G;
+    lo[jj] = g[gj];
+    hi[jj] = gj + 1 < POIS_G ? g[gj + 1] : POIS_KMAX - 1;
   }
-  double gl = gl0 / x0 + 0.5 * 1.8378770664093453e+00 + (x0 - 0.5) * log(x0) - x0;
-  for (int k = 1; k <= n; ++k) {
-    gl -= log(x0 - 1.0);
-    x0 -= 1.0;
-  }
-  return gl;
-}
-
-constexpr int LOGGAM_TAB = 1024;  // loggam(k + 1) for k < 1024 (a workgroup table in LDS)
-
-__device__ double poisson_sample(const PoisConst& p, PhiloxStream& rs,
-                                 const double* loggam_tab = nullptr) {
-  const double lam = p.lam;
-  if (lam == 0.0) return 0.0;
-  if (lam < 10.0) {
-    double prod = 1.0;
-    int x = 0;
-    for (int it = 0; it < 1000; ++it) {
-      prod *= rs.next();
-      if (prod > p.enlam) ++x;
-      else return (double)x;
+  for (int round = 0; round < 10; ++round) {  // brackets are < 512 wide: at most 9 rounds
+    double c[NE];
+#pragma unroll
+    for (int jj = 0; jj < NE; ++jj)
+      c[jj] = lo[jj] < hi[jj] ? pt.cdf[row[jj] * POIS_KMAX + ((lo[jj] + hi[jj]) >> 1)] : 0.0;
+    bool open = false;
+#pragma unroll
+    for (int jj = 0; jj < NE; ++jj) {
+      if (lo[jj] < hi[jj]) {
+        const int mid = (lo[jj] + hi[jj]) >> 1;
+        if (c[jj] <= u[jj]) lo[jj] = mid + 1;
+        else hi[jj] = mid;
+        open |= lo[jj] < hi[jj];
+      }
     }
-    return (double)x;
+    if (!__any(open)) break;
   }
-  for (int it = 0; it < 1000; ++it) {
-    const double U = rs.next() - 0.5;
-    const double V = rs.next();
-    const double us = 0.5 - fabs(U);
-    const double k = floor((2 * p.a / us + p.b) * U + lam + 0.43);
-    if (us >= 0.07 && V <= p.vr) return k;
-    if (k < 0 || (us < 0.013 && V > us)) continue;
-    const double lg = (loggam_tab && k < LOGGAM_TAB) ? loggam_tab[(int)k] : np_loggam(k + 1);
-    if (log(V) + p.loginvalpha - log(p.a / (us * us) + p.b) <= -lam + k * p.loglam - lg)
-      return k;
-  }
-  return floor(lam);  // unreachable in practice (bounded loop)
 }
 
-__global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a) {
+__global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a, PoisTables pt) {
   const int64_t total = a.elems * a.n;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -342,116 +335,77 @@ __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a) {
     const int ch = (int)(e - pix * a.c);
     const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
     const int64_t boff =
-        (int64_t)img * a.h * a.row_stride + (int64_t)y * a.row_stride + (int64_t)x * a.c + ch;
+        slot_of(a, img) * a.h * a.row_stride + (int64_t)y * a.row_stride + (int64_t)x * a.c + ch;
     const double vals = (double)a.vals[img];
     double k;
     if (a.replay) {
       k = a.replay[t];
     } else {
-      const uint64_t gimg = image_id(a, img);
-      PhiloxStream rs{a.key, (uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg,
-                      (uint32_t)(gimg >> 32)};
-      k = poisson_sample(pois_const(__dmul_rn(img_as_float(a.src[boff]), vals)), rs);
+      const u32x4 r = pois_block(a.key, (uint64_t)e >> 1, image_id(a, img));
+      const double u[1] = {(e & 1) ? u01_closed_open(r.z, r.w) : u01_closed_open(r.x, r.y)};
+      const size_t row[1] = {(size_t)vals_index(a.vals[img]) * 256 + a.src[boff]};
+      int lo[1];
+      pois_invert_n<1>(pt, row, u, lo);
+      k = (double)lo[0];
     }
     store_out(a, img, e, boff, clip01(k / vals));
   }
 }
 
 // flat Poisson (compact rows, Philox stream): 16 consecutive elements per thread, image =
-// blockIdx.y, the 256 per-value lambda constants tabulated in LDS; same streams and arithmetic
-// as noise_poisson_kernel, so the two forms agree bit for bit
-__global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a) {
-  __shared__ PoisConst tab[256];
-  __shared__ double lgt[LOGGAM_TAB];
+// blockIdx.y; the same uniforms and tables as noise_poisson_kernel, so the two forms agree bit
+// for bit
+__global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a, PoisTables pt) {
   const int img = blockIdx.y;
-  const double vals = (double)a.vals[img];
-  tab[threadIdx.x] = pois_const(__dmul_rn(img_as_float(threadIdx.x), vals));
-  for (int k = threadIdx.x; k < LOGGAM_TAB; k += 256) lgt[k] = np_loggam((double)k + 1.0);
-  __syncthreads();
   const uint32_t chunk = blockIdx.x * 256u + threadIdx.x;
   const int64_t e0 = (int64_t)chunk * 16;
-  if (e0 >= a.elems) return;
+  if (__all(e0 >= a.elems)) return;
+  const bool live = e0 < a.elems;  // dead lanes still take part in the lockstep rounds
+  const uint32_t vraw = a.vals[img];
+  const double vals = (double)vraw;
   const uint64_t gimg = image_id(a, img);
-  const v4u raw = *reinterpret_cast<const v4u*>(a.src + (int64_t)img * a.elems + e0);
+  v4u raw = {0u, 0u, 0u, 0u};
+  const int64_t base = slot_of(a, img) * a.elems + e0;
+  if (live) raw = *reinterpret_cast<const v4u*>(a.src + base);
   const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
-  double* of = a.out_f64 ? a.out_f64 + (int64_t)img * a.elems + e0 : nullptr;
-  uint32_t* o8 = a.out_u8 ? reinterpret_cast<uint32_t*>(a.out_u8 + (int64_t)img * a.elems + e0) : nullptr;
-  // Each lane walks its 16 elements with its own rejection state: one loop iteration is one
-  // attempt (PTRS) or one factor (multiplication method) of the lane's current element, and a
-  // lane moves on as soon as its element is accepted -- the wave never waits for the unluckiest
-  // lane of every element (the element kernel's max over 64 geometric attempt counts).
-  // Per element the draws and arithmetic are exactly poisson_sample's.
-  auto byte_of = [&](int j) -> uint32_t {
-    const uint32_t dw = (j >> 2) == 0 ? in[0] : (j >> 2) == 1 ? in[1] : (j >> 2) == 2 ? in[2] : in[3];
-    return (dw >> (8 * (j & 3))) & 0xFFu;
-  };
-  int j = 0, it = 0, x = 0;
-  double prod = 1.0;
-  PoisConst pc = tab[byte_of(0)];
-  PhiloxStream rs{a.key, (uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)gimg, (uint32_t)(gimg >> 32)};
-  uint32_t o = 0u;
-  while (j < 16) {
-    bool done = false;
-    double k = 0.0;
-    if (pc.lam == 0.0) {
-      done = true;
-    } else if (pc.lam < 10.0) {
-      prod *= rs.next();
-      if (prod > pc.enlam) {
-        ++x;
-        if (++it >= 1000) done = true;
-      } else {
-        done = true;
-      }
-      k = (double)x;
-    } else {
-      const double U = rs.next() - 0.5;
-      const double V = rs.next();
-      const double us = 0.5 - fabs(U);
-      k = floor((2 * pc.a / us + pc.b) * U + pc.lam + 0.43);
-      if (us >= 0.07 && V <= pc.vr) {
-        done = true;
-      } else if (!(k < 0 || (us < 0.013 && V > us))) {
-        const double lg = k < LOGGAM_TAB ? lgt[(int)k] : np_loggam(k + 1);
-        done = log(V) + pc.loginvalpha - log(pc.a / (us * us) + pc.b) <= -pc.lam + k * pc.loglam - lg;
-      }
-      if (!done && ++it >= 1000) {
-        done = true;
-        k = floor(pc.lam);
-      }
-    }
-    if (done) {
-      const double out = clip01(k / vals);
-      o |= (uint32_t)u8_of(out) << (8 * (j & 3));
-      if (of) of[j] = out;
-      if ((j & 3) == 3) {
-        if (o8) o8[j >> 2] = o;
-        o = 0u;
-      }
-      ++j;
-      if (j < 16) {
-        const int64_t e = e0 + j;
-        pc = tab[byte_of(j)];
-        rs = PhiloxStream{a.key, (uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg,
-                          (uint32_t)(gimg >> 32)};
-        it = 0;
-        x = 0;
-        prod = 1.0;
-      }
-    }
+  const size_t tab0 = (size_t)vals_index(vraw) * 256;
+  double u[16];
+  size_t row[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {  // element pairs (2q, 2q+1) share one Philox block
+    const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 1) + q, gimg);
+    u[2 * q] = u01_closed_open(r.x, r.y);
+    u[2 * q + 1] = u01_closed_open(r.z, r.w);
   }
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) row[jj] = tab0 + ((in[jj >> 2] >> (8 * (jj & 3))) & 0xFFu);
+  int lo[16];
+  pois_invert_n<16>(pt, row, u, lo);
+  if (!live) return;
+  double* of = a.out_f64 ? a.out_f64 + base : nullptr;
+  uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) {
+    const double out = clip01((double)lo[jj] / vals);
+    o[jj >> 2] |= (uint32_t)u8_of(out) << (8 * (jj & 3));
+    if (of) of[jj] = out;
+  }
+  if (a.out_u8)
+    *reinterpret_cast<v4u*>(a.out_u8 + base) = v4u{o[0], o[1], o[2], o[3]};
 }
 
 // flat per-image distinct-value mask: 16 bytes per thread per step, a private 256-bit mask per
 // thread, OR-reduced over the wave before one LDS atomic per word
 __global__ __launch_bounds__(256) void unique_mask_flat_kernel(const uint8_t* __restrict__ src,
                                                                int64_t per_img,
+                                                               const int64_t* __restrict__ slots,
                                                                uint32_t* __restrict__ mask) {
   __shared__ uint32_t m[8];
   if (threadIdx.x < 8) m[threadIdx.x] = 0;
   __syncthreads();
   const int img = blockIdx.y;
-  const v4u* s = reinterpret_cast<const v4u*>(src + (int64_t)img * per_img);
+  const v4u* s =
+      reinterpret_cast<const v4u*>(src + (slots ? slots[img] : (int64_t)img) * per_img);
   const int64_t nq = per_img / 16;
   uint32_t mk[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
@@ -486,12 +440,14 @@ __device__ __forceinline__ uint32_t addsat_u8x4(uint32_t a, uint32_t b) {
 __global__ __launch_bounds__(256) void add_pattern_flat_kernel(const uint8_t* __restrict__ src,
                                                                const uint8_t* __restrict__ pat,
                                                                uint8_t* __restrict__ dst,
-                                                               int64_t per_img) {
+                                                               int64_t per_img,
+                                                               const int64_t* __restrict__ slots) {
   const int img = blockIdx.y;
   const int64_t nq = per_img / 16;
-  const v4u* s = reinterpret_cast<const v4u*>(src + (int64_t)img * per_img);
+  const int64_t base = (slots ? slots[img] : (int64_t)img) * per_img;
+  const v4u* s = reinterpret_cast<const v4u*>(src + base);
   const v4u* p = reinterpret_cast<const v4u*>(pat);
-  v4u* d = reinterpret_cast<v4u*>(dst + (int64_t)img * per_img);
+  v4u* d = reinterpret_cast<v4u*>(dst + base);
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
        q += (int64_t)gridDim.x * blockDim.x) {
     const v4u a = s[q], b = p[q];
@@ -516,7 +472,8 @@ __global__ __launch_bounds__(256) void periodic_kernel(uint8_t* __restrict__ pat
 __global__ __launch_bounds__(256) void add_pattern_kernel(const uint8_t* __restrict__ src,
                                                           const uint8_t* __restrict__ pat,
                                                           uint8_t* __restrict__ dst, int n, int h,
-                                                          int rowbytes, int64_t row_stride) {
+                                                          int rowbytes, int64_t row_stride,
+                                                          const int64_t* __restrict__ slots) {
   const int64_t per_img = (int64_t)h * rowbytes;
   const int64_t total = per_img * n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -524,7 +481,8 @@ __global__ __launch_bounds__(256) void add_pattern_kernel(const uint8_t* __restr
     const int img = (int)(i / per_img);
     const int64_t e = i - (int64_t)img * per_img;
     const int y = (int)(e / rowbytes);
-    const int64_t off = (int64_t)img * h * row_stride + (int64_t)y * row_stride + (e - (int64_t)y * rowbytes);
+    const int64_t off = (slots ? slots[img] : (int64_t)img) * h * row_stride +
+                        (int64_t)y * row_stride + (e - (int64_t)y * rowbytes);
     const uint32_t s = (uint32_t)src[off] + (uint32_t)pat[e];
     dst[off] = (uint8_t)(s > 255u ? 255u : s);
   }
@@ -538,15 +496,21 @@ static unsigned grid_for(int64_t work, int64_t cap = 65536) {
 
 }  // namespace idn
 
+// poisson: per-image distinct-value masks + vals, then the inversion tables (256-byte aligned)
+static size_t pois_tables_off(int n) {
+  return ((size_t)n * 9 * sizeof(uint32_t) + 255) & ~(size_t)255;
+}
 extern "C" size_t idn_noise_workspace_size(int kind, int n) {
   if (kind != IDN_NOISE_POISSON || n <= 0) return 0;
-  return (size_t)n * 9 * sizeof(uint32_t);
+  return pois_tables_off(n) + (size_t)idn::POIS_NV * 256 *
+                                  (idn::POIS_KMAX * sizeof(double) + idn::POIS_G * sizeof(uint16_t));
 }
 
 namespace idn {
 static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
                          int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
-                         uint64_t offset, const uint64_t* ids, const double* replay,
+                         uint64_t offset, const uint64_t* ids, const int64_t* slots,
+                         const double* replay,
                          void* workspace, size_t ws_bytes, void* stream) {
   IDN_CHECK_ARG(src, "idn_noise_u8: null src");
   IDN_CHECK_ARG(out_u8 || out_f64, "idn_noise_u8: at least one of out_u8 / out_f64 is required");
@@ -572,6 +536,7 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
   a.key = seed ^ (KIND_TAG * (uint64_t)(kind + 1));
   a.offset = offset;
   a.ids = ids;
+  a.slots = slots;
   // flat form: Philox stream, compact rows, 16-element chunks that never straddle images
   const bool flat = !replay && row_stride == (int64_t)w * c && a.elems % 16 == 0 &&
                     ((uintptr_t)src & 15) == 0 && ((uintptr_t)out_u8 & 15) == 0 &&
@@ -633,19 +598,28 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
                            ((uintptr_t)src & 15) == 0;
       if (compact) {
         hipLaunchKernelGGL(unique_mask_flat_kernel, dim3(16, (unsigned)n), dim3(256), 0, st, src,
-                           per_img, mask);
+                           per_img, slots, mask);
       } else {
         unsigned gx = grid_for(per_img, 64);
         hipLaunchKernelGGL(unique_mask_kernel, dim3(gx, (unsigned)n), dim3(256), 0, st, src, h,
-                           w * c, row_stride, mask);
+                           w * c, row_stride, slots, mask);
       }
       hipLaunchKernelGGL(vals_from_mask_kernel, dim3((n + 255) / 256), dim3(256), 0, st, mask, n);
       a.vals = mask + 8 * n;
+      PoisTables pt;
+      pt.cdf = reinterpret_cast<double*>((char*)workspace + pois_tables_off(n));
+      pt.guide = reinterpret_cast<uint16_t*>(pt.cdf + (size_t)POIS_NV * 256 * POIS_KMAX);
+      if (!replay) {
+        hipLaunchKernelGGL(pois_cdf_kernel, dim3(POIS_NV * 256 / 64), dim3(64), 0, st, pt);
+        hipLaunchKernelGGL(pois_guide_kernel, dim3(POIS_NV * 256 * POIS_G / 256), dim3(256), 0, st,
+                           pt);
+      }
       if (flat) {
         const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
-        hipLaunchKernelGGL(noise_poisson_flat_kernel, grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(noise_poisson_flat_kernel, grid, dim3(256), 0, st, a, pt);
       } else {
-        hipLaunchKernelGGL(noise_poisson_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(noise_poisson_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a,
+                           pt);
       }
       break;
     }
@@ -660,7 +634,7 @@ extern "C" int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64
                             uint64_t seed, uint64_t offset, const double* replay, void* workspace,
                             size_t ws_bytes, void* stream) {
   return idn::noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed,
-                            offset, nullptr, replay, workspace, ws_bytes, stream);
+                            offset, nullptr, nullptr, replay, workspace, ws_bytes, stream);
 }
 
 extern "C" int idn_noise_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n,
@@ -670,7 +644,19 @@ extern "C" int idn_noise_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out
   using namespace idn;
   IDN_CHECK_ARG(image_ids || n == 0, "idn_noise_ids_u8: null image_ids");
   return noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed, 0,
-                       image_ids, nullptr, workspace, ws_bytes, stream);
+                       image_ids, nullptr, nullptr, workspace, ws_bytes, stream);
+}
+
+extern "C" int idn_noise_slots_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n,
+                                  int h, int w, int c, int64_t row_stride, int kind, double p0,
+                                  double p1, uint64_t seed, const uint64_t* image_ids,
+                                  const int64_t* slots, void* workspace, size_t ws_bytes,
+                                  void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(image_ids || n == 0, "idn_noise_slots_u8: null image_ids");
+  IDN_CHECK_ARG(slots || n == 0, "idn_noise_slots_u8: null slots");
+  return noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed, 0,
+                       image_ids, slots, nullptr, workspace, ws_bytes, stream);
 }
 
 extern "C" int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, double amplitude,
@@ -687,9 +673,10 @@ extern "C" int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, do
   return IDN_OK;
 }
 
-extern "C" int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n,
-                                  int h, int w, int c, int64_t row_stride, void* stream) {
-  using namespace idn;
+namespace idn {
+static int add_pattern_impl(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n,
+                            int h, int w, int c, int64_t row_stride, const int64_t* slots,
+                            void* stream) {
   IDN_CHECK_ARG(src && pattern && dst, "idn_add_pattern_u8: null pointer");
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c > 0, "idn_add_pattern_u8: bad shape");
   IDN_CHECK_ARG(row_stride >= (int64_t)w * c, "idn_add_pattern_u8: row_stride < w*c");
@@ -700,11 +687,57 @@ extern "C" int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, ui
     const int64_t nq = per_img / 16;
     const unsigned gx = (unsigned)std::min<int64_t>((nq + 255) / 256, 1024);
     hipLaunchKernelGGL(add_pattern_flat_kernel, dim3(gx, (unsigned)n), dim3(256), 0,
-                       as_stream(stream), src, pattern, dst, per_img);
+                       as_stream(stream), src, pattern, dst, per_img, slots);
   } else {
     hipLaunchKernelGGL(add_pattern_kernel, dim3(grid_for((int64_t)n * h * w * c)), dim3(256), 0,
-                       as_stream(stream), src, pattern, dst, n, h, w * c, row_stride);
+                       as_stream(stream), src, pattern, dst, n, h, w * c, row_stride, slots);
   }
   IDN_CHECK_LAUNCH("idn_add_pattern_u8");
+  return IDN_OK;
+}
+
+// dst image slots[i] = src image slots[i] (compact images, 16 bytes per thread where aligned)
+__global__ __launch_bounds__(256) void copy_slots_kernel(const uint8_t* __restrict__ src,
+                                                         uint8_t* __restrict__ dst,
+                                                         int64_t per_img,
+                                                         const int64_t* __restrict__ slots) {
+  const int64_t base = slots[blockIdx.y] * per_img;
+  if ((per_img & 15) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const v4u* s = reinterpret_cast<const v4u*>(src + base);
+    v4u* d = reinterpret_cast<v4u*>(dst + base);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < per_img / 16;
+         q += (int64_t)gridDim.x * blockDim.x)
+      d[q] = s[q];
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_img;
+         i += (int64_t)gridDim.x * blockDim.x)
+      dst[base + i] = src[base + i];
+  }
+}
+}  // namespace idn
+
+extern "C" int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n,
+                                  int h, int w, int c, int64_t row_stride, void* stream) {
+  return idn::add_pattern_impl(src, pattern, dst, n, h, w, c, row_stride, nullptr, stream);
+}
+
+extern "C" int idn_add_pattern_slots_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst,
+                                        int n, int h, int w, int c, const int64_t* slots,
+                                        void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(slots || n == 0, "idn_add_pattern_slots_u8: null slots");
+  return add_pattern_impl(src, pattern, dst, n, h, w, c, (int64_t)w * c, slots, stream);
+}
+
+extern "C" int idn_copy_slots_u8(const uint8_t* src, uint8_t* dst, int n, int64_t per_img,
+                                 const int64_t* slots, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(src && dst && (slots || n == 0), "idn_copy_slots_u8: null pointer");
+  IDN_CHECK_ARG(n >= 0 && n <= 65535 && per_img > 0, "idn_copy_slots_u8: bad shape");
+  if (n == 0 || src == dst) return IDN_OK;
+  const unsigned gx = (unsigned)std::min<int64_t>((per_img / 16 + 255) / 256, 1024);
+  hipLaunchKernelGGL(copy_slots_kernel, dim3(gx < 1 ? 1 : gx, (unsigned)n), dim3(256), 0,
+                     as_stream(stream), src, dst, per_img, slots);
+  IDN_CHECK_LAUNCH("idn_copy_slots_u8");
   return IDN_OK;
 }

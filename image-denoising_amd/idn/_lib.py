@@ -33,6 +33,9 @@ SIGNATURES = {
     "idn_noise_workspace_size": (_c_size, [_c_int, _c_int]),
     "idn_noise_ids_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64,
                                   _c_int, _c_dbl, _c_dbl, _c_u64, _c_vp, _c_vp, _c_size, _c_vp]),
+    "idn_noise_slots_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64,
+                                    _c_int, _c_dbl, _c_dbl, _c_u64, _c_vp, _c_vp, _c_vp, _c_size,
+                                    _c_vp]),
     "idn_noise_add_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
                                   _c_dbl, _c_dbl, _c_u64, _c_u64, _c_f64p, _c_vp, _c_size, _c_vp]),
     "idn_noise_add_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
@@ -41,6 +44,9 @@ SIGNATURES = {
                                       _c_vp]),
     "idn_periodic_pattern_u8": (_c_int, [_c_u8p, _c_int, _c_int, _c_int, _c_dbl, _c_vp]),
     "idn_add_pattern_u8": (_c_int, [_c_u8p, _c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
+    "idn_add_pattern_slots_u8": (_c_int, [_c_u8p, _c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_vp,
+                                          _c_vp]),
+    "idn_copy_slots_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_i64, _c_vp, _c_vp]),
     "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_i64,
                                         _c_int, _c_int, _c_vp, _c_size, _c_vp]),
     "idn_wavelet_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),

@@ -121,7 +121,7 @@ def _ids_tensor(image_ids, n: int, device) -> torch.Tensor:
 def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, var: float = 0.01,
                  amount: float = 0.05, salt_vs_pepper: float = 0.5, seed: int = 0,
                  offset: int = 0, replay: Optional[torch.Tensor] = None, out: str = "u8",
-                 out_u8: Optional[torch.Tensor] = None, image_ids=None):
+                 out_u8: Optional[torch.Tensor] = None, image_ids=None, slots=None):
     """skimage.util.random_noise(x, mode, ...) on a uint8 batch, plus the caller's U8 cast.
 
     out="u8"   -> (255 * random_noise(...)).astype(np.uint8)   (denoise-branch input)
@@ -133,7 +133,13 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
     Poisson draws), which makes the result bit-exact with the reference.
     image_ids: optional per-image ids (Philox stream only) instead of offset + index -- one launch
     for any subset of a batch, drawing what per-image calls with offset = id would.
+    slots: with image_ids, an int64 device tensor of batch positions: only images x[slots] are
+    noised, written to out_u8[slots] (out="u8", out_u8 required, the rest of out_u8 untouched) --
+    a mixed batch's per-type group with no gather / scatter of its images.
     """
+    if slots is not None:
+        return _random_noise_slots(x, mode, mean, var, amount, salt_vs_pepper, seed, out, out_u8,
+                                   image_ids, slots)
     kind = NOISE_KINDS.get(mode.lower())
     if kind is None:
         raise ValueError(f"random_noise: unsupported mode {mode!r}; supported: {sorted(NOISE_KINDS)}")
@@ -186,6 +192,42 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
     if out == "f64":
         return _finish(y64, sq)
     return _finish(y8, sq), _finish(y64, sq)
+
+
+def _slots_tensor(slots, device) -> torch.Tensor:
+    if not (isinstance(slots, torch.Tensor) and slots.device == device
+            and slots.dtype == torch.int64):
+        raise ValueError("slots must be an int64 tensor on the batch's device")
+    return slots.reshape(-1).contiguous()
+
+
+def _random_noise_slots(x, mode, mean, var, amount, salt_vs_pepper, seed, out, out_u8, image_ids,
+                        slots):
+    kind = NOISE_KINDS.get(mode.lower())
+    if kind is None:
+        raise ValueError(f"random_noise: unsupported mode {mode!r}; supported: {sorted(NOISE_KINDS)}")
+    if out != "u8" or out_u8 is None or image_ids is None:
+        raise ValueError("random_noise: slots needs out='u8', out_u8 and image_ids")
+    xb, _ = _u8_batch(x, "random_noise")
+    nb, h, w, c = xb.shape
+    y8 = out_u8.view(nb, h, w, c)
+    sl = _slots_tensor(slots, xb.device)
+    n = sl.numel()
+    ids = _ids_tensor(image_ids, n, xb.device)
+    if kind in (0, 1):
+        p0, p1 = float(mean), float(var)
+    elif kind == 2:
+        p0, p1 = float(amount), float(salt_vs_pepper)
+    else:
+        p0 = p1 = 0.0
+    lib = _lib.load()
+    ws_bytes = lib.idn_noise_workspace_size(kind, n)
+    ws = _workspace(ws_bytes, xb.device) if ws_bytes else None
+    rc = lib.idn_noise_slots_u8(xb.data_ptr(), y8.data_ptr(), None, n, h, w, c, w * c, kind, p0, p1,
+                                int(seed) & (2 ** 64 - 1), ids.data_ptr(), sl.data_ptr(),
+                                ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+    _lib.check(rc, "idn_noise_slots_u8")
+    return out_u8
 
 
 ADD_NOISE_KINDS = {"uniform": 4, "gamma": 5, "rayleigh": 6, "brownian": 7}
@@ -265,12 +307,23 @@ def periodic_pattern(h: int, w: int, c: int, amplitude: float, device=None) -> t
     return pat
 
 
-def add_pattern(x: torch.Tensor, pattern: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """cv2.add(x, pattern) (u8 saturating), pattern broadcast over the batch."""
+def add_pattern(x: torch.Tensor, pattern: torch.Tensor, out: Optional[torch.Tensor] = None,
+                slots=None) -> torch.Tensor:
+    """cv2.add(x, pattern) (u8 saturating), pattern broadcast over the batch.  slots (int64 device
+    tensor, out required): only images x[slots] -> out[slots]."""
     xb, sq = _u8_batch(x, "add_pattern")
     n, h, w, c = xb.shape
     if tuple(pattern.shape) != (h, w, c) or pattern.dtype != torch.uint8:
         raise ValueError(f"add_pattern: pattern must be uint8 {(h, w, c)}, got {tuple(pattern.shape)}")
+    if slots is not None:
+        if out is None:
+            raise ValueError("add_pattern: slots needs out")
+        sl = _slots_tensor(slots, xb.device)
+        rc = _lib.load().idn_add_pattern_slots_u8(xb.data_ptr(), pattern.contiguous().data_ptr(),
+                                                  out.data_ptr(), sl.numel(), h, w, c,
+                                                  sl.data_ptr(), _stream())
+        _lib.check(rc, "idn_add_pattern_slots_u8")
+        return out
     y = torch.empty_like(xb) if out is None else out.view(n, h, w, c)
     rc = _lib.load().idn_add_pattern_u8(xb.data_ptr(), pattern.contiguous().data_ptr(), y.data_ptr(),
                                         n, h, w, c, w * c, _stream())
@@ -278,11 +331,25 @@ def add_pattern(x: torch.Tensor, pattern: torch.Tensor, out: Optional[torch.Tens
     return _finish(y, sq)
 
 
-def periodic_noise(x: torch.Tensor, amplitude: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def periodic_noise(x: torch.Tensor, amplitude: float, out: Optional[torch.Tensor] = None,
+                   slots=None) -> torch.Tensor:
     """add_periodic_noise: cv2.add(img, U8(255*sin(linspace(-A, A, img.size))).reshape(h,w,3))."""
     xb, _ = _as_batch(x, "periodic_noise")
     _, h, w, c = xb.shape
-    return add_pattern(x, periodic_pattern(h, w, c, amplitude, xb.device), out=out)
+    return add_pattern(x, periodic_pattern(h, w, c, amplitude, xb.device), out=out, slots=slots)
+
+
+def copy_slots(x: torch.Tensor, out: torch.Tensor, slots) -> torch.Tensor:
+    """out[slots] = x[slots] for a uint8 batch (the noise-free members of a mixed batch)."""
+    xb, _ = _u8_batch(x, "copy_slots")
+    if out.shape != x.shape or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise ValueError("copy_slots: out must be a contiguous uint8 tensor shaped like x")
+    sl = _slots_tensor(slots, xb.device)
+    per_img = xb[0].numel() if xb.shape[0] else 1
+    rc = _lib.load().idn_copy_slots_u8(xb.data_ptr(), out.data_ptr(), sl.numel(), per_img,
+                                       sl.data_ptr(), _stream())
+    _lib.check(rc, "idn_copy_slots_u8")
+    return out
 
 
 # ---- blob epilogue -----------------------------------------------------------------------------

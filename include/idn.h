@@ -108,6 +108,14 @@ size_t idn_noise_workspace_size(int kind, int n);
 int idn_noise_ids_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
                      int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
                      const uint64_t* image_ids, void* workspace, size_t ws_bytes, void* stream);
+/* As idn_noise_ids_u8, addressing the batch through a device array of n slots (int64): image i
+ * of the launch reads src image slots[i] and writes out_u8 / out_f64 image slots[i] (compact
+ * h*w*c images; row_stride must be w*c).  A mixed batch's per-type group then runs in place in
+ * the full batch with no gather / scatter of its images. */
+int idn_noise_slots_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
+                       int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
+                       const uint64_t* image_ids, const int64_t* slots, void* workspace,
+                       size_t ws_bytes, void* stream);
 
 /* The reference's own additive noises (not skimage), SURVEY §8f:
  *   IDN_NOISE_UNIFORM   p0 = high   out = img_as_float(x) + U(0, high)         (test.py:767-903)
@@ -147,6 +155,14 @@ int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, double amplit
 /* cv2.add(img, pattern) on u8 (saturating), pattern broadcast over the batch. */
 int idn_add_pattern_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n, int h,
                        int w, int c, int64_t row_stride, void* stream);
+/* idn_add_pattern_u8 on the batch images slots[0..n) (compact h*w*c images, see
+ * idn_noise_slots_u8). */
+int idn_add_pattern_slots_u8(const uint8_t* src, const uint8_t* pattern, uint8_t* dst, int n,
+                             int h, int w, int c, const int64_t* slots, void* stream);
+/* dst image slots[i] = src image slots[i] for i < n (per_img bytes per image): the noise-free
+ * ("original") members of a mixed batch. */
+int idn_copy_slots_u8(const uint8_t* src, uint8_t* dst, int n, int64_t per_img,
+                      const int64_t* slots, void* stream);
 
 /* ---- wavelet denoise (skimage 0.14.2 denoise_wavelet, BayesShrink, soft, YCbCr) -------- */
 

@@ -166,6 +166,25 @@ def test_philox_poisson_statistics(dev):
         assert abs((r ** 2).mean() / lam[sel].mean() - 1) < 0.02
 
 
+def test_philox_poisson_distribution(dev):
+    """the inversion sampler's law: for several lambdas the empirical CDF of the counts matches
+    the exact Poisson CDF (scipy.stats) within the KS 99.9 % bound 1.95 / sqrt(n)"""
+    from scipy.stats import poisson
+    # every u8 value equally often -> vals = 256, lambda = v / 255 * 256
+    flat = np.arange(8 * 240 * 400 * 3) % 256
+    img = flat.astype(np.uint8).reshape(8, 240, 400, 3)
+    _, f64 = _philox(img, "poisson", seed=21)
+    k = np.round(f64 * 256).astype(np.int64)
+    for v in (1, 4, 10, 40, 128, 200):
+        lam = v / 255 * 256
+        sel = (img == v) & (f64 < 1)  # clip(k / 256) saturates k >= 256
+        ks = k[sel]
+        n = int((img == v).sum())
+        emp = np.bincount(ks, minlength=256)[:256].cumsum() / n
+        ref = poisson.cdf(np.arange(256), lam)
+        assert np.max(np.abs(emp - ref)) < 1.95 / np.sqrt(n), v
+
+
 def test_poisson_vals_per_image(dev):
     """vals = 2**ceil(log2(#unique)) per image: image with 3 distinct values -> vals 4"""
     import torch
@@ -256,8 +275,8 @@ def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
 
 
 def test_poisson_flat_matches_element_kernel(dev, monkeypatch):
-    """the flat Poisson kernel (per-value constants and loggam tabulated in LDS) draws the same
-    per-element streams with the same arithmetic as the element kernel: identical outputs"""
+    """the flat Poisson kernel (16 elements per thread, lockstep bisection) takes the same
+    per-element uniforms and CDF tables as the element kernel: identical outputs"""
     import torch
     import idn
     imgs = np.stack([make_img(48, 64, s) for s in (1, 2)])
@@ -292,3 +311,34 @@ def test_image_ids_match_per_image_offsets(dev, mode, kw):
     assert torch.equal(dev8, u8)
     with pytest.raises(ValueError):
         idn.ops.random_noise(x, mode, seed=6, image_ids=torch.tensor(ids[:3], device="cuda"), **kw)
+
+
+@pytest.mark.parametrize("mode,kw", [("gaussian", {"var": 1.0}), ("speckle", {"var": 1.0}),
+                                     ("s&p", {"amount": 0.4}), ("poisson", {}),
+                                     ("periodic", {}), ("original", {})])
+@pytest.mark.parametrize("flat", ["0", "1"])
+def test_slots_match_gather_noise_scatter(dev, monkeypatch, mode, kw, flat):
+    """slot-addressed noise (idn_noise_slots_u8 / idn_add_pattern_slots_u8 / idn_copy_slots_u8)
+    writes exactly what gather -> per-group launch with image ids -> scatter writes, and leaves
+    every other image of the output untouched"""
+    import torch
+    import idn
+    monkeypatch.setenv("IDN_NOISE_FLAT", flat)
+    imgs = np.stack([make_img(32, 48, s) for s in range(7)])
+    x = torch.from_numpy(imgs).cuda()
+    idx = torch.tensor([5, 1, 3], dtype=torch.int64, device="cuda")
+    ops = idn.ops
+    got = torch.full_like(x, 77)
+    ref = torch.full_like(x, 77)
+    xs = x.index_select(0, idx)
+    if mode == "original":
+        ops.copy_slots(x, got, idx)
+        ys = xs
+    elif mode == "periodic":
+        ops.periodic_noise(x, 100.0, out=got, slots=idx)
+        ys = ops.periodic_noise(xs, 100.0)
+    else:
+        ops.random_noise(x, mode, seed=4, image_ids=idx, slots=idx, out_u8=got, **kw)
+        ys = ops.random_noise(xs, mode, seed=4, image_ids=idx, out="u8", **kw)
+    ref.index_copy_(0, idx, ys)
+    assert torch.equal(got, ref)
