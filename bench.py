@@ -41,14 +41,19 @@ OPS = {
     "noise_gaussian": ("gaussian_var1.0 noise",
                        lambda idn, x, y: idn.ops.random_noise(x, "gaussian", var=1.0, seed=3, out="u8",
                                                               out_u8=y), 6, "noise_gauss"),
+    # skimage random_noise('poisson') + U8 cast, Philox stream (BASELINE config 5 noise type)
+    "noise_poisson": ("poisson noise",
+                      lambda idn, x, y: idn.ops.random_noise(x, "poisson", seed=3, out="u8",
+                                                             out_u8=y), 6, "noise_poisson"),
     # 3-level Haar BayesShrink soft threshold (BASELINE config 5 denoiser), fp64 pipeline
     "wavelet_haar3": ("3-level Haar wavelet",
                       lambda idn, x, y: idn.ops.denoise_wavelet(x, "db1", 3, out_u8=y), 6, "wl_"),
 }
 # arithmetic type each op computes in (the filters are integer SWAR / fixed point)
-DTYPE = {"noise_gaussian": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
+DTYPE = {"noise_gaussian": "f64", "noise_poisson": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
          "cfg3": "f64", "cfg4": "f64", "cfg5": "f64"}
 PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
+          "noise_poisson": "skimage random_noise('poisson') law (bit-exact under replay)",
           "wavelet_haar3": "skimage 0.14 denoise_wavelet within 1e-5",
           "bilateral": "cv2.bilateralFilter within 1 LSB",
           "cfg2": "Philox noise + cv2.blur bit-exact", "cfg3": "Philox s&p + cv2.medianBlur bit-exact",
@@ -150,6 +155,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "bilateral": lambda a: oracle.cv.bilateral_filter(a, 9, 75.0, 75.0),
         "noise_gaussian": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_gaussian(
             a, np.random.normal(0.0, 1.0, a.shape))),
+        "noise_poisson": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_poisson(
+            a[0], np.random.poisson(oracle.sk.poisson_lambda(a[0])))),
         "wavelet_haar3": lambda a: oracle.sk.to_u8(255 * oracle.wavelet.denoise_wavelet(a[0], "db1", 3)),
         "cfg2": lambda a: oracle.cv.blur(oracle.sk.to_u8(255 * oracle.sk.noise_gaussian(
             a, np.random.normal(0.0, 1.0, a.shape))), 3),
@@ -170,7 +177,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         el = time.perf_counter() - t0
         if el >= budget_s or n_img >= 2000:
             break
-    if op in ("noise_gaussian", "wavelet_haar3", "cfg5"):
+    if op in ("noise_gaussian", "noise_poisson", "wavelet_haar3", "cfg5"):
         threads, src = 1, "numpy, single thread"
     elif op in ("cfg2", "cfg3", "cfg4"):
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))

@@ -254,7 +254,8 @@ constexpr int POIS_KMAX = 512;   // CDF entries per lambda
 constexpr int POIS_G = 1024;     // guide entries per lambda
 struct PoisTables {
   double* cdf;      // [POIS_NV][256][POIS_KMAX]
-  uint16_t* guide;  // [POIS_NV][256][POIS_G]: smallest k with cdf[k] > j / POIS_G
+  uint32_t* guide;  // [POIS_NV][256][POIS_G]: g(j) | g(j + 1) << 16, g(j) = smallest k with
+                    // cdf[k] > j / POIS_G (g(POIS_G) = POIS_KMAX - 1): one load per bracket
 };
 // one thread per (vals, v): the CDF by the recurrence p(k+1) = p(k) * lambda / (k+1)
 __global__ __launch_bounds__(64) void pois_cdf_kernel(PoisTables t) {
@@ -270,20 +271,25 @@ __global__ __launch_bounds__(64) void pois_cdf_kernel(PoisTables t) {
     p = p * lam / (double)(k + 1);
   }
 }
-// one thread per guide entry: the smallest k with cdf[k] > j / POIS_G (bisection)
-__global__ __launch_bounds__(256) void pois_guide_kernel(PoisTables t) {
-  const int id = blockIdx.x * 256 + threadIdx.x;  // (vi * 256 + v) * POIS_G + j
-  if (id >= POIS_NV * 256 * POIS_G) return;
-  const int row = id / POIS_G, j = id % POIS_G;
-  const double* cdf = t.cdf + (size_t)row * POIS_KMAX;
-  const double q = (double)j / POIS_G;
+// one thread per guide entry: g(j) and g(j + 1) by bisection of the CDF row
+__device__ __forceinline__ int pois_first_above(const double* cdf, double q) {
   int lo = 0, hi = POIS_KMAX - 1;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (cdf[mid] > q) hi = mid;
     else lo = mid + 1;
   }
-  t.guide[id] = (uint16_t)lo;
+  return lo;
+}
+__global__ __launch_bounds__(256) void pois_guide_kernel(PoisTables t) {
+  const int id = blockIdx.x * 256 + threadIdx.x;  // (vi * 256 + v) * POIS_G + j
+  if (id >= POIS_NV * 256 * POIS_G) return;
+  const int row = id / POIS_G, j = id % POIS_G;
+  const double* cdf = t.cdf + (size_t)row * POIS_KMAX;
+  const uint32_t g0 = (uint32_t)pois_first_above(cdf, (double)j / POIS_G);
+  const uint32_t g1 =
+      j + 1 < POIS_G ? (uint32_t)pois_first_above(cdf, (double)(j + 1) / POIS_G) : POIS_KMAX - 1;
+  t.guide[id] = g0 | (g1 << 16);
 }
 // element e's uniform: element pairs share one Philox block (counter (e/2, tag, image id)),
 // element 2q takes words (x, y), element 2q+1 words (z, w)
@@ -293,24 +299,25 @@ __device__ __forceinline__ u32x4 pois_block(uint64_t key, uint64_t q, uint64_t g
 }
 __device__ __forceinline__ int vals_index(uint32_t vals) { return __ffs((int)vals) - 1; }
 
-// NE elements of one thread: bracket from the guide (all reads issued together), then bisection
-// rounds in lockstep, each round issuing the probes of every unfinished element at once
+// NE elements of one thread (row = vals index * 256 + u8 value, 32-bit offsets off the uniform
+// table bases): bracket from the guide (all reads issued together), then bisection rounds in
+// lockstep, each round issuing the probes of every unfinished element at once
 template <int NE>
-__device__ __forceinline__ void pois_invert_n(const PoisTables& pt, const size_t (&row)[NE],
+__device__ __forceinline__ void pois_invert_n(const PoisTables& pt, const uint32_t (&row)[NE],
                                               const double (&u)[NE], int (&lo)[NE]) {
   int hi[NE];
 #pragma unroll
   for (int jj = 0; jj < NE; ++jj) {
-    const int gj = (int)(u[jj] * POIS_G);
-    const uint16_t* g = pt.guide + row[jj] * POIS_G;
-    lo[jj] = g[gj];
-    hi[jj] = gj + 1 < POIS_G ? g[gj + 1] : POIS_KMAX - 1;
+    const uint32_t g = pt.guide[row[jj] * POIS_G + (uint32_t)(u[jj] * POIS_G)];
+    lo[jj] = (int)(g & 0xFFFFu);
+    hi[jj] = (int)(g >> 16);
   }
   for (int round = 0; round < 10; ++round) {  // brackets are < 512 wide: at most 9 rounds
     double c[NE];
 #pragma unroll
     for (int jj = 0; jj < NE; ++jj)
-      c[jj] = lo[jj] < hi[jj] ? pt.cdf[row[jj] * POIS_KMAX + ((lo[jj] + hi[jj]) >> 1)] : 0.0;
+      c[jj] = lo[jj] < hi[jj] ? pt.cdf[row[jj] * POIS_KMAX + (uint32_t)((lo[jj] + hi[jj]) >> 1)]
+                              : 0.0;
     bool open = false;
 #pragma unroll
     for (int jj = 0; jj < NE; ++jj) {
@@ -343,7 +350,7 @@ __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a, PoisTab
     } else {
       const u32x4 r = pois_block(a.key, (uint64_t)e >> 1, image_id(a, img));
       const double u[1] = {(e & 1) ? u01_closed_open(r.z, r.w) : u01_closed_open(r.x, r.y)};
-      const size_t row[1] = {(size_t)vals_index(a.vals[img]) * 256 + a.src[boff]};
+      const uint32_t row[1] = {(uint32_t)vals_index(a.vals[img]) * 256u + a.src[boff]};
       int lo[1];
       pois_invert_n<1>(pt, row, u, lo);
       k = (double)lo[0];
@@ -368,28 +375,39 @@ __global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a, Po
   const int64_t base = slot_of(a, img) * a.elems + e0;
   if (live) raw = *reinterpret_cast<const v4u*>(a.src + base);
   const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
-  const size_t tab0 = (size_t)vals_index(vraw) * 256;
-  double u[16];
-  size_t row[16];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {  // element pairs (2q, 2q+1) share one Philox block
-    const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 1) + q, gimg);
-    u[2 * q] = u01_closed_open(r.x, r.y);
-    u[2 * q + 1] = u01_closed_open(r.z, r.w);
-  }
-#pragma unroll
-  for (int jj = 0; jj < 16; ++jj) row[jj] = tab0 + ((in[jj >> 2] >> (8 * (jj & 3))) & 0xFFu);
-  int lo[16];
-  pois_invert_n<16>(pt, row, u, lo);
-  if (!live) return;
-  double* of = a.out_f64 ? a.out_f64 + base : nullptr;
+  const uint32_t tab0 = (uint32_t)vals_index(vraw) * 256u;
+  const double inv_vals = 1.0 / vals;  // vals is a power of two: k * inv_vals == k / vals
+  double* of = a.out_f64 && live ? a.out_f64 + base : nullptr;
   uint32_t o[4] = {0u, 0u, 0u, 0u};
+  // PQ groups of 16 / PQ elements (fewer live registers than 16 at once, so more waves per SIMD
+  // to hide the table reads)
+  constexpr int PQ = 4, PE = 16 / PQ;
 #pragma unroll
-  for (int jj = 0; jj < 16; ++jj) {
-    const double out = clip01((double)lo[jj] / vals);
-    o[jj >> 2] |= (uint32_t)u8_of(out) << (8 * (jj & 3));
-    if (of) of[jj] = out;
+  for (int hf = 0; hf < PQ; ++hf) {
+    double u[PE];
+    uint32_t row[PE];
+#pragma unroll
+    for (int q = 0; q < PE / 2; ++q) {  // element pairs (2q, 2q+1) share one Philox block
+      const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 1) + (PE / 2) * hf + q, gimg);
+      u[2 * q] = u01_closed_open(r.x, r.y);
+      u[2 * q + 1] = u01_closed_open(r.z, r.w);
+    }
+#pragma unroll
+    for (int jj = 0; jj < PE; ++jj) {
+      const int el = PE * hf + jj;
+      row[jj] = tab0 + ((in[el >> 2] >> (8 * (el & 3))) & 0xFFu);
+    }
+    int lo[PE];
+    pois_invert_n<PE>(pt, row, u, lo);
+#pragma unroll
+    for (int jj = 0; jj < PE; ++jj) {
+      const int el = PE * hf + jj;
+      const double out = clip01(__dmul_rn((double)lo[jj], inv_vals));
+      o[el >> 2] |= (uint32_t)u8_of(out) << (8 * (el & 3));
+      if (of) of[el] = out;
+    }
   }
+  if (!live) return;
   if (a.out_u8)
     *reinterpret_cast<v4u*>(a.out_u8 + base) = v4u{o[0], o[1], o[2], o[3]};
 }
@@ -503,7 +521,7 @@ static size_t pois_tables_off(int n) {
 extern "C" size_t idn_noise_workspace_size(int kind, int n) {
   if (kind != IDN_NOISE_POISSON || n <= 0) return 0;
   return pois_tables_off(n) + (size_t)idn::POIS_NV * 256 *
-                                  (idn::POIS_KMAX * sizeof(double) + idn::POIS_G * sizeof(uint16_t));
+                                  (idn::POIS_KMAX * sizeof(double) + idn::POIS_G * sizeof(uint32_t));
 }
 
 namespace idn {
@@ -608,7 +626,7 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       a.vals = mask + 8 * n;
       PoisTables pt;
       pt.cdf = reinterpret_cast<double*>((char*)workspace + pois_tables_off(n));
-      pt.guide = reinterpret_cast<uint16_t*>(pt.cdf + (size_t)POIS_NV * 256 * POIS_KMAX);
+      pt.guide = reinterpret_cast<uint32_t*>(pt.cdf + (size_t)POIS_NV * 256 * POIS_KMAX);
       if (!replay) {
         hipLaunchKernelGGL(pois_cdf_kernel, dim3(POIS_NV * 256 / 64), dim3(64), 0, st, pt);
         hipLaunchKernelGGL(pois_guide_kernel, dim3(POIS_NV * 256 * POIS_G / 256), dim3(256), 0, st,
