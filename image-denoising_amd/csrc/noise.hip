@@ -291,8 +291,14 @@ __global__ __launch_bounds__(256) void pois_guide_kernel(PoisTables t) {
       j + 1 < POIS_G ? (uint32_t)pois_first_above(cdf, (double)(j + 1) / POIS_G) : POIS_KMAX - 1;
   t.guide[id] = g0 | (g1 << 16);
 }
-// element e's uniform: element pairs share one Philox block (counter (e/2, tag, image id)),
-// element 2q takes words (x, y), element 2q+1 words (z, w)
+
+// element e's uniform: 4 consecutive elements share one Philox block (counter (e/4, tag, image
+// id)), element e takes word e % 4 as u = (word + 1/2) / 2^32 in (0, 1).  The 2^-32 grid changes
+// the law only on events of probability below 2^-32 (as the float Box-Muller of the Gaussian
+// kind does), and the top 10 bits of the word are the guide index directly.
+__device__ __forceinline__ double pois_u(uint32_t w) {
+  return fma((double)w, 0x1p-32, 0x1p-33);  // exact: 33 significant bits
+}
 __device__ __forceinline__ u32x4 pois_block(uint64_t key, uint64_t q, uint64_t gimg) {
   return philox4x32(u32x4{(uint32_t)q, (uint32_t)(q >> 32) ^ 0x80000000u, (uint32_t)gimg,
                           (uint32_t)(gimg >> 32)}, key);
@@ -304,11 +310,14 @@ __device__ __forceinline__ int vals_index(uint32_t vals) { return __ffs((int)val
 // lockstep, each round issuing the probes of every unfinished element at once
 template <int NE>
 __device__ __forceinline__ void pois_invert_n(const PoisTables& pt, const uint32_t (&row)[NE],
-                                              const double (&u)[NE], int (&lo)[NE]) {
+                                              const uint32_t (&w)[NE], int (&lo)[NE]) {
+  static_assert(POIS_G == 1024, "guide index = top 10 bits of the uniform word");
   int hi[NE];
+  double u[NE];
 #pragma unroll
   for (int jj = 0; jj < NE; ++jj) {
-    const uint32_t g = pt.guide[row[jj] * POIS_G + (uint32_t)(u[jj] * POIS_G)];
+    u[jj] = pois_u(w[jj]);
+    const uint32_t g = pt.guide[row[jj] * POIS_G + (w[jj] >> 22)];
     lo[jj] = (int)(g & 0xFFFFu);
     hi[jj] = (int)(g >> 16);
   }
@@ -348,8 +357,9 @@ __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a, PoisTab
     if (a.replay) {
       k = a.replay[t];
     } else {
-      const u32x4 r = pois_block(a.key, (uint64_t)e >> 1, image_id(a, img));
-      const double u[1] = {(e & 1) ? u01_closed_open(r.z, r.w) : u01_closed_open(r.x, r.y)};
+      const u32x4 r = pois_block(a.key, (uint64_t)e >> 2, image_id(a, img));
+      const int q = (int)(e & 3);
+      const uint32_t u[1] = {q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w};
       const uint32_t row[1] = {(uint32_t)vals_index(a.vals[img]) * 256u + a.src[boff]};
       int lo[1];
       pois_invert_n<1>(pt, row, u, lo);
@@ -384,14 +394,10 @@ __global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a, Po
   constexpr int PQ = 4, PE = 16 / PQ;
 #pragma unroll
   for (int hf = 0; hf < PQ; ++hf) {
-    double u[PE];
+    static_assert(PE == 4, "one Philox block per group");
+    const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 2) + hf, gimg);
+    const uint32_t u[PE] = {r.x, r.y, r.z, r.w};
     uint32_t row[PE];
-#pragma unroll
-    for (int q = 0; q < PE / 2; ++q) {  // element pairs (2q, 2q+1) share one Philox block
-      const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 1) + (PE / 2) * hf + q, gimg);
-      u[2 * q] = u01_closed_open(r.x, r.y);
-      u[2 * q + 1] = u01_closed_open(r.z, r.w);
-    }
 #pragma unroll
     for (int jj = 0; jj < PE; ++jj) {
       const int el = PE * hf + jj;
@@ -413,29 +419,54 @@ __global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a, Po
 }
 
 // flat per-image distinct-value mask: 16 bytes per thread per step, a private 256-bit mask per
-// thread, OR-reduced over the wave before one LDS atomic per word
+// thread, OR-reduced over the wave before one LDS atomic per word.  vals only needs the count
+// up to 2^ceil(log2(count)): once a block's own mask holds more than 128 values, vals = 256 is
+// certain whatever the rest of the image holds, so the block stops (checked every 4 steps).
 __global__ __launch_bounds__(256) void unique_mask_flat_kernel(const uint8_t* __restrict__ src,
                                                                int64_t per_img,
                                                                const int64_t* __restrict__ slots,
                                                                uint32_t* __restrict__ mask) {
   __shared__ uint32_t m[8];
+  __shared__ int full;
   if (threadIdx.x < 8) m[threadIdx.x] = 0;
   __syncthreads();
   const int img = blockIdx.y;
   const v4u* s =
       reinterpret_cast<const v4u*>(src + (slots ? slots[img] : (int64_t)img) * per_img);
   const int64_t nq = per_img / 16;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   uint32_t mk[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    const v4u v = s[q];
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // block-uniform trip count: every thread reaches the __syncthreads of the checks
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t steps = q0 < nq ? (nq - q0 + stride - 1) / stride : 0;
+  for (int64_t it = 0; it < steps; ++it, q += stride) {
+    if (q < nq) {
+      const v4u v = s[q];
+      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const uint32_t x = (d[b >> 2] >> (8 * (b & 3))) & 0xFFu;
-      const uint32_t bit = 1u << (x & 31u), word = x >> 5;
+      for (int b = 0; b < 16; ++b) {
+        const uint32_t x = (d[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+        const uint32_t bit = 1u << (x & 31u), word = x >> 5;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) mk[k] |= word == (uint32_t)k ? bit : 0u;
+        for (int k = 0; k < 8; ++k) mk[k] |= word == (uint32_t)k ? bit : 0u;
+      }
+    }
+    if ((it & 3) == 3 && it + 1 < steps) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t v = mk[k];
+        for (int off = 32; off > 0; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off);
+        if ((threadIdx.x & 63) == 0 && v) atomicOr(&m[k], v);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int cnt = 0;
+        for (int k = 0; k < 8; ++k) cnt += __popc(m[k]);
+        full = cnt > 128;
+      }
+      __syncthreads();
+      if (full) break;
     }
   }
 #pragma unroll

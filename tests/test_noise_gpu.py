@@ -275,12 +275,15 @@ def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
 
 
 def test_poisson_flat_matches_element_kernel(dev, monkeypatch):
-    """the flat Poisson kernel (16 elements per thread, lockstep bisection) takes the same
-    per-element uniforms and CDF tables as the element kernel: identical outputs"""
+    """the flat Poisson kernel (16 elements per thread, lockstep bisection) and the element kernel
+    (IDN_NOISE_FLAT=0) take the same uniforms and invert the same CDF tables: identical outputs,
+    over images of several vals (3, 16 and 256 distinct values)"""
     import torch
     import idn
-    imgs = np.stack([make_img(48, 64, s) for s in (1, 2)])
-    imgs[0, :8] //= 16  # dark rows: lambda < 10 takes the multiplication method
+    imgs = np.stack([make_img(48, 64, s) for s in (1, 2, 3, 4)])
+    imgs[0, :8] //= 16  # dark rows: small lambda
+    imgs[2] = (imgs[2] // 86) * 86  # 3 distinct values -> vals 4
+    imgs[3] = (imgs[3] // 16) * 16  # 16 distinct values -> vals 16
     x = torch.from_numpy(imgs).cuda()
     res = {}
     for flat in ("0", "1"):
