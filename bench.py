@@ -196,7 +196,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
 
 
 def load_traffic(op: str):
-    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json), or None."""
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json), or None.
+    Not measured in this run: the counters need their own rocprofv3 --pmc passes."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
@@ -207,36 +208,117 @@ def load_traffic(op: str):
         return None
 
 
-def main():
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: start the N ranks as ONE child process group
+    (python -m torch.distributed.run, one process per GPU) before anything touches the GPU, pass
+    rank 0's JSON line through, and return the child's exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=0, help="images per GPU (default: 256, or the "
-                    "config's per-GPU batch for cfg2..cfg5)")
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU (weak scaling; default "
+                    "256, or the config's per-GPU batch for cfg2..cfg5) or in total (strong)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: every rank filters --batch images; strong: --batch images in "
+                         "total, split into contiguous shards over the ranks")
     ap.add_argument("--op", default="gauss5", choices=sorted(OPS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-copy", action="store_true", help="skip the same-run copy ceiling")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: also time reassembling the filtered batch on every rank with one "
                          "RCCL all-gather over xGMI per step (reported as 'allgather')")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="resolve ranks and shards and print them without touching a GPU (tests)")
+    return ap.parse_args(argv)
+
+
+def copy_ceiling(idn, torch, x, y, reps: int = 20):
+    """Same-run copy ceiling over the op's own buffers (x -> y, x.nbytes read + written): the
+    flat burst copy at default and nontemporal policy, HIP events over `reps` launches each."""
+    out = {}
+    for pol, name in ((0, "default"), (1, "nontemporal")):
+        for _ in range(3):
+            idn.ops.copy_flat(x, y, pol)
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            idn.ops.copy_flat(x, y, pol)
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[name] = round(2 * x.nbytes / (ms * 1e-3) / 1e9, 1)
+    return {"copy_ceiling_GBps": max(out.values()), "by_policy": out,
+            "bytes_per_launch": 2 * x.nbytes, "kernel": "copy_burst_kernel"}
+
+
+def main():
+    args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N ranks with "
+              f"torch.distributed.run --nproc-per-node {args.gpus} (or drop WORLD_SIZE and let "
+              f"bench.py start them)", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.batch <= 0:
+        args.batch = PIPELINES[args.op][1] if args.op in PIPELINES else 256
+    if args.scaling == "strong":
+        from idn.parallel import shard_range
+        lo, hi = shard_range(args.batch, rank, world)
+        total_images = args.batch
+    else:
+        lo, hi = rank * args.batch, (rank + 1) * args.batch
+        total_images = args.batch * world
+    my_batch = hi - lo
+    if args.dry_run:
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+            got = [None] * world
+            dist.all_gather_object(got, [rank, lo, hi])
+            dist.destroy_process_group()
+        else:
+            got = [[0, lo, hi]]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": args.scaling,
+                              "total_images": total_images, "shards": got}), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
     import idn
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     label, call, bpp, kname = OPS[args.op]
-    if args.batch <= 0:
-        args.batch = PIPELINES[args.op][1] if args.op in PIPELINES else 256
-    x = synth_batch(torch, args.batch, dev, seed=3 + rank)
+    x = synth_batch(torch, my_batch, dev, seed=3 + rank)
     y = torch.empty_like(x)
     torch.cuda.synchronize()
 
@@ -273,14 +355,17 @@ def main():
     gather = None
     if world > 1 and args.gather:
         # end-to-end figure = filter step + all-gather of every rank's u8 output
-        full = torch.empty((world * args.batch, H, W, C), dtype=torch.uint8, device=dev)
+        from idn.parallel import all_gather_batch
+        full =torch.empty((world * my_batch, H, W, C), dtype=torch.uint8, device=dev)
+        gather_once = ((lambda: all_gather_batch(y, total_images)) if args.scaling == "strong"
+                       else (lambda: dist.all_gather_into_tensor(full, y)))
         for _ in range(2):
-            dist.all_gather_into_tensor(full, y)
+            gather_once()
         torch.cuda.synchronize()
         barrier()
         g0 = time.perf_counter()
         for _ in range(args.steps):
-            dist.all_gather_into_tensor(full, y)
+            gather_once()
         torch.cuda.synchronize()
         barrier()
         gt = torch.tensor([time.perf_counter() - g0], device=dev, dtype=torch.float64)
@@ -290,9 +375,13 @@ def main():
         gather = {"ms_per_step": round(g_ms, 4), "bytes_per_rank": int(y.numel()),
                   "algbw_GBps": round(y.numel() * (world - 1) / (g_ms * 1e-3) / 1e9, 1)}
 
-    pix_step = args.batch * H * W * world
+    ceiling = None
+    if not args.no_copy and rank == 0:
+        ceiling = copy_ceiling(idn, torch, x, y)
+
+    pix_step = total_images * H * W
     value = pix_step * args.steps / wall / 1e6
-    achieved_gbs = bpp * args.batch * H * W / (avg_kern_ms * 1e-3) / 1e9
+    achieved_gbs = bpp * my_batch * H * W / (avg_kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.op)
 
     if rank == 0:
@@ -306,15 +395,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": DTYPE.get(args.op, "u8"),
             "data": "synthetic (on-device textured pattern, seed 3+rank)",
             "config": {
-                "workload": f"{label}, batch {args.batch}x600x1000x3 uint8 per GPU, "
+                "workload": f"{label}, batch {my_batch}x600x1000x3 uint8 per GPU "
+                            f"({total_images} in total, {args.scaling} scaling), "
                             + PARITY.get(args.op, "cv2 semantics bit-exact"),
                 "op": args.op,
-                "batch_per_gpu": args.batch,
+                "batch_per_gpu": my_batch,
+                "total_images": total_images,
                 "image": [H, W, C],
                 "parallelism": f"image-sharded x{world} (no collective in the timed region)",
             },
@@ -325,13 +416,20 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": "profiles/pmc_traffic.json (committed rocprofv3 FETCH_SIZE x2 + "
+                                  "WRITE_SIZE passes; not measured in this run)" if traffic else None,
                 "kernel": kname,
                 "kernel_ms_avg": round(avg_kern_ms, 5),
                 "kernel_ms_median": round(kern_ms[len(kern_ms) // 2], 5),
-                "algorithmic_bytes_per_launch": bpp * args.batch * H * W,
+                "algorithmic_bytes_per_launch": bpp * my_batch * H * W,
             },
             "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(args.op),
         }
+        if ceiling is not None:
+            rec["copy_ceiling_GBps"] = ceiling["copy_ceiling_GBps"]
+            rec["roofline"]["frac_of_copy_ceiling"] = round(
+                achieved_gbs / ceiling["copy_ceiling_GBps"], 4)
+            rec["copy_ceiling"] = ceiling
         if args.op == "cfg5":  # the drawn noise mix (record it in the output)
             rec["config"]["mix"] = {k: len(v[0]) for k, v in call.state["groups"].items()}
         if gather is not None:

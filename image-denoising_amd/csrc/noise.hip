@@ -564,6 +564,8 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
   IDN_CHECK_ARG(src, "idn_noise_u8: null src");
   IDN_CHECK_ARG(out_u8 || out_f64, "idn_noise_u8: at least one of out_u8 / out_f64 is required");
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0 && c >= 1 && c <= 4, "idn_noise_u8: bad shape");
+  // the per-image kernels put the image on gridDim.y
+  IDN_CHECK_ARG(n <= 65535, "idn_noise_u8: at most 65535 images per call (got %d)", n);
   IDN_CHECK_ARG(row_stride >= (int64_t)w * c, "idn_noise_u8: row_stride < w*c");
   IDN_CHECK_ARG(kind >= 0 && kind <= 3, "idn_noise_u8: unknown noise kind %d", kind);
   IDN_CHECK_ARG((const void*)out_u8 != (const void*)src || kind != IDN_NOISE_POISSON,
@@ -704,6 +706,8 @@ extern "C" int idn_noise_slots_u8(const uint8_t* src, uint8_t* out_u8, double* o
   using namespace idn;
   IDN_CHECK_ARG(image_ids || n == 0, "idn_noise_slots_u8: null image_ids");
   IDN_CHECK_ARG(slots || n == 0, "idn_noise_slots_u8: null slots");
+  IDN_CHECK_ARG(row_stride == (int64_t)w * c, "idn_noise_slots_u8: slots need compact rows "
+                "(row_stride %lld != w*c)", (long long)row_stride);
   return noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed, 0,
                        image_ids, slots, nullptr, workspace, ws_bytes, stream);
 }

@@ -1,3 +1,7 @@
+# Portions of this file (get_minibatch's blob / label assembly) follow Fast R-CNN's
+#   lib/roi_data_layer/minibatch.py -- Fast R-CNN, Copyright (c) 2015 Microsoft,
+#   Licensed under The MIT License, written by Ross Girshick and Xinlei Chen.
+# The drop-in keeps that function's behaviour (asserts and messages included) line for line.
 """Drop-in for the training-side data path: lib/roi_data_layer/minibatch.py get_minibatch (42-75)
 and _get_image_blob (77-1690), with the per-image noise + denoise recipe of the roidb entry's
 `noise_type` executed on the GPU (idn.pipeline) instead of the closures at minibatch.py:87-1673.

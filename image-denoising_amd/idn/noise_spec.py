@@ -40,6 +40,9 @@ LEVELS = {
     "brownian": (("var0.9", 0.9), ("var0.09", 0.09), ("var0.009", 0.009)),  # dt
     "gamma": (("var0.05", 0.05), ("var0.1", 0.1), ("var0.2", 0.2)),         # scale
     "rayleigh": (("var0.1", 0.1), ("var0.2", 0.2), ("var0.3", 0.3)),        # scale
+    # MiniBatchKMeans(n_clusters=k) colour quantisation in LAB (test.py:592-765,
+    # minibatch.py:492-667); tested in this order, so 'var10' is reached only without var3/var7
+    "quant": (("var3", 3), ("var7", 7), ("var10", 10)),                       # clusters
 }
 ADDITIVE = ("uniform", "gamma", "rayleigh")  # float64 x + noise, unclipped (cv2.add on floats)
 
@@ -93,7 +96,7 @@ MIX_KEYS = ("var_low", "var_medium", "var_high", "var_all")  # reference test or
 class Step:
     """One kernel step.  op in:
     noise:    ('gaussian', var) ('speckle', var) ('sap', amount) ('poisson',) ('periodic', amp)
-              ('original',) ('bloom',) ('shader',)
+              ('quant', k) ('original',) ('bloom', [circles]) ('shader',)
     cast_u8:  U8(255*x) of a float64 image
     filter:   ('gaus_blur', k) ('mean', k) ('median', k) ('bilateral', d, sc, ss)
               ('wavelet', wavelet, levels)
@@ -164,6 +167,12 @@ def _noise_branch(noise: str, noise_type: str, mode: str):
             val = 0.6  # minibatch.py:367: the plain var0.8 branch draws amount=0.6
         noise_step = Step("noise", "sap" if noise == "sap" else noise, (val,))
     steps = [noise_step]
+    if noise == "quant":
+        # cvtColor(LAB2BGR) of the quantised image is already u8; every denoiser (wavelet
+        # included) runs on it (test.py:600-757)
+        if den is not None:
+            steps.append(_filter_step(den))
+        return steps, "u8"
     if noise == "brownian":
         # cv2.add(img, U8(255 * B)) is already u8 (test.py:1095-1124); denoisers run on it
         if den is not None:
@@ -210,12 +219,8 @@ def _closure(noise_type: str, mode: str, top_level: bool):
     for noise in ("gaussian", "poisson", "sap", "speckle", "periodic", "brownian", "quant",
                   "uniform", "gamma", "rayleigh"):
         if noise in noise_type:
-            if noise == "quant":
-                if mode == "test_v0" and top_level:
-                    return [Step("noise", "original")], "u8"
-                raise NotImplementedError(
-                    "noise type 'quant' (MiniBatchKMeans colour quantisation) is not implemented "
-                    "on the GPU path (SURVEY §8f row 4)")
+            if noise == "quant" and mode == "test_v0" and top_level:
+                return [Step("noise", "original")], "u8"  # test.py:1719-1725 adds no noise
             if mode == "test_v0" and top_level and noise == "sap":
                 return [Step("noise", "original")], "u8"  # test.py:1691-1697
             return _noise_branch(noise, noise_type, mode)
@@ -256,14 +261,36 @@ def _post_hook(noise: str, steps, out_dtype: str, mode: str):
     return steps + [_filter_step(den)], out_dtype
 
 
-def plan(noise: str, mode: str = "canonical", rng: Optional[_random.Random] = None) -> Plan:
+def plan(noise: str, mode: str = "canonical", rng: Optional[_random.Random] = None,
+         hw: Optional[Tuple[int, int]] = None) -> Plan:
     """Resolve the recipe for ONE image.  `rng` provides random.choice (the reference uses the
-    unseeded global `random`); pass a seeded random.Random for reproducible batches."""
+    unseeded global `random`); pass a seeded random.Random for reproducible batches.
+
+    hw = (H, W) of the image: a `bloom` step then carries its add_sun_flare circles, drawn from
+    `rng` right after the noise-type choice -- the order the reference's loop draws them in
+    (test.py:1590-1617: random.choice, then Automold's random.uniform / randint calls) -- so the
+    draws belong to the plan, not to whichever process later executes it."""
     if mode not in MODES:
         raise ValueError(f"mode must be one of {MODES}")
     rng = rng or _random
-    if mode == "canonical":
-        return _plan_canonical(noise, rng)
+    p = _plan_canonical(noise, rng) if mode == "canonical" else _plan_mode(noise, mode, rng)
+    if hw is not None and any(st.op == "bloom" and not st.args for st in p.steps):
+        p = _with_bloom_draws(p, hw, rng)
+    return p
+
+
+def _with_bloom_draws(p: Plan, hw: Tuple[int, int], rng) -> Plan:
+    from . import automold
+    circ, wts = automold.sun_flare_circles(int(hw[0]), int(hw[1]), flare_center=(100, 100),
+                                           angle=-math.pi / 4, rng=rng)
+    args = (tuple(tuple(int(v) for v in r) for r in circ),
+            tuple(tuple(float(v) for v in r) for r in wts))
+    steps = tuple(Step("noise", "bloom", args) if (st.op == "bloom" and not st.args) else st
+                  for st in p.steps)
+    return Plan(p.spec, p.noise_type, steps, p.out_dtype, p.log)
+
+
+def _plan_mode(noise: str, mode: str, rng) -> Plan:
     mix = MIX_TEST if mode == "test_v0" else MIX_TRAIN
     if "mix" in noise:
         for key in MIX_KEYS:
@@ -314,8 +341,8 @@ def _plan_canonical(noise: str, rng) -> Plan:
         if key is None:
             raise ValueError(f"mix spec {noise!r} needs var_low / var_medium / var_high / var_all")
         pool = [t for t in MIX_TEST[key] if t.split("_")[0] in
-                ("gaussian", "poisson", "speckle", "sap", "periodic", "original") + ADDITIVE +
-                ("brownian",)]
+                ("gaussian", "poisson", "speckle", "sap", "periodic", "original", "quant") +
+                ADDITIVE + ("brownian",)]
         base = rng.choice(pool)
         noise_type = base if den is None else _insert_denoiser(base, den)
         return _plan_canonical(noise_type, rng)._replace_spec(noise)
@@ -324,7 +351,8 @@ def _plan_canonical(noise: str, rng) -> Plan:
     if s.startswith("original_") and den is not None:
         return Plan(noise, s, (Step("noise", "original"), _filter_step(den)), "u8")
     head = s.split("_")[0]
-    if head not in ("gaussian", "sap", "speckle", "poisson", "periodic") + ADDITIVE + ("brownian",):
+    if head not in ("gaussian", "sap", "speckle", "poisson", "periodic", "quant") + ADDITIVE + \
+            ("brownian",):
         raise ValueError(f"unknown or unsupported noise spec {noise!r}")
     steps, out = _noise_branch(head, s, "canonical")
     return Plan(noise, s, tuple(steps), out)

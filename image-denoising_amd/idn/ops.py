@@ -195,6 +195,8 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
 
 
 def _slots_tensor(slots, device) -> torch.Tensor:
+    """The caller owns slot validity (0 <= slot < batch size, as for device image-id tensors):
+    checking a device tensor's values would cost a host sync per launch."""
     if not (isinstance(slots, torch.Tensor) and slots.device == device
             and slots.dtype == torch.int64):
         raise ValueError("slots must be an int64 tensor on the batch's device")
@@ -210,6 +212,11 @@ def _random_noise_slots(x, mode, mean, var, amount, salt_vs_pepper, seed, out, o
         raise ValueError("random_noise: slots needs out='u8', out_u8 and image_ids")
     xb, _ = _u8_batch(x, "random_noise")
     nb, h, w, c = xb.shape
+    if not (isinstance(out_u8, torch.Tensor) and out_u8.dtype == torch.uint8
+            and out_u8.device == xb.device and out_u8.is_contiguous()
+            and tuple(out_u8.shape) in ((nb, h, w, c), (h, w, c) if nb == 1 else ())):
+        raise ValueError("random_noise: slots needs out_u8 = a contiguous uint8 tensor shaped "
+                         "like x on x's device")
     y8 = out_u8.view(nb, h, w, c)
     sl = _slots_tensor(slots, xb.device)
     n = sl.numel()
@@ -352,6 +359,75 @@ def copy_slots(x: torch.Tensor, out: torch.Tensor, slots) -> torch.Tensor:
     return out
 
 
+# ---- quant: colour quantisation by k-means in 8-bit Lab ----------------------------------------
+
+def quantize(x: torch.Tensor, k: int, *, seed: int = 0, offset: int = 0, image_ids=None,
+             centers: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+             return_labels: bool = False, return_centers: bool = False):
+    """The reference's `quant` noise (lib/model/test.py:592-765): per image
+    LAB2BGR(MiniBatchKMeans(n_clusters=k).fit(BGR2LAB(x)).cluster_centers_.astype(uint8)[labels]).
+
+    centers None: device k-means (greedy k-means++ + Lloyd, Philox draws keyed by (seed, image
+    id = offset + i or image_ids[i])).  centers (float64 (N, k, 3) on the device, e.g. sklearn's
+    cluster_centers_): replay -- labels exactly as sklearn assigns them.
+    Returns out, plus labels (uint8 (N, H, W)) and / or the centres used ((N, k, 3) float64)."""
+    xb, sq = _u8_batch(x, "quantize")
+    n, h, w, c = xb.shape
+    if c != 3:
+        raise ValueError("quantize: needs 3-channel BGR images")
+    k = int(k)
+    y = torch.empty_like(xb) if out is None else out.view(n, h, w, c)
+    lab = torch.empty((n, h, w), dtype=torch.uint8, device=xb.device) if return_labels else None
+    cen_out = (torch.empty((n, k, 3), dtype=torch.float64, device=xb.device)
+               if return_centers else None)
+    cin = None
+    if centers is not None:
+        if centers.device != xb.device or centers.dtype != torch.float64 or \
+                tuple(centers.shape) != (n, k, 3):
+            raise ValueError(f"quantize: centers must be float64 {(n, k, 3)} on the batch's device")
+        cin = centers.contiguous()
+    ids = _ids_tensor(image_ids, n, xb.device) if image_ids is not None else None
+    lib = _lib.load()
+    ws_bytes = lib.idn_quant_workspace_size(n, k)
+    ws = _workspace(ws_bytes, xb.device) if ws_bytes else None
+    rc = lib.idn_quant_u8(xb.data_ptr(), y.data_ptr(), lab.data_ptr() if lab is not None else None,
+                          n, h, w, w * 3, k, int(seed) & (2 ** 64 - 1), int(offset),
+                          ids.data_ptr() if ids is not None else None,
+                          cin.data_ptr() if cin is not None else None,
+                          cen_out.data_ptr() if cen_out is not None else None,
+                          ws.data_ptr() if ws is not None else None, ws_bytes, _stream())
+    _lib.check(rc, "idn_quant_u8")
+    res = [_finish(y, sq)]
+    if return_labels:
+        res.append(_finish(lab, sq))
+    if return_centers:
+        res.append(_finish(cen_out, sq))
+    return res[0] if len(res) == 1 else tuple(res)
+
+
+def cvt_color_lab(x: torch.Tensor, to_lab: bool = True) -> torch.Tensor:
+    """cv2.cvtColor(x, COLOR_BGR2LAB) (to_lab) or (x, COLOR_LAB2BGR) on 8-bit 3-channel images."""
+    xb, sq = _u8_batch(x, "cvt_color_lab")
+    n, h, w, c = xb.shape
+    if c != 3:
+        raise ValueError("cvt_color_lab: needs 3 channels")
+    y = torch.empty_like(xb)
+    fn = "idn_bgr2lab_u8" if to_lab else "idn_lab2bgr_u8"
+    _lib.check(getattr(_lib.load(), fn)(xb.data_ptr(), y.data_ptr(), n, h, w, w * 3, _stream()), fn)
+    return _finish(y, sq)
+
+
+def copy_flat(x: torch.Tensor, out: torch.Tensor, policy: int = 0) -> torch.Tensor:
+    """out <- x as one flat byte copy (the bench's copy ceiling; policy 1 = nontemporal)."""
+    if x.device.type != "cuda" or out.device != x.device:
+        raise ValueError("copy_flat: both tensors must be on the same GPU")
+    if not (x.is_contiguous() and out.is_contiguous()) or x.nbytes != out.nbytes:
+        raise ValueError("copy_flat: contiguous tensors of equal byte size required")
+    rc = _lib.load().idn_copy_u8(x.data_ptr(), out.data_ptr(), x.nbytes, int(policy), _stream())
+    _lib.check(rc, "idn_copy_u8")
+    return out
+
+
 # ---- blob epilogue -----------------------------------------------------------------------------
 
 def blob(x: torch.Tensor, pixel_means=PIXEL_MEANS, out_hw: Optional[Tuple[int, int]] = None,
@@ -374,8 +450,9 @@ _WS_CACHE: dict = {}
 
 
 def _workspace(nbytes: int, device) -> torch.Tensor:
-    """grow-only per-device scratch (the C-ABI never allocates)."""
-    key = str(device)
+    """grow-only scratch per (device, current stream) (the C-ABI never allocates): calls on one
+    stream are ordered, so they may share it; calls on two streams get separate buffers."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     ws = _WS_CACHE.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
@@ -463,17 +540,25 @@ def shader(x: torch.Tensor, factor: float = 3.0) -> torch.Tensor:
     return _finish(y, sq)
 
 
-def bloom(x: torch.Tensor, rng=None, **flare_kw) -> torch.Tensor:
+def bloom(x: torch.Tensor, rng=None, circles=None, **flare_kw) -> torch.Tensor:
     """add_bloom: Automold.add_sun_flare(img, flare_center=(100,100), angle=-pi/4) per image, the
-    random draws taken from `rng` (default: the global `random`, like the reference)."""
+    random draws taken from `rng` (default: the global `random`, like the reference), or given
+    per image as `circles` = [(circles int32 [k, 8], weights float32 [k, 2]), ...] (what
+    automold.sun_flare_circles returns; plans carry them, idn.noise_spec.plan(hw=...))."""
     import math
     from . import automold
     xb, sq = _u8_batch(x, "bloom")
     n, h, w, c = xb.shape
-    kw = dict(flare_center=(100, 100), angle=-math.pi / 4)
-    kw.update(flare_kw)
-    circ, wts = zip(*[automold.sun_flare_circles(h, w, rng=rng, **kw) for _ in range(n)])
-    circ, wts = np.stack(circ), np.stack(wts)
+    if circles is not None:
+        if len(circles) != n:
+            raise ValueError(f"bloom: {len(circles)} circle sets for {n} images")
+        circ = np.stack([np.asarray(a, np.int32).reshape(-1, 8) for a, _ in circles])
+        wts = np.stack([np.asarray(b, np.float32).reshape(-1, 2) for _, b in circles])
+    else:
+        kw = dict(flare_center=(100, 100), angle=-math.pi / 4)
+        kw.update(flare_kw)
+        circ, wts = zip(*[automold.sun_flare_circles(h, w, rng=rng, **kw) for _ in range(n)])
+        circ, wts = np.stack(circ), np.stack(wts)
     rmax = int(circ[..., 2].max()) if circ.size else 0
     spans = torch.from_numpy(automold.span_table(max(rmax, 1))).to(xb.device)
     circ_t = torch.from_numpy(np.ascontiguousarray(circ)).to(xb.device)

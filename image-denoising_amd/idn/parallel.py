@@ -79,8 +79,10 @@ class ShardedPreprocessor:
     """Preprocessor over a global batch: this rank runs its shard, optionally all-gathers.
 
     Plans are resolved for the WHOLE batch from the shared seeded rng on every rank (cheap host
-    work), so a rank's images get the same recipes they would get on one GPU; device noise is
-    keyed by the global image id, so results do not depend on the world size."""
+    work), bloom circle draws included (idn.noise_spec.plan(hw=...)), so a rank's images get the
+    same recipes -- and every rank's rng advances identically, batch after batch -- as on one
+    GPU; device noise is keyed by the global image id, so results do not depend on the world
+    size."""
 
     def __init__(self, noise: str, mode: str = "canonical", seed: int = 3, rng=None,
                  group=None):
@@ -88,15 +90,23 @@ class ShardedPreprocessor:
         self.pre = Preprocessor(noise, mode, seed=seed, rng=rng, noise_rng="philox")
         self.group = group
 
-    def __call__(self, shard: torch.Tensor, n_total: int, gather: bool = False,
-                 plans: Optional[Sequence] = None):
+    def assign(self, n_total: int, hw: Tuple[int, int], plans: Optional[Sequence] = None):
+        """(lo, hi, global image ids, this shard's plans, all plans) for this rank; draws the
+        whole batch's plans from the shared rng when `plans` is None."""
         world = dist.get_world_size(self.group) if dist.is_initialized() else 1
         rank = dist.get_rank(self.group) if dist.is_initialized() else 0
         lo, hi = shard_range(n_total, rank, world)
+        all_plans = list(plans) if plans is not None else self.pre.plans(n_total, hw=hw)
+        if len(all_plans) != n_total:
+            raise ValueError(f"{len(all_plans)} plans for a batch of {n_total}")
+        return lo, hi, list(range(lo, hi)), all_plans[lo:hi], all_plans
+
+    def __call__(self, shard: torch.Tensor, n_total: int, gather: bool = False,
+                 plans: Optional[Sequence] = None):
+        lo, hi, ids, mine, all_plans = self.assign(n_total, tuple(shard.shape[1:3]), plans)
         if shard.shape[0] != hi - lo:
-            raise ValueError(f"rank {rank}: shard of {shard.shape[0]} images, expected {hi - lo}")
-        all_plans = list(plans) if plans is not None else self.pre.plans(n_total)
-        outs, _ = self.pre(shard, image_ids=list(range(lo, hi)), plans=all_plans[lo:hi])
+            raise ValueError(f"shard of {shard.shape[0]} images, expected {hi - lo}")
+        outs, _ = self.pre(shard, image_ids=ids, plans=mine)
         if not gather:
             return outs, all_plans
         if len({(o.dtype, tuple(o.shape)) for o in outs}) > 1:

@@ -41,8 +41,10 @@ class Preprocessor:
         self.noise_rng = noise_rng
 
     # ---- planning ------------------------------------------------------------------------
-    def plans(self, n: int) -> List[ns.Plan]:
-        return [ns.plan(self.noise, self.mode, self.rng) for _ in range(n)]
+    def plans(self, n: int, hw: Optional[Tuple[int, int]] = None) -> List[ns.Plan]:
+        """n plans in image order; with hw = (H, W) bloom plans carry their circle draws (so the
+        rng sequence is the reference's per-image order and does not depend on execution)."""
+        return [ns.plan(self.noise, self.mode, self.rng, hw=hw) for _ in range(n)]
 
     # ---- execution -----------------------------------------------------------------------
     def __call__(self, batch: torch.Tensor, image_ids: Optional[Sequence[int]] = None,
@@ -51,12 +53,13 @@ class Preprocessor:
         if batch.dim() == 3:
             batch = batch.unsqueeze(0)
         n = batch.shape[0]
-        plans = list(plans) if plans is not None else self.plans(n)
+        plans = list(plans) if plans is not None else self.plans(n, hw=tuple(batch.shape[1:3]))
         ids = list(image_ids) if image_ids is not None else list(range(n))
         groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
         for i, p in enumerate(plans):
-            # numpy-stream mode draws image by image, in order, like the reference's loop
-            key = (i,) if self.noise_rng == "numpy" else p.steps
+            # numpy-stream mode draws image by image, in order, like the reference's loop;
+            # bloom images share one launch whatever their (per-image) circle draws
+            key = (i,) if self.noise_rng == "numpy" else _group_key(p.steps)
             groups.setdefault(key, []).append(i)
         outs: List[Optional[torch.Tensor]] = [None] * n
         for _, idx in groups.items():
@@ -65,6 +68,8 @@ class Preprocessor:
                 sub = batch
             else:
                 sub = batch.index_select(0, torch.as_tensor(idx, device=batch.device))
+            self._bloom_draws = [next((st.args for st in plans[i].steps if st.op == "bloom"), ())
+                                 for i in idx]
             res = self._run_steps(sub, steps, [ids[i] for i in idx])
             for k, i in enumerate(idx):
                 outs[i] = res[k]
@@ -86,8 +91,16 @@ class Preprocessor:
             return ops.periodic_noise(x, ns.periodic_amplitude(step.args[0], h * w * c))
         if op == "shader":
             return ops.shader(x, 3.0)
+        if op == "quant":
+            if ids != list(range(ids[0], ids[0] + len(ids))):
+                return ops.quantize(x, int(step.args[0]), seed=self.seed, image_ids=ids)
+            return ops.quantize(x, int(step.args[0]), seed=self.seed, offset=int(ids[0]))
         if op == "bloom":
-            return ops.bloom(x, rng=self.rng)
+            draws = getattr(self, "_bloom_draws", None) or []
+            if len(draws) == x.shape[0] and all(draws):
+                return ops.bloom(x, circles=[(np.asarray(c, np.int32), np.asarray(w, np.float32))
+                                             for c, w in draws])
+            return ops.bloom(x, rng=self.rng)  # a plan resolved without (H, W): draw now
         if op in ops.ADD_NOISE_KINDS:
             out = "u8" if (op == "brownian" or (nxt is not None and nxt.kind == "cast_u8")) else "f64"
             level = float(step.args[0])
@@ -189,6 +202,10 @@ class Preprocessor:
                 cur = self._filter(cur, st)
             i += 1
         return list(cur.unbind(0))
+
+
+def _group_key(steps: Tuple[ns.Step, ...]) -> tuple:
+    return tuple(ns.Step(st.kind, st.op) if st.op == "bloom" else st for st in steps)
 
 
 def blob_from_outputs(outs: Sequence[torch.Tensor], pixel_means=ops.PIXEL_MEANS,

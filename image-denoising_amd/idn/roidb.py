@@ -1,3 +1,7 @@
+# Portions of this file (prepare_roidb's body) follow Fast R-CNN's
+#   lib/roi_data_layer/roidb.py -- Fast R-CNN, Copyright (c) 2015 Microsoft,
+#   Licensed under The MIT License, written by Ross Girshick.
+# The drop-in keeps that function's behaviour line for line so callers see identical entries.
 """Drop-in for lib/roi_data_layer/roidb.py:prepare_roidb(imdb, noise) (19-50): the step that
 stamps the `--noise` spec on every roidb entry (roidb.py:50), i.e. the plugin surface on the
 training side.  The derived-overlap fields are kept so get_minibatch's consumers see the same

@@ -164,6 +164,37 @@ int idn_add_pattern_slots_u8(const uint8_t* src, const uint8_t* pattern, uint8_t
 int idn_copy_slots_u8(const uint8_t* src, uint8_t* dst, int n, int64_t per_img,
                       const int64_t* slots, void* stream);
 
+/* ---- quant noise (colour quantisation by k-means in 8-bit Lab) ---------------------------- */
+
+/* Per image: lab = cv2.cvtColor(img, COLOR_BGR2LAB); k-means with k clusters on the Lab pixels;
+ * out = cv2.cvtColor(centres.astype(uint8)[labels], COLOR_LAB2BGR).  Replaces the
+ * MiniBatchKMeans(n_clusters=k).fit_predict blocks of lib/model/test.py:592-765 and
+ * lib/roi_data_layer/minibatch.py:492-667.  C = 3 (BGR), 1 <= k <= 16, h*w >= k.
+ *   centers_in == NULL: device fit -- greedy k-means++ seeding + Lloyd to a fixed point on up to
+ *     8192 Lab samples of the image (all pixels when h*w <= 8192, else Philox draws keyed by
+ *     (seed, image id = offset + i or image_ids[i])).
+ *   centers_in != NULL: replay -- the caller's fitted centres (double [n][k][3], e.g. sklearn's
+ *     cluster_centers_): labels = argmin_j ||c_j||^2 - 2 x.c_j in float64 (sklearn's
+ *     _labels_inertia), bit-exact given the centres.
+ * labels_out (nullable): uint8 [n][h][w] cluster index per pixel.  centers_out (nullable):
+ * double [n][k][3], the centres used.  8-bit Lab follows OpenCV's integer RGB2Lab_b /
+ * Lab2RGBinteger paths (parity vs cv2 unpinned: no cv2 in the build container). */
+int idn_quant_u8(const uint8_t* src, uint8_t* dst, uint8_t* labels_out, int n, int h, int w,
+                 int64_t row_stride, int k, uint64_t seed, uint64_t offset,
+                 const uint64_t* image_ids, const double* centers_in, double* centers_out,
+                 void* workspace, size_t ws_bytes, void* stream);
+size_t idn_quant_workspace_size(int n, int k);
+/* cv2.cvtColor(img, COLOR_BGR2LAB) / (lab, COLOR_LAB2BGR) on 8-bit 3-channel images. */
+int idn_bgr2lab_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t row_stride,
+                   void* stream);
+int idn_lab2bgr_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t row_stride,
+                   void* stream);
+
+/* Flat copy of nbytes (multiple of 16, 16-byte aligned pointers).  policy 0 = default cache
+ * policy, 1 = nontemporal loads and stores.  Not a reference interface: the bench's same-run
+ * copy ceiling (SURVEY §8d "also report a measured copy-kernel peak"). */
+int idn_copy_u8(const uint8_t* src, uint8_t* dst, int64_t nbytes, int policy, void* stream);
+
 /* ---- wavelet denoise (skimage 0.14.2 denoise_wavelet, BayesShrink, soft, YCbCr) -------- */
 
 /* out_u8 = (255*denoise_wavelet(img, method='BayesShrink', mode='soft', wavelet=wavelet,
@@ -171,7 +202,8 @@ int idn_copy_slots_u8(const uint8_t* src, uint8_t* dst, int n, int64_t per_img,
  * c = 3.  levels <= 0 selects skimage's default max(dwt_max_level - 3, 1).  in_f64 (nullable)
  * replaces src when the caller holds a float image in [0,1] (the reference's f64 branches, dense
  * n*h*w*3).  out_f32 (nullable) receives the float result before the U8 cast (dense n*h*w*3).
- * Computed in fp32 with fp64 reductions: |out - reference| <= 1e-5 before the cast.
+ * Computed in fp64 throughout (out_f32 is only a rounded side output):
+ * |out - reference| <= 1e-5 before the cast.
  * Replaces lib/model/test.py:197-201,1807-1810, minibatch.py:1653-1656,
  * minibatch_before_curvelet.py:85-87. */
 int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,

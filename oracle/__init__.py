@@ -6,4 +6,4 @@ __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package,
 checker or the timed CPU baseline.  The product (image-denoising_amd/idn) never imports it and
 fails loudly when its HIP library is missing.
 """
-from . import automold, cv, cvf, sk, wavelet  # noqa: F401
+from . import automold, cv, cvf, cvlab, sk, wavelet  # noqa: F401

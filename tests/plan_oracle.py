@@ -9,10 +9,16 @@ import oracle
 from oracle import sk
 
 
-def _noise(img, step, nxt, rng):
+def _noise(img, step, nxt, rng, quant=None):
     op = step.op
     if op == "original":
         return img
+    if op == "quant":
+        # the device k-means is seeded by Philox, not numpy: the caller supplies the fitted
+        # centres' result (checked against oracle.cvlab.quantize_apply by the caller)
+        if quant is None:
+            raise ValueError("run_plan: a quant step needs the quant callback")
+        return quant(img, int(step.args[0]))
     if op == "periodic":
         from idn import noise_spec as ns
         h, w, c = img.shape
@@ -64,15 +70,15 @@ def _filter(x, step):
     raise ValueError(op)
 
 
-def run_plan(img: np.ndarray, steps, rng):
-    """Returns (output, touched_by_wavelet)."""
+def run_plan(img: np.ndarray, steps, rng, quant=None):
+    """Returns (output, touched_by_wavelet).  quant(img, k) -> u8 image for a quant step."""
     cur, wl = img, False
     i = 0
     while i < len(steps):
         st = steps[i]
         nxt = steps[i + 1] if i + 1 < len(steps) else None
         if st.kind == "noise":
-            cur = _noise(cur, st, nxt, rng)
+            cur = _noise(cur, st, nxt, rng, quant)
         elif st.kind == "cast_u8":
             cur = sk.to_u8(255 * cur)
         else:

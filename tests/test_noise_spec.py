@@ -89,12 +89,9 @@ def test_test_v0_curvelet_discarded():
 def test_test_v0_mix_pool_and_bloom():
     seen = set()
     for s in range(400):
-        try:
-            p = ns.plan("noise_mix_var_low", "test_v0", R(s))
-        except NotImplementedError:
-            continue
+        p = ns.plan("noise_mix_var_low", "test_v0", R(s))  # quant included: no draw raises
         seen.add(p.noise_type)
-    assert "bloom" in seen and "sap_var0.2" in seen
+    assert {"bloom", "sap_var0.2", "quant_var3"} <= seen
     assert ops(ns.plan("bloom", "test_v0", R(0))) == [("noise", "bloom")]
 
 
@@ -128,10 +125,7 @@ def test_train_v0_hook_on_float64_mean_and_failures():
 
 def test_train_v0_mix_bloom_runs_shader():
     for s in range(400):
-        try:
-            p = ns.plan("noise_mix_var_low", "train_v0", R(s))
-        except NotImplementedError:
-            continue
+        p = ns.plan("noise_mix_var_low", "train_v0", R(s))
         if p.noise_type == "bloom":
             assert ops(p) == [("noise", "shader")]  # minibatch.py:1571-1572
             return
@@ -143,9 +137,23 @@ def test_unknown_level_unbound_in_test_v0():
         ns.plan("speckle_var9.9", "test_v0", R(0))
 
 
-def test_quant_not_implemented_and_additive_noises_planned():
-    with pytest.raises(NotImplementedError):
-        ns.plan("quant_var3", "train_v0", R(0))  # MiniBatchKMeans: SURVEY §8f row 4
+def test_quant_and_additive_noises_planned():
+    # MiniBatchKMeans(n_clusters=k) in LAB, then LAB->BGR: u8 (minibatch.py:492-667)
+    assert ops(ns.plan("quant_var3", "train_v0", R(0))) == [("noise", "quant", 3)]
+    assert ops(ns.plan("quant_var10", "canonical", R(0))) == [("noise", "quant", 10)]
+    assert ops(ns.plan("quant_median_var7", "canonical", R(0))) == [
+        ("noise", "quant", 7), ("filter", "median", 3)]
+    assert ops(ns.plan("quant_wavelet_var10", "canonical", R(0))) == [
+        ("noise", "quant", 10), ("filter", "wavelet", "bior1.5", None)]
+    # train_v0: closure median + post-hook median (double filtering, as for the other noises)
+    assert ops(ns.plan("quant_median_var3", "train_v0", R(0))) == [
+        ("noise", "quant", 3), ("filter", "median", 3), ("filter", "median", 3)]
+    with pytest.raises(AttributeError):
+        ns.plan("quant_var5", "train_v0", R(0))  # `im = []` returned (minibatch.py:493)
+    for s in range(50):  # every mix list resolves (quant was the last unplanned type)
+        for key in ("var_low", "var_medium", "var_high", "var_all"):
+            for mode in ("test_v0", "train_v0", "canonical"):
+                ns.plan(f"noise_mix_{key}", mode, R(s))
     assert ops(ns.plan("uniform_var0.6", "train_v0", R(0))) == [("noise", "uniform", 0.6)]
     assert ns.plan("uniform_var0.6", "train_v0", R(0)).out_dtype == "f64"  # minibatch.py:787
     assert ops(ns.plan("gamma_var0.2", "test_v0", R(0))) == [("noise", "gamma", 0.2), ("cast_u8", "u8")]

@@ -91,3 +91,53 @@ def _bad_worker(rank, port, q):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+# ---- ShardedPreprocessor: plan assignment and image ids per rank (no GPU work) ---------------
+
+def _plan_worker(rank, world, port, sizes, spec, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        parallel.init_from_env(backend="gloo")
+        sp = parallel.ShardedPreprocessor(spec, mode, seed=26)
+        got = []
+        for n_total in sizes:  # consecutive batches: every rank's rng must stay in step
+            lo, hi, ids, mine, _ = sp.assign(n_total, (600, 1000))
+            got.append((lo, hi, ids, mine))
+        q.put((rank, got, None))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sizes", [(2, (7, 5)), (3, (7, 4)), (3, (2, 8))])
+def test_sharded_preprocessor_assignment_matches_one_process(world, sizes):
+    """Each rank's shard gets the plans (bloom circle draws included) and global image ids a
+    single process would give those images, over two consecutive uneven batches."""
+    import random
+    from idn.pipeline import Preprocessor
+    spec, mode = "noise_mix_var_low", "test_v0"
+    ref_pre = Preprocessor(spec, mode, seed=26, rng=random.Random(26))
+    ref = [ref_pre.plans(n, hw=(600, 1000)) for n in sizes]
+    assert any(st.op == "bloom" and st.args for b in ref for p in b for st in p.steps), \
+        "the seed must draw at least one bloom to exercise the circle draws"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, sizes, spec, mode, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, got, err in res:
+        assert err is None, f"rank {rank}: {err}"
+        for b, n_total in enumerate(sizes):
+            lo, hi, ids, mine = got[b]
+            assert (lo, hi) == parallel.shard_range(n_total, rank, world)
+            assert ids == list(range(lo, hi))
+            assert mine == ref[b][lo:hi]

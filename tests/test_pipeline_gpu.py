@@ -16,27 +16,37 @@ SPECS = {
                   "periodic_mean_var100", "original_median", "shader", "bloom",
                   "sap_wavelet_var0.2", "noise_mix_var_low_median", "speckle_mean_var2.0",
                   "uniform_median_var0.6", "gamma_wavelet_var0.1", "brownian_mean_var0.09",
-                  "rayleigh_var0.2", "noise_mix_var_all"],
+                  "rayleigh_var0.2", "noise_mix_var_all", "quant_var7", "quant_median_var3",
+                  "quant_wavelet_var10"],
     "test_v0": ["gaussian_var1.0", "sap_median_var0.4", "speckle_mean_var1.0", "poisson_wavelet",
                 "anything_else", "noise_mix_var_all", "bloom", "gaussian_wavelet_var0.1",
                 "periodic_bilateral_varsize"],
     "train_v0": ["gaussian_mean_var0.1", "speckle_var2.0", "gaussian_gaus_blur_var1.5",
                  "sap_var0.8", "periodic_median_var3.14", "noise_mix_var_medium",
                  "poisson_median", "sap_bilateral_var0.2", "uniform_var0.2",
-                 "rayleigh_gaus_blur_var0.3", "gamma_var0.05", "brownian_wavelet_var0.9"],
+                 "rayleigh_gaus_blur_var0.3", "gamma_var0.05", "brownian_wavelet_var0.9",
+                 "quant_bilateral_var10", "noise_mix_var_high"],
 }
 
 
 def _plans(spec, mode, n, seed):
     from idn import noise_spec as ns
-    out, s = [], seed
-    while len(out) < n:
-        try:
-            out.append(ns.plan(spec, mode, random.Random(s)))
-        except NotImplementedError:
-            pass  # a mix draw landed on a §8f "next" noise type; draw again
-        s += 1000
-    return out
+    return [ns.plan(spec, mode, random.Random(seed + 1000 * i)) for i in range(n)]
+
+
+def _quant_checker(seed, image_id):
+    """quant step of the oracle run: the device fit's centres for this image (Philox-seeded,
+    keyed by (seed, image id) as the pipeline keys it), re-applied by the oracle."""
+    def quant(img, k):
+        import idn
+        import torch
+        from oracle import cvlab
+        x = torch.from_numpy(np.ascontiguousarray(img[None])).cuda()
+        out, cen = idn.ops.quantize(x, k, seed=seed, image_ids=[image_id], return_centers=True)
+        ref, _, _ = cvlab.quantize_apply(img, cen[0].cpu().numpy())
+        assert np.array_equal(out[0].cpu().numpy(), ref)
+        return ref
+    return quant
 
 
 @pytest.mark.parametrize("mode,spec", [(m, s) for m, ss in SPECS.items() for s in ss])
@@ -53,7 +63,7 @@ def test_plan_parity(dev, mode, spec):
     np.random.seed(123)
     orng = random.Random(77)
     for i, p in enumerate(plans):
-        ref, wl = run_plan(imgs[i], p.steps, orng)
+        ref, wl = run_plan(imgs[i], p.steps, orng, quant=_quant_checker(pre.seed, i))
         got = outs[i].cpu().numpy()
         assert got.dtype == ref.dtype == (np.uint8 if p.out_dtype == "u8" else np.float64), p
         if got.dtype == np.float64:
@@ -63,8 +73,12 @@ def test_plan_parity(dev, mode, spec):
         has_bil = any(s.op == "bilateral" for s in p.steps)
         has_bloom = any(s.op == "bloom" for s in p.steps)
         if wl:
-            # fp64 wavelet vs numpy: last-bit differences flip U8 casts only at integer boundaries
-            assert d.max() <= 2 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
+            # fp64 wavelet vs numpy: last-bit differences flip a U8 cast only where 255*x sits
+            # at an integer boundary (<= 1 LSB per wavelet step); train_v0's double filtering
+            # (closure wavelet + hook wavelet) feeds such a flipped pixel into the second
+            # wavelet, so the bound is one LSB per wavelet step in the plan
+            n_wl = sum(s.op == "wavelet" for s in p.steps)
+            assert d.max() <= n_wl and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
         elif has_bil or has_bloom:
             assert d.max() <= 1 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
         else:
