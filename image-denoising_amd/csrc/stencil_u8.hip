@@ -26,6 +26,8 @@
 //   stencil_u8_generic  one thread per pixel for shapes the lane layout does not accept
 #include "stripe.hpp"
 
+#include <type_traits>
+
 namespace idn {
 
 enum StencilOp { OP_GAUSS3 = 0, OP_GAUSS5 = 1, OP_BOX3 = 2 };
@@ -377,6 +379,142 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
 }
 
 
+// ---- streaming ring form ---------------------------------------------------------------------
+// One workgroup (3 waves) walks a STRIP of consecutive bands of one image top to bottom.  The
+// image's bytes stream through an LDS ring of RING bytes in 1 KB chunks by LDS-DMA
+// (buffer_load_dwordx4 ... lds), PD bands ahead of the band being filtered: every input byte is
+// fetched from HBM once per strip (no halo re-reads by neighbouring bands), so loads and stores
+// may both take the nontemporal policy -- the copy that reaches ~6.5 TB/s on this chip
+// (nontemporal loads AND stores) instead of ~5.6 TB/s (default policy, which the band-tiled form
+// needs to keep its halo rows in L2).
+//   chunk m (image bytes [1024 m, 1024 m + 1024)) lives in ring slot m mod (RING / 1024), so
+//   image byte B sits at ring offset B mod RING and a row is read with the same lane layout as
+//   the tile form (two 8-byte LDS reads per lane, each wrapping independently).
+// Synchronisation per band i (all counts wave-uniform, so one immediate vmcnt serves every wave):
+//   issue band i+PD's new chunks (exactly MAXC DMAs per wave; the unused ones land in a dump
+//   slot) -> s_waitcnt vmcnt(PD*MAXC + PD*2*NB) retires band i's chunks (younger: PD bands of
+//   DMAs and PD bands of 2*NB stores; the prologue issues PD*2*NB dummy stores so the count
+//   holds from the first band) -> s_barrier -> filter + store NB rows -> s_barrier (the ring
+//   slots of band i's oldest rows may now be refilled).
+constexpr int RING_WGT = 192;
+
+template <int NB, int PD, int RLOG>
+struct RingShape {
+  static constexpr int RING = 1 << RLOG;
+  static constexpr int NSLOT = RING >> 10;
+  // chunks a band's new rows can touch (<= 3024-byte rows), split over 3 waves
+  static constexpr int MAXC = ((NB * TILE_RBMAX + 1023) / 1024 + 1 + 2) / 3;
+  static constexpr int MAXC0 = (((NB + 4) * TILE_RBMAX + 1023) / 1024 + 1 + 2) / 3;
+  static constexpr int VMCNT = PD * MAXC + PD * 2 * NB;
+  static_assert((NB * (PD + 1) + 4) * TILE_RBMAX + 2048 <= RING, "ring too small for NB / PD");
+  static_assert(VMCNT <= 63, "vmcnt field is 6 bits");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt at their maxima); asm so no memory op moves
+  // across it
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int C, int OP, int NB, int PD, int RLOG, int LAUX, int SAUX>
+__global__ __launch_bounds__(RING_WGT) void stencil_u8_ring(const uint8_t* __restrict__ src,
+                                                           uint8_t* __restrict__ dst, int h, int rb,
+                                                           int nseg, int seg_len, int bands,
+                                                           int strips_per_img, int bands_per_strip) {
+  constexpr int K = Stencil<OP>::K;
+  constexpr int R = K / 2;
+  using RS = RingShape<NB, PD, RLOG>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[RS::RING + 1024];
+  uint8_t* const ring = lds;
+  uint8_t* const dump = lds + RS::RING;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int strip = blockIdx.x;
+  const int img = strip / strips_per_img;
+  const int b0 = (strip % strips_per_img) * bands_per_strip;
+  const int nbands = min(b0 + bands_per_strip, bands) - b0;
+  if (nbands <= 0) return;  // whole workgroup: no barrier is pending
+  const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
+  const rsrc_t rs = make_rsrc(src + (size_t)img * img_bytes, img_bytes);
+  const rsrc_t rd = make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
+
+  // chunk bookkeeping (wave-uniform): band g of the strip needs image rows up to
+  // min(y0(g) + NB + R, h) resident; F = next chunk not yet fetched
+  auto chunk_end = [&](int g) -> uint32_t {
+    const int yend = min((b0 + g) * NB + NB + R, h);
+    return ((uint32_t)yend * (uint32_t)rb + 1023u) >> 10;
+  };
+  uint32_t F = ((uint32_t)max(b0 * NB - R, 0) * (uint32_t)rb) >> 10;
+  auto issue = [&](uint32_t to, int maxc) {
+    for (int i = 0; i < maxc; ++i) {
+      const uint32_t m = F + (uint32_t)wave + 3u * (uint32_t)i;
+      const bool valid = m < to;
+      uint8_t* d = valid ? ring + ((m & (RS::NSLOT - 1)) << 10) : dump;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)d, 16,
+          valid ? (m << 10) + 16u * (uint32_t)lane : OOB_OFF, 0, 0, LAUX);
+    }
+    F = max(F, to);
+  };
+
+  // prologue: band 0's whole tile, then the new rows of bands 1..PD-1; PD*2*NB dummy stores
+  issue(chunk_end(0), RS::MAXC0);
+  for (int g = 1; g < PD; ++g) issue(g < nbands ? chunk_end(g) : F, RS::MAXC);
+  for (int i = 0; i < PD * NB; ++i) {
+    const v4u z = {0u, 0u, 0u, 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(z, rd, OOB_OFF, 0, SAUX);
+    __builtin_amdgcn_raw_buffer_store_b64(v2u{0u, 0u}, rd, OOB_OFF, 0, SAUX);
+  }
+
+  const bool active = wave < nseg;
+  const StripeGeom g = stripe_geom(min(wave, nseg - 1), lane, rb, nseg, seg_len, 1);
+  const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
+  const StoreOffs so = store_offs(g);
+  constexpr uint32_t RMASK = (uint32_t)RS::RING - 1u;
+
+  for (int i = 0; i < nbands; ++i) {
+    issue(i + PD < nbands ? chunk_end(i + PD) : F, RS::MAXC);
+    wait_vmcnt<RS::VMCNT>();
+    asm volatile("s_barrier" ::: "memory");
+    const int y0 = (b0 + i) * NB;
+    const int y1 = min(y0 + NB, h);
+    const int nin = (y1 - y0) + 2 * R;
+    // all of the band's LDS reads first (one wait), then the arithmetic
+    v4u raw[NB + 2 * R];
+#pragma unroll
+    for (int r = 0; r < NB + 2 * R; ++r) {
+      const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
+      const uint32_t B = (uint32_t)y * (uint32_t)rb + ld_off;
+      const v2u lo = *reinterpret_cast<const v2u*>(&ring[B & RMASK]);
+      const v2u hi = *reinterpret_cast<const v2u*>(&ring[(B + 8u) & RMASK]);
+      raw[r] = v4u{lo.x, lo.y, hi.x, hi.y};
+    }
+    uint32_t Rg[K][8];
+    auto take_row = [&](int r) {
+      v4u Lv = raw[r];
+      const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
+      const v4u F4 = v4u{lead_fix<C, BORDER_REFLECT101>(L, -8),
+                         lead_fix<C, BORDER_REFLECT101>(L, -4), L[0], L[1]};
+      Lv = g.lead ? F4 : Lv;
+      unpack_row(Lv, Rg[r % K]);
+    };
+#pragma unroll
+    for (int r = 0; r < 2 * R; ++r) take_row(r);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int r = 2 * R + u;
+      take_row(r);
+      const int y = y0 + u;
+      ring_out_row<C, OP, (SAUX & 2)>(Rg, r % K, g, rd, so,
+                                      (active && y < y1) ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 // ---- generic path ------------------------------------------------------------------------
 template <int OP>
 __global__ __launch_bounds__(256) void stencil_u8_generic(const uint8_t* __restrict__ src,
@@ -505,7 +643,44 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
   const int tile_mode = env_int("IDN_STENCIL_TILE", 1);
   const bool ntst = (env_int("IDN_STENCIL_NT", 0) & 2) != 0;  // nontemporal stores (tuning)
   const int map = env_int("IDN_STENCIL_MAP", 1) == 2 ? 2 : 1;
-  if (tile_mode && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
+  const int ring_cfg = env_int("IDN_STENCIL_RING", 1);
+  if (ring_cfg > 0 && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
+      rb <= TILE_RBMAX && h > 2 * R && n <= 65535) {
+    const int nseg = (int)((rb + 1007) / 1008);
+    const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
+    // strips per image: about two resident workgroups per CU over the batch
+    auto go = [&](auto nb_c, auto pd_c, auto rlog_c, auto laux_c, auto saux_c, int wg_per_cu) {
+      constexpr int NBV = decltype(nb_c)::value;
+      const int bands = (h + NBV - 1) / NBV;
+      const int64_t target = (int64_t)256 * wg_per_cu;
+      int spi = (int)std::max<int64_t>(1, (target + n - 1) / n);
+      spi = std::min(spi, std::max(1, bands / 4));  // strips of >= 4 bands
+      const int bps = (bands + spi - 1) / spi;
+      spi = (bands + bps - 1) / bps;
+      IDN_CHECK_ARG((int64_t)n * spi < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
+      hipLaunchKernelGGL((stencil_u8_ring<3, OP, NBV, decltype(pd_c)::value,
+                                          decltype(rlog_c)::value, decltype(laux_c)::value,
+                                          decltype(saux_c)::value>),
+                         dim3((unsigned)(n * spi)), dim3(RING_WGT), 0, st, src, dst, h, (int)rb,
+                         nseg, seg_len, bands, spi, bps);
+      return 0;
+    };
+    using I = std::integral_constant<int, 0>;
+    (void)sizeof(I);
+#define IC(v) std::integral_constant<int, v>()
+    switch (ring_cfg) {
+      case 2: go(IC(4), IC(2), IC(16), IC(2), IC(2), 2); break;
+      case 3: go(IC(8), IC(1), IC(16), IC(2), IC(2), 2); break;
+      case 4: go(IC(6), IC(3), IC(17), IC(2), IC(2), 1); break;
+      case 5: go(IC(8), IC(2), IC(17), IC(2), IC(2), 1); break;
+      case 6: go(IC(6), IC(1), IC(16), IC(0), IC(0), 2); break;
+      case 7: go(IC(6), IC(1), IC(16), IC(2), IC(0), 2); break;
+      case 8: go(IC(6), IC(1), IC(16), IC(0), IC(2), 2); break;
+      case 9: go(IC(4), IC(4), IC(17), IC(2), IC(2), 1); break;
+      default: go(IC(6), IC(1), IC(16), IC(2), IC(2), 2); break;
+    }
+#undef IC
+  } else if (tile_mode && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
       rb <= TILE_RBMAX && h > 2 * R) {
     const int nseg = (int)((rb + 1007) / 1008);
     const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);

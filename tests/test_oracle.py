@@ -319,3 +319,13 @@ def test_additive_noises_vs_fixtures(gold):
         u8, f = additive_oracle(case["mode"], case["level"], img, field)
         assert np.array_equal(u8, g[case["key"] + "_u8"]), case
         assert sha(np.ascontiguousarray(f, np.float64)) == case["sha_f64"], case
+
+
+def test_fast_cpu_baseline_bitexact_with_scalar_oracle():
+    """bench.py's cpu_baseline times oracle/baseline_fast.c; it must compute the same filter."""
+    rs = np.random.RandomState(4)
+    for shape in [(2, 120, 200, 3), (1, 5, 6, 3), (1, 33, 17, 3), (2, 9, 40, 1)]:
+        img = rs.randint(0, 256, size=shape).astype(np.uint8)
+        for k in (3, 5):
+            assert np.array_equal(oracle.cv.gaussian_blur_fast(img, k),
+                                  oracle.cv.gaussian_blur(img, k)), (shape, k)
