@@ -48,15 +48,29 @@ OPS = {
     # 3-level Haar BayesShrink soft threshold (BASELINE config 5 denoiser), fp64 pipeline
     "wavelet_haar3": ("3-level Haar wavelet",
                       lambda idn, x, y: idn.ops.denoise_wavelet(x, "db1", 3, out_u8=y), 6, "wl_"),
+    # bior1.5, default levels (the reference's live denoiser: test.py:1807-1810)
+    "wavelet_bior15": ("bior1.5 wavelet (default levels)",
+                       lambda idn, x, y: idn.ops.denoise_wavelet(x, "bior1.5", None, out_u8=y), 6,
+                       "wl_"),
+    # 5x5 Gaussian straight into the float32 blob (3 B read + 12 B written per pixel)
+    "gauss5_blob": ("5x5 Gaussian -> f32 blob", None, 15, "stencil_u8"),
+    # quant noise, k = 7 (MiniBatchKMeans colour quantisation in Lab: fit + apply)
+    "quant7": ("quant k=7", lambda idn, x, y: idn.ops.quantize(x, 7, seed=3, out=y), 6, "quant_"),
 }
 # arithmetic type each op computes in (the filters are integer SWAR / fixed point)
 DTYPE = {"noise_gaussian": "f64", "noise_poisson": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
+         "cfg2f": "f64", "cfg2p": "f64", "wavelet_bior15": "f64", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
          "cfg3": "f64", "cfg4": "f64", "cfg5": "f64"}
 PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
           "noise_poisson": "skimage random_noise('poisson') law (bit-exact under replay)",
           "wavelet_haar3": "skimage 0.14 denoise_wavelet within 1e-5",
           "bilateral": "cv2.bilateralFilter within 1 LSB",
           "cfg2": "Philox noise + cv2.blur bit-exact", "cfg3": "Philox s&p + cv2.medianBlur bit-exact",
+          "cfg2f": "Philox noise + cv2.blur bit-exact", "cfg2p": "Philox noise + cv2.blur bit-exact",
+          "wavelet_bior15": "skimage 0.14 denoise_wavelet within 1e-5",
+          "gauss5_blob": "cv2.GaussianBlur + blob.py float32 LUT, bit-exact",
+          "quant7": "OpenCV 8-bit Lab + k-means (sklearn-replay bit-exact; device fit within 5% "
+                    "inertia)",
           "cfg4": "Philox speckle + cv2.bilateralFilter within 1 LSB",
           "cfg5": "Philox/periodic noise + denoise_wavelet within 1e-5"}
 
@@ -71,9 +85,13 @@ def _pipeline(kind):
         if t is None or t.shape != x.shape:
             t = state["t"] = x.new_empty(x.shape)
         ops = idn.ops
-        if kind == "cfg2":    # gaussian_var1.0 + mean 3x3
+        if kind == "cfg2":    # gaussian_var1.0 + mean 3x3: noise launch, then the filter
             ops.random_noise(x, "gaussian", var=1.0, seed=3, out="u8", out_u8=t)
             idn.blur(t, 3, out=y)
+        elif kind == "cfg2f":  # the same in one fused pass (LDS ring)
+            ops.noise_filter(x, "gaussian", "mean", 3, var=1.0, seed=3, out=y, form="fused")
+        elif kind == "cfg2p":  # chunked: noise of chunk k+1 beside the filter of chunk k
+            ops.noise_filter(x, "gaussian", "mean", 3, var=1.0, seed=3, out=y, form="pipelined")
         elif kind == "cfg3":  # sap_var0.4 + median 5x5
             ops.random_noise(x, "s&p", amount=0.4, seed=3, out="u8", out_u8=t)
             idn.median_blur(t, 5, out=y)
@@ -115,12 +133,26 @@ def _pipeline(kind):
 
 PIPELINES = {
     "cfg2": ("gaussian_var1.0 + 3x3 mean (config 2)", 256),
+    "cfg2f": ("gaussian_var1.0 + 3x3 mean (config 2, fused one-pass form)", 256),
+    "cfg2p": ("gaussian_var1.0 + 3x3 mean (config 2, chunk-pipelined on two streams)", 256),
     "cfg3": ("sap_var0.4 + 5x5 median (config 3)", 1024),
     "cfg4": ("speckle_var1.0 + bilateral d=9 s=75/75 (config 4)", 512),
     "cfg5": ("mixed noise + 3-level Haar wavelet (config 5)", 512),
 }
 for _k, (_lbl, _b) in PIPELINES.items():
     OPS[_k] = (_lbl, _pipeline(_k), 6, "pipeline")
+
+
+def _gauss5_blob(idn, x, y):
+    st = _gauss5_blob.__dict__
+    b = st.get("blob")
+    if b is None or b.shape != x.shape:
+        import torch
+        b = st["blob"] = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    idn.ops.gaussian_blob(x, 5, out=b)
+
+
+OPS["gauss5_blob"] = (OPS["gauss5_blob"][0], _gauss5_blob, 15, "stencil_u8")
 
 METRIC = "Mpix/s filtered (5\u00d75 Gaussian, 1000\u00d7600) at 1/2/4/8 GPUs; % HBM roofline"
 
@@ -146,7 +178,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
     import numpy as np
     import oracle
     sys.path.insert(0, str(ROOT / "tests"))
-    fn = {
+    table = {
         "gauss5": lambda a: oracle.cv.gaussian_blur_fast(a, 5),
         "gauss3": lambda a: oracle.cv.gaussian_blur_fast(a, 3),
         "box3": lambda a: oracle.cv.blur(a, 3),
@@ -166,9 +198,16 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
             a, np.random.normal(0.0, 1.0, a.shape))), 9, 75.0, 75.0),
         "cfg5": lambda a: oracle.sk.to_u8(255 * oracle.wavelet.denoise_wavelet(oracle.sk.to_u8(
             255 * oracle.sk.noise_gaussian(a[0], np.random.normal(0.0, 1.0, a[0].shape))), "db1", 3)),
-    }[op]
+        "wavelet_bior15": lambda a: oracle.sk.to_u8(
+            255 * oracle.wavelet.denoise_wavelet(a[0], "bior1.5", None)),
+        "gauss5_blob": lambda a: oracle.sk.blob_f32(oracle.cv.gaussian_blur_fast(a, 5)),
+    }
+    table["cfg2f"] = table["cfg2p"] = table["cfg2"]
+    fn = table.get(op)
+    if fn is None:
+        return None
     rs = np.random.RandomState(3)
-    nb = 16 if op in ("gauss5", "gauss3") else 1  # the threaded filters get a batch per call
+    nb = 16 if op in ("gauss5", "gauss3", "gauss5_blob") else 1  # threaded: a batch per call
     img = np.clip(128 + rs.uniform(-64, 64, size=(nb, H, W, C)), 0, 255).astype(np.uint8)
     fn(img)  # warm (build + page in)
     n_img, t0 = 0, time.perf_counter()
@@ -178,12 +217,12 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         el = time.perf_counter() - t0
         if el >= budget_s or n_img >= 20000:
             break
-    if op in ("noise_gaussian", "noise_poisson", "wavelet_haar3", "cfg5"):
+    if op in ("noise_gaussian", "noise_poisson", "wavelet_haar3", "cfg5", "wavelet_bior15"):
         threads, src = 1, "numpy, single thread"
-    elif op in ("cfg2", "cfg3", "cfg4"):
+    elif op in ("cfg2", "cfg2f", "cfg2p", "cfg3", "cfg4"):
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
         src = "numpy noise (1 thread) + oracle/filters.c OpenMP"
-    elif op in ("gauss5", "gauss3"):
+    elif op in ("gauss5", "gauss3", "gauss5_blob"):
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
         src = ("oracle/baseline_fast.c: separable 16-bit SIMD (AVX2) + OpenMP, OpenCV's 8-bit "
                "scheme, bit-exact with the scalar oracle")

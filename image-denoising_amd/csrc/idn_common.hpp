@@ -87,10 +87,13 @@ __host__ __device__ __forceinline__ void philox_round(u32x4& c, uint32_t k0, uin
   c = u32x4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
 }
 
+// ROUNDS = 10 is Random123's default; Salmon et al. (SC'11, Table 2) report Philox4x32 with 7
+// rounds already passing TestU01 BigCrush, and the Gaussian flat stream uses 7 (noise_apply.hpp)
+template <int ROUNDS = 10>
 __host__ __device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint64_t key) {
   uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < ROUNDS; ++r) {
     philox_round(ctr, k0, k1);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;

@@ -8,38 +8,20 @@
 // with a replayed random field (numpy's own draws) the outputs are bit-exact; with the Philox
 // stream they are statistically equivalent (tests/test_noise_gpu.py).
 //
-// RNG: Philox4x32-10 keyed by (seed ^ kind tag); counter = (element pair / draw, image id).
+// RNG: Philox4x32 keyed by (seed ^ kind tag); counter = (element group / draw, image id)
+// (the flat Gaussian / speckle stream: Philox4x32-7 and 16-bit uniforms, noise_apply.hpp).
 // Image id = offset + image index, so a rank that owns images [a, b) of a batch draws exactly
 // what a single GPU would for those images.
 //
 // Also: periodic noise pattern (add_periodic_noise, test.py:1128-1298) and cv2.add(u8, u8).
 #include "idn_common.hpp"
+#include "noise_apply.hpp"
 
 #include <math.h>
 
 #include <algorithm>
 
 namespace idn {
-
-__device__ __forceinline__ double img_as_float(uint32_t v) { return __dmul_rn((double)v, 1.0 / 255.0); }
-
-// np.clip(v, 0, 1) for non-NaN v (v_max_f64 / v_min_f64)
-__device__ __forceinline__ double clip01(double v) { return __builtin_fmin(__builtin_fmax(v, 0.0), 1.0); }
-
-// (255 * out).astype(np.uint8) for out in [0, 1]: truncation (out is never negative here)
-__device__ __forceinline__ uint8_t u8_of(double out) { return (uint8_t)(int)__dmul_rn(out, 255.0); }
-
-// two standard normals from one Philox block (Box-Muller, fp32 hardware transcendentals:
-// v_log/v_sqrt/v_sin/v_cos; sin/cos take revolutions, so theta = u2 needs no 2*pi multiply, and
-// the raw v_sqrt_f32 (1 ulp) replaces the 13-instruction correctly rounded sqrtf sequence)
-__device__ __forceinline__ void normal2(const u32x4& r, float& z0, float& z1) {
-  const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
-  const float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);           // [0, 1)
-  const float rad =
-      __builtin_amdgcn_sqrtf(-2.0f * 0.6931471805599453f * __builtin_amdgcn_logf(u1));
-  z0 = rad * __builtin_amdgcn_cosf(u2);
-  z1 = rad * __builtin_amdgcn_sinf(u2);
-}
 
 constexpr uint64_t KIND_TAG = 0x9E3779B97F4A7C15ull;
 
@@ -114,20 +96,9 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
 }
 
 // ---- flat form (compact rows, Philox stream): 16 consecutive elements per thread -------------
-// One 16-byte load / store per lane, image = blockIdx.y, no 64-bit index division.  Stream:
-//   gaussian / speckle  counter (e/4, 0, image id) -> 4 u32 -> two Box-Muller pairs -> the 4
-//                       normals of elements 4q..4q+3
-//   s&p                 counter (e/2, 1, image id) -> (U1, U2) of elements 2q and 2q+1 as 32-bit
-//                       uniforms compared against integer thresholds (|P - p| < 2^-32)
-// The apply is the same float64 expression as the element kernels above.
-__device__ __forceinline__ void normal4(const u32x4& r, float (&z)[4]) {
-  normal2(r, z[0], z[1]);
-  const u32x4 r2{r.z, r.w, 0u, 0u};
-  normal2(r2, z[2], z[3]);
-}
-
-// MEAN0: mean == 0.0, so mean + sd*z is sd*z exactly up to the sign of a zero, which the
-// following x + n / x + x*n (x >= 0) cannot see: one float64 add per element less
+// One 16-byte load / store per lane, image = blockIdx.y, no 64-bit index division; the stream and
+// the float64 apply are noise16_u8 (noise_apply.hpp), shared with the fused noise -> filter
+// kernel (stencil_u8.hip), so the fused and two-step results are identical.
 template <int KIND, bool MEAN0 = false>
 __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t t_flip,
                                                            uint32_t t_salt) {
@@ -137,49 +108,10 @@ __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t
   if (e0 >= a.elems) return;
   const uint64_t gimg = image_id(a, img);
   const int64_t base = slot_of(a, img) * a.elems + e0;
-  const uint8_t* src = a.src + base;
-  const v4u raw = *reinterpret_cast<const v4u*>(src);
-  const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
-  uint32_t o[4] = {0u, 0u, 0u, 0u};
-  double* of = a.out_f64 ? a.out_f64 + base : nullptr;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {  // elements 4k .. 4k+3
-    double outv[4];
-    if constexpr (KIND == IDN_NOISE_SAP) {
-#pragma unroll
-      for (int hlf = 0; hlf < 2; ++hlf) {
-        const uint32_t q = chunk * 8u + (uint32_t)(2 * k + hlf);
-        const u32x4 r = philox4x32(u32x4{q, 1u, (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
-        const uint32_t u1[2] = {r.x, r.z}, u2[2] = {r.y, r.w};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int b = 2 * hlf + j;
-          const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
-          outv[b] = u1[j] < t_flip ? (u2[j] < t_salt ? 1.0 : 0.0) : xv;
-        }
-      }
-    } else {
-      const uint32_t q = chunk * 4u + (uint32_t)k;
-      const u32x4 r = philox4x32(u32x4{q, 0u, (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
-      float z[4];
-      normal4(r, z);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const double sz = __dmul_rn(a.p1, (double)z[b]);
-        const double nz = MEAN0 ? sz : __dadd_rn(a.p0, sz);
-        const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
-        if (KIND == IDN_NOISE_GAUSSIAN) outv[b] = clip01(__dadd_rn(xv, nz));
-        else outv[b] = clip01(__dadd_rn(xv, __dmul_rn(xv, nz)));
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      o[k] |= (uint32_t)u8_of(outv[b]) << (8 * b);
-      if (of) of[4 * k + b] = outv[b];
-    }
-  }
-  if (a.out_u8)
-    *reinterpret_cast<v4u*>(a.out_u8 + base) = v4u{o[0], o[1], o[2], o[3]};
+  const v4u raw = *reinterpret_cast<const v4u*>(a.src + base);
+  const v4u o = noise16_u8<KIND, MEAN0>(raw, chunk, gimg, a.key, a.p0, a.p1, t_flip, t_salt,
+                                        a.out_f64 ? a.out_f64 + base : nullptr);
+  if (a.out_u8) *reinterpret_cast<v4u*>(a.out_u8 + base) = o;
 }
 
 // salt & pepper: flipped = U1 < cdf0(amount), salted = U2 < cdf0(salt_vs_pepper)
@@ -625,13 +557,9 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       a.p1 = p1 / (p1 + (1.0 - p1));
       if (flat) {
         // 32-bit uniform thresholds: P(u < t / 2^32) within 2^-32 of cdf0
-        auto thr = [](double pp) -> uint32_t {
-          const double t = ceil(pp * 4294967296.0);
-          return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-        };
         const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
         hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SAP>, grid, dim3(256), 0, st, a,
-                           thr(a.p0), thr(a.p1));
+                           sap_threshold(a.p0), sap_threshold(a.p1));
       } else {
         hipLaunchKernelGGL(noise_sap_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
       }

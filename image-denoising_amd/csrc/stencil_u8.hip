@@ -25,6 +25,7 @@
 //   stencil_u8_vf   (strided rows) the same arithmetic loading each row segment from HBM
 //   stencil_u8_generic  one thread per pixel for shapes the lane layout does not accept
 #include "stripe.hpp"
+#include "noise_apply.hpp"
 
 #include <type_traits>
 
@@ -296,6 +297,51 @@ __device__ __forceinline__ void lds_take_row(const uint8_t* tile, uint32_t o, bo
   unpack_row(Lv, U);
 }
 
+constexpr int RING_WGT = 192;
+enum RingPre { PRE_NONE = 0, PRE_GAUSSIAN = 1, PRE_SPECKLE = 2, PRE_SAP = 3 };
+enum RingEpi { EPI_U8 = 0, EPI_BLOB = 1 };
+
+struct RingArgs {
+  const uint8_t* src;
+  uint8_t* dst;
+  float* blob;
+  int h, rb, nseg, seg_len, bands, strips_per_img, bands_per_strip;
+  uint64_t key, offset;
+  const uint64_t* ids;
+  double p1;
+  uint32_t t_flip, t_salt;
+  double mean[3];
+};
+
+// the blob of one lane's 16 output bytes at row byte offset q: 16 floats, 4 (full chunk) or
+// 2 (half chunk) 16-byte stores; always 6 store instructions (unused ones out of range)
+__device__ __forceinline__ void blob_store16(const v4u& o, const double (&means)[3],
+                                             rsrc_t rb_rsrc, const StoreOffs& so,
+                                             uint32_t row_off, int m0) {
+  const uint32_t b[4] = {o.x, o.y, o.z, o.w};
+  float f[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ch = (m0 + i) % 3;
+    const double mean = ch == 0 ? means[0] : ch == 1 ? means[1] : means[2];
+    f[i] = (float)__dsub_rn((double)((b[i >> 2] >> (8 * (i & 3))) & 0xFFu), mean);
+  }
+  auto v = [&](int k) {
+    return v4u{__float_as_uint(f[4 * k]), __float_as_uint(f[4 * k + 1]),
+               __float_as_uint(f[4 * k + 2]), __float_as_uint(f[4 * k + 3])};
+  };
+  const uint32_t full = so.full + row_off, half = so.half + row_off;  // byte offsets
+  // full chunk: bytes q..q+15 -> floats at 4*(q..q+15)
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    __builtin_amdgcn_raw_buffer_store_b128(v(k), rb_rsrc, full >= OOB_OFF ? OOB_OFF : 4u * full + 16u * k, 0, 0);
+  // half chunk: bytes 0..7 (at q) or 8..15 (at q + 8) of the chunk
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    __builtin_amdgcn_raw_buffer_store_b128(so.hi ? v(2 + k) : v(k), rb_rsrc,
+                                           half >= OOB_OFF ? OOB_OFF : 4u * half + 16u * k, 0, 0);
+}
+
 // ---- LDS-tiled form --------------------------------------------------------------------------
 // One workgroup = one band of NB output rows of one image, nseg waves (<= 3: rows <= 3024 bytes).
 // The band's NB + 2R input rows are contiguous in HBM (row_stride == row bytes), so the whole
@@ -311,14 +357,19 @@ struct TileShape {
   static constexpr int ROWS = NB + K - 1;
   static constexpr int BYTES = ROWS * TILE_RBMAX + 16;           // + alignment shift
   static constexpr int NL = (BYTES + 16 * TILE_WGT - 1) / (16 * TILE_WGT);
-  static constexpr int LDS = NL * 16 * TILE_WGT;
+  // exact footprint (the fetch never writes past the tile's bytes): one more resident
+  // workgroup per CU for some band heights than a whole number of fetch rounds would allow
+  static constexpr int LDS = (BYTES + 15) / 16 * 16;
 };
 
-template <int C, int OP, int NB, int NT>
+template <int C, int OP, int NB, int NT, int EPI = EPI_U8>
 __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __restrict__ src,
                                                           uint8_t* __restrict__ dst, int h, int rb,
                                                           int nseg, int seg_len, int bands,
-                                                          int total_items, int map) {
+                                                          int total_items, int map,
+                                                          float* __restrict__ blob = nullptr,
+                                                          double mb = 0.0, double mg = 0.0,
+                                                          double mr = 0.0) {
   constexpr int K = Stencil<OP>::K;
   constexpr int R = K / 2;
   using TS = TileShape<NB, K>;
@@ -332,7 +383,8 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
   const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
   const rsrc_t rs = make_rsrc(src + (size_t)g.img * img_bytes, img_bytes);
-  const rsrc_t rd = make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes);
+  const rsrc_t rd = EPI == EPI_U8 ? make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes)
+                                  : make_rsrc(blob + (size_t)g.img * img_bytes, 4u * img_bytes);
 
   const int y0 = g.band * NB;
   const int y1 = min(y0 + NB, h);
@@ -374,85 +426,92 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     const int r = 2 * R + u;
     take_row(r);
     const int y = y0 + u;
-    ring_out_row<C, OP, NT>(Rg, r % K, g, rd, so, y < y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
+    const uint32_t row_off = y < y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF;
+    if constexpr (EPI == EPI_BLOB) {
+      const double means[3] = {mb, mg, mr};
+      blob_store16(ring_row<C, OP>(Rg, r % K, g), means, rd, so, row_off, ((g.q % 3) + 3) % 3);
+    } else {
+      ring_out_row<C, OP, NT>(Rg, r % K, g, rd, so, row_off);
+    }
   }
 }
 
 
-// ---- streaming ring form ---------------------------------------------------------------------
+// ---- streaming ring form (+ fused noise prologue / blob epilogue) ------------------------------
 // One workgroup (3 waves) walks a STRIP of consecutive bands of one image top to bottom.  The
-// image's bytes stream through an LDS ring of RING bytes in 1 KB chunks by LDS-DMA
+// image's bytes stream through an LDS ring of NSLOT 1 KB chunks by LDS-DMA
 // (buffer_load_dwordx4 ... lds), PD bands ahead of the band being filtered: every input byte is
-// fetched from HBM once per strip (no halo re-reads by neighbouring bands), so loads and stores
-// may both take the nontemporal policy -- the copy that reaches ~6.5 TB/s on this chip
-// (nontemporal loads AND stores) instead of ~5.6 TB/s (default policy, which the band-tiled form
-// needs to keep its halo rows in L2).
-//   chunk m (image bytes [1024 m, 1024 m + 1024)) lives in ring slot m mod (RING / 1024), so
-//   image byte B sits at ring offset B mod RING and a row is read with the same lane layout as
-//   the tile form (two 8-byte LDS reads per lane, each wrapping independently).
-// Synchronisation per band i (all counts wave-uniform, so one immediate vmcnt serves every wave):
-//   issue band i+PD's new chunks (exactly MAXC DMAs per wave; the unused ones land in a dump
-//   slot) -> s_waitcnt vmcnt(PD*MAXC + PD*2*NB) retires band i's chunks (younger: PD bands of
-//   DMAs and PD bands of 2*NB stores; the prologue issues PD*2*NB dummy stores so the count
-//   holds from the first band) -> s_barrier -> filter + store NB rows -> s_barrier (the ring
-//   slots of band i's oldest rows may now be refilled).
-constexpr int RING_WGT = 192;
-
-template <int NB, int PD, int RLOG>
+// fetched from HBM once per strip (no halo re-reads by neighbouring bands) and, with a noise
+// prologue, noised once per strip -- which is what makes it the form for the fused
+// noise -> filter step (BASELINE config 2: random_noise + cv2.blur, lib/model/test.py:220-241):
+// the noise is VALU-bound, and the band-tiled form would recompute it for every halo row.
+//   chunk m (image bytes [1024 m, 1024 m + 1024)) lives in ring slot m mod NSLOT; image byte B
+//   sits at ring offset (B >> 10) mod NSLOT * 1024 + (B & 1023); a row is read with the tile
+//   form's lane layout (two 8-byte LDS reads per lane, each in one chunk).
+// Per band i (all counts wave-uniform, so one immediate vmcnt serves every wave):
+//   issue band i+PD's new chunks (exactly MAXC DMAs per wave; unused ones land in a dump slot)
+//   -> s_waitcnt vmcnt(PD*MAXC + PD*NB*SPR) retires band i's chunks (younger: PD bands of DMAs
+//   and PD bands of NB*SPR stores; the prologue issues PD*NB*SPR dummy stores so the count holds
+//   from the first band) -> s_barrier -> [noise prologue: the waves noise band i's new chunks in
+//   place in LDS, s_barrier] -> filter + store NB rows (u8, or the float32 blob) -> s_barrier.
+// Epilogue EPI_BLOB: blob = float32(float64(v) - PIXEL_MEANS[ch]) (lib/utils/blob.py:35-36,
+// numpy's float64 subtract then float32 store), written straight from the filter registers:
+// the blob of a filtered image without the u8 round trip through HBM.
+template <int NB, int PD, int NSLOT, int EPI>
 struct RingShape {
-  static constexpr int RING = 1 << RLOG;
-  static constexpr int NSLOT = RING >> 10;
+  static constexpr int RING = NSLOT * 1024;
   // chunks a band's new rows can touch (<= 3024-byte rows), split over 3 waves
   static constexpr int MAXC = ((NB * TILE_RBMAX + 1023) / 1024 + 1 + 2) / 3;
   static constexpr int MAXC0 = (((NB + 4) * TILE_RBMAX + 1023) / 1024 + 1 + 2) / 3;
-  static constexpr int VMCNT = PD * MAXC + PD * 2 * NB;
+  static constexpr int SPR = EPI == EPI_BLOB ? 6 : 2;  // stores per output row per lane
+  static constexpr int VMCNT = PD * MAXC + PD * NB * SPR;
   static_assert((NB * (PD + 1) + 4) * TILE_RBMAX + 2048 <= RING, "ring too small for NB / PD");
   static_assert(VMCNT <= 63, "vmcnt field is 6 bits");
 };
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt at their maxima); asm so no memory op moves
-  // across it
+  // s_waitcnt vmcnt(N) only; asm (with a memory clobber) so no memory op moves across it
   static_assert(N >= 0 && N <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int C, int OP, int NB, int PD, int RLOG, int LAUX, int SAUX>
-__global__ __launch_bounds__(RING_WGT) void stencil_u8_ring(const uint8_t* __restrict__ src,
-                                                           uint8_t* __restrict__ dst, int h, int rb,
-                                                           int nseg, int seg_len, int bands,
-                                                           int strips_per_img, int bands_per_strip) {
+template <int C, int OP, int NB, int PD, int NSLOT, int LAUX, int SAUX, int PRE, int EPI>
+__global__ __launch_bounds__(RING_WGT) void stencil_u8_ring(RingArgs a) {
   constexpr int K = Stencil<OP>::K;
   constexpr int R = K / 2;
-  using RS = RingShape<NB, PD, RLOG>;
+  using RS = RingShape<NB, PD, NSLOT, EPI>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[RS::RING + 1024];
   uint8_t* const ring = lds;
   uint8_t* const dump = lds + RS::RING;
 
+  const int h = a.h, rb = a.rb;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int strip = blockIdx.x;
-  const int img = strip / strips_per_img;
-  const int b0 = (strip % strips_per_img) * bands_per_strip;
-  const int nbands = min(b0 + bands_per_strip, bands) - b0;
+  const int img = strip / a.strips_per_img;
+  const int b0 = (strip % a.strips_per_img) * a.bands_per_strip;
+  const int nbands = min(b0 + a.bands_per_strip, a.bands) - b0;
   if (nbands <= 0) return;  // whole workgroup: no barrier is pending
   const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
-  const rsrc_t rs = make_rsrc(src + (size_t)img * img_bytes, img_bytes);
-  const rsrc_t rd = make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
+  const rsrc_t rs = make_rsrc(a.src + (size_t)img * img_bytes, img_bytes);
+  const rsrc_t rd = EPI == EPI_U8 ? make_rsrc(a.dst + (size_t)img * img_bytes, img_bytes)
+                                  : make_rsrc(a.blob + (size_t)img * img_bytes, 4u * img_bytes);
+  const uint64_t gimg = a.ids ? a.ids[img] : a.offset + (uint64_t)img;
 
-  // chunk bookkeeping (wave-uniform): band g of the strip needs image rows up to
-  // min(y0(g) + NB + R, h) resident; F = next chunk not yet fetched
+  auto slot_off = [](uint32_t m) -> uint32_t { return (m % (uint32_t)NSLOT) << 10; };
+  // band g of the strip needs image rows up to min(y0(g) + NB + R, h) resident
   auto chunk_end = [&](int g) -> uint32_t {
     const int yend = min((b0 + g) * NB + NB + R, h);
     return ((uint32_t)yend * (uint32_t)rb + 1023u) >> 10;
   };
-  uint32_t F = ((uint32_t)max(b0 * NB - R, 0) * (uint32_t)rb) >> 10;
+  const uint32_t first = ((uint32_t)max(b0 * NB - R, 0) * (uint32_t)rb) >> 10;
+  uint32_t F = first;
   auto issue = [&](uint32_t to, int maxc) {
     for (int i = 0; i < maxc; ++i) {
       const uint32_t m = F + (uint32_t)wave + 3u * (uint32_t)i;
       const bool valid = m < to;
-      uint8_t* d = valid ? ring + ((m & (RS::NSLOT - 1)) << 10) : dump;
+      uint8_t* d = valid ? ring + slot_off(m) : dump;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs, (__attribute__((address_space(3))) void*)d, 16,
           valid ? (m << 10) + 16u * (uint32_t)lane : OOB_OFF, 0, 0, LAUX);
@@ -460,25 +519,43 @@ __global__ __launch_bounds__(RING_WGT) void stencil_u8_ring(const uint8_t* __res
     F = max(F, to);
   };
 
-  // prologue: band 0's whole tile, then the new rows of bands 1..PD-1; PD*2*NB dummy stores
+  // prologue: band 0's whole tile, then the new rows of bands 1..PD-1; dummy stores
   issue(chunk_end(0), RS::MAXC0);
   for (int g = 1; g < PD; ++g) issue(g < nbands ? chunk_end(g) : F, RS::MAXC);
-  for (int i = 0; i < PD * NB; ++i) {
-    const v4u z = {0u, 0u, 0u, 0u};
-    __builtin_amdgcn_raw_buffer_store_b128(z, rd, OOB_OFF, 0, SAUX);
-    __builtin_amdgcn_raw_buffer_store_b64(v2u{0u, 0u}, rd, OOB_OFF, 0, SAUX);
-  }
+  // (distinct out-of-range offsets: identical stores to one address would be merged away, and
+  // the vmcnt arithmetic counts every one of them)
+  for (int i = 0; i < PD * NB * RS::SPR; ++i)
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, rd, OOB_OFF + 16u * (uint32_t)i,
+                                           0, SAUX);
 
-  const bool active = wave < nseg;
-  const StripeGeom g = stripe_geom(min(wave, nseg - 1), lane, rb, nseg, seg_len, 1);
+  const StripeGeom g = stripe_geom(min(wave, a.nseg - 1), lane, rb, a.nseg, a.seg_len, 1);
+  const bool active = wave < a.nseg;
   const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
   const StoreOffs so = store_offs(g);
-  constexpr uint32_t RMASK = (uint32_t)RS::RING - 1u;
+  // channel of chunk byte 0 (q may be -8 for the row's lead lane)
+  const int m0 = ((g.q % 3) + 3) % 3;
+  const double means[3] = {a.mean[0], a.mean[1], a.mean[2]};
 
   for (int i = 0; i < nbands; ++i) {
     issue(i + PD < nbands ? chunk_end(i + PD) : F, RS::MAXC);
     wait_vmcnt<RS::VMCNT>();
     asm volatile("s_barrier" ::: "memory");
+    if constexpr (PRE != PRE_NONE) {
+      // noise the chunks that became resident for this band, in place
+      const uint32_t lo = i == 0 ? first : max(first, chunk_end(i - 1));
+      const uint32_t hi = max(lo, chunk_end(i));
+      for (uint32_t m = lo + (uint32_t)wave; m < hi; m += 3u) {
+        const uint32_t e0 = (m << 10) + 16u * (uint32_t)lane;
+        if (e0 < img_bytes) {
+          v4u* p = reinterpret_cast<v4u*>(ring + slot_off(m) + 16u * (uint32_t)lane);
+          constexpr int KIND = PRE == PRE_GAUSSIAN ? IDN_NOISE_GAUSSIAN
+                               : PRE == PRE_SPECKLE ? IDN_NOISE_SPECKLE : IDN_NOISE_SAP;
+          *p = noise16_u8<KIND, true>(*p, e0 >> 4, gimg, a.key, 0.0, a.p1, a.t_flip, a.t_salt,
+                                      nullptr);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     const int y0 = (b0 + i) * NB;
     const int y1 = min(y0 + NB, h);
     const int nin = (y1 - y0) + 2 * R;
@@ -488,8 +565,9 @@ __global__ __launch_bounds__(RING_WGT) void stencil_u8_ring(const uint8_t* __res
     for (int r = 0; r < NB + 2 * R; ++r) {
       const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
       const uint32_t B = (uint32_t)y * (uint32_t)rb + ld_off;
-      const v2u lo = *reinterpret_cast<const v2u*>(&ring[B & RMASK]);
-      const v2u hi = *reinterpret_cast<const v2u*>(&ring[(B + 8u) & RMASK]);
+      const v2u lo = *reinterpret_cast<const v2u*>(&ring[slot_off(B >> 10) + (B & 1023u)]);
+      const uint32_t B8 = B + 8u;
+      const v2u hi = *reinterpret_cast<const v2u*>(&ring[slot_off(B8 >> 10) + (B8 & 1023u)]);
       raw[r] = v4u{lo.x, lo.y, hi.x, hi.y};
     }
     uint32_t Rg[K][8];
@@ -508,8 +586,12 @@ __global__ __launch_bounds__(RING_WGT) void stencil_u8_ring(const uint8_t* __res
       const int r = 2 * R + u;
       take_row(r);
       const int y = y0 + u;
-      ring_out_row<C, OP, (SAUX & 2)>(Rg, r % K, g, rd, so,
-                                      (active && y < y1) ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
+      const uint32_t row_off = (active && y < y1) ? (uint32_t)y * (uint32_t)rb : OOB_OFF;
+      if constexpr (EPI == EPI_BLOB) {
+        blob_store16(ring_row<C, OP>(Rg, r % K, g), means, rd, so, row_off, m0);
+      } else {
+        ring_out_row<C, OP, (SAUX & 2)>(Rg, r % K, g, rd, so, row_off);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
@@ -630,6 +712,31 @@ static int launch_f64(const double* src, double* dst, int n, int h, int w, int c
   return IDN_OK;
 }
 
+// ---- ring launch helpers -------------------------------------------------------------------------
+inline bool ring_ok(int c, int64_t rb, int64_t row_stride, int h, const void* src, const void* dst,
+                    int n, int K) {
+  return stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb && rb <= TILE_RBMAX &&
+         h > K && n <= 65535;
+}
+
+// strips per image: about wg_per_cu resident workgroups per CU over the batch, strips of at
+// least 4 bands
+template <int OP, int NB, int PD, int NSLOT, int LAUX, int SAUX, int PRE, int EPI>
+static void launch_ring(RingArgs a, int n, int h, int rb, int wg_per_cu, hipStream_t st) {
+  a.h = h;
+  a.rb = rb;
+  a.nseg = (rb + 1007) / 1008;
+  a.seg_len = ((rb + a.nseg - 1) / a.nseg + 7) / 8 * 8;
+  a.bands = (h + NB - 1) / NB;
+  const int64_t target = (int64_t)256 * wg_per_cu;
+  int spi = (int)std::max<int64_t>(1, (target + n - 1) / n);
+  spi = std::min(spi, std::max(1, a.bands / 4));
+  a.bands_per_strip = (a.bands + spi - 1) / spi;
+  a.strips_per_img = (a.bands + a.bands_per_strip - 1) / a.bands_per_strip;
+  hipLaunchKernelGGL((stencil_u8_ring<3, OP, NB, PD, NSLOT, LAUX, SAUX, PRE, EPI>),
+                     dim3((unsigned)(n * a.strips_per_img)), dim3(RING_WGT), 0, st, a);
+}
+
 // ---- host launchers --------------------------------------------------------------------------
 // Band heights measured best on MI355X (256 x 600 x 1000 x 3 batch, tools/sweep_stencil.py):
 // the tiled kernel with 6-row bands (10 / 8 input rows in LDS, 30 / 24 KB per workgroup, up to
@@ -641,57 +748,41 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
   constexpr int R = K / 2;
   const int64_t rb = (int64_t)w * c;
   const int tile_mode = env_int("IDN_STENCIL_TILE", 1);
-  const bool ntst = (env_int("IDN_STENCIL_NT", 0) & 2) != 0;  // nontemporal stores (tuning)
+  const int ntmode = env_int("IDN_STENCIL_NT", 0) & 3;  // cache-policy variants (tuning)
+  const bool ntst = (ntmode & 2) != 0;  // nontemporal stores
   const int map = env_int("IDN_STENCIL_MAP", 1) == 2 ? 2 : 1;
-  const int ring_cfg = env_int("IDN_STENCIL_RING", 1);
-  if (ring_cfg > 0 && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
-      rb <= TILE_RBMAX && h > 2 * R && n <= 65535) {
-    const int nseg = (int)((rb + 1007) / 1008);
-    const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
-    // strips per image: about two resident workgroups per CU over the batch
-    auto go = [&](auto nb_c, auto pd_c, auto rlog_c, auto laux_c, auto saux_c, int wg_per_cu) {
-      constexpr int NBV = decltype(nb_c)::value;
-      const int bands = (h + NBV - 1) / NBV;
-      const int64_t target = (int64_t)256 * wg_per_cu;
-      int spi = (int)std::max<int64_t>(1, (target + n - 1) / n);
-      spi = std::min(spi, std::max(1, bands / 4));  // strips of >= 4 bands
-      const int bps = (bands + spi - 1) / spi;
-      spi = (bands + bps - 1) / bps;
-      IDN_CHECK_ARG((int64_t)n * spi < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
-      hipLaunchKernelGGL((stencil_u8_ring<3, OP, NBV, decltype(pd_c)::value,
-                                          decltype(rlog_c)::value, decltype(laux_c)::value,
-                                          decltype(saux_c)::value>),
-                         dim3((unsigned)(n * spi)), dim3(RING_WGT), 0, st, src, dst, h, (int)rb,
-                         nseg, seg_len, bands, spi, bps);
-      return 0;
-    };
-    using I = std::integral_constant<int, 0>;
-    (void)sizeof(I);
-#define IC(v) std::integral_constant<int, v>()
+  const int ring_cfg = env_int("IDN_STENCIL_RING", 0);  // the band-tiled form is faster plain
+  if (ring_cfg > 0 && ring_ok(c, rb, row_stride, h, src, dst, n, K)) {
+    RingArgs a{};
+    a.src = src;
+    a.dst = dst;
     switch (ring_cfg) {
-      case 2: go(IC(4), IC(2), IC(16), IC(2), IC(2), 2); break;
-      case 3: go(IC(8), IC(1), IC(16), IC(2), IC(2), 2); break;
-      case 4: go(IC(6), IC(3), IC(17), IC(2), IC(2), 1); break;
-      case 5: go(IC(8), IC(2), IC(17), IC(2), IC(2), 1); break;
-      case 6: go(IC(6), IC(1), IC(16), IC(0), IC(0), 2); break;
-      case 7: go(IC(6), IC(1), IC(16), IC(2), IC(0), 2); break;
-      case 8: go(IC(6), IC(1), IC(16), IC(0), IC(2), 2); break;
-      case 9: go(IC(4), IC(4), IC(17), IC(2), IC(2), 1); break;
-      default: go(IC(6), IC(1), IC(16), IC(2), IC(2), 2); break;
+      case 2: launch_ring<OP, 4, 1, 38, 0, 0, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 4, st); break;
+      case 3: launch_ring<OP, 4, 1, 38, 2, 2, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 4, st); break;
+      case 4: launch_ring<OP, 6, 1, 50, 0, 0, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 3, st); break;
+      case 5: launch_ring<OP, 2, 3, 38, 0, 0, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 4, st); break;
+      default: launch_ring<OP, 6, 1, 64, 0, 0, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 2, st); break;
     }
-#undef IC
   } else if (tile_mode && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
       rb <= TILE_RBMAX && h > 2 * R) {
     const int nseg = (int)((rb + 1007) / 1008);
     const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
     constexpr int NB1 = 6, NB2 = K == 5 ? 11 : 10, NB3 = K == 5 ? 8 : 4;
-    const int nb = tile_mode == 2 ? NB2 : tile_mode == 3 ? NB3 : NB1;
+    const int nb = tile_mode == 2 ? NB2 : tile_mode == 3 ? NB3 : tile_mode == 4 ? 5
+                 : tile_mode == 5 ? 4 : tile_mode == 6 ? 7 : NB1;
     const int bands = (h + nb - 1) / nb;
     const int64_t total = (int64_t)n * bands * nseg;
     IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
     const dim3 grid((unsigned)((int64_t)n * bands)), block(TILE_WGT);
+#define IDN_LAUNCH_TILE_NT(NBX, NTV)                                                              \
+  hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, NTV>), grid, block, 0, st, src, dst, h, (int)rb,   \
+                     nseg, seg_len, bands, (int)total, map)
 #define IDN_LAUNCH_TILE(NBX)                                                                      \
-  if (ntst)                                                                                       \
+  if (ntmode == 1)                                                                                \
+    IDN_LAUNCH_TILE_NT(NBX, 1);                                                                   \
+  else if (ntmode == 3)                                                                           \
+    IDN_LAUNCH_TILE_NT(NBX, 3);                                                                   \
+  else if (ntst)                                                                                  \
     hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, 2>), grid, block, 0, st, src, dst, h, (int)rb, \
                        nseg, seg_len, bands, (int)total, map);                                    \
   else                                                                                            \
@@ -701,10 +792,17 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
       IDN_LAUNCH_TILE(NB2);
     } else if (tile_mode == 3) {
       IDN_LAUNCH_TILE(NB3);
+    } else if (tile_mode == 4) {
+      IDN_LAUNCH_TILE(5);
+    } else if (tile_mode == 5) {
+      IDN_LAUNCH_TILE(4);
+    } else if (tile_mode == 6) {
+      IDN_LAUNCH_TILE(7);
     } else {
       IDN_LAUNCH_TILE(NB1);
     }
 #undef IDN_LAUNCH_TILE
+#undef IDN_LAUNCH_TILE_NT
   } else if (stripe_ok(c, rb, row_stride, h, src, dst)) {
     // strided or wide rows: stripe form.  Rows of <= 4 segments: short bands, one workgroup per
     // band, all band rows loaded up front; wider rows: long bands of independent waves.
@@ -799,4 +897,101 @@ extern "C" int idn_box_blur_f64(const double* src, double* dst, int n, int h, in
   if (n == 0) return IDN_OK;
   if (ksize == 3) return launch_f64<OP_BOX3>(src, dst, n, h, w, c, as_stream(stream), "idn_box_blur_f64");
   return set_error(IDN_EUNSUPPORTED, "idn_box_blur_f64: ksize %d not supported", ksize);
+}
+
+// ---- fused entry points -----------------------------------------------------------------------
+// noise -> filter in one pass (BASELINE config 2: random_noise(img, 'gaussian', var) + U8 +
+// cv2.blur / cv2.GaussianBlur, lib/model/test.py:220-241, minibatch.py:115-146): the same
+// Philox stream and float64 apply as idn_noise_u8 (flat form), so the result equals
+// idn_noise_u8 followed by the filter bit for bit.  Supported: compact 3-channel rows of
+// <= 3024 bytes, kind gaussian / speckle with mean 0, or s&p; otherwise IDN_EUNSUPPORTED and the
+// caller runs the two steps.
+extern "C" int idn_noise_filter_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                                   int64_t row_stride, int kind, double p0, double p1,
+                                   uint64_t seed, uint64_t offset, const uint64_t* image_ids,
+                                   int filter, int ksize, void* stream) {
+  using namespace idn;
+  if (int e = check_filter_args(src, dst, n, h, w, c, row_stride, "idn_noise_filter_u8")) return e;
+  IDN_CHECK_ARG(n <= 65535, "idn_noise_filter_u8: at most 65535 images per call");
+  if (n == 0) return IDN_OK;
+  const int64_t rb = (int64_t)w * c;
+  const int op = filter == 0 ? (ksize == 5 ? OP_GAUSS5 : ksize == 3 ? OP_GAUSS3 : -1)
+                             : (filter == 1 && ksize == 3 ? OP_BOX3 : -1);
+  const int K = ksize;
+  // the flat noise stream (noise16_u8) is what idn_noise_u8 draws only for 16-element images
+  // on 16-byte aligned buffers; other layouts use its element stream, so they are not fused
+  const bool flat = ((int64_t)h * rb) % 16 == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+  if (op < 0 || !flat || !ring_ok(c, rb, row_stride, h, src, dst, n, K) ||
+      (kind != IDN_NOISE_SAP && p0 != 0.0) || kind < 0 || kind > IDN_NOISE_SAP)
+    return set_error(IDN_EUNSUPPORTED, "idn_noise_filter_u8: combination not fused");
+  RingArgs a{};
+  a.src = src;
+  a.dst = dst;
+  a.key = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(kind + 1));  // noise.hip KIND_TAG
+  a.offset = offset;
+  a.ids = image_ids;
+  if (kind == IDN_NOISE_SAP) {
+    IDN_CHECK_ARG(p0 >= 0.0 && p0 <= 1.0 && p1 >= 0.0 && p1 <= 1.0,
+                  "idn_noise_filter_u8: amount / salt_vs_pepper must be in [0, 1]");
+    a.t_flip = sap_threshold(p0 / (p0 + (1.0 - p0)));
+    a.t_salt = sap_threshold(p1 / (p1 + (1.0 - p1)));
+  } else {
+    IDN_CHECK_ARG(p1 >= 0.0, "idn_noise_filter_u8: var must be >= 0");
+    a.p1 = pow(p1, 0.5);
+  }
+  hipStream_t st = as_stream(stream);
+#define IDN_NF(OPV, PREV) launch_ring<OPV, 4, 1, 38, 0, 0, PREV, EPI_U8>(a, n, h, (int)rb, 4, st)
+#define IDN_NF_OP(PREV)                     \
+  if (op == OP_GAUSS5) IDN_NF(OP_GAUSS5, PREV); \
+  else if (op == OP_GAUSS3) IDN_NF(OP_GAUSS3, PREV); \
+  else IDN_NF(OP_BOX3, PREV)
+  if (kind == IDN_NOISE_GAUSSIAN) {
+    IDN_NF_OP(PRE_GAUSSIAN);
+  } else if (kind == IDN_NOISE_SPECKLE) {
+    IDN_NF_OP(PRE_SPECKLE);
+  } else if (kind == IDN_NOISE_SAP) {
+    IDN_NF_OP(PRE_SAP);
+  } else {
+    return set_error(IDN_EUNSUPPORTED, "idn_noise_filter_u8: poisson is not fused");
+  }
+#undef IDN_NF_OP
+#undef IDN_NF
+  IDN_CHECK_LAUNCH("idn_noise_filter_u8");
+  return IDN_OK;
+}
+
+// cv2.GaussianBlur(u8, (k, k), 0) -> prep_im_for_blob at scale 1.0 (lib/utils/blob.py:33-47,
+// lib/model/test.py:49-83): blob = float32(float64(filtered) - mean[ch]), dense (n, h, w, 3)
+// float32, written by the filter kernel itself (the u8 filtered image never reaches HBM).
+extern "C" int idn_gaussian_blob_f32(const uint8_t* src, float* blob, int n, int h, int w, int c,
+                                     int64_t row_stride, int ksize, const double* mean,
+                                     void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(blob && mean, "idn_gaussian_blob_f32: null pointer");
+  if (int e = check_filter_args(src, (uint8_t*)blob, n, h, w, c, row_stride,
+                                "idn_gaussian_blob_f32")) return e;
+  if (n == 0) return IDN_OK;
+  const int64_t rb = (int64_t)w * c;
+  IDN_CHECK_ARG(ksize == 3 || ksize == 5, "idn_gaussian_blob_f32: ksize must be 3 or 5");
+  if (!(stripe_ok(c, rb, row_stride, h, src, blob) && row_stride == rb && rb <= TILE_RBMAX &&
+        h > ksize && ((uintptr_t)blob & 15) == 0))
+    return set_error(IDN_EUNSUPPORTED, "idn_gaussian_blob_f32: layout not fused");
+  const int nseg = (int)((rb + 1007) / 1008);
+  const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
+  constexpr int NB = 6;
+  const int bands = (h + NB - 1) / NB;
+  const int64_t total = (int64_t)n * bands * nseg;
+  IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "idn_gaussian_blob_f32: batch too large");
+  const dim3 grid((unsigned)((int64_t)n * bands)), block(TILE_WGT);
+  hipStream_t st = as_stream(stream);
+  if (ksize == 5)
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP_GAUSS5, NB, 0, EPI_BLOB>), grid, block, 0, st, src,
+                       nullptr, h, (int)rb, nseg, seg_len, bands, (int)total, 1, blob, mean[0],
+                       mean[1], mean[2]);
+  else
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP_GAUSS3, NB, 0, EPI_BLOB>), grid, block, 0, st, src,
+                       nullptr, h, (int)rb, nseg, seg_len, bands, (int)total, 1, blob, mean[0],
+                       mean[1], mean[2]);
+  IDN_CHECK_LAUNCH("idn_gaussian_blob_f32");
+  return IDN_OK;
 }

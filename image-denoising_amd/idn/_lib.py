@@ -52,6 +52,10 @@ SIGNATURES = {
     "idn_quant_workspace_size": (_c_size, [_c_int, _c_int]),
     "idn_bgr2lab_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
     "idn_lab2bgr_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
+    "idn_noise_filter_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
+                                     _c_dbl, _c_dbl, _c_u64, _c_u64, _c_vp, _c_int, _c_int, _c_vp]),
+    "idn_gaussian_blob_f32": (_c_int, [_c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
+                                       ctypes.POINTER(ctypes.c_double), _c_vp]),
     "idn_copy_u8": (_c_int, [_c_u8p, _c_u8p, _c_i64, _c_int, _c_vp]),
     "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_i64,
                                         _c_int, _c_int, _c_vp, _c_size, _c_vp]),

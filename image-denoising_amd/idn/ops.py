@@ -359,6 +359,111 @@ def copy_slots(x: torch.Tensor, out: torch.Tensor, slots) -> torch.Tensor:
     return out
 
 
+# ---- fused steps -------------------------------------------------------------------------------
+
+FILTERS = {"gaus_blur": 0, "mean": 1}
+
+
+def noise_filter(x: torch.Tensor, mode: str, filter: str, ksize: int, *, var: float = 0.01,
+                 amount: float = 0.05, salt_vs_pepper: float = 0.5, seed: int = 0,
+                 offset: int = 0, image_ids=None, out: Optional[torch.Tensor] = None,
+                 form: str = "serial"):
+    """random_noise(x, mode, ...) -> U8 -> cv2.GaussianBlur (filter 'gaus_blur') or cv2.blur
+    ('mean'); the result is identical in every form (Philox stream keyed by (seed, image id)).
+      form 'serial'    the noise launch, then the filter launch (the default: fastest measured,
+                       profiles/r02/README.md -- the noise is VALU-bound and neither fused form
+                       overlaps it with the filter's memory traffic well enough to win)
+      form 'fused'     one pass (idn_noise_filter_u8: LDS ring, every byte fetched and noised
+                       once) when the layout allows, else 'serial'
+      form 'pipelined' the batch in chunks: the noise of chunk k+1 (VALU-bound) runs on a side
+                       stream beside the filter of chunk k (HBM-bound), whose input is still in
+                       the 256 MB Infinity Cache"""
+    if form == "pipelined":
+        return _noise_filter_pipelined(x, mode, filter, ksize, var=var, amount=amount,
+                                       salt_vs_pepper=salt_vs_pepper, seed=seed, offset=offset,
+                                       image_ids=image_ids, out=out)
+    if form not in ("fused", "serial"):
+        raise ValueError("noise_filter: form must be 'fused', 'serial' or 'pipelined'")
+    kind = NOISE_KINDS.get(mode.lower())
+    if kind is None or kind == 3:
+        raise ValueError(f"noise_filter: mode {mode!r} not supported (gaussian, speckle, s&p)")
+    if filter not in FILTERS:
+        raise ValueError(f"noise_filter: filter must be one of {sorted(FILTERS)}")
+    xb, sq = _u8_batch(x, "noise_filter")
+    n, h, w, c = xb.shape
+    y = torch.empty_like(xb) if out is None else out.view(n, h, w, c)
+    p0, p1 = (float(amount), float(salt_vs_pepper)) if kind == 2 else (0.0, float(var))
+    ids = _ids_tensor(image_ids, n, xb.device) if image_ids is not None else None
+    lib = _lib.load()
+    rc = -2 if form == "serial" else lib.idn_noise_filter_u8(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c, kind, p0, p1,
+                                 int(seed) & (2 ** 64 - 1), int(offset),
+                                 ids.data_ptr() if ids is not None else None, FILTERS[filter],
+                                 int(ksize), _stream())
+    if rc == -2:  # IDN_EUNSUPPORTED: not fusable for this layout -- run the two steps
+        kw = dict(amount=amount, salt_vs_pepper=salt_vs_pepper) if kind == 2 else dict(var=var)
+        t = random_noise(xb, mode, seed=seed, offset=offset, image_ids=image_ids, out="u8", **kw)
+        return _finish((gaussian_blur if filter == "gaus_blur" else blur)(t, ksize, out=y), sq)
+    _lib.check(rc, "idn_noise_filter_u8")
+    return _finish(y, sq)
+
+
+_PIPE_STREAMS: dict = {}
+
+
+def _noise_filter_pipelined(x, mode, filter, ksize, *, var, amount, salt_vs_pepper, seed, offset,
+                            image_ids, out, chunk: int = 32):
+    xb, sq = _u8_batch(x, "noise_filter")
+    n = xb.shape[0]
+    y = torch.empty_like(xb) if out is None else out.view(xb.shape)
+    main = torch.cuda.current_stream(xb.device)
+    side = _PIPE_STREAMS.get(xb.device)
+    if side is None:
+        side = _PIPE_STREAMS[xb.device] = torch.cuda.Stream(device=xb.device)
+    tmp = _workspace(xb.numel(), xb.device)[: xb.numel()].view(xb.shape)
+    kw = dict(amount=amount, salt_vs_pepper=salt_vs_pepper) if mode in ("s&p", "sap") else \
+        dict(var=var)
+    flt = gaussian_blur if filter == "gaus_blur" else blur
+    side.wait_stream(main)  # inputs / outputs are ready on the caller's stream
+    ids_all = _ids_tensor(image_ids, n, xb.device) if image_ids is not None else None
+    prev = None
+    for lo in range(0, n, chunk):
+        hi = min(lo + chunk, n)
+        with torch.cuda.stream(side):
+            if ids_all is None:
+                random_noise(xb[lo:hi], mode, seed=seed, offset=offset + lo, out="u8",
+                             out_u8=tmp[lo:hi], **kw)
+            else:
+                random_noise(xb[lo:hi], mode, seed=seed, image_ids=ids_all[lo:hi], out="u8",
+                             out_u8=tmp[lo:hi], **kw)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        if prev is not None:
+            main.wait_event(prev[2])
+            flt(tmp[prev[0]:prev[1]], ksize, out=y[prev[0]:prev[1]])
+        prev = (lo, hi, ev)
+    if prev is not None:
+        main.wait_event(prev[2])
+        flt(tmp[prev[0]:prev[1]], ksize, out=y[prev[0]:prev[1]])
+    side.wait_stream(main)  # tmp (shared scratch) is not reused by the side stream early
+    return _finish(y, sq)
+
+
+def gaussian_blob(x: torch.Tensor, ksize: int = 5, pixel_means=PIXEL_MEANS,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """blob(gaussian_blur(x, ksize)) at scale 1.0 in one pass: float32 (N, H, W, 3)
+    float32(float64(v) - mean[ch]) written by the filter (idn_gaussian_blob_f32)."""
+    xb, _ = _u8_batch(x, "gaussian_blob")
+    n, h, w, c = xb.shape
+    y = torch.empty((n, h, w, c), dtype=torch.float32, device=xb.device) if out is None else out
+    m = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(pixel_means, np.float64).reshape(-1)])
+    rc = _lib.load().idn_gaussian_blob_f32(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c,
+                                           int(ksize), m, _stream())
+    if rc == -2:
+        return blob(gaussian_blur(xb, ksize), pixel_means, out=y)
+    _lib.check(rc, "idn_gaussian_blob_f32")
+    return y
+
+
 # ---- quant: colour quantisation by k-means in 8-bit Lab ----------------------------------------
 
 def quantize(x: torch.Tensor, k: int, *, seed: int = 0, offset: int = 0, image_ids=None,

@@ -190,6 +190,25 @@ int idn_bgr2lab_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_
 int idn_lab2bgr_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t row_stride,
                    void* stream);
 
+/* ---- fused steps (one pass over HBM instead of two) ------------------------------------------ */
+
+/* idn_noise_u8(kind, p0, p1, seed, offset | image_ids, U8 out) followed by
+ * cv2.GaussianBlur(ksize) (filter 0) or cv2.blur(3) (filter 1), bit-exact with running the two
+ * steps: the noise -> denoise branches of lib/model/test.py:220-241 / minibatch.py:115-146
+ * (BASELINE config 2).  Each input byte is fetched and noised once.  Returns IDN_EUNSUPPORTED
+ * (nothing launched) unless: C = 3, compact rows of 8k <= 3024 bytes, kind gaussian / speckle
+ * with p0 (mean) == 0 or s&p.  image_ids (nullable) as for idn_noise_ids_u8. */
+int idn_noise_filter_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
+                        int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
+                        uint64_t offset, const uint64_t* image_ids, int filter, int ksize,
+                        void* stream);
+/* cv2.GaussianBlur(img, (ksize, ksize), 0) then prep_im_for_blob at scale 1.0
+ * (lib/utils/blob.py:33-47): blob = float32(float64(v) - mean[ch]), dense (n, h, w, c) float32
+ * written by the filter kernel (the filtered u8 image never reaches HBM).  mean: host double[3].
+ * IDN_EUNSUPPORTED unless C = 3 and compact rows of 8k <= 3024 bytes. */
+int idn_gaussian_blob_f32(const uint8_t* src, float* blob, int n, int h, int w, int c,
+                          int64_t row_stride, int ksize, const double* mean, void* stream);
+
 /* Flat copy of nbytes (multiple of 16, 16-byte aligned pointers).  policy 0 = default cache
  * policy, 1 = nontemporal loads and stores.  Not a reference interface: the bench's same-run
  * copy ceiling (SURVEY §8d "also report a measured copy-kernel peak"). */
