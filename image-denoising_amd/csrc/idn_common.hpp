@@ -52,6 +52,21 @@ inline int env_int(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
+// compute units of the current device (host; cached per device)
+inline int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
 // ---- small integer helpers ------------------------------------------------------------------
 // OpenCV BORDER_REFLECT_101 index (cv::borderInterpolate; repeats for overshoot >= len)
 __host__ __device__ __forceinline__ int reflect101(int i, int len) {

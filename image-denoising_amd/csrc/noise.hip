@@ -20,6 +20,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <mutex>
 
 namespace idn {
 
@@ -175,37 +176,53 @@ __global__ void vals_from_mask_kernel(uint32_t* mask, int n) {
 }
 
 // Philox-stream Poisson by inversion of the exact CDF.  lambda = img_as_float(v) * vals takes one
-// of 256 values per power-of-two vals (vals <= 256), so the CDF of every
-// (vals, v) pair is tabulated once per call (POIS_KMAX entries; P(X >= 512) < 1e-25 at
-// lambda = 256) with a 1024-entry guide table.  A draw is one 53-bit uniform; the guide entries
-// of its quantile interval bracket the answer (usually to one or two candidates) and a bisection
-// of the bracket finishes it.  The same law as numpy's multiplication / PTRS samplers (the replay
-// mode takes numpy's own draws), without their rejection loops.
+// of 256 values per power-of-two vals (vals <= 256), so the CDF row of every
+// (vals, v) is tabulated per call (POIS_KMAX entries; P(X >= 512) < 1e-25 at lambda = 256, the
+// largest).  A draw's 32-bit Philox word w gives u = (w + 1/2) / 2^32 and the count
+//   k = min { k : cdf[k] > u }  =  min { k : w < t_k },   t_k = ceil(cdf[k] * 2^32 - 1/2)
+// (the integer thresholds t_k are exact restatements of the double compares).  The law is
+// numpy's (Knuth / PTRS sample the same Poisson(lambda)); the replay mode takes numpy's own draws
+// bit-exactly.
+//
+// The tables depend on nothing but vals, so they are built once per device (pois_tables_for)
+// and kept.  Flat kernel (round 2): per vals level a 154 KB block staged in LDS, per v
+//   * the thresholds t_k over the window [lo_v, hi_v + 2], hi_v - lo_v = the counts of u in
+//     [2^-16, 1 - 2^-16]  (+-4.2 sd; 23.4 K u32 over the 256 v at vals = 256)
+//   * a guide over the bins of w, geometric towards both ends: per side, the octaves
+//     [2^p, 2^(p+1)) of the distance x from the nearer end for p = 16 .. 30, each split in
+//     POIS_S, and one deep bin (x < 2^16); it holds each bin's first count.  Every bin spans
+//     <= 3 counts, so k = first + [w >= t_first] + [w >= t_first+1] + [w >= t_first+2]:
+//     thresholds past the bin's last count exceed every w of the bin, so the sum needs no span.
+//   * a header: the LDS dword index of t_0 for v (window start - lo_v, biased by the T offset).
+// A draw is a header, a guide and 3 threshold reads -- branch-free.
+// The deep bins (u < 2^-16 or u > 1 - 2^-16, 1 draw in 32 K) bisect the global CDF row.
+// Round 1 bisected the global rows for every draw (1 guide + 1-3 CDF probes in L2, 64-byte
+// transactions for 4-8 useful bytes): L2-bound at 1.96 ms per 256 images.
 constexpr int POIS_NV = 9;       // vals = 1, 2, 4, ..., 256
 constexpr int POIS_KMAX = 512;   // CDF entries per lambda
-constexpr int POIS_G = 1024;     // guide entries per lambda
+constexpr int POIS_PMIN = 16;    // smallest octave exponent of a guided bin (x >= 2^16)
+constexpr int POIS_LS = 2;       // log2 of the bins per octave
+constexpr int POIS_S = 1 << POIS_LS;
+constexpr int POIS_NBH = 1 + (31 - POIS_PMIN) * POIS_S;  // bins per side, deep bin 0 (61)
+constexpr int POIS_NG = 2 * POIS_NBH;                    // guide entries per v (122)
+constexpr int POIS_SPAN = 3;                             // max counts per bin
+constexpr int POIS_TCAP = 23552;                         // window thresholds per level
+// level block: HDR[256] u32 (T_BASE + window start - lo_v), GUIDE[256][POIS_NG] u16 (first
+// count; side-major: [side][j]), T[POIS_TCAP] u32
+constexpr size_t POIS_LVL_G = 256 * sizeof(uint32_t);
+constexpr size_t POIS_LVL_T = (POIS_LVL_G + 256 * POIS_NG * sizeof(uint16_t) + 15) & ~(size_t)15;
+constexpr size_t POIS_LVL_BYTES = POIS_LVL_T + POIS_TCAP * sizeof(uint32_t);  // 157696
+constexpr uint32_t POIS_T_BASE = POIS_LVL_T / 4;
 struct PoisTables {
-  double* cdf;      // [POIS_NV][256][POIS_KMAX]
-  uint32_t* guide;  // [POIS_NV][256][POIS_G]: g(j) | g(j + 1) << 16, g(j) = smallest k with
-                    // cdf[k] > j / POIS_G (g(POIS_G) = POIS_KMAX - 1): one load per bracket
+  double* cdf;       // [POIS_NV][256][POIS_KMAX]
+  uint8_t* levels;   // [POIS_NV] blocks of POIS_LVL_BYTES
+  uint32_t* ntab;    // [POIS_NV] thresholds used per level (> POIS_TCAP: level not staged)
 };
-// one thread per (vals, v): the CDF by the recurrence p(k+1) = p(k) * lambda / (k+1)
-__global__ __launch_bounds__(64) void pois_cdf_kernel(PoisTables t) {
-  const int id = blockIdx.x * 64 + threadIdx.x;  // vi * 256 + v
-  if (id >= POIS_NV * 256) return;
-  const int vi = id >> 8, v = id & 255;
-  const double lam = __dmul_rn(img_as_float((uint32_t)v), (double)(1u << vi));
-  double* cdf = t.cdf + (size_t)id * POIS_KMAX;
-  double p = exp(-lam), acc = 0.0;
-  for (int k = 0; k < POIS_KMAX; ++k) {
-    acc += p;
-    cdf[k] = k == POIS_KMAX - 1 ? 1.0 : fmin(acc, 1.0);
-    p = p * lam / (double)(k + 1);
-  }
+__device__ __forceinline__ double pois_u(uint32_t w) {
+  return fma((double)w, 0x1p-32, 0x1p-33);  // exact: 33 significant bits
 }
-// one thread per guide entry: g(j) and g(j + 1) by bisection of the CDF row
 __device__ __forceinline__ int pois_first_above(const double* cdf, double q) {
-  int lo = 0, hi = POIS_KMAX - 1;
+  int lo = 0, hi = POIS_KMAX - 1;  // cdf[KMAX-1] = 1 > q
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (cdf[mid] > q) hi = mid;
@@ -213,66 +230,107 @@ __device__ __forceinline__ int pois_first_above(const double* cdf, double q) {
   }
   return lo;
 }
-__global__ __launch_bounds__(256) void pois_guide_kernel(PoisTables t) {
-  const int id = blockIdx.x * 256 + threadIdx.x;  // (vi * 256 + v) * POIS_G + j
-  if (id >= POIS_NV * 256 * POIS_G) return;
-  const int row = id / POIS_G, j = id % POIS_G;
-  const double* cdf = t.cdf + (size_t)row * POIS_KMAX;
-  const uint32_t g0 = (uint32_t)pois_first_above(cdf, (double)j / POIS_G);
-  const uint32_t g1 =
-      j + 1 < POIS_G ? (uint32_t)pois_first_above(cdf, (double)(j + 1) / POIS_G) : POIS_KMAX - 1;
-  t.guide[id] = g0 | (g1 << 16);
+// guide position of a word: side * POIS_NBH + j, j = 0 the deep bin.  x >> 7 < 2^24 converts to
+// float exactly; its exponent and top POIS_LS mantissa bits are the octave and the split.
+__device__ __forceinline__ uint32_t pois_side(uint32_t w) { return w >> 31; }
+__device__ __forceinline__ int pois_bin(uint32_t w) {
+  const uint32_t x = w ^ (uint32_t)((int32_t)w >> 31);  // distance from the nearer end, < 2^31
+  const int eb = (int)(__float_as_uint((float)(x >> 7)) >> (23 - POIS_LS));
+  return max(eb - (((127 - 7 + POIS_PMIN) << POIS_LS) - 1), 0);
+}
+// first distance x of bin j >= 1 (the octave 2^p, p = POIS_PMIN + (j-1) / S, split (j-1) % S)
+__device__ __forceinline__ uint32_t pois_x_start(int j) {
+  const int p = POIS_PMIN + (j - 1) / POIS_S, m = (j - 1) % POIS_S;
+  return (1u << p) + ((uint32_t)m << (p - POIS_LS));
+}
+__device__ __forceinline__ uint32_t pois_x_end(int j) {
+  return j == POIS_NBH - 1 ? 0x7FFFFFFFu : pois_x_start(j + 1) - 1u;
+}
+// the i-th bin endpoint in increasing w: side 0 bins j = 1 .. NBH-1 (start, end), then side 1
+// bins j = NBH-1 .. 1 (start, end) where side 1's w = ~x
+constexpr int POIS_NEP = 4 * (POIS_NBH - 1);
+__device__ __forceinline__ uint32_t pois_endpoint(int i) {
+  const int bin = i >> 1;
+  if (bin < POIS_NBH - 1) {
+    const int j = bin + 1;
+    return (i & 1) ? pois_x_end(j) : pois_x_start(j);
+  }
+  const int j = POIS_NBH - 1 - (bin - (POIS_NBH - 1));
+  return (i & 1) ? ~pois_x_start(j) : ~pois_x_end(j);
+}
+__device__ __forceinline__ uint32_t pois_threshold(double c) {
+  const double t = ceil(fma(c, 0x1p32, -0.5));  // exact: c * 2^32 <= 2^32 has ulp <= 2^-20
+  return t <= 0.0 ? 0u : t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+// one workgroup per vals level, thread = v: the CDF row by the recurrence
+// p(k+1) = p(k) * lambda / (k+1) (written to global for the element kernel and the deep bins),
+// with a two-pointer pass over the bin endpoints in the same loop; then the guide, the window
+// starts (prefix sum over v) and the thresholds
+__global__ __launch_bounds__(256) void pois_level_kernel(PoisTables t) {
+  __shared__ uint32_t scan[256];
+  __shared__ int bad;
+  const int vi = blockIdx.x, v = threadIdx.x;
+  double* cdf = t.cdf + ((size_t)vi * 256 + v) * POIS_KMAX;
+  uint8_t* lvl = t.levels + (size_t)vi * POIS_LVL_BYTES;
+  uint16_t* guide = reinterpret_cast<uint16_t*>(lvl + POIS_LVL_G) + (size_t)v * POIS_NG;
+  if (v == 0) bad = 0;
+  const double lam = __dmul_rn(img_as_float((uint32_t)v), (double)(1u << vi));
+  double p = exp(-lam), acc = 0.0;
+  int ep = 0, lo = 0, first = 0, hi = 0;
+  bool fits = true;
+  double ue = pois_u(pois_endpoint(0));
+  for (int k = 0; k < POIS_KMAX; ++k) {
+    acc += p;
+    const double c = k == POIS_KMAX - 1 ? 1.0 : fmin(acc, 1.0);
+    cdf[k] = c;
+    p = p * lam / (double)(k + 1);
+    while (ep < POIS_NEP && c > ue) {  // endpoint ep's count is k
+      if (ep == 0) lo = k;
+      if (!(ep & 1)) {
+        first = k;
+      } else {  // bin ep/2 spans counts [first, k]
+        const int bin = ep >> 1;
+        const int pos = bin < POIS_NBH - 1 ? bin + 1 : POIS_NG - 1 - (bin - (POIS_NBH - 1));
+        fits &= k - first <= POIS_SPAN;
+        guide[pos] = (uint16_t)first;
+        hi = k;
+      }
+      if (++ep < POIS_NEP) ue = pois_u(pois_endpoint(ep));
+    }
+  }
+  guide[0] = (uint16_t)lo;
+  guide[POIS_NBH] = (uint16_t)lo;  // deep bins: any in-window read, the result is replaced
+  __syncthreads();
+  if (!fits) bad = 1;
+  const uint32_t width = (uint32_t)(hi - lo + 3);  // thresholds lo .. hi + 2
+  scan[v] = width;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive scan
+    const uint32_t add = v >= d ? scan[v - d] : 0u;
+    __syncthreads();
+    scan[v] += add;
+    __syncthreads();
+  }
+  const uint32_t start = scan[v] - width, total = scan[255];
+  reinterpret_cast<uint32_t*>(lvl)[v] = POIS_T_BASE + start - (uint32_t)lo;
+  if (total > POIS_TCAP || bad || hi + 2 >= POIS_KMAX) {
+    if (v == 0) t.ntab[vi] = POIS_TCAP + 1;  // not staged: the flat kernel bisects the rows
+    return;
+  }
+  if (v == 0) t.ntab[vi] = total;
+  uint32_t* T = reinterpret_cast<uint32_t*>(lvl + POIS_LVL_T);
+  for (uint32_t i = 0; i < width; ++i) T[start + i] = pois_threshold(cdf[lo + i]);
 }
 
 // element e's uniform: 4 consecutive elements share one Philox block (counter (e/4, tag, image
-// id)), element e takes word e % 4 as u = (word + 1/2) / 2^32 in (0, 1).  The 2^-32 grid changes
-// the law only on events of probability below 2^-32 (as the float Box-Muller of the Gaussian
-// kind does), and the top 10 bits of the word are the guide index directly.
-__device__ __forceinline__ double pois_u(uint32_t w) {
-  return fma((double)w, 0x1p-32, 0x1p-33);  // exact: 33 significant bits
-}
+// id)), element e takes word e % 4
 __device__ __forceinline__ u32x4 pois_block(uint64_t key, uint64_t q, uint64_t gimg) {
-  return philox4x32(u32x4{(uint32_t)q, (uint32_t)(q >> 32) ^ 0x80000000u, (uint32_t)gimg,
-                          (uint32_t)(gimg >> 32)}, key);
+  return philox4x32<7>(u32x4{(uint32_t)q, (uint32_t)(q >> 32) ^ 0x80000000u, (uint32_t)gimg,
+                             (uint32_t)(gimg >> 32)}, key);
 }
 __device__ __forceinline__ int vals_index(uint32_t vals) { return __ffs((int)vals) - 1; }
 
-// NE elements of one thread (row = vals index * 256 + u8 value, 32-bit offsets off the uniform
-// table bases): bracket from the guide (all reads issued together), then bisection rounds in
-// lockstep, each round issuing the probes of every unfinished element at once
-template <int NE>
-__device__ __forceinline__ void pois_invert_n(const PoisTables& pt, const uint32_t (&row)[NE],
-                                              const uint32_t (&w)[NE], int (&lo)[NE]) {
-  static_assert(POIS_G == 1024, "guide index = top 10 bits of the uniform word");
-  int hi[NE];
-  double u[NE];
-#pragma unroll
-  for (int jj = 0; jj < NE; ++jj) {
-    u[jj] = pois_u(w[jj]);
-    const uint32_t g = pt.guide[row[jj] * POIS_G + (w[jj] >> 22)];
-    lo[jj] = (int)(g & 0xFFFFu);
-    hi[jj] = (int)(g >> 16);
-  }
-  for (int round = 0; round < 10; ++round) {  // brackets are < 512 wide: at most 9 rounds
-    double c[NE];
-#pragma unroll
-    for (int jj = 0; jj < NE; ++jj)
-      c[jj] = lo[jj] < hi[jj] ? pt.cdf[row[jj] * POIS_KMAX + (uint32_t)((lo[jj] + hi[jj]) >> 1)]
-                              : 0.0;
-    bool open = false;
-#pragma unroll
-    for (int jj = 0; jj < NE; ++jj) {
-      if (lo[jj] < hi[jj]) {
-        const int mid = (lo[jj] + hi[jj]) >> 1;
-        if (c[jj] <= u[jj]) lo[jj] = mid + 1;
-        else hi[jj] = mid;
-        open |= lo[jj] < hi[jj];
-      }
-    }
-    if (!__any(open)) break;
-  }
-}
-
+// the element form: the definition, bisecting the CDF row in global memory
 __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a, PoisTables pt) {
   const int64_t total = a.elems * a.n;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -291,63 +349,91 @@ __global__ __launch_bounds__(256) void noise_poisson_kernel(NoiseArgs a, PoisTab
     } else {
       const u32x4 r = pois_block(a.key, (uint64_t)e >> 2, image_id(a, img));
       const int q = (int)(e & 3);
-      const uint32_t u[1] = {q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w};
-      const uint32_t row[1] = {(uint32_t)vals_index(a.vals[img]) * 256u + a.src[boff]};
-      int lo[1];
-      pois_invert_n<1>(pt, row, u, lo);
-      k = (double)lo[0];
+      const uint32_t w = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+      const double* cdf =
+          pt.cdf + ((size_t)vals_index(a.vals[img]) * 256 + a.src[boff]) * POIS_KMAX;
+      k = (double)pois_first_above(cdf, pois_u(w));
     }
     store_out(a, img, e, boff, clip01(k / vals));
   }
 }
 
-// flat Poisson (compact rows, Philox stream): 16 consecutive elements per thread, image =
-// blockIdx.y; the same uniforms and tables as noise_poisson_kernel, so the two forms agree bit
-// for bit
-__global__ __launch_bounds__(256) void noise_poisson_flat_kernel(NoiseArgs a, PoisTables pt) {
-  const int img = blockIdx.y;
-  const uint32_t chunk = blockIdx.x * 256u + threadIdx.x;
-  const int64_t e0 = (int64_t)chunk * 16;
-  if (__all(e0 >= a.elems)) return;
-  const bool live = e0 < a.elems;  // dead lanes still take part in the lockstep rounds
-  const uint32_t vraw = a.vals[img];
-  const double vals = (double)vraw;
-  const uint64_t gimg = image_id(a, img);
-  v4u raw = {0u, 0u, 0u, 0u};
-  const int64_t base = slot_of(a, img) * a.elems + e0;
-  if (live) raw = *reinterpret_cast<const v4u*>(a.src + base);
-  const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
-  const uint32_t tab0 = (uint32_t)vals_index(vraw) * 256u;
-  const double inv_vals = 1.0 / vals;  // vals is a power of two: k * inv_vals == k / vals
-  double* of = a.out_f64 && live ? a.out_f64 + base : nullptr;
-  uint32_t o[4] = {0u, 0u, 0u, 0u};
-  // PQ groups of 16 / PQ elements (fewer live registers than 16 at once, so more waves per SIMD
-  // to hide the table reads)
-  constexpr int PQ = 4, PE = 16 / PQ;
-#pragma unroll
-  for (int hf = 0; hf < PQ; ++hf) {
-    static_assert(PE == 4, "one Philox block per group");
-    const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 2) + hf, gimg);
-    const uint32_t u[PE] = {r.x, r.y, r.z, r.w};
-    uint32_t row[PE];
-#pragma unroll
-    for (int jj = 0; jj < PE; ++jj) {
-      const int el = PE * hf + jj;
-      row[jj] = tab0 + ((in[el >> 2] >> (8 * (el & 3))) & 0xFFu);
+// flat Poisson (compact rows, Philox stream): work units = (image, part) pairs over a grid of one
+// workgroup per CU, the unit's level block staged in LDS (re-staged only when the level changes),
+// 16 consecutive elements per thread per step; the same uniforms and the same inversion as
+// noise_poisson_kernel, so the two forms agree bit for bit
+constexpr int POIS_FLAT_WGT = 1024;
+__global__ __launch_bounds__(POIS_FLAT_WGT) void noise_poisson_flat_kernel(NoiseArgs a,
+                                                                           PoisTables pt,
+                                                                           int parts) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[POIS_LVL_BYTES];
+  const uint32_t* HDR = reinterpret_cast<const uint32_t*>(lds);
+  const uint16_t* GUIDE = reinterpret_cast<const uint16_t*>(lds + POIS_LVL_G);
+  const uint32_t* L32 = reinterpret_cast<const uint32_t*>(lds);  // T[k] of v: L32[HDR[v] + k]
+  const int64_t nq = a.elems / 16;
+  const int units = a.n * parts;
+  int staged = -1;
+  for (int unit = blockIdx.x; unit < units; unit += gridDim.x) {
+    const int img = unit / parts, part = unit - img * parts;
+    const uint32_t vraw = a.vals[img];
+    const int vi = vals_index(vraw);
+    const bool in_lds = pt.ntab[vi] <= (uint32_t)POIS_TCAP;
+    if (vi != staged) {  // uniform over the workgroup
+      __syncthreads();
+      if (in_lds) {
+        const v4u* src = reinterpret_cast<const v4u*>(pt.levels + (size_t)vi * POIS_LVL_BYTES);
+        const int n16 = (int)((POIS_LVL_T + pt.ntab[vi] * sizeof(uint32_t) + 15) / 16);
+        v4u* dst = reinterpret_cast<v4u*>(lds);
+        for (int i = threadIdx.x; i < n16; i += POIS_FLAT_WGT) dst[i] = src[i];
+      }
+      __syncthreads();
+      staged = vi;
     }
-    int lo[PE];
-    pois_invert_n<PE>(pt, row, u, lo);
+    const double* cdf_lvl = pt.cdf + (size_t)vi * 256 * POIS_KMAX;
+    const double inv_vals = 1.0 / (double)vraw;  // power of two: k * inv_vals == k / vals
+    const uint64_t gimg = image_id(a, img);
+    const int64_t q0 = nq * part / parts, q1 = nq * (part + 1) / parts;
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += POIS_FLAT_WGT) {
+      const int64_t e0 = q * 16;
+      const int64_t base = slot_of(a, img) * a.elems + e0;
+      const v4u raw = *reinterpret_cast<const v4u*>(a.src + base);
+      const uint32_t in[4] = {raw.x, raw.y, raw.z, raw.w};
+      double* of = a.out_f64 ? a.out_f64 + base : nullptr;
+      uint32_t o[4];
 #pragma unroll
-    for (int jj = 0; jj < PE; ++jj) {
-      const int el = PE * hf + jj;
-      const double out = clip01(__dmul_rn((double)lo[jj], inv_vals));
-      o[el >> 2] |= (uint32_t)u8_of(out) << (8 * (el & 3));
-      if (of) of[el] = out;
+      for (int hf = 0; hf < 4; ++hf) {  // 4 groups of 4 elements, one Philox block each
+        const u32x4 r = pois_block(a.key, (uint64_t)(e0 >> 2) + hf, gimg);
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+        int k[4], jmin = POIS_NBH;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t v = (in[hf] >> (8 * i)) & 0xFFu;
+          const int j = pois_bin(w[i]);
+          jmin = min(jmin, j);
+          const uint32_t k0 = GUIDE[v * POIS_NG + pois_side(w[i]) * POIS_NBH + j];
+          const uint32_t* t = L32 + HDR[v] + k0;
+          const uint32_t t0 = t[0], t1 = t[1], t2 = t[2];
+          k[i] = (int)k0 + (w[i] >= t0) + (w[i] >= t1) + (w[i] >= t2);
+        }
+        if (!in_lds || __any(jmin == 0)) {  // deep bins (1 draw in 32 K) or an unstaged level
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (!in_lds || pois_bin(w[i]) == 0) {
+              const uint32_t v = (in[hf] >> (8 * i)) & 0xFFu;
+              k[i] = pois_first_above(cdf_lvl + (size_t)v * POIS_KMAX, pois_u(w[i]));
+            }
+          }
+        }
+        o[hf] = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // trunc(255 * min(k / vals, 1)), exact in integers
+          o[hf] |= min((uint32_t)(255 * k[i]) >> vi, 255u) << (8 * i);
+          if (of) of[4 * hf + i] = clip01(__dmul_rn((double)k[i], inv_vals));
+        }
+      }
+      if (a.out_u8) *reinterpret_cast<v4u*>(a.out_u8 + base) = v4u{o[0], o[1], o[2], o[3]};
     }
   }
-  if (!live) return;
-  if (a.out_u8)
-    *reinterpret_cast<v4u*>(a.out_u8 + base) = v4u{o[0], o[1], o[2], o[3]};
 }
 
 // flat per-image distinct-value mask: 16 bytes per thread per step, a private 256-bit mask per
@@ -483,8 +569,54 @@ static size_t pois_tables_off(int n) {
 }
 extern "C" size_t idn_noise_workspace_size(int kind, int n) {
   if (kind != IDN_NOISE_POISSON || n <= 0) return 0;
-  return pois_tables_off(n) + (size_t)idn::POIS_NV * 256 *
-                                  (idn::POIS_KMAX * sizeof(double) + idn::POIS_G * sizeof(uint32_t));
+  return pois_tables_off(n);  // per-image distinct-value masks and vals
+}
+
+namespace idn {
+// the Poisson tables of the current device, built on first use (on `st`, then synchronised) and
+// kept for the life of the process: 9.4 MB of CDF rows + 9 level blocks of 154 KB
+static int pois_tables_for(hipStream_t st, PoisTables* out) {
+  static std::mutex mu;
+  static PoisTables cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+    return set_error(IDN_EHIP, "poisson tables: no device");
+  std::lock_guard<std::mutex> lock(mu);
+  if (!cache[dev].cdf) {
+    PoisTables pt;
+    const size_t cdf_bytes = (size_t)POIS_NV * 256 * POIS_KMAX * sizeof(double);
+    const size_t bytes = cdf_bytes + (size_t)POIS_NV * POIS_LVL_BYTES + 16 * sizeof(uint32_t);
+    void* mem = nullptr;
+    if (hipMalloc(&mem, bytes) != hipSuccess)
+      return set_error(IDN_EHIP, "poisson tables: hipMalloc(%zu) failed", bytes);
+    pt.cdf = reinterpret_cast<double*>(mem);
+    pt.levels = reinterpret_cast<uint8_t*>(mem) + cdf_bytes;
+    pt.ntab = reinterpret_cast<uint32_t*>(pt.levels + (size_t)POIS_NV * POIS_LVL_BYTES);
+    hipLaunchKernelGGL(pois_level_kernel, dim3(POIS_NV), dim3(256), 0, st, pt);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipFree(mem);
+      return set_error(IDN_EHIP, "poisson tables: build failed");
+    }
+    cache[dev] = pt;
+  }
+  *out = cache[dev];
+  return IDN_OK;
+}
+}  // namespace idn
+
+extern "C" int idn_poisson_levels(uint32_t* ntab_out, uint32_t* cap_out, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(ntab_out && cap_out, "idn_poisson_levels: null pointer");
+  hipStream_t st = as_stream(stream);
+  PoisTables pt;
+  const int rc = pois_tables_for(st, &pt);
+  if (rc != IDN_OK) return rc;
+  if (hipMemcpyAsync(ntab_out, pt.ntab, POIS_NV * sizeof(uint32_t), hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return set_error(IDN_EHIP, "idn_poisson_levels: copy failed");
+  cap_out[0] = POIS_TCAP;
+  return IDN_OK;
 }
 
 namespace idn {
@@ -585,17 +717,21 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       }
       hipLaunchKernelGGL(vals_from_mask_kernel, dim3((n + 255) / 256), dim3(256), 0, st, mask, n);
       a.vals = mask + 8 * n;
-      PoisTables pt;
-      pt.cdf = reinterpret_cast<double*>((char*)workspace + pois_tables_off(n));
-      pt.guide = reinterpret_cast<uint32_t*>(pt.cdf + (size_t)POIS_NV * 256 * POIS_KMAX);
+      PoisTables pt{};
       if (!replay) {
-        hipLaunchKernelGGL(pois_cdf_kernel, dim3(POIS_NV * 256 / 64), dim3(64), 0, st, pt);
-        hipLaunchKernelGGL(pois_guide_kernel, dim3(POIS_NV * 256 * POIS_G / 256), dim3(256), 0, st,
-                           pt);
+        const int rc = pois_tables_for(st, &pt);
+        if (rc != IDN_OK) return rc;
       }
       if (flat) {
-        const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
-        hipLaunchKernelGGL(noise_poisson_flat_kernel, grid, dim3(256), 0, st, a, pt);
+        // one 154 KB-LDS workgroup per CU, looping over (image, part) units; ~8 units per
+        // workgroup keeps the tail short
+        const int cus = cu_count();
+        const int64_t nq = a.elems / 16;
+        const int parts = (int)std::max<int64_t>(
+            1, std::min<int64_t>((8LL * cus + n - 1) / n, (nq + POIS_FLAT_WGT - 1) / POIS_FLAT_WGT));
+        const int units = n * parts;
+        hipLaunchKernelGGL(noise_poisson_flat_kernel, dim3((unsigned)std::min(units, cus)),
+                           dim3(POIS_FLAT_WGT), 0, st, a, pt, parts);
       } else {
         hipLaunchKernelGGL(noise_poisson_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a,
                            pt);

@@ -95,12 +95,18 @@ int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int 
  *     SAP: f64 [2][n*h*w*c] = (random_sample for `flipped`, random_sample for `salted`);
  *     POISSON: f64 per-element Poisson draws (n*h*w*c).  NULL = Philox stream (seed, offset).
  *   workspace: POISSON needs idn_noise_workspace_size() bytes (per-image `vals`); else unused.
+ *     (POISSON's CDF / level tables are built once per device by the library and kept.)
  * Replaces skimage random_noise at lib/model/test.py:193-590, minibatch.py:87-490. */
 int idn_noise_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
                  int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
                  uint64_t offset, const double* replay, void* workspace, size_t ws_bytes,
                  void* stream);
 size_t idn_noise_workspace_size(int kind, int n);
+/* Diagnostics for the POISSON flat kernel: builds (once per device) the per-vals level tables
+ * (vals = 1 .. 256) and copies to ntab_out[9] the thresholds each level holds; a value above
+ * cap_out[0] (the LDS capacity) means that level's draws would bisect the global CDF rows
+ * instead of the LDS tables.  Synchronous on `stream`. */
+int idn_poisson_levels(uint32_t* ntab_out, uint32_t* cap_out, void* stream);
 /* As idn_noise_u8 (Philox stream only) with an explicit device array of n image ids instead of
  * offset + i: a mixed batch's images of one noise type (any ids) run as one launch and draw
  * exactly what per-image calls with offset = id would.  Replaces the per-image dispatch of the

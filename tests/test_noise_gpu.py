@@ -274,9 +274,25 @@ def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
     assert abs(d.mean() - ref["1"].mean()) < 4e-3
 
 
+def test_poisson_levels_staged(dev):
+    """every vals level's guide + threshold window fits the flat kernel's LDS block, so its draws
+    take the LDS path (a level over capacity would silently fall back to bisecting the rows)"""
+    import ctypes
+    import torch
+    import idn
+    from idn import _lib
+    lib = _lib.load()
+    ntab = (ctypes.c_uint32 * 9)()
+    cap = (ctypes.c_uint32 * 1)()
+    _lib.check(lib.idn_poisson_levels(ntab, cap, torch.cuda.current_stream().cuda_stream),
+               "idn_poisson_levels")
+    assert all(0 < t <= cap[0] for t in ntab), (list(ntab), cap[0])
+    assert ntab[8] > ntab[0]  # vals = 256: the widest windows
+
+
 def test_poisson_flat_matches_element_kernel(dev, monkeypatch):
-    """the flat Poisson kernel (16 elements per thread, lockstep bisection) and the element kernel
-    (IDN_NOISE_FLAT=0) take the same uniforms and invert the same CDF tables: identical outputs,
+    """the flat Poisson kernel (16 elements per thread, LDS bucket tables) and the element kernel
+    (IDN_NOISE_FLAT=0) take the same uniforms, buckets and walk: identical outputs,
     over images of several vals (3, 16 and 256 distinct values)"""
     import torch
     import idn
