@@ -71,6 +71,7 @@ inline int wl_max_level(int n, int F) {
 }
 
 constexpr int WL_MAXL = 12;
+constexpr int RB_TY = 8, RB_TX = 32, RB_R = 4;  // analysis tile (wl_dwt_rb)
 constexpr int WL_STATS = 256;  // doubles of per-image stats
 
 struct WlLayout {
@@ -137,8 +138,8 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   Lt.stats_off = (size_t)n * Lt.img_floats * sizeof(wreal);
   size_t tiles_tot = 0;
   for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
-    Lt.tiles_x[l] = (Lt.W[l] + 15) / 16;
-    Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + 15) / 16);
+    Lt.tiles_x[l] = (Lt.W[l] + RB_TX - 1) / RB_TX;  // wl_dwt_rb tiles
+    Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + RB_TY - 1) / RB_TY);
     Lt.part_tile0[l] = tiles_tot;
     tiles_tot += (size_t)Lt.tiles[l];
   }
@@ -155,6 +156,7 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
 }
 
 __device__ __forceinline__ int sym_idx(int i, int n) {  // pywt 'symmetric' (half-sample)
+  if ((unsigned)i < (unsigned)n) return i;  // interior: no division
   const int period = 2 * n;
   i %= period;
   if (i < 0) i += period;
@@ -295,7 +297,6 @@ __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict
 }
 
 // ---- 2: one analysis level ----------------------------------------------------------------------
-constexpr int DT = 16;  // output tile (DT x DT coefficients per band)
 
 // channel c of skimage rgb2ycbcr for one pixel (same fma chain as ycbcr64)
 __device__ __forceinline__ double ycbcr_c(const double (&v)[3], int c) {
@@ -304,105 +305,168 @@ __device__ __forceinline__ double ycbcr_c(const double (&v)[3], int c) {
   return __dadd_rn(dot3(v[0], v[1], v[2], 112.0, -93.786, -18.214), 128.0);
 }
 
+// Register-blocked analysis tile: RB_TY x RB_TX output coefficients per band, all three channels
+// in one 256-thread workgroup.
+//   axis 0: thread (c, q) owns staged input column q of channel c (3 x NX threads); it loads the
+//           NY input samples of its column (u8 / f64 pixels normalised on the fly, or the level
+//           above's 'aa' plane), all loads in flight at once, and runs the F-tap lowpass and
+//           highpass down the column in registers into S.vl / S.vh.
+//   axis 1: thread (c, ii, group) computes R consecutive output columns of all four bands from
+//           2R + F - 2 staged values of S.vl and S.vh (wave w = channel w).
+//   the four bands go out through LDS (reusing vl / vh) as whole rows, so each wave's stores are
+//   contiguous (register-blocked lanes stored 8-byte pieces at a 32-byte stride: 4x the L2 write
+//   requests).
+// LDS traffic is ~10 accesses per input pixel (round 1's per-output gathers: ~42).
 template <int WV>
-__global__ __launch_bounds__(256) void wl_dwt(wreal* __restrict__ ws, size_t img_floats,
-                                              const double* __restrict__ stats, int level,
-                                              size_t in_off, int Hin, int Win, size_t out_off,
-                                              int Ho, int Wo, int tiles_x,
-                                              const uint8_t* __restrict__ src,
-                                              const double* __restrict__ in64, int64_t row_stride,
-                                              double* __restrict__ part, size_t part_per_img,
-                                              size_t part_tile0, int ntiles) {
-  using Wv = Wav<WV>;
-  constexpr int F = Wv::F;
-  constexpr int NI = 2 * DT + F - 2;  // staged input rows / cols
-  __shared__ wreal xin[NI][NI + 1];
-  __shared__ wreal vl[DT][NI + 1], vh[DT][NI + 1];
+struct DwtRB {
+  static constexpr int F = Wav<WV>::F;
+  static constexpr int NX = 2 * RB_TX + F - 2;  // staged input columns
+  static constexpr int NY = 2 * RB_TY + F - 2;  // input rows per column
+  wreal vl[3][RB_TY][NX + 1], vh[3][RB_TY][NX + 1];
+};
+static_assert(3 * RB_TY * (RB_TX / RB_R) == 192, "axis-1 items: one per thread of waves 0-2");
+static_assert(2 * 3 * RB_TY * (2 * RB_TX + 1 - 2 + 1) >= 3 * 4 * RB_TY * RB_TX,
+              "the band staging buffer fits in vl + vh (F >= 2)");
 
-  const int img = blockIdx.z / 3, c = blockIdx.z % 3;
+// SRC: 0 = u8 image, 1 = f64 image (level 1, normalised per channel), 2 = the 'aa' planes of the
+// level above (levels >= 2).  Grid (tiles, 1, n).
+template <int WV, int SRC>
+__global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t img_floats,
+                                                 const double* __restrict__ stats, size_t in_off,
+                                                 int Hin, int Win, size_t out_off, int Ho, int Wo,
+                                                 int tiles_x, const uint8_t* __restrict__ src,
+                                                 const double* __restrict__ in64,
+                                                 int64_t row_stride, double* __restrict__ part,
+                                                 size_t part_per_img, size_t part_tile0) {
+  using Wv = Wav<WV>;
+  constexpr int F = Wv::F, NX = DwtRB<WV>::NX, NY = DwtRB<WV>::NY;
+  __shared__ DwtRB<WV> S;
+  const int img = blockIdx.z;
   wreal* base = ws + img * img_floats;
-  const wreal* X = base + in_off + (size_t)c * ((level == 1) ? (size_t)Hin * Win : (size_t)4 * Hin * Win);
-  // level 1 reads plane c; deeper levels read band 'aa' (slot 0) of channel c of the level above
-  const size_t bsz = (size_t)Ho * Wo;
-  wreal* out = base + out_off + (size_t)c * 4 * bsz;  // [aa, ad, da, dd]
-  wreal mn = 0, inv = 1;
-  bool norm = false;
-  if (level == 1) {
-    wreal mx;
-    wl_minmax64(stats + (size_t)img * WL_STATS, c, mn, mx);
-    inv = mx - mn;
-    norm = true;
-  }
-  const int ti = blockIdx.x / tiles_x, tj = blockIdx.x % tiles_x;
-  const int i0 = ti * DT, j0 = tj * DT;
+  const int ti = blockIdx.x / tiles_x, tj = blockIdx.x - ti * tiles_x;
+  const int i0 = ti * RB_TY, j0 = tj * RB_TX;
   const int r0 = 2 * i0 + 2 - F, q0 = 2 * j0 + 2 - F;  // input coordinate of staged [0][0]
-  for (int k = threadIdx.x; k < NI * NI; k += 256) {
-    const int r = k / NI, q = k % NI;
-    const int yy = sym_idx(r0 + r, Hin), xx = sym_idx(q0 + q, Win);
-    wreal v;
-    if (norm) {  // level 1: the YCbCr channel straight from the source image
-      double px[3];
-      load_rgb64(src, in64, img, Hin, Win, row_stride, yy, xx, px);
-      v = (ycbcr_c(px, c) - mn) / inv;  // skimage: channel = out - min; channel /= max - min
-    } else {
-      v = X[(size_t)yy * Win + xx];
-    }
-    xin[r][q] = v;
-  }
-  __syncthreads();
-  // axis 0 first (pywt dwtn order): output row i uses staged rows 2ii + F-1-p
-  for (int k = threadIdx.x; k < DT * NI; k += 256) {
-    const int ii = k / NI, q = k % NI;
-    wreal lo = 0, hi = 0;
+  const int t = threadIdx.x;
+  if (t < 3 * NX) {
+    const int c = t / NX, q = t - c * NX;
+    const int xx = sym_idx(q0 + q, Win);
+    wreal x[NY];
+    if (SRC == 2) {
+      const wreal* X = base + in_off + (size_t)c * 4 * Hin * Win + xx;
 #pragma unroll
-    for (int p = 0; p < F; ++p) {
-      const wreal v = xin[2 * ii + F - 1 - p][q];
-      if (Wv::dlo[p] != 0) lo = lo + Wv::dlo[p] * v;  // no FMA: pywt's mul-then-add
-      if (Wv::dhi[p] != 0) hi = hi + Wv::dhi[p] * v;
+      for (int r = 0; r < NY; ++r) x[r] = X[(size_t)sym_idx(r0 + r, Hin) * Win];
+    } else {
+      const double* st = stats + (size_t)img * WL_STATS;
+      wreal mn, mx;
+      wl_minmax64(st, c, mn, mx);
+      const wreal inv = mx - mn, rcp = 1.0 / inv;
+      if (SRC == 0) {
+        const uint8_t* col = src + (int64_t)img * Hin * row_stride + (int64_t)xx * 3;
+        uint32_t raw[NY];
+#pragma unroll
+        for (int r = 0; r < NY; ++r) {  // all loads in flight before any use
+          const uint8_t* p = col + (int64_t)sym_idx(r0 + r, Hin) * row_stride;
+          raw[r] = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16;
+        }
+#pragma unroll
+        for (int r = 0; r < NY; ++r) {
+          double px[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) px[k] = (double)((raw[r] >> (8 * k)) & 0xFFu) * (1.0 / 255.0);
+          // skimage: channel = out - min; channel /= max - min, as the IEEE quotient (reciprocal
+          // multiply + one Markstein correction, exact over every u8 triple: tools/check_div.c)
+          const wreal a = ycbcr_c(px, c) - mn;
+          const wreal qq = a * rcp;
+          x[r] = __fma_rn(__fma_rn(-qq, inv, a), rcp, qq);
+        }
+      } else {
+        double px[NY][3];
+#pragma unroll
+        for (int r = 0; r < NY; ++r)
+          load_rgb64(src, in64, img, Hin, Win, row_stride, sym_idx(r0 + r, Hin), xx, px[r]);
+#pragma unroll
+        for (int r = 0; r < NY; ++r) x[r] = (ycbcr_c(px[r], c) - mn) / inv;
+      }
     }
-    vl[ii][q] = lo;
-    vh[ii][q] = hi;
+    // axis 0 first (pywt dwtn order): output row ii uses staged rows 2ii + F-1-p
+#pragma unroll
+    for (int ii = 0; ii < RB_TY; ++ii) {
+      wreal lo = 0, hi = 0;
+#pragma unroll
+      for (int p = 0; p < F; ++p) {
+        const wreal v = x[2 * ii + F - 1 - p];
+        if (Wv::dlo[p] != 0) lo = __dadd_rn(lo, __dmul_rn(Wv::dlo[p], v));  // pywt: mul, then add
+        if (Wv::dhi[p] != 0) hi = __dadd_rn(hi, __dmul_rn(Wv::dhi[p], v));
+      }
+      S.vl[c][ii][q] = lo;
+      S.vh[c][ii][q] = hi;
+    }
   }
   __syncthreads();
-  const int ii = threadIdx.x / DT, jj = threadIdx.x % DT;
-  const int i = i0 + ii, j = j0 + jj;
+  const int c = t >> 6, ii = (t >> 3) & 7, g = t & 7;  // wave = channel (waves 0-2)
+  const int i = i0 + ii, jl = g * RB_R;
+  constexpr int NC = 2 * RB_R + F - 2;  // staged columns one thread reads
+  wreal l[NC], h[NC];
+  if (t < 192) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      l[k] = S.vl[c][ii][2 * jl + k];
+      h[k] = S.vh[c][ii][2 * jl + k];
+    }
+  }
+  __syncthreads();  // vl / vh become the output staging buffer
+  wreal(*ob)[4][RB_TY][RB_TX] = reinterpret_cast<wreal(*)[4][RB_TY][RB_TX]>(&S.vl[0][0][0]);
   double sq[3] = {0.0, 0.0, 0.0};
-  if (i < Ho && j < Wo) {
+  if (t < 192) {
+#pragma unroll
+  for (int r = 0; r < RB_R; ++r) {
     wreal aa = 0, ad = 0, da = 0, dd = 0;
 #pragma unroll
-    for (int q = 0; q < F; ++q) {  // then axis 1: output column j uses staged cols 2jj + F-1-q
-      const wreal l = vl[ii][2 * jj + F - 1 - q], hh = vh[ii][2 * jj + F - 1 - q];
-      if (Wv::dlo[q] != 0) {
-        aa = aa + Wv::dlo[q] * l;   // key 'aa': axis 0 low, axis 1 low
-        da = da + Wv::dlo[q] * hh;  // key 'da': axis 0 high, axis 1 low
+    for (int qq = 0; qq < F; ++qq) {  // then axis 1: output column j uses staged cols 2j + F-1-q
+      const wreal lv = l[2 * r + F - 1 - qq], hv = h[2 * r + F - 1 - qq];
+      if (Wv::dlo[qq] != 0) {
+        aa = __dadd_rn(aa, __dmul_rn(Wv::dlo[qq], lv));  // key 'aa': axis 0 low, axis 1 low
+        da = __dadd_rn(da, __dmul_rn(Wv::dlo[qq], hv));  // key 'da': axis 0 high, axis 1 low
       }
-      if (Wv::dhi[q] != 0) {
-        ad = ad + Wv::dhi[q] * l;   // key 'ad': axis 0 low, axis 1 high
-        dd = dd + Wv::dhi[q] * hh;
+      if (Wv::dhi[qq] != 0) {
+        ad = __dadd_rn(ad, __dmul_rn(Wv::dhi[qq], lv));  // key 'ad': axis 0 low, axis 1 high
+        dd = __dadd_rn(dd, __dmul_rn(Wv::dhi[qq], hv));
       }
     }
-    const size_t o = (size_t)i * Wo + j;
-    out[o] = aa;
-    out[bsz + o] = ad;
-    out[2 * bsz + o] = da;
-    out[3 * bsz + o] = dd;
-    sq[0] = ad * ad;
-    sq[1] = da * da;
-    sq[2] = dd * dd;
+    ob[c][0][ii][jl + r] = aa;
+    ob[c][1][ii][jl + r] = ad;
+    ob[c][2][ii][jl + r] = da;
+    ob[c][3][ii][jl + r] = dd;
+    if (i < Ho && j0 + jl + r < Wo) {
+      sq[0] += ad * ad;
+      sq[1] += da * da;
+      sq[2] += dd * dd;
+    }
   }
-  // per-tile sums of squares of the three detail bands, fixed order (wl_sumsq adds the tiles)
-  __shared__ double red[3][4];
+  // per-tile sums of squares of the three detail bands of this wave's channel, fixed order
+  // (wl_sumsq adds the tiles)
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     double v = sq[b];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0) red[b][threadIdx.x >> 6] = v;
+    if ((t & 63) == 0)
+      part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 +
+           blockIdx.x] = v;
+  }
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
-    const int b = threadIdx.x;
-    const double t = (red[b][0] + red[b][1]) + (red[b][2] + red[b][3]);
-    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = t;
+  // coalesced band stores: rows of RB_TX coefficients, 16 lanes x 16 bytes per row
+  const size_t bsz = (size_t)Ho * Wo;
+  constexpr int PR = RB_TX / 2;  // coefficient pairs per row
+  for (int k = t; k < 3 * 4 * RB_TY * PR; k += 256) {
+    const int row = k / PR, pr = k - row * PR;  // row = (c * 4 + band) * RB_TY + ii
+    const int cb = row / RB_TY, iy = row - cb * RB_TY;
+    const int oi = i0 + iy, oj = j0 + 2 * pr;
+    if (oi >= Ho || oj >= Wo) continue;
+    const wreal* sv = &ob[0][0][0][0] + (size_t)row * RB_TX + 2 * pr;
+    wreal* dst = base + out_off + (size_t)cb * bsz + (size_t)oi * Wo + oj;
+    dst[0] = sv[0];
+    if (oj + 1 < Wo) dst[1] = sv[1];
   }
 }
 
@@ -644,129 +708,220 @@ __device__ __forceinline__ wreal soft(wreal d, wreal t) {
   return m > 0.0 ? __builtin_copysign(m, d) : 0.0;
 }
 
-// ---- 6: one synthesis level (levels L..2), output = approx of level l-1 -------------------------
+// ---- 6/7: synthesis, LDS-tiled and separable ---------------------------------------------------
+// One workgroup per ST_O x ST_O output tile of the level being synthesised: it stages the
+// (ST_O/2 + HF-1)^2 coefficients of the four bands the tile needs (details soft-thresholded on
+// load), runs pywt idwtn's axis-1 pass into LDS ('a' from
+// aa/ad, 'd' from da/dd) and then the axis-0 pass, each as upsampling_convolution_valid_sf's
+// sum_even / sum_odd (lowpass sum + highpass sum, multiply then add, zero taps skipped); each
+// thread computes an output pair from one set of HF coefficients.
+// Levels L..2 write the approximation of the level below (cropped to its size); level 1
+// (FINAL) runs the three channels of the tile in turn and fuses the inner clip [0, 1],
+// de-normalisation, YCbCr -> RGB, the outer clip and the U8 / f32 stores.
+// Round 1's per-pixel form gathered 36 coefficients per channel and pixel from L2 (7.0 ms per
+// 256 bior1.5 images for the last level alone).
+constexpr int ST_O = 32;
+
 template <int WV>
-__global__ __launch_bounds__(256) void wl_idwt(wreal* __restrict__ ws, size_t img_floats,
-                                               const double* __restrict__ stats, int level, int L,
-                                               size_t in_off, int Nh, int Nw, size_t out_off,
-                                               int Hout, int Wout, size_t out_chan_stride) {
+struct SynthTile {
+  static constexpr int F = Wav<WV>::F, HF = F / 2;
+  static constexpr int CR = ST_O / 2 + HF - 1;  // staged coefficient rows / cols
+  wreal co[4][CR][CR + 1];
+  wreal sa[CR][ST_O + 1], sd[CR][ST_O + 1];
+};
+
+// one upsampling_convolution_valid_sf output pair (even, odd) from the HF coefficients
+// c[j] = x[i - j]: lowpass part of the even / odd filter taps, multiply then add, zero taps
+// skipped (they add +-0)
+template <int WV, bool HI>
+__device__ __forceinline__ void synth_pair(const wreal (&c)[Wav<WV>::F / 2], wreal& ev, wreal& od) {
   using Wv = Wav<WV>;
-  constexpr int F = Wv::F, HF = F / 2;
-  const int img = blockIdx.z / 3, c = blockIdx.z % 3;
-  wreal* base = ws + img * img_floats;
-  const size_t bsz = (size_t)Nh * Nw;
-  const wreal* A = base + in_off + (size_t)c * 4 * bsz;
-  const wreal* AD = A + bsz;
-  const wreal* DA = A + 2 * bsz;
-  const wreal* DD = A + 3 * bsz;
-  const double* st = stats + (size_t)img * WL_STATS;
-  const wreal tad = st[WlStats::thr(c, level - 1, 0, L)];
-  const wreal tda = st[WlStats::thr(c, level - 1, 1, L)];
-  const wreal tdd = st[WlStats::thr(c, level - 1, 2, L)];
-  wreal* out = base + out_off + (size_t)c * out_chan_stride;
-  const int64_t total = (int64_t)Hout * Wout;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int p = (int)(k / Wout), q = (int)(k - (int64_t)p * Wout);
-    const int m = p >> 1, r = p & 1, nn = q >> 1, s = q & 1;
-    wreal acc = 0;
+  constexpr int HF = Wv::F / 2;
+  ev = 0;
+  od = 0;
 #pragma unroll
-    for (int j = 0; j < HF; ++j) {
-      const int row = m + HF - 1 - j;
-      const wreal fa0 = Wv::rlo[2 * j], fa1 = Wv::rlo[2 * j + 1];
-      const wreal fd0 = Wv::rhi[2 * j], fd1 = Wv::rhi[2 * j + 1];
-      const wreal fa = r ? fa1 : fa0, fd = r ? fd1 : fd0;
-#pragma unroll
-      for (int kk = 0; kk < HF; ++kk) {
-        const int col = nn + HF - 1 - kk;
-        const wreal ga0 = Wv::rlo[2 * kk], ga1 = Wv::rlo[2 * kk + 1];
-        const wreal gd0 = Wv::rhi[2 * kk], gd1 = Wv::rhi[2 * kk + 1];
-        const wreal ga = s ? ga1 : ga0, gd = s ? gd1 : gd0;
-        const size_t o = (size_t)row * Nw + col;
-        if ((fa0 != 0 || fa1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fa * ga * A[o];
-        if ((fa0 != 0 || fa1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fa * gd * (soft(AD[o], tad));
-        if ((fd0 != 0 || fd1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fd * ga * (soft(DA[o], tda));
-        if ((fd0 != 0 || fd1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fd * gd * (soft(DD[o], tdd));
-      }
-    }
-    out[(size_t)p * Wout + q] = acc;
+  for (int j = 0; j < HF; ++j) {
+    const wreal fe = HI ? Wv::rhi[2 * j] : Wv::rlo[2 * j];
+    const wreal fo = HI ? Wv::rhi[2 * j + 1] : Wv::rlo[2 * j + 1];
+    if (fe != 0) ev = __dadd_rn(ev, __dmul_rn(fe, c[j]));
+    if (fo != 0) od = __dadd_rn(od, __dmul_rn(fo, c[j]));
   }
 }
 
-// ---- 7: level 1 synthesis of all channels + colour + casts --------------------------------------
+// synthesise one channel's tile (bands at A, band size Nh x Nw, coefficient origin (m0, n0));
+// thread t receives the tile outputs (row 2 * (t / ST_O) + r, column t % ST_O) for the row pairs
+// of i (v[2 i + r])
 template <int WV>
-__global__ __launch_bounds__(256) void wl_idwt_final(const wreal* __restrict__ ws,
-                                                     size_t img_floats,
-                                                     const double* __restrict__ stats, int L,
-                                                     size_t in_off, int Nh, int Nw, int h, int w,
-                                                     uint8_t* __restrict__ out_u8,
-                                                     int64_t row_stride,
-                                                     float* __restrict__ out_f32) {
-  using Wv = Wav<WV>;
-  constexpr int F = Wv::F, HF = F / 2;
+__device__ __forceinline__ void synth_tile(SynthTile<WV>& S, const wreal* __restrict__ A,
+                                           size_t bsz, int Nh, int Nw, int m0, int n0,
+                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256]) {
+  constexpr int HF = SynthTile<WV>::HF, CR = SynthTile<WV>::CR;
+  constexpr int RPT = 256 / CR;            // staging: band rows per pass (CR columns each)
+  constexpr int NRW = 4 * CR;              // band rows to stage
+  constexpr int NLD = (NRW + RPT - 1) / RPT;
+  const int cc = threadIdx.x % CR, rr0 = threadIdx.x / CR;
+  // coefficients past the band's end feed only outputs past the level's valid length (pywt's
+  // stage-2 valid convolution), which are never stored: clamped reads keep them finite
+  const wreal* Ac = A + min(n0 + cc, Nw - 1);
+  wreal x[NLD];
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {  // all loads in flight before any use
+    const int br = min(rr0 + RPT * u, NRW - 1);  // band * CR + row
+    const int b = br / CR, r = br - b * CR;
+    x[u] = Ac[(size_t)b * bsz + (size_t)min(m0 + r, Nh - 1) * Nw];
+  }
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {
+    const int br = rr0 + RPT * u;
+    if (rr0 < RPT && br < NRW) {
+      const int b = br / CR, r = br - b * CR;
+      S.co[b][r][cc] = b > 0 ? soft(x[u], thr[b - 1]) : x[u];
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < CR * (ST_O / 2); k += 256) {  // axis 1: column pairs
+    const int r = k / (ST_O / 2), nn = k - r * (ST_O / 2);
+    wreal c0[HF], c1[HF], c2[HF], c3[HF];
+#pragma unroll
+    for (int j = 0; j < HF; ++j) {
+      const int col = nn + HF - 1 - j;
+      c0[j] = S.co[0][r][col];
+      c1[j] = S.co[1][r][col];
+      c2[j] = S.co[2][r][col];
+      c3[j] = S.co[3][r][col];
+    }
+    wreal le, lo, he, ho;
+    synth_pair<WV, false>(c0, le, lo);
+    synth_pair<WV, true>(c1, he, ho);
+    S.sa[r][2 * nn] = __dadd_rn(le, he);
+    S.sa[r][2 * nn + 1] = __dadd_rn(lo, ho);
+    synth_pair<WV, false>(c2, le, lo);
+    synth_pair<WV, true>(c3, he, ho);
+    S.sd[r][2 * nn] = __dadd_rn(le, he);
+    S.sd[r][2 * nn + 1] = __dadd_rn(lo, ho);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < ST_O * ST_O / 512; ++i) {  // axis 0: row pairs
+    const int k = threadIdx.x + 256 * i;
+    const int m = k / ST_O, q = k - m * ST_O;
+    wreal ca[HF], cd[HF];
+#pragma unroll
+    for (int j = 0; j < HF; ++j) {
+      ca[j] = S.sa[m + HF - 1 - j][q];
+      cd[j] = S.sd[m + HF - 1 - j][q];
+    }
+    wreal le, lo, he, ho;
+    synth_pair<WV, false>(ca, le, lo);
+    synth_pair<WV, true>(cd, he, ho);
+    v[2 * i] = __dadd_rn(le, he);
+    v[2 * i + 1] = __dadd_rn(lo, ho);
+  }
+  __syncthreads();  // S is restaged by the next call
+}
+// output position of v[e] of thread t: (row, column) inside the tile
+__device__ __forceinline__ int synth_row(int e) {
+  return 2 * ((threadIdx.x + 256 * (e >> 1)) / ST_O) + (e & 1);
+}
+__device__ __forceinline__ int synth_col(int e) { return (threadIdx.x + 256 * (e >> 1)) % ST_O; }
+
+// levels L..2: grid (tiles, n * 3); the level-(l-1) 'aa' slot receives the reconstruction
+template <int WV>
+__global__ __launch_bounds__(256) void wl_synth(wreal* __restrict__ ws, size_t img_floats,
+                                                const double* __restrict__ stats, int level, int L,
+                                                size_t in_off, int Nh, int Nw, size_t out_off,
+                                                int Hout, int Wout, size_t out_chan_stride,
+                                                int tiles_x) {
+  __shared__ SynthTile<WV> S;
+  const int img = blockIdx.y / 3, c = blockIdx.y % 3;
+  wreal* base = ws + img * img_floats;
+  const size_t bsz = (size_t)Nh * Nw;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const wreal thr[3] = {st[WlStats::thr(c, level - 1, 0, L)], st[WlStats::thr(c, level - 1, 1, L)],
+                        st[WlStats::thr(c, level - 1, 2, L)]};
+  const int ti = blockIdx.x / tiles_x, tj = blockIdx.x - ti * tiles_x;
+  const int p0 = ti * ST_O, q0 = tj * ST_O;
+  wreal v[ST_O * ST_O / 256];
+  synth_tile<WV>(S, base + in_off + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v);
+  wreal* out = base + out_off + (size_t)c * out_chan_stride;
+#pragma unroll
+  for (int i = 0; i < ST_O * ST_O / 256; ++i) {
+    const int p = p0 + synth_row(i), q = q0 + synth_col(i);
+    if (p < Hout && q < Wout) out[(size_t)p * Wout + q] = v[i];
+  }
+}
+
+// level 1 of all three channels + colour + casts: grid (tiles, n)
+template <int WV>
+__global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ ws,
+                                                      size_t img_floats,
+                                                      const double* __restrict__ stats, int L,
+                                                      size_t in_off, int Nh, int Nw, int h, int w,
+                                                      int tiles_x, uint8_t* __restrict__ out_u8,
+                                                      int64_t row_stride,
+                                                      float* __restrict__ out_f32) {
+  __shared__ SynthTile<WV> S;
+  __shared__ uint32_t obuf[ST_O][ST_O * 3 / 4];  // the tile's U8 BGR rows
+  constexpr int NV = ST_O * ST_O / 256;
   const int img = blockIdx.y;
   const wreal* base = ws + img * img_floats + in_off;
   const size_t bsz = (size_t)Nh * Nw;
   const double* st = stats + (size_t)img * WL_STATS;
   const bool bad = st[WlStats::FLAG] != 0.0;
-  wreal t[3][3], mn[3], sc[3];
-#pragma unroll
+  const int ti = blockIdx.x / tiles_x, tj = blockIdx.x - ti * tiles_x;
+  const int p0 = ti * ST_O, q0 = tj * ST_O;
+  double ych[3][NV];
+#pragma unroll 1
   for (int c = 0; c < 3; ++c) {
-    wreal mx;
-    wl_minmax64(st, c, mn[c], mx);
-    sc[c] = mx - mn[c];
+    wreal mn, mx;
+    wl_minmax64(st, c, mn, mx);
+    const wreal sc = mx - mn;
+    const wreal thr[3] = {st[WlStats::thr(c, 0, 0, L)], st[WlStats::thr(c, 0, 1, L)],
+                          st[WlStats::thr(c, 0, 2, L)]};
+    wreal v[NV];
+    synth_tile<WV>(S, base + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v);
 #pragma unroll
-    for (int b = 0; b < 3; ++b) t[c][b] = st[WlStats::thr(c, 0, b, L)];
-  }
-  const int64_t total = (int64_t)h * w;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int p = (int)(k / w), q = (int)(k - (int64_t)p * w);
-    const int m = p >> 1, r = p & 1, nn = q >> 1, s = q & 1;
-    double ych[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const wreal* A = base + (size_t)c * 4 * bsz;
-      wreal acc = 0;
-#pragma unroll
-      for (int j = 0; j < HF; ++j) {
-        const int row = m + HF - 1 - j;
-        const wreal fa0 = Wv::rlo[2 * j], fa1 = Wv::rlo[2 * j + 1];
-        const wreal fd0 = Wv::rhi[2 * j], fd1 = Wv::rhi[2 * j + 1];
-        const wreal fa = r ? fa1 : fa0, fd = r ? fd1 : fd0;
-#pragma unroll
-        for (int kk = 0; kk < HF; ++kk) {
-          const int col = nn + HF - 1 - kk;
-          const wreal ga0 = Wv::rlo[2 * kk], ga1 = Wv::rlo[2 * kk + 1];
-          const wreal gd0 = Wv::rhi[2 * kk], gd1 = Wv::rhi[2 * kk + 1];
-          const wreal ga = s ? ga1 : ga0, gd = s ? gd1 : gd0;
-          const size_t o = (size_t)row * Nw + col;
-          if ((fa0 != 0 || fa1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fa * ga * A[o];
-          if ((fa0 != 0 || fa1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fa * gd * (soft(A[bsz + o], t[c][0]));
-          if ((fd0 != 0 || fd1 != 0) && (ga0 != 0 || ga1 != 0)) acc = acc + fd * ga * (soft(A[2 * bsz + o], t[c][1]));
-          if ((fd0 != 0 || fd1 != 0) && (gd0 != 0 || gd1 != 0)) acc = acc + fd * gd * (soft(A[3 * bsz + o], t[c][2]));
-        }
-      }
+    for (int i = 0; i < NV; ++i) {
       // inner denoise_wavelet clip (0.14.2), then * (max - min) + min
-      const double v = fmin(fmax((double)acc, 0.0), 1.0);
-      ych[c] = v * sc[c] + mn[c];
+      const double x = fmin(fmax((double)v[i], 0.0), 1.0);
+      const double yv = x * sc + mn;
+      if (c == 0) ych[0][i] = yv;  // (selects: no dynamic register indexing)
+      else if (c == 1) ych[1][i] = yv;
+      else ych[2][i] = yv;
     }
+  }
+  uint8_t* ob = reinterpret_cast<uint8_t*>(&obuf[0][0]);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int y = p0 + synth_row(i), x = q0 + synth_col(i);
     // ycbcr2rgb: (arr - [16,128,128]) @ inv(ycbcr_from_rgb).T (numpy.linalg.inv, full precision,
     // fma-chain dot as numpy's matmul), then clip [0, 1]
-    const double Y = ych[0] - 16.0, Cb = ych[1] - 128.0, Cr = ych[2] - 128.0;
+    const double Y = ych[0][i] - 16.0, Cb = ych[1][i] - 128.0, Cr = ych[2][i] - 128.0;
     double o3[3];
     o3[0] = dot3(Y, Cb, Cr, 0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937);
     o3[1] = dot3(Y, Cb, Cr, 0.004566210045662101, -0.0015363236860449021, -0.003188110949655707);
     o3[2] = dot3(Y, Cb, Cr, 0.004566210045662101, 0.007910716233554741, 1.1977497040511743e-08);
-    const int y = p, x = q;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      double v = fmin(fmax(o3[c], 0.0), 1.0);
-      if (bad) v = 0.0;
-      if (out_u8)
-        out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3 + c] =
-            (uint8_t)(int)(255.0 * v);
-      if (out_f32) out_f32[(((int64_t)img * h + y) * w + x) * 3 + c] = (float)v;
+      double vv = fmin(fmax(o3[c], 0.0), 1.0);
+      if (bad) vv = 0.0;
+      ob[synth_row(i) * (ST_O * 3) + synth_col(i) * 3 + c] = (uint8_t)(int)(255.0 * vv);
+      if (out_f32 && y < h && x < w) out_f32[(((int64_t)img * h + y) * w + x) * 3 + c] = (float)vv;
+    }
+  }
+  if (!out_u8) return;
+  __syncthreads();
+  uint8_t* orow = out_u8 + (int64_t)img * h * row_stride + (int64_t)q0 * 3;
+  if (q0 + ST_O <= w && ((uintptr_t)orow & 3) == 0 && (row_stride & 3) == 0) {
+    for (int k = threadIdx.x; k < ST_O * ST_O * 3 / 4; k += 256) {  // whole dwords of full rows
+      const int r = k / (ST_O * 3 / 4), d = k - r * (ST_O * 3 / 4);
+      if (p0 + r < h)
+        reinterpret_cast<uint32_t*>(orow + (int64_t)(p0 + r) * row_stride)[d] = obuf[r][d];
+    }
+  } else {
+    for (int k = threadIdx.x; k < ST_O * ST_O * 3; k += 256) {
+      const int r = k / (ST_O * 3), b = k - r * (ST_O * 3);
+      if (p0 + r < h && q0 + b / 3 < w) orow[(int64_t)(p0 + r) * row_stride + b] = ob[r * (ST_O * 3) + b];
     }
   }
 }
@@ -1519,31 +1674,39 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   }
   double* part = (double*)((char*)ws + Lt.part_off);
   for (int l = 1; l <= Lt.L; ++l) {
-    const size_t in_off = (l == 1) ? 0 : Lt.off_band[l - 1];
-    const int tx = Lt.tiles_x[l];
-    hipLaunchKernelGGL((wl_dwt<WV>), dim3(Lt.tiles[l], 1, n * 3), dim3(256), 0, st, wsf,
-                       Lt.img_floats, stats, l, in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l],
-                       Lt.H[l], Lt.W[l], tx, src, in64, row_stride, part, Lt.part_per_img,
-                       Lt.part_tile0[l], Lt.tiles[l]);
+    const dim3 grid(Lt.tiles[l], 1, n);
+    const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
+    if (l > 1)
+      hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
+                         in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
+                         Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
+                         Lt.part_tile0[l]);
+    else if (in64)
+      hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
+                         in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
+                         Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
+                         Lt.part_tile0[1]);
+    else
+      hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
+                         in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
+                         Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
+                         Lt.part_tile0[1]);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   for (int l = Lt.L; l >= 2; --l) {
-    const int64_t tot = (int64_t)Lt.H[l - 1] * Lt.W[l - 1];
-    int gx = (int)((tot + 255) / 256);
-    if (gx > 1024) gx = 1024;
     // the level-(l-1) 'aa' slot (consumed by the analysis already) receives the reconstruction
-    hipLaunchKernelGGL((wl_idwt<WV>), dim3(gx, 1, n * 3), dim3(256), 0, st, wsf, Lt.img_floats, stats,
-                       l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Lt.H[l - 1],
-                       Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1]);
+    const int tx = (Lt.W[l - 1] + ST_O - 1) / ST_O, ty = (Lt.H[l - 1] + ST_O - 1) / ST_O;
+    hipLaunchKernelGGL((wl_synth<WV>), dim3(tx * ty, n * 3), dim3(256), 0, st, wsf, Lt.img_floats,
+                       stats, l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1],
+                       Lt.H[l - 1], Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1], tx);
   }
   {
-    const int64_t tot = (int64_t)Lt.h * Lt.w;
-    int gx = (int)((tot + 255) / 256);
-    if (gx > 2048) gx = 2048;
-    hipLaunchKernelGGL((wl_idwt_final<WV>), dim3(gx, n), dim3(256), 0, st, wsf, Lt.img_floats, stats,
-                       Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h, Lt.w, out_u8, row_stride, out_f32);
+    const int tx = (Lt.w + ST_O - 1) / ST_O, ty = (Lt.h + ST_O - 1) / ST_O;
+    hipLaunchKernelGGL((wl_synth_final<WV>), dim3(tx * ty, n), dim3(256), 0, st, wsf,
+                       Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h, Lt.w,
+                       tx, out_u8, row_stride, out_f32);
   }
   return IDN_OK;
 }
