@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256) void bilateral_u8_kernel(const uint8_t* __rest
 // formed (the same float multiply, so the same bits): a tap is v_sad_u8 + one shift + one LDS read
 // + two packed FMAs.  Each thread owns 4 output rows of one column and walks the (4 + 2R) x (2R+1)
 // input pixels of their union once: every pixel is read from LDS and converted to float once and
-// feeds each of the (up to 4) outputs it is a tap of.
+// feeds each of the (up to 4) outputs it is a tap of.  512-thread workgroups (32-row tiles): the
+// 34 KB of tables per workgroup then allow 6 waves per SIMD (256 threads: 3).
 template <int R>
 struct Rsq {  // the distinct r^2 <= R^2 that are taps: table slot of each r^2, r^2 of each slot
   int n = 0;
@@ -142,14 +143,16 @@ struct Rsq {  // the distinct r^2 <= R^2 that are taps: table slot of each r^2, 
   }
 };
 
+constexpr int BLP_NW = 8;  // waves per workgroup of the pre-multiplied kernel
 template <int R, int RPT>
-__global__ __launch_bounds__(256) void bilateral_u8_pre_kernel(const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre_kernel(const uint8_t* __restrict__ src,
                                                                uint8_t* __restrict__ dst, int h,
                                                                int w, int64_t row_stride,
                                                                int tiles_x, int tiles_y,
                                                                int ntiles, BilateralTaps taps) {
   constexpr int LW = BL_TW + 2 * R;
-  constexpr int TH = 4 * RPT;  // tile height: 4 waves x RPT rows
+  constexpr int NT = 64 * BLP_NW;
+  constexpr int TH = BLP_NW * RPT;  // tile height: one wave per RPT rows
   constexpr int LH = TH + 2 * R;
   constexpr Rsq<R> RS;
   __shared__ uint32_t tile[LH * LW];
@@ -157,12 +160,12 @@ __global__ __launch_bounds__(256) void bilateral_u8_pre_kernel(const uint8_t* __
   __shared__ float wt[RS.n * BL_LUT];
 
   // the weight tables, once per (persistent) workgroup
-  for (int i = threadIdx.x; i < BL_LUT; i += 256) cw[i] = (float)exp((double)(i * i) * taps.gcc);
+  for (int i = threadIdx.x; i < BL_LUT; i += NT) cw[i] = (float)exp((double)(i * i) * taps.gcc);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < RS.n; ++k) {
     const float sw = taps.swq[RS.q[k]];
-    for (int i = threadIdx.x; i < BL_LUT; i += 256)
+    for (int i = threadIdx.x; i < BL_LUT; i += NT)
       wt[k * BL_LUT + i] = sw * cw[i];  // OpenCV: space_weight[k] * color_weight[dist]
   }
 
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(256) void bilateral_u8_pre_kernel(const uint8_t* __
     uint8_t* d = dst + (int64_t)img * h * row_stride;
     const int x0 = tx * BL_TW, y0 = ty * TH;
     __syncthreads();  // the previous tile is consumed (and the tables are built)
-    for (int i = threadIdx.x; i < LH * LW; i += 256) {
+    for (int i = threadIdx.x; i < LH * LW; i += NT) {
       const int ly = i / LW, lx = i % LW;
       tile[i] = load_px<3>(s, row_stride, h, w, y0 + ly - R, x0 + lx - R);
     }
@@ -233,11 +236,14 @@ __global__ __launch_bounds__(256) void bilateral_u8_pre_kernel(const uint8_t* __
 template <int R, int RPT>
 static void launch_bl_pre_rpt(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
                               const BilateralTaps& taps, hipStream_t st) {
-  const int tiles_x = (w + BL_TW - 1) / BL_TW, tiles_y = (h + 4 * RPT - 1) / (4 * RPT);
+  const int tiles_x = (w + BL_TW - 1) / BL_TW;
+  const int tiles_y = (h + BLP_NW * RPT - 1) / (BLP_NW * RPT);
   const int64_t ntiles = (int64_t)n * tiles_x * tiles_y;
-  // persistent workgroups: the weight tables are built once per workgroup
-  const int64_t grid = ntiles < 2048 ? ntiles : 2048;
-  hipLaunchKernelGGL((bilateral_u8_pre_kernel<R, RPT>), dim3((unsigned)grid), dim3(256), 0, st, src,
+  // persistent workgroups, as many as are resident (3 per CU: LDS): the weight tables are built
+  // once per workgroup
+  const int64_t res = (int64_t)cu_count() * 3;
+  const int64_t grid = ntiles < res ? ntiles : res;
+  hipLaunchKernelGGL((bilateral_u8_pre_kernel<R, RPT>), dim3((unsigned)grid), dim3(64 * BLP_NW), 0, st, src,
                      dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
 }
 
