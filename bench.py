@@ -41,6 +41,10 @@ OPS = {
     "noise_gaussian": ("gaussian_var1.0 noise",
                        lambda idn, x, y: idn.ops.random_noise(x, "gaussian", var=1.0, seed=3, out="u8",
                                                               out_u8=y), 6, "noise_gauss"),
+    # skimage random_noise('s&p', amount=0.4) + U8 cast, Philox stream (BASELINE config 3 noise)
+    "noise_sap": ("sap_var0.4 noise",
+                  lambda idn, x, y: idn.ops.random_noise(x, "s&p", amount=0.4, seed=3, out="u8",
+                                                         out_u8=y), 6, "noise_flat16"),
     # skimage random_noise('poisson') + U8 cast, Philox stream (BASELINE config 5 noise type)
     "noise_poisson": ("poisson noise",
                       lambda idn, x, y: idn.ops.random_noise(x, "poisson", seed=3, out="u8",
@@ -58,11 +62,12 @@ OPS = {
     "quant7": ("quant k=7", lambda idn, x, y: idn.ops.quantize(x, 7, seed=3, out=y), 6, "quant_"),
 }
 # arithmetic type each op computes in (the filters are integer SWAR / fixed point)
-DTYPE = {"noise_gaussian": "f64", "noise_poisson": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
+DTYPE = {"noise_gaussian": "f64", "noise_sap": "f64", "noise_poisson": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
          "cfg2f": "f64", "cfg2p": "f64", "wavelet_bior15": "f64", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
          "cfg3": "f64", "cfg4": "f64", "cfg5": "f64"}
 PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
           "noise_poisson": "skimage random_noise('poisson') law (bit-exact under replay)",
+          "noise_sap": "skimage random_noise('s&p') law (bit-exact under replay)",
           "wavelet_haar3": "skimage 0.14 denoise_wavelet within 1e-5",
           "bilateral": "cv2.bilateralFilter within 1 LSB",
           "cfg2": "Philox noise + cv2.blur bit-exact", "cfg3": "Philox s&p + cv2.medianBlur bit-exact",
@@ -187,6 +192,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "bilateral": lambda a: oracle.cv.bilateral_filter(a, 9, 75.0, 75.0),
         "noise_gaussian": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_gaussian(
             a, np.random.normal(0.0, 1.0, a.shape))),
+        "noise_sap": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_sap(
+            a, np.random.random_sample(a.shape), np.random.random_sample(a.shape), 0.4)),
         "noise_poisson": lambda a: oracle.sk.to_u8(255 * oracle.sk.noise_poisson(
             a[0], np.random.poisson(oracle.sk.poisson_lambda(a[0])))),
         "wavelet_haar3": lambda a: oracle.sk.to_u8(255 * oracle.wavelet.denoise_wavelet(a[0], "db1", 3)),
@@ -217,7 +224,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         el = time.perf_counter() - t0
         if el >= budget_s or n_img >= 20000:
             break
-    if op in ("noise_gaussian", "noise_poisson", "wavelet_haar3", "cfg5", "wavelet_bior15"):
+    if op in ("noise_gaussian", "noise_sap", "noise_poisson", "wavelet_haar3", "cfg5",
+              "wavelet_bior15"):
         threads, src = 1, "numpy, single thread"
     elif op in ("cfg2", "cfg2f", "cfg2p", "cfg3", "cfg4"):
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))

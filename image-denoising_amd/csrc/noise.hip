@@ -688,7 +688,7 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       a.p0 = p0 / (p0 + (1.0 - p0));
       a.p1 = p1 / (p1 + (1.0 - p1));
       if (flat) {
-        // 32-bit uniform thresholds: P(u < t / 2^32) within 2^-32 of cdf0
+        // 16-bit uniform thresholds: P(u < t / 2^16) within 2^-16 of cdf0
         const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
         hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SAP>, grid, dim3(256), 0, st, a,
                            sap_threshold(a.p0), sap_threshold(a.p1));

@@ -51,8 +51,9 @@ __device__ __forceinline__ void normal8_16(const u32x4& r, float (&z)[8]) {
 // element index): the flat16 stream --
 //   gaussian / speckle  counter (e/8, 0, image id) -> Philox4x32-7 -> 8 16-bit uniforms -> four
 //                       Box-Muller pairs -> the 8 normals of elements 8q..8q+7
-//   s&p                 counter (e/2, 1, image id) -> (U1, U2) of elements 2q and 2q+1 as 32-bit
-//                       uniforms compared against integer thresholds (|P - p| < 2^-32)
+//   s&p                 counter (e/4, 1, image id) -> Philox4x32-7 -> word b holds (U1, U2) of
+//                       element 4q+b as 16-bit uniforms compared against integer thresholds
+//                       (|P - p| < 2^-16); round 1 spent one Philox4x32-10 block per 2 elements
 // MEAN0: mean == 0.0, so mean + sd*z is sd*z exactly up to the sign of a zero, which the
 // following x + n / x + x*n (x >= 0) cannot see: one float64 add per element less.
 // Returns the U8 bytes; `of` (nullable) receives the 16 float64 values.
@@ -67,17 +68,15 @@ __device__ __forceinline__ v4u noise16_u8(const v4u raw, uint32_t chunk, uint64_
   for (int k = 0; k < 4; ++k) {  // elements 4k .. 4k+3
     double outv[4];
     if constexpr (KIND == IDN_NOISE_SAP) {
+      // one Philox4x32-7 block per 4 elements (e / 4 = chunk * 4 + k): element b takes word b,
+      // low 16 bits the `flipped` uniform, high 16 bits the `salted` one
+      const uint32_t q = chunk * 4u + (uint32_t)k;
+      const u32x4 r = philox4x32<7>(u32x4{q, 1u, (uint32_t)gimg, (uint32_t)(gimg >> 32)}, key);
+      const uint32_t wd[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-      for (int hlf = 0; hlf < 2; ++hlf) {
-        const uint32_t q = chunk * 8u + (uint32_t)(2 * k + hlf);
-        const u32x4 r = philox4x32(u32x4{q, 1u, (uint32_t)gimg, (uint32_t)(gimg >> 32)}, key);
-        const uint32_t u1[2] = {r.x, r.z}, u2[2] = {r.y, r.w};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int b = 2 * hlf + j;
-          const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
-          outv[b] = u1[j] < t_flip ? (u2[j] < t_salt ? 1.0 : 0.0) : xv;
-        }
+      for (int b = 0; b < 4; ++b) {
+        const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
+        outv[b] = (wd[b] & 0xFFFFu) < t_flip ? ((wd[b] >> 16) < t_salt ? 1.0 : 0.0) : xv;
       }
     } else {
       // one Philox4x32-7 block -> 8 16-bit uniforms -> 4 Box-Muller pairs -> 8 normals, for
@@ -106,10 +105,10 @@ __device__ __forceinline__ v4u noise16_u8(const v4u raw, uint32_t chunk, uint64_
   return v4u{o[0], o[1], o[2], o[3]};
 }
 
-// 32-bit uniform thresholds of the s&p flat stream: P(u < t / 2^32) within 2^-32 of cdf0
+// 16-bit uniform thresholds of the s&p flat stream: P(u < t / 2^16) within 2^-16 of cdf0
 inline uint32_t sap_threshold(double pp) {
-  const double t = ceil(pp * 4294967296.0);
-  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  const double t = ceil(pp * 65536.0);
+  return t <= 0.0 ? 0u : t >= 65536.0 ? 65536u : (uint32_t)t;
 }
 
 }  // namespace idn
