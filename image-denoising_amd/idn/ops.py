@@ -703,3 +703,52 @@ def resize_linear(x: torch.Tensor, fx: float, fy: float) -> torch.Tensor:
                                                  float(fx), float(fy), _stream()),
                "idn_resize_linear_f32")
     return _finish(y, sq)
+
+
+# ---- decode front-end (cv2.imread: lib/model/test.py:191, minibatch.py:85) ------------------
+def _file_ptrs(files):
+    bufs = [bytes(f) for f in files]
+    ptrs = (ctypes.c_void_p * len(bufs))(
+        *[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value for b in bufs])
+    lens = (ctypes.c_size_t * len(bufs))(*[len(b) for b in bufs])
+    return bufs, ptrs, lens
+
+
+def jpeg_info(data: bytes) -> Tuple[int, int, int]:
+    """(height, width, components) of a JPEG held in memory; IdnError if the decoder does not
+    take it (progressive, arithmetic, CMYK, ...)."""
+    lib = _lib.load()
+    h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    buf = bytes(data)
+    _lib.check(lib.idn_jpeg_info(ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p), len(buf),
+                                 ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)),
+               "idn_jpeg_info")
+    return h.value, w.value, c.value
+
+
+def jpeg_decode(files, out: Optional[torch.Tensor] = None, device=None) -> torch.Tensor:
+    """cv2.imread(path) for a batch of same-size baseline JPEG files (bytes in host memory):
+    (n, h, w, 3) uint8 BGR on the GPU, bit-exact with libjpeg's default decode."""
+    files = list(files)
+    if not files:
+        raise ValueError("jpeg_decode: no files")
+    h, w, _ = jpeg_info(files[0])
+    n = len(files)
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if out is None:
+        out = torch.empty((n, h, w, 3), dtype=torch.uint8, device=dev)
+    elif (out.dtype != torch.uint8 or tuple(out.shape) != (n, h, w, 3) or not out.is_contiguous()
+          or out.device.type != "cuda"):
+        raise ValueError("jpeg_decode: out must be a contiguous (n, h, w, 3) uint8 CUDA tensor")
+    lib = _lib.load()
+    bufs, ptrs, lens = _file_ptrs(files)
+    ws_bytes = lib.idn_jpeg_workspace_size(ptrs, lens, n)
+    if ws_bytes == 0:
+        raise _lib.IdnError("jpeg_decode: unsupported or corrupt JPEG in the batch")
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=out.device)
+    with torch.cuda.device(out.device):
+        rc = lib.idn_jpeg_decode_u8(ptrs, lens, n, out.data_ptr(), h, w, w * 3, ws.data_ptr(),
+                                    ws_bytes, _stream())
+    _lib.check(rc, "idn_jpeg_decode_u8")
+    del bufs
+    return out

@@ -282,6 +282,22 @@ int idn_blob_from_f64(const double* src, float* blob, int n, int h, int w, int o
 int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int c, int out_h,
                           int out_w, double fx, double fy, void* stream);
 
+/* ---- decode front-end (cv2.imread: lib/model/test.py:191, minibatch.py:85) --------------- */
+
+/* Header of one JPEG file in host memory (SOI .. SOS): height, width, components (1 or 3).
+ * IDN_EUNSUPPORTED for anything the decoder does not take (progressive, arithmetic, 12-bit,
+ * CMYK / Adobe RGB, multi-scan, chroma sampling other than 4:4:4 / 4:2:2 / 4:2:0). */
+int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
+/* device workspace for decoding these files (0 if any is unsupported) */
+size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n);
+/* cv2.imread(path) (IMREAD_COLOR) of n baseline JPEG files held in host memory, all h x w, into
+ * the device u8 BGR NHWC batch dst (row_stride bytes per row): libjpeg's default decode (ISLOW
+ * IDCT, fancy upsampling, integer YCbCr tables) -- bit-exact with PIL / libjpeg-turbo.  The
+ * entropy-coded segments are copied to the workspace in one transfer; synchronous on `stream`. */
+int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* lens, int n, uint8_t* dst,
+                       int h, int w, int64_t row_stride, void* workspace, size_t ws_bytes,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,61 @@
+"""Fixtures for the GPU JPEG decode front-end (tests/test_jpeg*.py).
+
+* the reference's own sample images, copied as data: /root/reference/data/demo/*.jpg (VOC, 500x375,
+  baseline 4:2:0) -> tests/golden/jpeg/demo_*.jpg
+* synthetic files written by Pillow 12.2 (libjpeg-turbo 3.x encoder) covering what the decoder
+  takes: 4:2:0 / 4:2:2 / 4:4:4, grayscale, restart intervals (per row and every 3 MCUs), odd sizes,
+  quality 10 .. 100, optimised Huffman tables, and a progressive file the decoder must reject.
+
+The expected pixels are PIL's own decode of each file, made at test time (same library on the GPU
+box): cv2.imread and PIL both decode with libjpeg(-turbo) defaults (ISLOW IDCT, fancy upsampling).
+
+  python tests/golden/make_jpeg_fixtures.py
+"""
+import io
+import shutil
+from pathlib import Path
+
+import numpy as np
+from PIL import Image
+
+OUT = Path(__file__).resolve().parent / "jpeg"
+DEMO = Path("/root/reference/data/demo")
+
+
+def textured(h, w, seed):
+    rs = np.random.RandomState(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = 128 + 60 * np.sin(x / 17.0 + seed) * np.cos(y / 23.0) + rs.normal(0, 18, (h, w))
+    img = np.stack([base, np.roll(base, 7, 1) * 0.8 + 30, 255 - base], -1)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def save(name, arr, **kw):
+    b = io.BytesIO()
+    Image.fromarray(arr).save(b, "JPEG", **kw)
+    (OUT / name).write_bytes(b.getvalue())
+
+
+def main():
+    OUT.mkdir(exist_ok=True)
+    if DEMO.is_dir():
+        for f in sorted(DEMO.glob("*.jpg")):
+            shutil.copyfile(f, OUT / f"demo_{f.name}")
+    save("s420_q90_600x1000.jpg", textured(600, 1000, 1), quality=90, subsampling=2)
+    save("s420_q75_odd_37x53.jpg", textured(37, 53, 2), quality=75, subsampling=2)
+    save("s422_q85_120x200.jpg", textured(120, 200, 3), quality=85, subsampling=1)
+    save("s444_q95_96x128.jpg", textured(96, 128, 4), quality=95, subsampling=0)
+    save("s420_q100_64x80.jpg", textured(64, 80, 5), quality=100, subsampling=2)
+    save("s420_q10_75x99.jpg", textured(75, 99, 6), quality=10, subsampling=2)
+    save("s420_opt_130x170.jpg", textured(130, 170, 7), quality=80, subsampling=2, optimize=True)
+    save("s420_rstrow_120x160.jpg", textured(120, 160, 8), quality=80, subsampling=2,
+         restart_marker_rows=1)
+    save("s444_rst3_70x90.jpg", textured(70, 90, 9), quality=85, subsampling=0,
+         restart_marker_blocks=3)
+    save("gray_q80_91x77.jpg", textured(91, 77, 10)[..., 0], quality=80)
+    save("gray_rst2_48x64.jpg", textured(48, 64, 11)[..., 0], quality=70, restart_marker_blocks=2)
+    save("progressive_64x64.jpg", textured(64, 64, 12), quality=80, progressive=True)
+
+
+if __name__ == "__main__":
+    main()
