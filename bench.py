@@ -64,7 +64,7 @@ OPS = {
 # arithmetic type each op computes in (the filters are integer SWAR / fixed point)
 DTYPE = {"noise_gaussian": "f64", "noise_sap": "f64", "noise_poisson": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
          "cfg2f": "f64", "cfg2p": "f64", "wavelet_bior15": "f64", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
-         "cfg3": "f64", "cfg4": "f64", "cfg5": "f64"}
+         "cfg3": "f64", "cfg4": "f64", "cfg5": "f64", "jpeg_decode": "i32"}
 PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
           "noise_poisson": "skimage random_noise('poisson') law (bit-exact under replay)",
           "noise_sap": "skimage random_noise('s&p') law (bit-exact under replay)",
@@ -77,7 +77,8 @@ PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under rep
           "quant7": "OpenCV 8-bit Lab + k-means (sklearn-replay bit-exact; device fit within 5% "
                     "inertia)",
           "cfg4": "Philox speckle + cv2.bilateralFilter within 1 LSB",
-          "cfg5": "Philox/periodic noise + denoise_wavelet within 1e-5"}
+          "cfg5": "Philox/periodic noise + denoise_wavelet within 1e-5",
+          "jpeg_decode": "libjpeg(-turbo) default decode (ISLOW, fancy upsampling), bit-exact vs PIL"}
 
 def _pipeline(kind):
     """BASELINE.json configs 2-5 as one step = noise + denoise over the batch (intermediate u8
@@ -159,6 +160,32 @@ def _gauss5_blob(idn, x, y):
 
 OPS["gauss5_blob"] = (OPS["gauss5_blob"][0], _gauss5_blob, 15, "stencil_u8")
 
+
+def _jpeg_files(x, quality=90):
+    """the batch encoded once (untimed) by Pillow: baseline 4:2:0 JPEG files in host memory"""
+    import io
+    from PIL import Image
+    arr = x.cpu().numpy()
+    out = []
+    for im in arr:
+        b = io.BytesIO()
+        Image.fromarray(im[..., ::-1]).save(b, "JPEG", quality=quality, subsampling=2)
+        out.append(b.getvalue())
+    return out
+
+
+def _jpeg_decode(idn, x, y):
+    st = _jpeg_decode.__dict__
+    if st.get("n") != x.shape[0]:
+        st["files"] = _jpeg_files(x)
+        st["n"] = x.shape[0]
+    idn.ops.jpeg_decode(st["files"], out=y)
+
+
+# cv2.imread of the batch's JPEG files (host memory -> one H2D copy -> GPU decode), q90 4:2:0
+OPS["jpeg_decode"] = ("JPEG decode (cv2.imread), q90 4:2:0 files in host memory", _jpeg_decode, 3,
+                      "jpeg_")
+
 METRIC = "Mpix/s filtered (5\u00d75 Gaussian, 1000\u00d7600) at 1/2/4/8 GPUs; % HBM roofline"
 
 
@@ -210,6 +237,19 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "gauss5_blob": lambda a: oracle.sk.blob_f32(oracle.cv.gaussian_blur_fast(a, 5)),
     }
     table["cfg2f"] = table["cfg2p"] = table["cfg2"]
+    if op == "jpeg_decode":  # Pillow's libjpeg-turbo decode of the same kind of file
+        import io
+        from PIL import Image
+        rs0 = np.random.RandomState(3)
+        src = np.clip(128 + rs0.uniform(-64, 64, size=(H, W, C)), 0, 255).astype(np.uint8)
+        bio = io.BytesIO()
+        Image.fromarray(src).save(bio, "JPEG", quality=90, subsampling=2)
+        data = bio.getvalue()
+
+        def _pil(a):
+            with Image.open(io.BytesIO(data)) as im:
+                return np.asarray(im.convert("RGB"))
+        table["jpeg_decode"] = _pil
     fn = table.get(op)
     if fn is None:
         return None
@@ -227,6 +267,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
     if op in ("noise_gaussian", "noise_sap", "noise_poisson", "wavelet_haar3", "cfg5",
               "wavelet_bior15"):
         threads, src = 1, "numpy, single thread"
+    elif op == "jpeg_decode":
+        threads, src = 1, "PIL (libjpeg-turbo) decode, single thread"
     elif op in ("cfg2", "cfg2f", "cfg2p", "cfg3", "cfg4"):
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
         src = "numpy noise (1 thread) + oracle/filters.c OpenMP"

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace idn {
@@ -40,6 +41,13 @@ struct JpegDev {
   int dw[3], dh[3];         // downsampled component size (libjpeg downsampled_width / _height)
   uint64_t blk_off[3];      // first block of each component in the batch coefficient buffer
   uint64_t pl_off[3];       // component plane byte offset in the batch plane buffer
+  uint64_t ub_off;          // unstuffed entropy bytes (workspace), capacity scan_len + 64
+  uint32_t iv_off;          // first entry of the image's interval-start table (bits)
+  uint32_t ch_off, nchunks; // the image's chunks in the batch chunk arrays
+  uint32_t chunk_bits;
+  int bpm;                  // blocks per MCU (1 for a single-component scan)
+  uint32_t total_blocks;    // MCUs x bpm
+  uint8_t ph_comp[10], ph_dv[10], ph_dh[10];  // block of the MCU -> component, block row, column
   uint16_t q[4][64];        // quantisation tables, natural order
   uint16_t lut[4][1 << JPG_LUTB];  // [DC0, DC1, AC0, AC1]: len << 8 | symbol, 0 = longer code
   int32_t maxcode[4][18];   // libjpeg jdhuff: largest code of each length (-1: none), [17] sentinel
@@ -236,35 +244,74 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 }
 
 // ---- device: entropy decoding -----------------------------------------------------------------
-struct BitReader {
-  const uint8_t* p;
-  uint32_t pos, end;
-  uint64_t acc;  // left-aligned
-  int nb;
-  bool marker;   // hit a marker: feed zero bits (libjpeg does the same)
-  __device__ __forceinline__ void fill() {
-    while (nb <= 56) {
-      uint32_t b = 0;
-      if (!marker && pos < end) {
-        b = p[pos];
-        if (b == 0xFF) {
-          const uint32_t b2 = pos + 1 < end ? p[pos + 1] : 0xD9u;
-          if (b2 == 0x00) {
-            pos += 2;
-          } else {
-            marker = true;  // pos stays on the 0xFF
-            b = 0;
-          }
-        } else {
-          ++pos;
-        }
-      }
-      acc |= (uint64_t)b << (56 - nb);
-      nb += 8;
+// Stage 1, jpeg_unstuff_kernel (one workgroup per image): the entropy-coded segment without its
+// stuffed 0x00 bytes, fill bytes and RST markers, and the bit offset where each restart interval
+// starts.  The decoders then read a plain big-endian bit string.
+//
+// Stage 2, images without restart markers: the scan is cut into JPG_CHUNK-bit chunks, one thread
+// each, decoded in parallel by self-synchronisation (Huffman codes and the block structure
+// resynchronise: from an arbitrary start state a trajectory joins the true one after ~0.8 kbit
+// median, 9 kbit max on the test images).  A decoder state is (bit position, block of the MCU,
+// coefficient index z; z = 0: a DC symbol is next).
+//   pass A   every chunk from (its first bit, block 0, z 0)              -> end state
+//   pass B   every chunk from its predecessor's end state, repeated until no end state changes
+//            (chunk 0 starts from the true state, so the chain is then exact by induction); the
+//            final pass also counts the chunk's DC symbols and per-component DC differences
+//   prefix   per image: each chunk's first block index and DC predictors
+//   write    every chunk again from its exact start state, writing coefficient blocks
+// Images with restart markers: one thread per restart interval (true start state known).
+constexpr int JPG_CHUNK = 4096;  // default bits per chunk (IDN_JPEG_CHUNK overrides; measured
+                                 // 256 x 600x1000 q90: 2048 11.9, 4096 10.4, 8192 11.8 ms)
+
+__device__ __forceinline__ uint32_t jpg_be32(const uint8_t* __restrict__ p) {
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+  return __builtin_bswap32(w);
+}
+
+// reads a plain big-endian bit string (16-byte aligned, zero padded >= 48 bytes): the words of
+// the current 16-byte group in registers, the next group's load already in flight (a chain of
+// dependent loads per symbol made the decode latency-bound: 2100 cycles per symbol)
+struct BitStream {
+  const uint4* g;  // 16-byte groups
+  uint64_t acc;    // left-aligned
+  int nb, idx;
+  uint32_t gi;
+  uint32_t buf[4];
+  uint4 pre;
+  __device__ __forceinline__ void take(const uint4 v) {
+    buf[0] = __builtin_bswap32(v.x);
+    buf[1] = __builtin_bswap32(v.y);
+    buf[2] = __builtin_bswap32(v.z);
+    buf[3] = __builtin_bswap32(v.w);
+  }
+  __device__ __forceinline__ uint32_t word() {
+    const uint32_t w = idx == 0 ? buf[0] : idx == 1 ? buf[1] : idx == 2 ? buf[2] : buf[3];
+    if (++idx == 4) {
+      take(pre);
+      pre = g[++gi + 1];
+      idx = 0;
+    }
+    return w;
+  }
+  __device__ __forceinline__ void start(const uint8_t* base, uint32_t pos) {
+    g = reinterpret_cast<const uint4*>(base);
+    const uint32_t wi = pos >> 5;
+    gi = wi >> 2;
+    idx = (int)(wi & 3);
+    take(g[gi]);
+    pre = g[gi + 1];
+    const uint32_t w0 = word(), w1 = word();
+    acc = ((uint64_t)w0 << 32 | w1) << (pos & 31);
+    nb = 64 - (int)(pos & 31);
+  }
+  __device__ __forceinline__ void refill() {
+    if (nb < 32) {
+      acc |= (uint64_t)word() << (32 - nb);
+      nb += 32;
     }
   }
-  __device__ __forceinline__ uint32_t bits(int s) {  // s <= 16, nb >= s
-    const uint32_t r = (uint32_t)(acc >> (64 - s));
+  __device__ __forceinline__ uint32_t bits(int s) {
+    const uint32_t r = s ? (uint32_t)(acc >> (64 - s)) : 0u;
     acc <<= s;
     nb -= s;
     return r;
@@ -275,119 +322,372 @@ __device__ __forceinline__ int jpg_extend(uint32_t v, int s) {  // HUFF_EXTEND
   return (int)v < (1 << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v;
 }
 
-// one Huffman symbol (nb >= 16 on entry)
-__device__ __forceinline__ int jpg_decode(BitReader& br, const uint16_t* __restrict__ lut,
-                                          const int32_t* __restrict__ maxcode,
-                                          const int32_t* __restrict__ valoff,
-                                          const uint8_t* __restrict__ huffval) {
-  const uint32_t e = lut[br.acc >> (64 - JPG_LUTB)];
-  if (e) {
-    br.acc <<= e >> 8;
-    br.nb -= e >> 8;
-    return e & 0xFF;
-  }
-  int l = JPG_LUTB + 1;
-  int32_t code = (int32_t)(br.acc >> (64 - l));
-  while (code > maxcode[l]) {
-    ++l;
-    code = (int32_t)(br.acc >> (64 - l));
-  }
-  if (l > 16) {  // corrupt data: libjpeg warns and returns 0
-    br.acc <<= 16;
-    br.nb -= 16;
-    return 0;
-  }
-  br.acc <<= l;
-  br.nb -= l;
-  return huffval[(valoff[l] + code) & 0xFF];
-}
-
 struct JpegLds {
   uint16_t lut[4][1 << JPG_LUTB];
   int32_t maxcode[4][18], valoff[4][18];
   uint8_t huffval[4][256];
 };
 
-__global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegDev* __restrict__ imgs,
-                                                       const uint8_t* __restrict__ scans,
-                                                       int16_t* __restrict__ coef) {
-  __shared__ JpegLds T;
-  const JpegDev& D = imgs[blockIdx.x];
-  {  // tables into LDS
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(&D.lut[0][0]);
-    uint32_t* d = reinterpret_cast<uint32_t*>(&T.lut[0][0]);
-    for (int k = threadIdx.x; k < (int)(sizeof(T.lut) / 4); k += 64) d[k] = s[k];
-    for (int k = threadIdx.x; k < 4 * 18; k += 64) {
-      (&T.maxcode[0][0])[k] = (&D.maxcode[0][0])[k];
-      (&T.valoff[0][0])[k] = (&D.valoff[0][0])[k];
+// one Huffman symbol (nb >= 32 on entry); returns the symbol and its code length in *len
+__device__ __forceinline__ int jpg_decode(const BitStream& br, const JpegLds& T, int t, int* len) {
+  const uint32_t e = T.lut[t][br.acc >> (64 - JPG_LUTB)];
+  if (e) {
+    *len = (int)(e >> 8);
+    return e & 0xFF;
+  }
+  int l = JPG_LUTB + 1;
+  int32_t code = (int32_t)(br.acc >> (64 - l));
+  while (l <= 16 && code > T.maxcode[t][l]) {
+    ++l;
+    code = (int32_t)(br.acc >> (64 - l));
+  }
+  if (l > 16) {  // not a code (only on a speculative trajectory or a corrupt file): skip 16 bits
+    *len = 16;
+    return 0;
+  }
+  *len = l;
+  return T.huffval[t][(T.valoff[t][l] + code) & 0xFF];
+}
+
+__device__ __forceinline__ void jpg_load_tables(JpegLds& T, const JpegDev& D) {
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&D.lut[0][0]);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&T.lut[0][0]);
+  for (int k = threadIdx.x; k < (int)(sizeof(T.lut) / 4); k += blockDim.x) d[k] = s[k];
+  for (int k = threadIdx.x; k < 4 * 18; k += blockDim.x) {
+    (&T.maxcode[0][0])[k] = (&D.maxcode[0][0])[k];
+    (&T.valoff[0][0])[k] = (&D.valoff[0][0])[k];
+  }
+  for (int k = threadIdx.x; k < 4 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&D.huffval[0][0])[k];
+}
+
+// decoder state packed in 64 bits: bit position | block of the MCU << 32 | z << 40
+__device__ __forceinline__ uint64_t jpg_state(uint32_t pos, uint32_t ph, uint32_t z) {
+  return (uint64_t)pos | (uint64_t)ph << 32 | (uint64_t)z << 40;
+}
+
+struct ChunkOut {
+  uint32_t nblk;
+  int32_t dcsum[3];
+};
+
+// the per-image constants jpg_run needs, loaded once into (scalar) registers: inside the symbol
+// loop a lane-indexed read of JpegDev (phase -> component -> tables) was a global load on the
+// critical path of every symbol
+struct JpgConst {
+  uint64_t phase_info;  // per block of the MCU, 6 bits: component | DC table << 2 | AC table << 4
+  uint64_t phase_pos;   // per block of the MCU, 6 bits: block row | block column << 3
+  // per-component values packed into integers and picked by shifts: selecting among fields of a
+  // local struct was turned into a lane-indexed load from a stack copy (scratch)
+  uint32_t bo0;          // first block of component 0
+  uint64_t bo12;         // first blocks of components 1, 2 relative to component 0 (32 bits each)
+  uint64_t bw;           // blocks per row, 16 bits per component
+  uint32_t vshs;         // per component 4 bits: vertical | horizontal blocks per MCU << 2
+  int mcux, bpm;
+  uint32_t total_blocks;
+};
+
+__device__ __forceinline__ JpgConst jpg_const(const JpegDev& D) {
+  JpgConst K;
+  K.phase_info = 0;
+  K.phase_pos = 0;
+  for (int p = 0; p < D.bpm; ++p) {
+    const int c = D.ph_comp[p];
+    K.phase_info |= (uint64_t)(c | D.td[c] << 2 | (2 + D.ta[c]) << 4) << (6 * p);
+    K.phase_pos |= (uint64_t)(D.ph_dv[p] | D.ph_dh[p] << 3) << (6 * p);
+  }
+  const bool one = D.ncomp == 1;
+  K.bo0 = (uint32_t)D.blk_off[0];
+  K.bo12 = (uint64_t)(uint32_t)(D.blk_off[1] - D.blk_off[0]) |
+           (uint64_t)(uint32_t)(D.blk_off[2] - D.blk_off[0]) << 32;
+  K.bw = (uint64_t)(D.bw[0] & 0xFFFF) | (uint64_t)(D.bw[1] & 0xFFFF) << 16 |
+         (uint64_t)(D.bw[2] & 0xFFFF) << 32;
+  K.vshs = 0;
+  for (int c = 0; c < 3; ++c)
+    K.vshs |= (uint32_t)((one ? 1 : D.cv[c]) | (one ? 1 : D.ch[c]) << 2) << (4 * c);
+  K.mcux = D.mcux;
+  K.bpm = D.bpm;
+  K.total_blocks = D.total_blocks;
+  return K;
+}
+
+__device__ __forceinline__ int16_t* jpg_block(const JpgConst& K, int16_t* coef, int32_t blk,
+                                              uint32_t ph, int c) {
+  if (blk < 0 || (uint32_t)blk >= K.total_blocks) return nullptr;
+  const int mcu = blk / K.bpm;
+  const int my = mcu / K.mcux, mx = mcu - my * K.mcux;
+  const uint32_t pp = (uint32_t)(K.phase_pos >> (6 * ph));
+  const uint32_t vh = K.vshs >> (4 * c);
+  const int vs = (int)(vh & 3), hs = (int)((vh >> 2) & 3);
+  const int bw = (int)((K.bw >> (16 * c)) & 0xFFFF);
+  const uint64_t bo = (uint64_t)K.bo0 + (c ? (uint32_t)(K.bo12 >> (32 * (c - 1))) : 0u);
+  const int by = my * vs + (int)(pp & 7), bx = mx * hs + (int)((pp >> 3) & 7);
+  return coef + (bo + (uint64_t)by * bw + bx) * 64;
+}
+
+// Decode symbols from state st while the next symbol starts before end_bit (and at most dc_limit
+// DC symbols).  WRITE: coefficient blocks (blk = the block in progress; a DC symbol starts blk + 1)
+// with DC predictors pred[]; else count DC symbols and DC differences.  Returns the end state.
+template <bool WRITE>
+__device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T, const uint8_t* __restrict__ ub,
+                            uint64_t st, uint32_t end_bit, ChunkOut* cnt, int32_t blk,
+                            int (&pred)[3], int16_t* __restrict__ coef,
+                            uint32_t dc_limit = 0xFFFFFFFFu) {
+  uint32_t ndc = 0;
+  uint32_t pos = (uint32_t)st, ph = (uint32_t)(st >> 32) & 0xFF, z = (uint32_t)(st >> 40) & 0xFF;
+  BitStream br;
+  br.start(ub, pos);
+  int16_t* bp = nullptr;
+  if (WRITE && z != 0) bp = jpg_block(K, coef, blk, ph, (int)(K.phase_info >> (6 * ph)) & 3);
+  int32_t s0 = 0, s1 = 0, s2 = 0, nblk = 0;
+  int p0 = pred[0], p1 = pred[1], p2 = pred[2];
+  while (pos < end_bit) {
+    br.refill();
+    const uint32_t info = (uint32_t)(K.phase_info >> (6 * ph));
+    const int c = info & 3;
+    int len;
+    if (z == 0) {  // DC
+      if (ndc == dc_limit) break;
+      ++ndc;
+      const int s = jpg_decode(br, T, (info >> 2) & 3, &len);
+      br.bits(len);
+      const int diff = s ? jpg_extend(br.bits(s), s) : 0;
+      pos += len + s;
+      if (WRITE) {
+        ++blk;
+        const int p = (c == 0 ? p0 : c == 1 ? p1 : p2) + diff;
+        if (c == 0) p0 = p;
+        else if (c == 1) p1 = p;
+        else p2 = p;
+        bp = jpg_block(K, coef, blk, ph, c);
+        if (bp) bp[0] = (int16_t)p;
+      } else {  // (selects: a dynamic index would put the sums in scratch)
+        ++nblk;
+        if (c == 0) s0 += diff;
+        else if (c == 1) s1 += diff;
+        else s2 += diff;
+      }
+      z = 1;
+    } else {
+      const int rs = jpg_decode(br, T, (info >> 4) & 3, &len);
+      br.bits(len);
+      const int r = rs >> 4, s = rs & 15;
+      pos += len + s;
+      if (s) {
+        z += r;
+        const int val = jpg_extend(br.bits(s), s);
+        if (WRITE && bp) bp[jpg_natural[min(z, 79u)]] = (int16_t)val;  // libjpeg's overrun guard
+        ++z;
+      } else if (r == 15) {
+        z += 16;
+      } else {
+        z = 64;  // EOB
+      }
+      if (z >= 64) {
+        z = 0;
+        ph = ph + 1 == (uint32_t)K.bpm ? 0 : ph + 1;
+      }
     }
-    for (int k = threadIdx.x; k < 4 * 256; k += 64) (&T.huffval[0][0])[k] = (&D.huffval[0][0])[k];
+  }
+  pred[0] = p0;
+  pred[1] = p1;
+  pred[2] = p2;
+  if (!WRITE) {
+    cnt->nblk += nblk;
+    cnt->dcsum[0] += s0;
+    cnt->dcsum[1] += s1;
+    cnt->dcsum[2] += s2;
+  }
+  return jpg_state(pos, ph, z);
+}
+
+// stage 1: unstuff (one 1024-thread workgroup per image, 16-byte tiles per thread)
+__global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const JpegDev* __restrict__ imgs,
+                                                            const uint8_t* __restrict__ scans,
+                                                            uint8_t* __restrict__ ub,
+                                                            uint32_t* __restrict__ ivstart,
+                                                            uint32_t* __restrict__ ublen) {
+  __shared__ uint32_t wsum[16], carry_s, rst_s;
+  const JpegDev& D = imgs[blockIdx.x];
+  const uint8_t* in = scans + D.scan_off;
+  uint8_t* out = ub + D.ub_off;
+  const uint32_t n = D.scan_len;
+  if (threadIdx.x == 0) {
+    carry_s = 0;
+    rst_s = 0;
+    ivstart[D.iv_off] = 0;
   }
   __syncthreads();
-  const int nint = D.nintervals;
-  const int mcus = D.mcux * D.mcuy;
-  const int per = D.restart ? D.restart : mcus;
-  for (int iv = threadIdx.x; iv < nint; iv += 64) {
-    // the interval's first byte: lane 0 starts at the scan start; other intervals start right
-    // after their RST marker (found by a forward scan: a marker is 0xFF followed by 0xD0-0xD7)
-    BitReader br;
-    br.p = scans + D.scan_off;
-    br.end = D.scan_len;
-    br.pos = 0;
-    if (iv > 0) {
-      int seen = 0;
-      uint32_t q = 0;
-      while (q + 1 < br.end) {
-        if (br.p[q] == 0xFF && br.p[q + 1] >= 0xD0 && br.p[q + 1] <= 0xD7) {
-          if (++seen == iv) {
-            q += 2;
-            break;
-          }
-          q += 2;
-        } else {
-          ++q;
-        }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t base = 0; base < n; base += 1024 * 16) {
+    const uint32_t i0 = base + threadIdx.x * 16;
+    uint32_t keep = 0;  // bit k: byte i0 + k is data
+    uint32_t rstm = 0;  // bit k: a RST marker ends at byte i0 + k
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t i = i0 + k;
+      if (i >= n) break;
+      const uint32_t b = in[i];
+      const uint32_t pv = i > 0 ? in[i - 1] : 0u;
+      bool kp;
+      if (pv == 0xFF && b == 0x00) {
+        kp = false;  // stuffing
+      } else if (pv == 0xFF && b >= 0xD0 && b <= 0xD7) {
+        kp = false;  // RST marker code
+        rstm |= 1u << k;
+      } else if (b == 0xFF) {
+        kp = i + 1 < n && in[i + 1] == 0x00;  // data 0xFF (stuffed); else fill / marker prefix
+      } else {
+        kp = true;
       }
-      br.pos = q;
+      if (kp) keep |= 1u << k;
     }
-    br.acc = 0;
-    br.nb = 0;
-    br.marker = false;
-    int pred[3] = {0, 0, 0};
-    const int m0 = iv * per, m1 = min(m0 + per, mcus);
-    for (int m = m0; m < m1; ++m) {
-      const int my = m / D.mcux, mx = m - my * D.mcux;
-      for (int c = 0; c < D.ncomp; ++c) {
-        const int hs = D.ncomp == 1 ? 1 : D.ch[c], vs = D.ncomp == 1 ? 1 : D.cv[c];
-        const int dct = D.td[c], act = 2 + D.ta[c];
-        for (int v = 0; v < vs; ++v)
-          for (int hh = 0; hh < hs; ++hh) {
-            const int by = my * vs + v, bx = mx * hs + hh;
-            int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
-            br.fill();
-            int s = jpg_decode(br, T.lut[dct], T.maxcode[dct], T.valoff[dct], T.huffval[dct]);
-            int diff = 0;
-            if (s) diff = jpg_extend(br.bits(s), s);
-            pred[c] += diff;
-            blk[0] = (int16_t)pred[c];
-            for (int k = 1; k < 64; ++k) {
-              br.fill();
-              const int rs = jpg_decode(br, T.lut[act], T.maxcode[act], T.valoff[act], T.huffval[act]);
-              const int r = rs >> 4;
-              s = rs & 15;
-              if (s) {
-                k += r;
-                const int val = jpg_extend(br.bits(s), s);
-                if (k < 64) blk[jpg_natural[k]] = (int16_t)val;
-              } else {
-                if (r != 15) break;  // EOB
-                k += 15;
-              }
-            }
-          }
+    // block-wide exclusive scan of kept-byte counts
+    const uint32_t cntk = __popc(keep);
+    uint32_t inc = cntk;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int k = 0; k < wv; ++k) wbase += wsum[k];
+    uint32_t total = 0;
+    for (int k = 0; k < 16; ++k) total += wsum[k];
+    uint32_t o = carry_s + wbase + inc - cntk;
+    // RST markers: the next interval starts at the unstuffed position after this byte
+    uint32_t orank = 0;
+    {
+      const uint32_t nr = __popc(rstm);
+      uint32_t rinc = nr;
+      for (int q = 1; q < 64; q <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)rinc, q);
+        if (lane >= q) rinc += t;
       }
+      __syncthreads();
+      if (lane == 63) wsum[wv] = rinc;
+      __syncthreads();
+      uint32_t rbase = 0;
+      for (int k = 0; k < wv; ++k) rbase += wsum[k];
+      orank = rst_s + rbase + rinc - nr;
+      uint32_t rt = 0;
+      for (int k = 0; k < 16; ++k) rt += wsum[k];
+      __syncthreads();
+      if (threadIdx.x == 0) rst_s += rt;
     }
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t i = i0 + k;
+      if (i >= n) break;
+      if (keep >> k & 1u) out[o++] = in[i];
+      if ((rstm >> k & 1u) && orank + 1 < (uint32_t)D.nintervals)
+        ivstart[D.iv_off + 1 + orank++] = o * 8u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s += total;
+    __syncthreads();
   }
+  // zero padding behind the data (the bit readers prefetch up to 40 bytes ahead)
+  const uint32_t len = carry_s;
+  if (threadIdx.x < 64) out[len + threadIdx.x] = 0;
+  if (threadIdx.x == 0) ublen[blockIdx.x] = len;
+}
+
+// stage 2a/2b: sync passes.  grid (max chunks per image, n).  PASS_A: start from the chunk's
+// own first bit; else from the predecessor's end state in `prev` (chunk 0: the true start).
+template <bool PASS_A>
+__global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict__ imgs,
+                                                       const uint8_t* __restrict__ ub,
+                                                       const uint32_t* __restrict__ ublen,
+                                                       const uint64_t* __restrict__ prev,
+                                                       uint64_t* __restrict__ next,
+                                                       ChunkOut* __restrict__ cnt,
+                                                       uint32_t* __restrict__ changed) {
+  __shared__ JpegLds T;
+  const JpegDev& D = imgs[blockIdx.y];
+  if (D.restart || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
+  jpg_load_tables(T, D);
+  __syncthreads();
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= D.nchunks) return;
+  const uint32_t nbits = ublen[blockIdx.y] * 8u;
+  const uint32_t b0 = min(t * D.chunk_bits, nbits), b1 = min(b0 + D.chunk_bits, nbits);
+  uint64_t st;
+  if (t == 0) st = 0;
+  else if (PASS_A) st = jpg_state(b0, 0, 0);
+  else st = prev[D.ch_off + t - 1];
+  ChunkOut co{0u, {0, 0, 0}};
+  int pred[3] = {0, 0, 0};
+  // a start state past the chunk (the predecessor ran over it) ends where it starts
+  const JpgConst K = jpg_const(D);
+  const uint64_t e = ((uint32_t)st >= b1) ? st
+                                         : jpg_run<false>(K, T, ub + D.ub_off, st, b1, &co, 0, pred, nullptr);
+  next[D.ch_off + t] = e;
+  if (!PASS_A) {
+    cnt[D.ch_off + t] = co;
+    if (e != prev[D.ch_off + t]) changed[0] = 1u;
+  }
+}
+
+// stage 2c: per image, the first block index and DC predictors of every chunk
+__global__ void jpeg_prefix_kernel(const JpegDev* __restrict__ imgs,
+                                   const ChunkOut* __restrict__ cnt, ChunkOut* __restrict__ start,
+                                   int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const JpegDev& D = imgs[i];
+  if (D.restart) return;
+  ChunkOut acc{0u, {0, 0, 0}};
+  for (uint32_t t = 0; t < D.nchunks; ++t) {
+    start[D.ch_off + t] = acc;
+    const ChunkOut c = cnt[D.ch_off + t];
+    acc.nblk += c.nblk;
+    for (int k = 0; k < 3; ++k) acc.dcsum[k] += c.dcsum[k];
+  }
+}
+
+// stage 2d: write pass.  Chunks of images without restart markers (grid.x over chunks), or
+// restart intervals (one thread each) of images with them.
+__global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restrict__ imgs,
+                                                        const uint8_t* __restrict__ ub,
+                                                        const uint32_t* __restrict__ ublen,
+                                                        const uint32_t* __restrict__ ivstart,
+                                                        const uint64_t* __restrict__ states,
+                                                        const ChunkOut* __restrict__ start,
+                                                        int16_t* __restrict__ coef) {
+  __shared__ JpegLds T;
+  const JpegDev& D = imgs[blockIdx.y];
+  const uint32_t nitems = D.restart ? (uint32_t)D.nintervals : D.nchunks;
+  if (blockIdx.x * 64 >= nitems) return;  // uniform per workgroup
+  jpg_load_tables(T, D);
+  __syncthreads();
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= nitems) return;
+  const uint32_t nbits = ublen[blockIdx.y] * 8u;
+  int pred[3] = {0, 0, 0};
+  uint64_t st;
+  uint32_t b1, dc_limit = 0xFFFFFFFFu;
+  int32_t blk;
+  if (D.restart) {  // interval t: restart MCUs from its first bit, DC predictors reset
+    const uint32_t b0 = ivstart[D.iv_off + t];
+    b1 = t + 1 < nitems ? ivstart[D.iv_off + t + 1] : nbits;
+    // stop after the interval's MCUs: the bits behind them are the encoder's padding (1s)
+    const uint32_t mcu0 = t * (uint32_t)D.restart;
+    dc_limit = min((uint32_t)D.restart, (uint32_t)(D.mcux * D.mcuy) - mcu0) * D.bpm;
+    st = jpg_state(b0, 0, 0);
+    blk = (int32_t)(mcu0 * D.bpm) - 1;
+  } else {  // chunk t from its exact start state, first block index and DC predictors
+    const uint32_t b0 = min(t * D.chunk_bits, nbits);
+    b1 = min(b0 + D.chunk_bits, nbits);
+    st = t == 0 ? 0ull : states[D.ch_off + t - 1];
+    const ChunkOut s0 = start[D.ch_off + t];
+    pred[0] = s0.dcsum[0];
+    pred[1] = s0.dcsum[1];
+    pred[2] = s0.dcsum[2];
+    blk = (int32_t)s0.nblk - 1;
+  }
+  if ((uint32_t)st >= b1) return;
+  ChunkOut dummy{0u, {0, 0, 0}};
+  const JpgConst K = jpg_const(D);
+  jpg_run<true>(K, T, ub + D.ub_off, st, b1, &dummy, blk, pred, coef, dc_limit);
 }
 
 // ---- device: ISLOW IDCT (jidctint.c) ------------------------------------------------------------
@@ -532,20 +832,12 @@ __device__ __forceinline__ int jpg_up(const uint8_t* __restrict__ P, int pw, int
 
 __device__ __forceinline__ uint32_t jpg_clamp(int v) { return (uint32_t)min(max(v, 0), 255); }
 
-// grid (row tiles, n): one thread per pixel of 256 consecutive pixels of one image
-__global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDev* __restrict__ imgs,
-                                                         const uint8_t* __restrict__ planes,
-                                                         uint8_t* __restrict__ dst, int h, int w,
-                                                         int64_t row_stride) {
-  const JpegDev& D = imgs[blockIdx.y];
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (int64_t)h * w) return;
-  const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
-  uint8_t* o = dst + (int64_t)blockIdx.y * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3;
+__device__ __forceinline__ void jpg_pixel(const JpegDev& D, const uint8_t* __restrict__ planes,
+                                          int x, int y, uint32_t (&bgr)[3]) {
   const int pw0 = D.bw[0] * 8;
   const int Y = planes[D.pl_off[0] + (int64_t)y * pw0 + x];
   if (D.ncomp == 1) {
-    o[0] = o[1] = o[2] = (uint8_t)Y;
+    bgr[0] = bgr[1] = bgr[2] = (uint32_t)Y;
     return;
   }
   int cb, cr;
@@ -564,28 +856,63 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDev* __restri
   }
   // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert (SCALEBITS 16)
   const int xb = cb - 128, xr = cr - 128;
-  const int r = Y + ((91881 * xr + 32768) >> 16);                    // FIX(1.40200)
-  const int g = Y + ((-46802 * xr + (-22554 * xb + 32768)) >> 16);   // FIX(0.71414), FIX(0.34414)
-  const int b = Y + ((116130 * xb + 32768) >> 16);                   // FIX(1.77200)
-  o[0] = (uint8_t)jpg_clamp(b);  // BGR, as cv2.imread
-  o[1] = (uint8_t)jpg_clamp(g);
-  o[2] = (uint8_t)jpg_clamp(r);
+  const int r = Y + ((91881 * xr + 32768) >> 16);                   // FIX(1.40200)
+  const int g = Y + ((-46802 * xr + (-22554 * xb + 32768)) >> 16);  // FIX(0.71414), FIX(0.34414)
+  const int b = Y + ((116130 * xb + 32768) >> 16);                  // FIX(1.77200)
+  bgr[0] = jpg_clamp(b);  // BGR, as cv2.imread
+  bgr[1] = jpg_clamp(g);
+  bgr[2] = jpg_clamp(r);
+}
+
+// grid (tiles of 256 x 4 pixels, n): each thread 4 consecutive pixels of a row, stored as three
+// dwords when the row is dword aligned (else byte by byte)
+__global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDev* __restrict__ imgs,
+                                                         const uint8_t* __restrict__ planes,
+                                                         uint8_t* __restrict__ dst, int h, int w,
+                                                         int64_t row_stride) {
+  const JpegDev& D = imgs[blockIdx.y];
+  const int qw = (w + 3) / 4;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)h * qw) return;
+  const int y = (int)(q / qw), x0 = 4 * (int)(q - (int64_t)y * qw);
+  uint8_t* o = dst + (int64_t)blockIdx.y * h * row_stride + (int64_t)y * row_stride + (int64_t)x0 * 3;
+  uint32_t px[4][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (x0 + k < w) jpg_pixel(D, planes, x0 + k, y, px[k]);
+    else px[k][0] = px[k][1] = px[k][2] = 0u;
+  }
+  if (x0 + 4 <= w && ((uintptr_t)o & 3) == 0) {
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(o);
+    o4[0] = px[0][0] | px[0][1] << 8 | px[0][2] << 16 | px[1][0] << 24;
+    o4[1] = px[1][1] | px[1][2] << 8 | px[2][0] << 16 | px[2][1] << 24;
+    o4[2] = px[2][2] | px[3][0] << 8 | px[3][1] << 16 | px[3][2] << 24;
+  } else {
+    for (int k = 0; k < 4 && x0 + k < w; ++k)
+      for (int c = 0; c < 3; ++c) o[3 * k + c] = (uint8_t)px[k][c];
+  }
 }
 
 // ---- host: batch plan ---------------------------------------------------------------------------
 struct JpegPlan {
   std::vector<JpegDev> dev;
   std::vector<uint64_t> blk_end;
-  uint64_t scan_bytes = 0, nblk = 0, plane_bytes = 0;
-  size_t off_imgs = 0, off_blkend = 0, off_scan = 0, off_coef = 0, off_planes = 0, total = 0;
+  std::vector<size_t> scan_begin;
+  uint64_t scan_bytes = 0, nblk = 0, plane_bytes = 0, ub_bytes = 0;
+  uint32_t nintervals = 0, nchunks = 0, max_items = 1;
+  bool any_chunked = false;
+  size_t off_imgs = 0, off_blkend = 0, off_scan = 0, off_coef = 0, off_planes = 0;
+  size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_s0 = 0, off_s1 = 0, off_cnt = 0,
+         off_start = 0, off_flag = 0, total = 0;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int h, int w,
-                     JpegPlan& P, std::string* err) {
+                     JpegPlan& P, std::string* err, bool tables = true) {
   P.dev.assign(n, JpegDev{});
   P.blk_end.assign(n, 0);
+  P.scan_begin.assign(n, 0);
   for (int i = 0; i < n; ++i) {
     JpegHost J;
     if (!files[i]) return jpg_fail(err, "null file pointer");
@@ -636,8 +963,18 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       P.plane_bytes += (uint64_t)D.bw[c] * 8 * D.bh[c] * 8;
     }
     P.blk_end[i] = P.nblk;
+    D.bpm = 0;
+    for (int c = 0; c < J.ncomp; ++c)
+      for (int v = 0; v < D.cv[c]; ++v)
+        for (int hh = 0; hh < D.ch[c]; ++hh) {
+          D.ph_comp[D.bpm] = (uint8_t)c;
+          D.ph_dv[D.bpm] = (uint8_t)v;
+          D.ph_dh[D.bpm] = (uint8_t)hh;
+          ++D.bpm;
+        }
+    D.total_blocks = (uint32_t)mcus * D.bpm;
     for (int t = 0; t < 4; ++t) memcpy(D.q[t], J.q[t], sizeof(D.q[t]));
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 4 && tables; ++t) {
       for (int k = 0; k < 18; ++k) D.maxcode[t][k] = -1;
       const HuffSpec& H = t < 2 ? J.dc[t] : J.ac[t - 2];
       if (!H.present) continue;
@@ -646,14 +983,36 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     }
     D.scan_off = P.scan_bytes;
     D.scan_len = (uint32_t)(J.scan_end - J.scan_begin);
+    P.scan_begin[i] = J.scan_begin;
+    if ((uint64_t)D.scan_len * 8 >= 0xFFFFFFF0ull) return jpg_fail(err, "scan too large");
     P.scan_bytes += (D.scan_len + 15) & ~15u;
+    D.ub_off = P.ub_bytes;
+    P.ub_bytes += (D.scan_len + 64 + 15) & ~15u;
+    D.iv_off = P.nintervals;
+    P.nintervals += (uint32_t)D.nintervals;
+    D.ch_off = P.nchunks;
+    D.chunk_bits = (uint32_t)std::max(512, env_int("IDN_JPEG_CHUNK", JPG_CHUNK));
+    D.nchunks = D.restart ? 0u
+                          : (uint32_t)(((uint64_t)D.scan_len * 8 + D.chunk_bits - 1) / D.chunk_bits);
+    if (D.nchunks == 0 && !D.restart) D.nchunks = 1;
+    P.nchunks += D.nchunks;
+    P.any_chunked |= D.restart == 0;
+    P.max_items = std::max(P.max_items, std::max(D.nchunks, (uint32_t)D.nintervals));
   }
   P.off_imgs = 0;
   P.off_blkend = align256(P.off_imgs + sizeof(JpegDev) * (size_t)n);
   P.off_scan = align256(P.off_blkend + sizeof(uint64_t) * (size_t)n);
   P.off_coef = align256(P.off_scan + P.scan_bytes + 16);
   P.off_planes = align256(P.off_coef + P.nblk * 128);
-  P.total = align256(P.off_planes + P.plane_bytes);
+  P.off_ub = align256(P.off_planes + P.plane_bytes);
+  P.off_iv = align256(P.off_ub + P.ub_bytes);
+  P.off_ublen = align256(P.off_iv + sizeof(uint32_t) * (size_t)P.nintervals);
+  P.off_s0 = align256(P.off_ublen + sizeof(uint32_t) * (size_t)n);
+  P.off_s1 = align256(P.off_s0 + sizeof(uint64_t) * (size_t)P.nchunks);
+  P.off_cnt = align256(P.off_s1 + sizeof(uint64_t) * (size_t)P.nchunks);
+  P.off_start = align256(P.off_cnt + sizeof(ChunkOut) * (size_t)P.nchunks);
+  P.off_flag = align256(P.off_start + sizeof(ChunkOut) * (size_t)P.nchunks);
+  P.total = align256(P.off_flag + 256);
   return IDN_OK;
 }
 
@@ -677,7 +1036,7 @@ extern "C" int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* 
 extern "C" size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n) {
   if (!files || !lens || n <= 0) return 0;
   JpegPlan P;
-  if (jpeg_plan(files, lens, n, 0, 0, P, nullptr) != IDN_OK) return 0;
+  if (jpeg_plan(files, lens, n, 0, 0, P, nullptr, false) != IDN_OK) return 0;
   return P.total;
 }
 
@@ -698,31 +1057,82 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
                      P.total, ws_bytes);
   hipStream_t st = as_stream(stream);
   uint8_t* ws = static_cast<uint8_t*>(workspace);
-  // one host staging buffer -> one copy: per-image descriptors, block ends, entropy segments
-  std::vector<uint8_t> host(P.off_coef);
-  memcpy(host.data() + P.off_imgs, P.dev.data(), sizeof(JpegDev) * (size_t)n);
-  memcpy(host.data() + P.off_blkend, P.blk_end.data(), sizeof(uint64_t) * (size_t)n);
-  for (int i = 0; i < n; ++i) {
-    JpegHost J;
-    jpeg_parse(files[i], lens[i], J, nullptr);
-    memcpy(host.data() + P.off_scan + P.dev[i].scan_off, files[i] + J.scan_begin,
-           P.dev[i].scan_len);
+  // one pinned host staging buffer (kept per thread, grown as needed; the call is synchronous, so
+  // the next call may reuse it) -> one copy: descriptors, block ends, entropy segments
+  static thread_local uint8_t* pin = nullptr;
+  static thread_local size_t pin_cap = 0;
+  if (pin_cap < P.off_coef) {
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pin_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&pin), P.off_coef, 0) != hipSuccess)
+      return set_error(IDN_EHIP, "idn_jpeg_decode_u8: pinned staging alloc failed");
+    pin_cap = P.off_coef;
   }
-  if (hipMemcpyAsync(ws, host.data(), host.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+  uint8_t* host = pin;
+  memcpy(host + P.off_imgs, P.dev.data(), sizeof(JpegDev) * (size_t)n);
+  memcpy(host + P.off_blkend, P.blk_end.data(), sizeof(uint64_t) * (size_t)n);
+  {  // the entropy segments, copied by a few host threads
+    const int nt = std::max(1, std::min(8, n / 8));
+    auto part = [&](int k) {
+      for (int i = k; i < n; i += nt)
+        memcpy(host + P.off_scan + P.dev[i].scan_off, files[i] + P.scan_begin[i],
+               P.dev[i].scan_len);
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < nt; ++k) th.emplace_back(part, k);
+    part(0);
+    for (auto& t : th) t.join();
+  }
+  if (hipMemcpyAsync(ws, host, P.off_coef, hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemsetAsync(ws + P.off_coef, 0, P.nblk * 128, st) != hipSuccess)
     return set_error(IDN_EHIP, "idn_jpeg_decode_u8: staging copy failed");
   const JpegDev* dimg = reinterpret_cast<const JpegDev*>(ws + P.off_imgs);
   int16_t* coef = reinterpret_cast<int16_t*>(ws + P.off_coef);
-  hipLaunchKernelGGL(jpeg_huff_kernel, dim3(n), dim3(64), 0, st, dimg, ws + P.off_scan, coef);
+  uint8_t* ub = ws + P.off_ub;
+  uint32_t* ivs = reinterpret_cast<uint32_t*>(ws + P.off_iv);
+  uint32_t* ublen = reinterpret_cast<uint32_t*>(ws + P.off_ublen);
+  uint64_t* S[2] = {reinterpret_cast<uint64_t*>(ws + P.off_s0),
+                    reinterpret_cast<uint64_t*>(ws + P.off_s1)};
+  ChunkOut* cnt = reinterpret_cast<ChunkOut*>(ws + P.off_cnt);
+  ChunkOut* cstart = reinterpret_cast<ChunkOut*>(ws + P.off_start);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(ws + P.off_flag);
+  hipLaunchKernelGGL(jpeg_unstuff_kernel, dim3(n), dim3(1024), 0, st, dimg, ws + P.off_scan, ub,
+                     ivs, ublen);
+  const dim3 gitems((P.max_items + 63) / 64, n);
+  int cur = 0;
+  if (P.any_chunked) {
+    // pass A, then pass B until no chunk's end state changes (typically twice)
+    hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
+                       S[0], cnt, flag);
+    for (uint32_t it = 0;; ++it) {
+      if (hipMemsetAsync(flag, 0, 4, st) != hipSuccess)
+        return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
+      hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
+                         S[cur], S[cur ^ 1], cnt, flag);
+      cur ^= 1;
+      uint32_t changed = 0;
+      if (hipMemcpyAsync(&changed, flag, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return set_error(IDN_EHIP, "idn_jpeg_decode_u8: sync pass failed");
+      if (!changed) break;
+      if (it > P.max_items + 2)
+        return set_error(IDN_EHIP, "idn_jpeg_decode_u8: entropy decoding did not converge");
+    }
+    hipLaunchKernelGGL(jpeg_prefix_kernel, dim3((n + 63) / 64), dim3(64), 0, st, dimg, cnt,
+                       cstart, n);
+  }
+  hipLaunchKernelGGL(jpeg_write_kernel, gitems, dim3(64), 0, st, dimg, ub, ublen, ivs, S[cur],
+                     cstart, coef);
   const uint64_t gb = (P.nblk + 255) / 256;
   IDN_CHECK_ARG(gb < 0x7FFFFFFF, "idn_jpeg_decode_u8: batch too large");
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)gb), dim3(256), 0, st, dimg,
                      reinterpret_cast<const uint64_t*>(ws + P.off_blkend), n, P.nblk, coef,
                      ws + P.off_planes);
-  const int64_t gx = ((int64_t)h * w + 255) / 256;
+  const int64_t gx = ((int64_t)h * ((w + 3) / 4) + 255) / 256;
   hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
                      ws + P.off_planes, dst, h, w, row_stride);
-  // the staging buffer must outlive the async copy
+  // the staging buffer is reused by the next call: finish here
   if (hipStreamSynchronize(st) != hipSuccess)
     return set_error(IDN_EHIP, "idn_jpeg_decode_u8: decode failed");
   IDN_CHECK_LAUNCH("idn_jpeg_decode_u8");

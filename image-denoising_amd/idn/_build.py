@@ -66,7 +66,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
     newest = max(o.stat().st_mtime for o in objs)
     if not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
         tmp = LIB_PATH.with_suffix(".so.tmp")
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp),
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(tmp),
                *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
