@@ -49,3 +49,16 @@ def test_size_mismatch_and_unsupported_raise(dev):
                          (JPEG / "s420_q100_64x80.jpg").read_bytes()])
     with pytest.raises(IdnError):
         ops.jpeg_decode([(JPEG / "progressive_64x64.jpg").read_bytes()])
+
+
+@pytest.mark.parametrize("chunk", ["512", "1024"])
+def test_small_chunks_stress_synchronisation(dev, monkeypatch, chunk):
+    """512-bit chunks: hundreds of chunks per file, most starting mid-symbol and mid-block; the
+    sync passes must still reach the exact trajectory (bit-exact output)"""
+    from idn import ops
+    monkeypatch.setenv("IDN_JPEG_CHUNK", chunk)
+    for p in sorted(JPEG.glob("*.jpg")):
+        if p.name.startswith("progressive"):
+            continue
+        got = ops.jpeg_decode([p.read_bytes()])[0].cpu().numpy()
+        assert np.array_equal(got, pil_bgr(p)), (chunk, p.name)
