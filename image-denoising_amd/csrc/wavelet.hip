@@ -1195,7 +1195,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_analyze(
 }
 
 template <int L>
-__global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
+__global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(3))) void wl_haar_synth(
     const uint8_t* __restrict__ src, const double* __restrict__ in64, int h, int w,
     int64_t row_stride, const double* __restrict__ stats, uint8_t* __restrict__ out_u8,
     float* __restrict__ out_f32) {
@@ -1248,30 +1248,42 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
     }
   }
   if (!act) return;
-  // level 1 per 2x2 group with the pixels' own details, colour, casts
+  // level 1 per 2x2 group with the pixels' own details, colour, casts.  A 4x4 sub-block's rows
+  // are 12 contiguous bytes: packed and stored as three dwords per row (single-byte stores made
+  // 14x the L2 write requests of the output bytes)
+  const bool dw =
+      QS == 2 && out_u8 && ((reinterpret_cast<uintptr_t>(out_u8) | (uintptr_t)row_stride) & 3) == 0;
+  uint32_t rowp[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
 #pragma unroll
   for (int k = 0; k < QS * QS; ++k) {
     const int qy = k / QS, qx = k % QS;
-    wreal o[2][2][3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const wreal A = a1[c][k];
-      const wreal AD = soft(d1[c][0][k], thr(c, 0, 0)), DA = soft(d1[c][1][k], thr(c, 0, 1));
-      const wreal DD = soft(d1[c][2][k], thr(c, 0, 2));
+    if (qx == 0) {
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          // inner denoise_wavelet clip (0.14.2), then * (max - min) + min
-          const double vv = fmin(fmax((double)ihaar(A, AD, DA, DD, r, s), 0.0), 1.0);
-          o[r][s][c] = vv * inv[c] + mn[c];
-        }
+        for (int j = 0; j < 3; ++j) rowp[r][j] = 0u;
+    }
+    wreal A[3], AD[3], DA[3], DD[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      A[c] = a1[c][k];
+      AD[c] = soft(d1[c][0][k], thr(c, 0, 0));
+      DA[c] = soft(d1[c][1][k], thr(c, 0, 1));
+      DD[c] = soft(d1[c][2][k], thr(c, 0, 2));
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const double Y = o[r][s][0] - 16.0, Cb = o[r][s][1] - 128.0, Cr = o[r][s][2] - 128.0;
+        // one pixel at a time (three channels live): inner denoise_wavelet clip (0.14.2), then
+        // * (max - min) + min, YCbCr -> RGB, clip, cast
+        wreal o[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const double vv = fmin(fmax((double)ihaar(A[c], AD[c], DA[c], DD[c], r, s), 0.0), 1.0);
+          o[c] = vv * inv[c] + mn[c];
+        }
+        const double Y = o[0] - 16.0, Cb = o[1] - 128.0, Cr = o[2] - 128.0;
         double o3[3];
         o3[0] = dot3(Y, Cb, Cr, 0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937);
         o3[1] = dot3(Y, Cb, Cr, 0.004566210045662101, -0.0015363236860449021, -0.003188110949655707);
@@ -1281,12 +1293,27 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth(
         for (int c = 0; c < 3; ++c) {
           double vv = fmin(fmax(o3[c], 0.0), 1.0);
           if (bad) vv = 0.0;
-          if (out_u8)
+          const uint32_t u = (uint32_t)(int)(255.0 * vv);
+          if (dw) {
+            const int bi = (2 * qx + s) * 3 + c;
+            rowp[r][bi >> 2] |= u << (8 * (bi & 3));
+          } else if (out_u8) {
             out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)x * 3 + c] =
-                (uint8_t)(int)(255.0 * vv);
+                (uint8_t)u;
+          }
           if (out_f32) out_f32[(((int64_t)img * h + y) * w + x) * 3 + c] = (float)vv;
         }
       }
+    if (dw && qx == QS - 1) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        uint32_t* p = reinterpret_cast<uint32_t*>(out_u8 + (int64_t)img * h * row_stride +
+                                                  (int64_t)(y0 + 2 * qy + r) * row_stride +
+                                                  (int64_t)x0 * 3);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) p[j] = rowp[r][j];
+      }
+    }
   }
 }
 
@@ -1368,6 +1395,234 @@ __device__ __forceinline__ unsigned long long wl_dd1_eval(const Dd1Raw& q, int c
   return absbits(dd);
 }
 
+// ---- Haar statistics for u8 input (L >= 2): integer moments instead of fp64 planes ---------------
+// BayesShrink needs per (channel, level, band) the sum of squared detail coefficients, and the
+// sigma median the fine-bin codes of the finest dd.  For u8 input every Haar detail is an integer
+// combination of the pixels times a constant (the channel offsets and the minimum cancel in the
+// +-1 combinations):
+//     d(c, l) = 2^-l (w_c . D) / (255000 (max_c - min_c)),   w_c = rgb2ycbcr row c x 1000
+// with D the integer RGB vector of the band's combination.  So the sums follow from exact integer
+// second moments of D (six per band), summed in int32 per thread and in fp64 after that -- a
+// rounding-level difference from pywt's own fp64 sums, like any other summation order -- and the
+// dd codes from T = w_c . D_dd, ~25 integer / fp64 ops per pixel where wl_haar_analyze recomputes
+// the normalised fp64 planes (~100).
+// The codes must equal those of the reference's fp64 dd (the median recomputes exact values per
+// code).  Its deviation from the exact value 0.5 T / (255000 inv) is below 1e-12 / inv (rounded
+// 1/255, YCbCr dot, offset, difference and quotient, each <= 2.8e-14 absolute at magnitude <= 256,
+// then the 2x2 combination), so |dd_ref - a| <= 2e-12 / inv for the fp64 approximation a, i.e.
+// a relative 1.02e-6 / |T| <= 3.4e-7 for |T| >= 3.  When the mantissa bits below the code's four
+// are >= 2^33 away from both ends, a is >= 2^-19 (relative) from every bin edge, so the code is
+// certain.  Everything else -- T == 0 (an exact zero or a rounding residue), |T| < 3, values next
+// to an edge -- is evaluated exactly (wl_dd1_key, the median's own evaluation): queued in LDS and
+// resolved at the end of the kernel, or, past the queue, stored as WL_CODE_EXACT for wl_haar_median.
+// Channels whose range is only rounding noise (Cb / Cr of a gray image, range ~1e-14) get sums
+// that differ from the fp64 planes' (which are noise themselves); their thresholds cannot move the
+// output, which is min + v * range for such a channel.
+__device__ __forceinline__ double uniform_f64(double v) {  // a wave-uniform double into SGPRs
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)b);
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+constexpr int WLS_IT = 16;  // sub-blocks per thread (int32 moments stay below 2^31: <= 1.07e9)
+constexpr uint32_t WL_CODE_EXACT = 0xFFFFu;  // dd code left for wl_haar_median to evaluate exactly
+constexpr int WLS_XCAP = 1024;  // per-workgroup queue of uncertain codes (expected: a few)
+__device__ __forceinline__ void haar_int(int x00, int x01, int x10, int x11, int& aa, int& ad,
+                                         int& da, int& dd) {
+  const int lo0 = x00 + x10, lo1 = x01 + x11, hi0 = x00 - x10, hi1 = x01 - x11;
+  aa = lo0 + lo1;
+  ad = lo0 - lo1;
+  da = hi0 + hi1;
+  dd = hi0 - hi1;
+}
+__device__ __forceinline__ void mom_add(int (&m)[6], int r, int g, int b) {
+  m[0] += __mul24(r, r);
+  m[1] += __mul24(g, g);
+  m[2] += __mul24(b, b);
+  m[3] += __mul24(r, g);
+  m[4] += __mul24(r, b);
+  m[5] += __mul24(g, b);
+}
+__device__ __forceinline__ int ycc_w(int c, int k) {  // rgb2ycbcr coefficients x 1000
+  constexpr int W[3][3] = {{65481, 128553, 24966}, {-37797, -74203, 112000}, {112000, -93786, -18214}};
+  return W[c][k];
+}
+
+template <int L>
+__global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
+    const uint8_t* __restrict__ src, int h, int w, int64_t row_stride, wreal* __restrict__ ws,
+    size_t img_floats, size_t dd_off, const double* __restrict__ stats, double* __restrict__ part,
+    size_t part_per_img) {
+  static_assert(L == 2 || L == 3, "4x4 sub-blocks per thread");
+  using HS = HaarSplit<L>;
+  constexpr int B = HS::B;
+  const int img = blockIdx.y;
+  const int nbx = w / B, nblk = nbx * (h / B);
+  const double* st = stats + (size_t)img * WL_STATS;
+  __shared__ double red[3 * L * 3][WLH_WG / 64];
+  __shared__ uint32_t xq[WLS_XCAP];  // queued uncertain codes: position * 4 + channel
+  __shared__ uint32_t xq_n;
+  if (threadIdx.x == 0) xq_n = 0u;
+  __syncthreads();
+  const size_t W1 = (size_t)(w / 2), bsz = (size_t)(h / 2) * W1;
+  // per-channel scales, uniform: kept in SGPRs (min / range / reciprocal are re-read by the rare
+  // exact path only) -- the moments already hold 54 VGPRs
+  wreal sc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    wreal mn, mx;
+    wl_minmax64(st, c, mn, mx);
+    sc[c] = uniform_f64(0.5 / (255000.0 * (mx - mn)));
+  }
+  int mom[L][3][6];
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) mom[l][b][k] = 0;
+  const uint8_t* ib = src + (int64_t)img * h * row_stride;
+  uint16_t* cdp0 = reinterpret_cast<uint16_t*>(ws + img * img_floats + dd_off + 3 * bsz);
+  // sub-block geometry of iteration `it`; its 4 rows x 12 bytes (dword aligned: checked on the
+  // host) are loaded one iteration ahead (two waves per SIMD at this register count)
+  auto geom = [&](int it, int& sub, int& y0, int& x0) -> bool {
+    const int tid = (blockIdx.x * WLS_IT + it) * WLH_WG + threadIdx.x;
+    const int blk = tid / HS::NS;
+    sub = tid % HS::NS;
+    const int by = blk / nbx, bx = blk - by * nbx;
+    y0 = by * B + (sub >> 1) * 4;
+    x0 = bx * B + (sub & 1) * 4;
+    return blk < nblk;  // uniform over each block's NS consecutive lanes
+  };
+  auto load_q = [&](int it, uint32_t (&qq)[4][3]) {
+    int sub, y0, x0;
+    if (!geom(it, sub, y0, x0)) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + (int64_t)(y0 + r) * row_stride +
+                                                            (int64_t)x0 * 3);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
+    }
+  };
+  uint32_t qn[4][3] = {};
+  load_q(0, qn);
+#pragma unroll 1
+  for (int it = 0; it < WLS_IT; ++it) {
+    int sub, y0, x0;
+    const bool act = geom(it, sub, y0, x0);
+    uint32_t q[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) q[r][k] = qn[r][k];
+    if (it + 1 < WLS_IT) load_q(it + 1, qn);
+    int a2[3] = {0, 0, 0};
+    if (act) {
+      auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+      int a1[4][3];
+#pragma unroll
+      for (int gy = 0; gy < 2; ++gy)
+#pragma unroll
+        for (int gx = 0; gx < 2; ++gx) {
+          int D[3][3];  // band (ad, da, dd) x rgb
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch)
+            haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch),
+                     px(2 * gy + 1, 6 * gx + ch), px(2 * gy + 1, 6 * gx + 3 + ch),
+                     a1[gy * 2 + gx][ch], D[0][ch], D[1][ch], D[2][ch]);
+#pragma unroll
+          for (int b = 0; b < 3; ++b) mom_add(mom[0][b], D[b][0], D[b][1], D[b][2]);
+          const size_t cpos = (size_t)(y0 / 2 + gy) * W1 + (size_t)(x0 / 2 + gx);
+          uint32_t code[3], unsure = 0u;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int T = __mul24(ycc_w(c, 0), D[2][0]) + __mul24(ycc_w(c, 1), D[2][1]) +
+                          __mul24(ycc_w(c, 2), D[2][2]);
+            const uint32_t aT = (uint32_t)(T < 0 ? -T : T);
+            const uint32_t hi = (uint32_t)__double2hiint((double)aT * sc[c]);
+            code[c] = (uint32_t)min(max((int)(hi >> 16) - (1023 - 61) * 16, 0), WL_FBINS - 1) + 1u;
+            if (!(aT >= 3u && (hi & 0xFFFFu) - 2u <= 0xFFFBu)) unsure |= 1u << c;
+          }
+          // uncertain codes (rare) are queued for the exact evaluation after the loop, when the
+          // moments no longer hold registers; past the queue's capacity they are stored as
+          // WL_CODE_EXACT and wl_haar_median evaluates them
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            uint16_t* dst = cdp0 + (size_t)c * 4 * bsz * (sizeof(wreal) / sizeof(uint16_t)) + cpos;
+            if ((unsure >> c) & 1u) {
+              const uint32_t slot = atomicAdd(&xq_n, 1u);
+              if (slot < WLS_XCAP) xq[slot] = (uint32_t)cpos * 4u + (uint32_t)c;
+              else *dst = (uint16_t)WL_CODE_EXACT;
+            } else {
+              *dst = (uint16_t)code[c];
+            }
+          }
+        }
+      int D2[3][3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        haar_int(a1[0][ch], a1[1][ch], a1[2][ch], a1[3][ch], a2[ch], D2[0][ch], D2[1][ch],
+                 D2[2][ch]);
+#pragma unroll
+      for (int b = 0; b < 3; ++b) mom_add(mom[1][b], D2[b][0], D2[b][1], D2[b][2]);
+    }
+    if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
+      const int base = (threadIdx.x & 63) & ~3;
+      int D3[3][3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        int aa;
+        haar_int(__shfl(a2[ch], base), __shfl(a2[ch], base + 1), __shfl(a2[ch], base + 2),
+                 __shfl(a2[ch], base + 3), aa, D3[0][ch], D3[1][ch], D3[2][ch]);
+      }
+      if (act && sub == 0)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) mom_add(mom[2][b], D3[b][0], D3[b][1], D3[b][2]);
+    }
+  }
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double w0 = ycc_w(c, 0), w1 = ycc_w(c, 1), w2 = ycc_w(c, 2);
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const double s = ldexp(sc[c], -l);  // 2^-(l+1) / (255000 inv)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int* m = mom[l][b];
+        double v = w0 * w0 * (double)m[0] + w1 * w1 * (double)m[1] + w2 * w2 * (double)m[2] +
+                   2.0 * (w0 * w1 * (double)m[3] + w0 * w2 * (double)m[4] + w1 * w2 * (double)m[5]);
+        v *= s * s;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0) red[(c * L + l) * 3 + b][wave] = v;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 * L * 3) {
+    const int k = threadIdx.x, b = k % 3, l = (k / 3) % L, c = k / (3 * L);
+    double t = red[k][0];
+#pragma unroll
+    for (int wv = 1; wv < WLH_WG / 64; ++wv) t += red[k][wv];
+    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + (size_t)l * gridDim.x +
+         blockIdx.x] = t;
+  }
+  // the queued uncertain codes: exact evaluation (the median's own, wl_dd1_key)
+  const uint32_t nq = min(xq_n, (uint32_t)WLS_XCAP);
+  for (uint32_t i = threadIdx.x; i < nq; i += WLH_WG) {
+    const uint32_t e = xq[i], pos = e >> 2;
+    const int c = (int)(e & 3u);
+    wreal mnc, mxc;
+    wl_minmax64(st, c, mnc, mxc);
+    const wreal invc = mxc - mnc;
+    const unsigned long long key = wl_dd1_key<true>(src, nullptr, img, h, w, row_stride, pos,
+                                                    (int)W1, c, mnc, invc, 1.0 / invc);
+    cdp0[(size_t)c * 4 * bsz * (sizeof(wreal) / sizeof(uint16_t)) + pos] =
+        (uint16_t)(key ? (uint32_t)wl_fbin(key) + 1u : 0u);
+  }
+}
+
 constexpr int WLM_WG = 256;  // threads per (image, channel): several workgroups per CU overlap phases
 constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slower: fewer workgroups per CU)
 template <int L>
@@ -1413,6 +1668,13 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
   auto code_at = [](const uint2& g, int q) -> uint32_t {
     return ((q < 2 ? g.x : g.y) >> (16 * (q & 1))) & 0xFFFFu;
   };
+  // codes wl_haar_stats could not certify: the exact evaluation (rare)
+  auto resolve = [&](uint32_t cd, uint32_t pos) -> uint32_t {
+    if (cd != WL_CODE_EXACT) return cd;
+    const unsigned long long key =
+        wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride, pos, W1, c, mn, inv, rcp);
+    return key ? (uint32_t)wl_fbin(key) + 1u : 0u;
+  };
   for (uint32_t g0 = threadIdx.x; g0 < ngrp; g0 += 8 * WLM_WG) {
     uint2 gv[8];
 #pragma unroll
@@ -1420,16 +1682,25 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       const uint32_t g = g0 + (uint32_t)u * WLM_WG;
       gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
     }
+    uint32_t emask = 0u;  // bit 4u + q: code q of group u is uncertified
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t cd = code_at(gv[u], q);
-        if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
+        emask |= (cd == WL_CODE_EXACT ? 1u : 0u) << (4 * u + q);
+        if (cd && cd != WL_CODE_EXACT)
+          atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
       }
+    while (emask) {  // rare: the uncertified codes, one exact evaluation each
+      const int i = __builtin_ctz(emask);
+      emask &= emask - 1u;
+      const uint32_t cd = resolve(WL_CODE_EXACT, 4 * (g0 + (uint32_t)(i >> 2) * WLM_WG) + (uint32_t)(i & 3));
+      if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
+    }
   }
   for (uint32_t k = ngrp * 4 + threadIdx.x; k < bsz; k += WLM_WG) {  // tail codes
-    const uint32_t cd = codes[k];
+    const uint32_t cd = resolve(codes[k], k);
     if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
   }
   __syncthreads();
@@ -1484,13 +1755,30 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
         gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
       }
       uint32_t cnt2 = 0;
+      uint32_t emask = 0u;
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t cd = code_at(gv[u], q);
           cnt2 += (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
+          emask |= (cd == WL_CODE_EXACT ? 1u : 0u) << (4 * u + q);
         }
+      // rare: the uncertified codes by their exact evaluation, kept for the placement below
+      uint32_t xcode[2] = {0u, 0u}, xpos[2] = {0u, 0u};
+      int nx = 0;
+      for (uint32_t m = emask; m; m &= m - 1u) {
+        const int i = __builtin_ctz(m);
+        const uint32_t p = 4 * (g0 + (uint32_t)(i >> 2) * WLM_WG) + (uint32_t)(i & 3);
+        const uint32_t cd = resolve(WL_CODE_EXACT, p);
+        if (cd != csel && cd != cnext) continue;
+        cnt2 += (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
+        if (nx < 2) {
+          xcode[nx] = cd;
+          xpos[nx] = p;
+        }
+        ++nx;
+      }
       if (__ballot(cnt2 != 0) == 0) continue;  // wave-uniform
       uint32_t os, on;
       place(cnt2, os, on);
@@ -1499,16 +1787,30 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
         for (int u = 0; u < 8; ++u)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const uint32_t cd = code_at(gv[u], q);
             const uint32_t p = 4 * (g0 + (uint32_t)u * WLM_WG) + (uint32_t)q;
+            const uint32_t cd = code_at(gv[u], q);
             if (cd == csel) pos_sel[os++] = p;
             if (cd == cnext) pos_next[on++] = p;
           }
+        if (nx > 2) {  // more than two matching uncertified codes in this lane: evaluate again
+          for (uint32_t m = emask; m; m &= m - 1u) {
+            const int i = __builtin_ctz(m);
+            const uint32_t p = 4 * (g0 + (uint32_t)(i >> 2) * WLM_WG) + (uint32_t)(i & 3);
+            const uint32_t cd = resolve(WL_CODE_EXACT, p);
+            if (cd == csel) pos_sel[os++] = p;
+            if (cd == cnext) pos_next[on++] = p;
+          }
+        } else {
+          for (int k = 0; k < nx; ++k) {
+            if (xcode[k] == csel) pos_sel[os++] = xpos[k];
+            if (xcode[k] == cnext) pos_next[on++] = xpos[k];
+          }
+        }
       }
     }
     for (uint32_t k0 = ngrp * 4; k0 < bsz; k0 += WLM_WG) {  // tail codes (every lane takes part)
       const uint32_t k = k0 + threadIdx.x;
-      const uint32_t cd = k < bsz ? codes[k] : 0u;
+      const uint32_t cd = k < bsz ? resolve(codes[k], k) : 0u;
       const uint32_t cnt2 = (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
       uint32_t os, on;
       place(cnt2, os, on);
@@ -1628,10 +1930,25 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
-  const int nwg_a = (nthr + WLH_WG * WLH_IT - 1) / (WLH_WG * WLH_IT);
-  hipLaunchKernelGGL((wl_haar_analyze<L>), dim3(nwg_a, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
-                     Lt.w, row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
-                     Lt.part_per_img);
+  int nwg_a;
+  if constexpr (L >= 2) {
+    if (src && env_int("IDN_WAVELET_INTSTATS", 1)) {
+      nwg_a = (nthr + WLH_WG * WLS_IT - 1) / (WLH_WG * WLS_IT);
+      hipLaunchKernelGGL((wl_haar_stats<L>), dim3(nwg_a, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+                         row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
+                         Lt.part_per_img);
+    } else {
+      nwg_a = (nthr + WLH_WG * WLH_IT - 1) / (WLH_WG * WLH_IT);
+      hipLaunchKernelGGL((wl_haar_analyze<L>), dim3(nwg_a, n), dim3(WLH_WG), 0, st, src, in64,
+                         Lt.h, Lt.w, row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
+                         Lt.part_per_img);
+    }
+  } else {
+    nwg_a = (nthr + WLH_WG * WLH_IT - 1) / (WLH_WG * WLH_IT);
+    hipLaunchKernelGGL((wl_haar_analyze<L>), dim3(nwg_a, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
+                       Lt.w, row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
+                       Lt.part_per_img);
+  }
   WlLayout Ls = Lt;  // wl_sumsq view of the fused partials: nwg per level, levels back to back
   for (int l = 1; l <= L; ++l) {
     Ls.tiles[l] = nwg_a;
@@ -1718,6 +2035,13 @@ extern "C" size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, i
   if (n <= 0 || h <= 0 || w <= 0 || (wavelet != IDN_WAVELET_DB1 && wavelet != IDN_WAVELET_BIOR15))
     return 0;
   return wl_layout(n, h, w, wavelet, levels).bytes;
+}
+
+extern "C" size_t idn_wavelet_stats_offset(int n, int h, int w, int wavelet, int levels) {
+  using namespace idn;
+  if (n <= 0 || h <= 0 || w <= 0 || (wavelet != IDN_WAVELET_DB1 && wavelet != IDN_WAVELET_BIOR15))
+    return 0;
+  return wl_layout(n, h, w, wavelet, levels).stats_off;
 }
 
 extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,

@@ -65,6 +65,7 @@ SIGNATURES = {
     "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_i64,
                                         _c_int, _c_int, _c_vp, _c_size, _c_vp]),
     "idn_wavelet_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    "idn_wavelet_stats_offset": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "idn_gaussian_blur_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp]),
     "idn_box_blur_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp]),
     "idn_shader_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_dbl, _c_vp]),

@@ -235,6 +235,9 @@ int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* ou
                            float* out_f32, int n, int h, int w, int64_t row_stride, int wavelet,
                            int levels, void* workspace, size_t ws_bytes, void* stream);
 size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels);
+/* diagnostics: byte offset in the workspace of the per-image statistics blocks (256 doubles per
+ * image: channel sums of squared details, sigma medians, thresholds) after a call */
+size_t idn_wavelet_stats_offset(int n, int h, int w, int wavelet, int levels);
 
 /* ---- float64 filters (the reference's quirk branches blur random_noise's float64 output) -- */
 
