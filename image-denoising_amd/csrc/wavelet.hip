@@ -1413,8 +1413,11 @@ __device__ __forceinline__ unsigned long long wl_dd1_eval(const Dd1Raw& q, int c
 // a relative 1.02e-6 / |T| <= 3.4e-7 for |T| >= 3.  When the mantissa bits below the code's four
 // are >= 2^33 away from both ends, a is >= 2^-19 (relative) from every bin edge, so the code is
 // certain.  Everything else -- T == 0 (an exact zero or a rounding residue), |T| < 3, values next
-// to an edge -- is evaluated exactly (wl_dd1_key, the median's own evaluation): queued in LDS and
-// resolved at the end of the kernel, or, past the queue, stored as WL_CODE_EXACT for wl_haar_median.
+// to an edge -- is evaluated exactly (wl_dd1_key, the median's own evaluation).  Groups whose
+// pixel pairs are equal RGB triples (rows or columns) have dd exactly 0 in the reference (x - x)
+// and need no evaluation; the rest are queued in LDS and evaluated densely by the whole workgroup
+// between iterations (heavily clipped noise makes ~6 % of the codes uncertain: evaluated inline,
+// every wave would pay for them).
 // Channels whose range is only rounding noise (Cb / Cr of a gray image, range ~1e-14) get sums
 // that differ from the fp64 planes' (which are noise themselves); their thresholds cannot move the
 // output, which is min + v * range for such a channel.
@@ -1425,8 +1428,8 @@ __device__ __forceinline__ double uniform_f64(double v) {  // a wave-uniform dou
   return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 constexpr int WLS_IT = 16;  // sub-blocks per thread (int32 moments stay below 2^31: <= 1.07e9)
-constexpr uint32_t WL_CODE_EXACT = 0xFFFFu;  // dd code left for wl_haar_median to evaluate exactly
-constexpr int WLS_XCAP = 1024;  // per-workgroup queue of uncertain codes (expected: a few)
+constexpr int WLS_XMAX = WLH_WG * 12;  // uncertain codes one iteration can queue (12 per thread)
+constexpr int WLS_XCAP = 2 * WLS_XMAX;  // the queue is evaluated once more than half full
 __device__ __forceinline__ void haar_int(int x00, int x01, int x10, int x11, int& aa, int& ad,
                                          int& da, int& dd) {
   const int lo0 = x00 + x10, lo1 = x01 + x11, hi0 = x00 - x10, hi1 = x01 - x11;
@@ -1505,8 +1508,10 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
       for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
     }
   };
-  uint32_t qn[4][3] = {};
+  // two iterations of loads in flight (the kernel runs at two waves per SIMD)
+  uint32_t qn[4][3] = {}, qn2[4][3] = {};
   load_q(0, qn);
+  load_q(1, qn2);
 #pragma unroll 1
   for (int it = 0; it < WLS_IT; ++it) {
     int sub, y0, x0;
@@ -1515,8 +1520,11 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) q[r][k] = qn[r][k];
-    if (it + 1 < WLS_IT) load_q(it + 1, qn);
+      for (int k = 0; k < 3; ++k) {
+        q[r][k] = qn[r][k];
+        qn[r][k] = qn2[r][k];
+      }
+    if (it + 2 < WLS_IT) load_q(it + 2, qn2);
     int a2[3] = {0, 0, 0};
     if (act) {
       auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
@@ -1544,19 +1552,24 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
             code[c] = (uint32_t)min(max((int)(hi >> 16) - (1023 - 61) * 16, 0), WL_FBINS - 1) + 1u;
             if (!(aT >= 3u && (hi & 0xFFFFu) - 2u <= 0xFFFBu)) unsure |= 1u << c;
           }
-          // uncertain codes (rare) are queued for the exact evaluation after the loop, when the
-          // moments no longer hold registers; past the queue's capacity they are stored as
-          // WL_CODE_EXACT and wl_haar_median evaluates them
+          if (unsure) {
+            // equal RGB triples along rows or columns: the reference's dd is x - x = 0 exactly
+            auto trip = [&](int r, int k) { return px(r, k) | (px(r, k + 1) << 8) | (px(r, k + 2) << 16); };
+            const int t00 = trip(2 * gy, 6 * gx), t01 = trip(2 * gy, 6 * gx + 3);
+            const int t10 = trip(2 * gy + 1, 6 * gx), t11 = trip(2 * gy + 1, 6 * gx + 3);
+            if ((t00 == t01 && t10 == t11) || (t00 == t10 && t01 == t11)) {
+#pragma unroll
+              for (int c = 0; c < 3; ++c)
+                if ((unsure >> c) & 1u) code[c] = 0u;
+              unsure = 0u;
+            }
+          }
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            uint16_t* dst = cdp0 + (size_t)c * 4 * bsz * (sizeof(wreal) / sizeof(uint16_t)) + cpos;
-            if ((unsure >> c) & 1u) {
-              const uint32_t slot = atomicAdd(&xq_n, 1u);
-              if (slot < WLS_XCAP) xq[slot] = (uint32_t)cpos * 4u + (uint32_t)c;
-              else *dst = (uint16_t)WL_CODE_EXACT;
-            } else {
-              *dst = (uint16_t)code[c];
-            }
+            if ((unsure >> c) & 1u)  // queued: evaluated exactly below (at most 12 per thread)
+              xq[atomicAdd(&xq_n, 1u)] = (uint32_t)cpos * 4u + (uint32_t)c;
+            else
+              cdp0[(size_t)c * 4 * bsz * (sizeof(wreal) / sizeof(uint16_t)) + cpos] = (uint16_t)code[c];
           }
         }
       int D2[3][3];
@@ -1579,6 +1592,26 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
       if (act && sub == 0)
 #pragma unroll
         for (int b = 0; b < 3; ++b) mom_add(mom[2][b], D3[b][0], D3[b][1], D3[b][2]);
+    }
+    // the queued uncertain codes, densely over the workgroup, once the queue could overflow in
+    // the next iteration (and after the last one)
+    __syncthreads();
+    const uint32_t nq = xq_n;  // workgroup-uniform
+    if (nq > (uint32_t)(WLS_XCAP - WLS_XMAX) || (it == WLS_IT - 1 && nq)) {
+      for (uint32_t i = threadIdx.x; i < nq; i += WLH_WG) {
+        const uint32_t e = xq[i], pos = e >> 2;
+        const int c = (int)(e & 3u);
+        wreal mnc, mxc;
+        wl_minmax64(st, c, mnc, mxc);
+        const wreal invc = mxc - mnc;
+        const unsigned long long key = wl_dd1_key<true>(src, nullptr, img, h, w, row_stride, pos,
+                                                        (int)W1, c, mnc, invc, 1.0 / invc);
+        cdp0[(size_t)c * 4 * bsz * (sizeof(wreal) / sizeof(uint16_t)) + pos] =
+            (uint16_t)(key ? (uint32_t)wl_fbin(key) + 1u : 0u);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) xq_n = 0u;
+      __syncthreads();
     }
   }
   const int wave = threadIdx.x >> 6;
@@ -1608,18 +1641,201 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
     part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + (size_t)l * gridDim.x +
          blockIdx.x] = t;
   }
-  // the queued uncertain codes: exact evaluation (the median's own, wl_dd1_key)
-  const uint32_t nq = min(xq_n, (uint32_t)WLS_XCAP);
-  for (uint32_t i = threadIdx.x; i < nq; i += WLH_WG) {
-    const uint32_t e = xq[i], pos = e >> 2;
-    const int c = (int)(e & 3u);
-    wreal mnc, mxc;
-    wl_minmax64(st, c, mnc, mxc);
-    const wreal invc = mxc - mnc;
-    const unsigned long long key = wl_dd1_key<true>(src, nullptr, img, h, w, row_stride, pos,
-                                                    (int)W1, c, mnc, invc, 1.0 / invc);
-    cdp0[(size_t)c * 4 * bsz * (sizeof(wreal) / sizeof(uint16_t)) + pos] =
-        (uint16_t)(key ? (uint32_t)wl_fbin(key) + 1u : 0u);
+}
+
+// ---- Haar synthesis for u8 input (L >= 2) from the integer combinations -------------------------
+// The same algebra as wl_haar_stats: with s1 = 0.5 / (255000 inv) and k = 2 (off - min) / inv,
+//     level-l detail  d_l = 2^-(l-1) s1 (w_c . D_l),     level-L approximation
+//     a_L = 2^-(L-1) s1 (w_c . S_L) + 2^(L-1) k          (S_L: the integer RGB sum of the block)
+// so no normalised plane is evaluated: per coefficient three 24-bit integer multiply-adds, one
+// conversion and one multiply.  pywt's idwt2 of one 2x2 group is 0.5 (A +- AD +- DA +- DD) in
+// its four outputs; the 0.5 is folded into the coefficients and the soft thresholds (a power of
+// two commutes with soft()) and the four outputs come from a butterfly: 8 adds per group and
+// channel where ihaar takes 4 multiplies + 4 adds per output.  De-normalisation, YCbCr -> RGB and
+// the x255 cast fold into three fma chains per pixel.  Every coefficient agrees with the fp64
+// planes' to a few ulps (the error analysis of wl_haar_stats), so outputs agree to ~1e-15 and
+// the U8 cast can differ only where 255 x sits on an integer (the documented tolerance).
+__device__ __forceinline__ double tdot_sum(int c, const int (&v)[3]) {
+  // w_c . S for the non-negative block sums: Y's weights are all positive and its dot reaches
+  // 3.6e9 at level 3, past int32: two exact signed parts (<= 2.1e9 each) added in fp64 (an
+  // unsigned sum was converted as signed by the compiler).  Cb / Cr stay within +-1.9e9
+  if (c == 0)
+    return (double)(__mul24(65481, v[0]) + __mul24(24966, v[2])) + (double)__mul24(128553, v[1]);
+  return (double)(__mul24(ycc_w(c, 0), v[0]) + __mul24(ycc_w(c, 1), v[1]) +
+                  __mul24(ycc_w(c, 2), v[2]));
+}
+__device__ __forceinline__ double tdot(int c, int d0, int d1, int d2) {  // details: |T| <= 1.83e9
+  return (double)(__mul24(ycc_w(c, 0), d0) + __mul24(ycc_w(c, 1), d1) + __mul24(ycc_w(c, 2), d2));
+}
+// outputs (r, s) = (0,0), (0,1), (1,0), (1,1) of A + g_s AD + f_r DA + f_r g_s DD
+__device__ __forceinline__ void haar_bfly(double A, double AD, double DA, double DD, double (&x)[4]) {
+  const double p = A + AD, m = A - AD, q0 = DA + DD, q1 = DA - DD;
+  x[0] = p + q0;
+  x[1] = m + q1;
+  x[2] = p - q0;
+  x[3] = m - q1;
+}
+
+template <int L>
+__global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __restrict__ src, int h,
+                                                            int w, int64_t row_stride,
+                                                            const double* __restrict__ stats,
+                                                            uint8_t* __restrict__ out_u8,
+                                                            float* __restrict__ out_f32) {
+  static_assert(L == 2 || L == 3, "4x4 sub-blocks per thread");
+  using HS = HaarSplit<L>;
+  constexpr int B = HS::B;
+  const int img = blockIdx.y;
+  const int nbx = w / B, nblk = nbx * (h / B);
+  const int tid = blockIdx.x * WLH_WG + threadIdx.x;
+  const int blk = tid / HS::NS, sub = tid % HS::NS;
+  const bool act = blk < nblk;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const bool bad = st[WlStats::FLAG] != 0.0;
+  int y0 = 0, x0 = 0;
+  uint32_t q[4][3] = {};
+  if (act) {
+    const int by = blk / nbx, bx = blk - by * nbx;
+    y0 = by * B + (sub >> 1) * 4;
+    x0 = bx * B + (sub & 1) * 4;
+    const uint8_t* ib = src + (int64_t)img * h * row_stride;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + (int64_t)(y0 + r) * row_stride +
+                                                            (int64_t)x0 * 3);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) q[r][k] = p[k];
+    }
+  }
+  auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+  // integer sums of the four level-1 groups and the level-2 combinations
+  int S4[4][3];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const int gy = g >> 1, gx = g & 1;
+      S4[g][ch] = px(2 * gy, 6 * gx + ch) + px(2 * gy, 6 * gx + 3 + ch) +
+                  px(2 * gy + 1, 6 * gx + ch) + px(2 * gy + 1, 6 * gx + 3 + ch);
+    }
+  int S16[3], D2[3][3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch)
+    haar_int(S4[0][ch], S4[1][ch], S4[2][ch], S4[3][ch], S16[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
+  int S64[3] = {0, 0, 0}, D3[3][3] = {};
+  if constexpr (L == 3) {  // level 3 across the block's 4 lanes
+    const int base = (threadIdx.x & 63) & ~3;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+      haar_int(__shfl(S16[ch], base), __shfl(S16[ch], base + 1), __shfl(S16[ch], base + 2),
+               __shfl(S16[ch], base + 3), S64[ch], D3[0][ch], D3[1][ch], D3[2][ch]);
+  }
+  if (!act) return;
+  // per-channel constants (uniform: SGPRs)
+  double mnc[3], invc[3], s1c[3], kc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double mn, mx;
+    wl_minmax64(st, c, mn, mx);
+    mnc[c] = mn;
+    invc[c] = mx - mn;
+    s1c[c] = uniform_f64(0.5 / (255000.0 * invc[c]));
+    kc[c] = uniform_f64(2.0 * ((c == 0 ? 16.0 : 128.0) - mn) / invc[c]);
+  }
+  // level L .. 2 per channel -> half the level-1 approximations of the four groups
+  double Ah1[4][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double s1 = s1c[c], k = kc[c];
+    auto th = [&](int l, int b) { return 0.5 * st[WlStats::thr(c, l, b, L)]; };
+    double a2;  // level-2 approximation at this sub-block (after level-3 synthesis)
+    if constexpr (L == 3) {
+      const double Ah = tdot_sum(c, S64) * ldexp(s1, -3) + 2.0 * k;
+      const double x3 = ldexp(s1, -3);
+      double x[4];
+      haar_bfly(Ah, soft(tdot(c, D3[0][0], D3[0][1], D3[0][2]) * x3, th(2, 0)),
+                soft(tdot(c, D3[1][0], D3[1][1], D3[1][2]) * x3, th(2, 1)),
+                soft(tdot(c, D3[2][0], D3[2][1], D3[2][2]) * x3, th(2, 2)), x);
+      a2 = sub == 0 ? x[0] : sub == 1 ? x[1] : sub == 2 ? x[2] : x[3];
+    } else {
+      a2 = tdot_sum(c, S16) * ldexp(s1, -1) + 2.0 * k;
+    }
+    const double x2 = ldexp(s1, -2);
+    double x[4];
+    haar_bfly(0.5 * a2, soft(tdot(c, D2[0][0], D2[0][1], D2[0][2]) * x2, th(1, 0)),
+              soft(tdot(c, D2[1][0], D2[1][1], D2[1][2]) * x2, th(1, 1)),
+              soft(tdot(c, D2[2][0], D2[2][1], D2[2][2]) * x2, th(1, 2)), x);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) Ah1[g][c] = 0.5 * x[g];
+  }
+  // YCbCr -> RGB x 255 (skimage's ycbcr2rgb rows) on (v' * inv + min - off)
+  constexpr double R[3][3] = {{0.004566210045662101 * 255, 1.1808799897950177e-09 * 255, 0.006258928969943937 * 255},
+                              {0.004566210045662101 * 255, -0.0015363236860449021 * 255, -0.003188110949655707 * 255},
+                              {0.004566210045662101 * 255, 0.007910716233554741 * 255, 1.1977497040511743e-08 * 255}};
+  const bool dw = out_u8 && ((reinterpret_cast<uintptr_t>(out_u8) | (uintptr_t)row_stride) & 3) == 0;
+  uint32_t rowp[2][3];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int gy = g >> 1, gx = g & 1;
+    if (gx == 0) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) rowp[r][j] = 0u;
+    }
+    double v[4][3];  // the group's four pixels, three channels: v' (normalised)
+    int D[3][3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      int aa;
+      haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
+               px(2 * gy + 1, 6 * gx + 3 + ch), aa, D[0][ch], D[1][ch], D[2][ch]);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double x1 = 0.5 * s1c[c];
+      auto th = [&](int b) { return 0.5 * st[WlStats::thr(c, 0, b, L)]; };
+      double x[4];
+      haar_bfly(Ah1[g][c], soft(tdot(c, D[0][0], D[0][1], D[0][2]) * x1, th(0)),
+                soft(tdot(c, D[1][0], D[1][1], D[1][2]) * x1, th(1)),
+                soft(tdot(c, D[2][0], D[2][1], D[2][2]) * x1, th(2)), x);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i][c] = x[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = i >> 1, s = i & 1;
+      double e[3];  // clip [0, 1] (0.14.2), de-normalise, minus the YCbCr offset
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        e[c] = __fma_rn(fmin(fmax(v[i][c], 0.0), 1.0), invc[c], mnc[c] - (c == 0 ? 16.0 : 128.0));
+      const int y = y0 + 2 * gy + r, xx = x0 + 2 * gx + s;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        double o = __fma_rn(e[2], R[c][2], __fma_rn(e[1], R[c][1], e[0] * R[c][0]));
+        o = fmin(fmax(o, 0.0), 255.0);
+        if (bad) o = 0.0;
+        const uint32_t u = (uint32_t)(int)o;
+        if (dw) {
+          const int bi = (2 * gx + s) * 3 + c;
+          rowp[r][bi >> 2] |= u << (8 * (bi & 3));
+        } else if (out_u8) {
+          out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] =
+              (uint8_t)u;
+        }
+        if (out_f32) out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = (float)(o * (1.0 / 255.0));
+      }
+    }
+    if (dw && gx == 1) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        uint32_t* p = reinterpret_cast<uint32_t*>(out_u8 + (int64_t)img * h * row_stride +
+                                                  (int64_t)(y0 + 2 * gy + r) * row_stride +
+                                                  (int64_t)x0 * 3);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) p[j] = rowp[r][j];
+      }
+    }
   }
 }
 
@@ -1668,13 +1884,6 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
   auto code_at = [](const uint2& g, int q) -> uint32_t {
     return ((q < 2 ? g.x : g.y) >> (16 * (q & 1))) & 0xFFFFu;
   };
-  // codes wl_haar_stats could not certify: the exact evaluation (rare)
-  auto resolve = [&](uint32_t cd, uint32_t pos) -> uint32_t {
-    if (cd != WL_CODE_EXACT) return cd;
-    const unsigned long long key =
-        wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride, pos, W1, c, mn, inv, rcp);
-    return key ? (uint32_t)wl_fbin(key) + 1u : 0u;
-  };
   for (uint32_t g0 = threadIdx.x; g0 < ngrp; g0 += 8 * WLM_WG) {
     uint2 gv[8];
 #pragma unroll
@@ -1682,25 +1891,16 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       const uint32_t g = g0 + (uint32_t)u * WLM_WG;
       gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
     }
-    uint32_t emask = 0u;  // bit 4u + q: code q of group u is uncertified
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t cd = code_at(gv[u], q);
-        emask |= (cd == WL_CODE_EXACT ? 1u : 0u) << (4 * u + q);
-        if (cd && cd != WL_CODE_EXACT)
-          atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
+        if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
       }
-    while (emask) {  // rare: the uncertified codes, one exact evaluation each
-      const int i = __builtin_ctz(emask);
-      emask &= emask - 1u;
-      const uint32_t cd = resolve(WL_CODE_EXACT, 4 * (g0 + (uint32_t)(i >> 2) * WLM_WG) + (uint32_t)(i & 3));
-      if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
-    }
   }
   for (uint32_t k = ngrp * 4 + threadIdx.x; k < bsz; k += WLM_WG) {  // tail codes
-    const uint32_t cd = resolve(codes[k], k);
+    const uint32_t cd = codes[k];
     if (cd) atomicAdd(&hist[(threadIdx.x & (WLM_NH - 1)) * WL_FBINS + cd - 1], 1u);
   }
   __syncthreads();
@@ -1755,30 +1955,13 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
         gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
       }
       uint32_t cnt2 = 0;
-      uint32_t emask = 0u;
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t cd = code_at(gv[u], q);
           cnt2 += (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
-          emask |= (cd == WL_CODE_EXACT ? 1u : 0u) << (4 * u + q);
         }
-      // rare: the uncertified codes by their exact evaluation, kept for the placement below
-      uint32_t xcode[2] = {0u, 0u}, xpos[2] = {0u, 0u};
-      int nx = 0;
-      for (uint32_t m = emask; m; m &= m - 1u) {
-        const int i = __builtin_ctz(m);
-        const uint32_t p = 4 * (g0 + (uint32_t)(i >> 2) * WLM_WG) + (uint32_t)(i & 3);
-        const uint32_t cd = resolve(WL_CODE_EXACT, p);
-        if (cd != csel && cd != cnext) continue;
-        cnt2 += (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
-        if (nx < 2) {
-          xcode[nx] = cd;
-          xpos[nx] = p;
-        }
-        ++nx;
-      }
       if (__ballot(cnt2 != 0) == 0) continue;  // wave-uniform
       uint32_t os, on;
       place(cnt2, os, on);
@@ -1787,30 +1970,16 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
         for (int u = 0; u < 8; ++u)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const uint32_t p = 4 * (g0 + (uint32_t)u * WLM_WG) + (uint32_t)q;
             const uint32_t cd = code_at(gv[u], q);
+            const uint32_t p = 4 * (g0 + (uint32_t)u * WLM_WG) + (uint32_t)q;
             if (cd == csel) pos_sel[os++] = p;
             if (cd == cnext) pos_next[on++] = p;
           }
-        if (nx > 2) {  // more than two matching uncertified codes in this lane: evaluate again
-          for (uint32_t m = emask; m; m &= m - 1u) {
-            const int i = __builtin_ctz(m);
-            const uint32_t p = 4 * (g0 + (uint32_t)(i >> 2) * WLM_WG) + (uint32_t)(i & 3);
-            const uint32_t cd = resolve(WL_CODE_EXACT, p);
-            if (cd == csel) pos_sel[os++] = p;
-            if (cd == cnext) pos_next[on++] = p;
-          }
-        } else {
-          for (int k = 0; k < nx; ++k) {
-            if (xcode[k] == csel) pos_sel[os++] = xpos[k];
-            if (xcode[k] == cnext) pos_next[on++] = xpos[k];
-          }
-        }
       }
     }
     for (uint32_t k0 = ngrp * 4; k0 < bsz; k0 += WLM_WG) {  // tail codes (every lane takes part)
       const uint32_t k = k0 + threadIdx.x;
-      const uint32_t cd = k < bsz ? resolve(codes[k], k) : 0u;
+      const uint32_t cd = k < bsz ? codes[k] : 0u;
       const uint32_t cnt2 = (cd == csel ? 1u : 0u) + (cd == cnext ? 0x10000u : 0u);
       uint32_t os, on;
       place(cnt2, os, on);
@@ -1958,6 +2127,13 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
   hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
                      wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  if constexpr (L >= 2) {
+    if (src && env_int("IDN_WAVELET_INTSYNTH", 1)) {
+      hipLaunchKernelGGL((wl_haar_synth_int<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+                         row_stride, stats, out_u8, out_f32);
+      return;
+    }
+  }
   hipLaunchKernelGGL((wl_haar_synth<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, in64, Lt.h,
                      Lt.w, row_stride, stats, out_u8, out_f32);
 }
