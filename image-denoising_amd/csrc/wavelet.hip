@@ -93,6 +93,8 @@ struct WlStats {
   __host__ __device__ static int sumsq(int c, int l, int b, int L) { return 8 + (c * L + l) * 3 + b; }
   __host__ __device__ static int median(int c, int L) { return 8 + 9 * L + c; }
   __host__ __device__ static int thr(int c, int l, int b, int L) { return 8 + 9 * L + 3 + (c * L + l) * 3 + b; }
+  // half thresholds for the integer Haar synthesis (written for L <= 3 only: [170, 197))
+  __host__ __device__ static int thrh(int c, int l, int b) { return 170 + (c * 3 + l) * 3 + b; }
   static constexpr int FLAG = 255;
   static constexpr int DIAG = 248;  // [248..251) nonzero count of the finest dd per channel
   static constexpr int MN64 = 200;  // [200..203) fp64 channel min (u64 bits), [203..206) max
@@ -696,6 +698,7 @@ __global__ void wl_thresh(double* __restrict__ stats, WlLayout Lt) {
         const double dvar = st[WlStats::sumsq(c, l, b, Lt.L)] / cnt;
         const double t = var / sqrt(fmax(dvar - var, 2.220446049250313e-16));
         st[WlStats::thr(c, l, b, Lt.L)] = t;
+        if (Lt.L <= 3) st[WlStats::thrh(c, l, b)] = 0.5 * t;
       }
   }
   st[WlStats::FLAG] = bad ? 1.0 : 0.0;
@@ -1487,7 +1490,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
   const uint8_t* ib = src + (int64_t)img * h * row_stride;
   uint16_t* cdp0 = reinterpret_cast<uint16_t*>(ws + img * img_floats + dd_off + 3 * bsz);
   // sub-block geometry of iteration `it`; its 4 rows x 12 bytes (dword aligned: checked on the
-  // host) are loaded one iteration ahead (two waves per SIMD at this register count)
+  // host) are loaded two iterations ahead (two waves per SIMD at this register count)
   auto geom = [&](int it, int& sub, int& y0, int& x0) -> bool {
     const int tid = (blockIdx.x * WLS_IT + it) * WLH_WG + threadIdx.x;
     const int blk = tid / HS::NS;
@@ -1508,7 +1511,6 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
       for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
     }
   };
-  // two iterations of loads in flight (the kernel runs at two waves per SIMD)
   uint32_t qn[4][3] = {}, qn2[4][3] = {};
   load_q(0, qn);
   load_q(1, qn2);
@@ -1667,6 +1669,9 @@ __device__ __forceinline__ double tdot_sum(int c, const int (&v)[3]) {
 __device__ __forceinline__ double tdot(int c, int d0, int d1, int d2) {  // details: |T| <= 1.83e9
   return (double)(__mul24(ycc_w(c, 0), d0) + __mul24(ycc_w(c, 1), d1) + __mul24(ycc_w(c, 2), d2));
 }
+// soft(x, t) as x - clamp(x, -t, t): the same value as soft() (x -+ t rounds alike; 0 inside),
+// three fp64 ops instead of a compare and two selects
+__device__ __forceinline__ double soft_c(double x, double t) { return x - fmin(fmax(x, -t), t); }
 // outputs (r, s) = (0,0), (0,1), (1,0), (1,1) of A + g_s AD + f_r DA + f_r g_s DD
 __device__ __forceinline__ void haar_bfly(double A, double AD, double DA, double DD, double (&x)[4]) {
   const double p = A + AD, m = A - AD, q0 = DA + DD, q1 = DA - DD;
@@ -1691,7 +1696,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
   const int blk = tid / HS::NS, sub = tid % HS::NS;
   const bool act = blk < nblk;
   const double* st = stats + (size_t)img * WL_STATS;
-  const bool bad = st[WlStats::FLAG] != 0.0;
+  const bool bad = st[WlStats::FLAG] != 0.0;  // image-uniform: zeros (0.14.2's NaN -> U8 0)
   int y0 = 0, x0 = 0;
   uint32_t q[4][3] = {};
   if (act) {
@@ -1731,6 +1736,17 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
                __shfl(S16[ch], base + 3), S64[ch], D3[0][ch], D3[1][ch], D3[2][ch]);
   }
   if (!act) return;
+  if (bad) {
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r)
+#pragma unroll 1
+      for (int k = 0; k < 12; ++k) {
+        const int y = y0 + r, xx = x0 + k / 3, c = k % 3;
+        if (out_u8) out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] = 0;
+        if (out_f32) out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = 0.0f;
+      }
+    return;
+  }
   // per-channel constants (uniform: SGPRs)
   double mnc[3], invc[3], s1c[3], kc[3];
 #pragma unroll
@@ -1747,24 +1763,24 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const double s1 = s1c[c], k = kc[c];
-    auto th = [&](int l, int b) { return 0.5 * st[WlStats::thr(c, l, b, L)]; };
+    auto th = [&](int l, int b) { return st[WlStats::thrh(c, l, b)]; };
     double a2;  // level-2 approximation at this sub-block (after level-3 synthesis)
     if constexpr (L == 3) {
       const double Ah = tdot_sum(c, S64) * ldexp(s1, -3) + 2.0 * k;
       const double x3 = ldexp(s1, -3);
       double x[4];
-      haar_bfly(Ah, soft(tdot(c, D3[0][0], D3[0][1], D3[0][2]) * x3, th(2, 0)),
-                soft(tdot(c, D3[1][0], D3[1][1], D3[1][2]) * x3, th(2, 1)),
-                soft(tdot(c, D3[2][0], D3[2][1], D3[2][2]) * x3, th(2, 2)), x);
+      haar_bfly(Ah, soft_c(tdot(c, D3[0][0], D3[0][1], D3[0][2]) * x3, th(2, 0)),
+                soft_c(tdot(c, D3[1][0], D3[1][1], D3[1][2]) * x3, th(2, 1)),
+                soft_c(tdot(c, D3[2][0], D3[2][1], D3[2][2]) * x3, th(2, 2)), x);
       a2 = sub == 0 ? x[0] : sub == 1 ? x[1] : sub == 2 ? x[2] : x[3];
     } else {
       a2 = tdot_sum(c, S16) * ldexp(s1, -1) + 2.0 * k;
     }
     const double x2 = ldexp(s1, -2);
     double x[4];
-    haar_bfly(0.5 * a2, soft(tdot(c, D2[0][0], D2[0][1], D2[0][2]) * x2, th(1, 0)),
-              soft(tdot(c, D2[1][0], D2[1][1], D2[1][2]) * x2, th(1, 1)),
-              soft(tdot(c, D2[2][0], D2[2][1], D2[2][2]) * x2, th(1, 2)), x);
+    haar_bfly(0.5 * a2, soft_c(tdot(c, D2[0][0], D2[0][1], D2[0][2]) * x2, th(1, 0)),
+              soft_c(tdot(c, D2[1][0], D2[1][1], D2[1][2]) * x2, th(1, 1)),
+              soft_c(tdot(c, D2[2][0], D2[2][1], D2[2][2]) * x2, th(1, 2)), x);
 #pragma unroll
     for (int g = 0; g < 4; ++g) Ah1[g][c] = 0.5 * x[g];
   }
@@ -1794,11 +1810,11 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const double x1 = 0.5 * s1c[c];
-      auto th = [&](int b) { return 0.5 * st[WlStats::thr(c, 0, b, L)]; };
+      auto th = [&](int b) { return st[WlStats::thrh(c, 0, b)]; };
       double x[4];
-      haar_bfly(Ah1[g][c], soft(tdot(c, D[0][0], D[0][1], D[0][2]) * x1, th(0)),
-                soft(tdot(c, D[1][0], D[1][1], D[1][2]) * x1, th(1)),
-                soft(tdot(c, D[2][0], D[2][1], D[2][2]) * x1, th(2)), x);
+      haar_bfly(Ah1[g][c], soft_c(tdot(c, D[0][0], D[0][1], D[0][2]) * x1, th(0)),
+                soft_c(tdot(c, D[1][0], D[1][1], D[1][2]) * x1, th(1)),
+                soft_c(tdot(c, D[2][0], D[2][1], D[2][2]) * x1, th(2)), x);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i][c] = x[i];
     }
@@ -1812,10 +1828,9 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
       const int y = y0 + 2 * gy + r, xx = x0 + 2 * gx + s;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        double o = __fma_rn(e[2], R[c][2], __fma_rn(e[1], R[c][1], e[0] * R[c][0]));
-        o = fmin(fmax(o, 0.0), 255.0);
-        if (bad) o = 0.0;
-        const uint32_t u = (uint32_t)(int)o;
+        const double o = __fma_rn(e[2], R[c][2], __fma_rn(e[1], R[c][1], e[0] * R[c][0]));
+        // clip [0, 255] after the truncation (v_med3): the same byte for every o
+        const uint32_t u = (uint32_t)min(max((int)o, 0), 255);
         if (dw) {
           const int bi = (2 * gx + s) * 3 + c;
           rowp[r][bi >> 2] |= u << (8 * (bi & 3));
@@ -1823,7 +1838,8 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
           out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] =
               (uint8_t)u;
         }
-        if (out_f32) out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = (float)(o * (1.0 / 255.0));
+        if (out_f32)
+          out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = (float)(fmin(fmax(o, 0.0), 255.0) * (1.0 / 255.0));
       }
     }
     if (dw && gx == 1) {
