@@ -1,6 +1,8 @@
 // Per-element noise arithmetic shared by the noise kernels (noise.hip) and the fused
-// noise -> filter kernels (stencil_u8.hip): skimage.util.random_noise's float64 apply in numpy's
-// op order plus the caller's U8 cast, on the Philox stream described in noise.hip.  Files that
+// noise -> filter kernels (stencil_u8.hip), on the Philox stream described in noise.hip:
+// skimage.util.random_noise's float64 apply in numpy's op order plus the caller's U8 cast; for
+// gaussian / speckle the U8 cast itself runs on the 0..255 scale in fp32 (floor(clip(v + 255 n)),
+// the same law; the float64 value is still produced for callers that keep it).  Files that
 // include this are compiled with -ffp-contract=off.
 #pragma once
 
@@ -89,12 +91,27 @@ __device__ __forceinline__ v4u noise16_u8(const v4u raw, uint32_t chunk, uint64_
       const float* z = z8 + 4 * (k & 1);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const double sz = __dmul_rn(p1, (double)z[b]);
-        const double nz = MEAN0 ? sz : __dadd_rn(p0, sz);
-        const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
-        if (KIND == IDN_NOISE_GAUSSIAN) outv[b] = clip01(__dadd_rn(xv, nz));
-        else outv[b] = clip01(__dadd_rn(xv, __dmul_rn(xv, nz)));
+        // the U8 result on the 0..255 scale in fp32: floor(clip(v + 255 n)) (gaussian) or
+        // floor(clip(v + v n)) (speckle) -- the law of (255 * clip(x + n)).astype(uint8) up to
+        // fp32 rounding next to integers; fewer than half the float64 apply's instructions
+        const float v = (float)((in[k] >> (8 * b)) & 0xFFu);
+        float ov;
+        if constexpr (KIND == IDN_NOISE_GAUSSIAN) {
+          ov = __builtin_fmaf((float)(255.0 * p1), z[b], MEAN0 ? v : v + (float)(255.0 * p0));
+        } else {
+          const float n = MEAN0 ? (float)p1 * z[b] : __builtin_fmaf((float)p1, z[b], (float)p0);
+          ov = __builtin_fmaf(v, n, v);
+        }
+        o[k] |= (uint32_t)__builtin_amdgcn_fmed3f(ov, 0.0f, 255.0f) << (8 * b);
+        if (of) {  // the float64 result (numpy's op order) for callers that keep it
+          const double sz = __dmul_rn(p1, (double)z[b]);
+          const double nz = MEAN0 ? sz : __dadd_rn(p0, sz);
+          const double xv = img_as_float((in[k] >> (8 * b)) & 0xFFu);
+          of[4 * k + b] = KIND == IDN_NOISE_GAUSSIAN ? clip01(__dadd_rn(xv, nz))
+                                                     : clip01(__dadd_rn(xv, __dmul_rn(xv, nz)));
+        }
       }
+      continue;
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {

@@ -250,7 +250,9 @@ def test_blob_bitexact(dev, flip):
                                      ("s&p", {"amount": 0.4})])
 def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
     """flat (16 elements / lane) and element kernels: U8 == trunc(255 * f64 out), same output
-    law (first two moments of out - x), deterministic, batch-split invariant"""
+    law (first two moments of out - x), deterministic, batch-split invariant.  The flat form
+    casts gaussian / speckle on the 0..255 scale in fp32 (noise_apply.hpp): its U8 may differ by
+    one from trunc(255 * f64) only where 255 * f64 lies within 3e-4 of an integer"""
     import oracle
     import torch
     import idn
@@ -259,7 +261,13 @@ def test_philox_forms_consistent(dev, monkeypatch, flat, mode, kw):
     x = torch.from_numpy(imgs).cuda()
     u8, f64 = idn.ops.random_noise(x, mode, seed=4, offset=7, out="both", **kw)
     u8, f64 = u8.cpu().numpy(), f64.cpu().numpy()
-    assert np.array_equal(u8, oracle.sk.to_u8(255 * f64))
+    cast = oracle.sk.to_u8(255 * f64)
+    d8 = u8.astype(int) - cast.astype(int)
+    assert np.abs(d8).max() <= 1
+    near = np.abs(255 * f64 - np.round(255 * f64)) < 3e-4
+    assert np.all(near[d8 != 0])
+    if flat == "0" or mode == "s&p":
+        assert np.array_equal(u8, cast)
     one8 = idn.ops.random_noise(x[1:2], mode, seed=4, offset=8, **kw).cpu().numpy()
     assert np.array_equal(one8[0], u8[1])
     xf = imgs.astype(np.float64) * (1.0 / 255.0)
