@@ -109,6 +109,9 @@ __device__ __forceinline__ int wl_ebin(unsigned long long key) {
 // fine bins of |dd| keys: exponent (clamped as wl_ebin) and the top 4 mantissa bits, monotone in
 // the key; the clamped exponent bins keep one sub-bin
 constexpr int WL_FBINS = WL_EBINS * 16;
+__device__ __forceinline__ unsigned long long absbits(double v) {
+  return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
+}
 __device__ __forceinline__ int wl_fbin(unsigned long long key) {
   const int e = (int)(key >> 52) - (1023 - 61);
   if (e < 0) return 0;
@@ -339,7 +342,8 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
                                                  int tiles_x, const uint8_t* __restrict__ src,
                                                  const double* __restrict__ in64,
                                                  int64_t row_stride, double* __restrict__ part,
-                                                 size_t part_per_img, size_t part_tile0) {
+                                                 size_t part_per_img, size_t part_tile0,
+                                                 int emit_codes) {
   using Wv = Wav<WV>;
   constexpr int F = Wv::F, NX = DwtRB<WV>::NX, NY = DwtRB<WV>::NY;
   __shared__ DwtRB<WV> S;
@@ -397,8 +401,11 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
 #pragma unroll
       for (int p = 0; p < F; ++p) {
         const wreal v = x[2 * ii + F - 1 - p];
-        if (Wv::dlo[p] != 0) lo = __dadd_rn(lo, __dmul_rn(Wv::dlo[p], v));  // pywt: mul, then add
-        if (Wv::dhi[p] != 0) hi = __dadd_rn(hi, __dmul_rn(Wv::dhi[p], v));
+        // the highpass keeps pywt's mul-then-add (dd's exact zeros feed the sigma median); the
+        // lowpass only reaches aa / ad / da, whose rounding the thresholds and the synthesis
+        // absorb (1e-16 relative), so it takes fmas
+        if (Wv::dlo[p] != 0) lo = __fma_rn(Wv::dlo[p], v, lo);
+        if (Wv::dhi[p] != 0) hi = __dadd_rn(hi, __dmul_rn(Wv::dhi[p], v));  // pywt: mul, then add
       }
       S.vl[c][ii][q] = lo;
       S.vh[c][ii][q] = hi;
@@ -427,13 +434,20 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     for (int qq = 0; qq < F; ++qq) {  // then axis 1: output column j uses staged cols 2j + F-1-q
       const wreal lv = l[2 * r + F - 1 - qq], hv = h[2 * r + F - 1 - qq];
       if (Wv::dlo[qq] != 0) {
-        aa = __dadd_rn(aa, __dmul_rn(Wv::dlo[qq], lv));  // key 'aa': axis 0 low, axis 1 low
-        da = __dadd_rn(da, __dmul_rn(Wv::dlo[qq], hv));  // key 'da': axis 0 high, axis 1 low
+        aa = __fma_rn(Wv::dlo[qq], lv, aa);  // key 'aa': axis 0 low, axis 1 low
+        da = __fma_rn(Wv::dlo[qq], hv, da);  // key 'da': axis 0 high, axis 1 low
       }
       if (Wv::dhi[qq] != 0) {
-        ad = __dadd_rn(ad, __dmul_rn(Wv::dhi[qq], lv));  // key 'ad': axis 0 low, axis 1 high
-        dd = __dadd_rn(dd, __dmul_rn(Wv::dhi[qq], hv));
+        ad = __fma_rn(Wv::dhi[qq], lv, ad);                 // key 'ad': axis 0 low, axis 1 high
+        dd = __dadd_rn(dd, __dmul_rn(Wv::dhi[qq], hv));  // pywt's order: exact zeros
       }
+    }
+    // level 1: the fine-bin code of |dd| (0: exact zero) for the sigma median
+    // (wl_haar_median<BAND>), in this channel's unused input-plane slot
+    if (emit_codes && i < Ho && j0 + jl + r < Wo) {
+      const unsigned long long key = absbits(dd);
+      reinterpret_cast<uint16_t*>(base + (size_t)c * Hin * Win)[(size_t)i * Wo + j0 + jl + r] =
+          (uint16_t)(key ? wl_fbin(key) + 1 : 0);
     }
     ob[c][0][ii][jl + r] = aa;
     ob[c][1][ii][jl + r] = ad;
@@ -512,9 +526,6 @@ struct RadixState {
   uint32_t rank;
 };
 
-__device__ __forceinline__ unsigned long long absbits(double v) {
-  return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
-}
 
 // block-wide selection over an LDS histogram: the bin holding rank `rank` and the rank within
 // it.  Thread i owns bins [i*per, (i+1)*per); the thread whose count range holds the rank finds
@@ -1857,7 +1868,10 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
 
 constexpr int WLM_WG = 256;  // threads per (image, channel): several workgroups per CU overlap phases
 constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slower: fewer workgroups per CU)
-template <int L>
+// BAND: the general path (any wavelet; level-1 dd stored in fp64 by wl_dwt_rb, which also left
+// the codes at the start of the channel's input-plane slot): the exact keys of a position are
+// read from the band instead of recomputed from the pixels.  L is unused then.
+template <int L, bool BAND = false>
 __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restrict__ src,
                                                        const double* __restrict__ in64,
                                                        int64_t row_stride,
@@ -1867,11 +1881,13 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
   const int img = blockIdx.x / 3, c = blockIdx.x % 3;
   const int W1 = Lt.W[1];
   const uint32_t bsz = (uint32_t)Lt.H[1] * (uint32_t)W1;
-  const uint16_t* codes = reinterpret_cast<const uint16_t*>(
-      ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz);
-  // scratch (the unused input-plane slot of this channel, h*w doubles): [0, bsz) keys of the
-  // selected bin, then positions of the selected bin and of the next bin
-  double* keys = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;
+  const wreal* band_dd = ws + img * img_floats + Lt.off_band[1] + (size_t)c * 4 * bsz + 3 * bsz;
+  double* slot = ws + img * img_floats + (size_t)c * Lt.h * Lt.w;
+  const uint16_t* codes = BAND ? reinterpret_cast<const uint16_t*>(slot)
+                               : reinterpret_cast<const uint16_t*>(band_dd);
+  // scratch (the unused input-plane slot of this channel, h*w doubles; after the codes in BAND
+  // mode): [0, bsz) keys of the selected bin, then positions of the selected bin and of the next
+  double* keys = slot + (BAND ? (bsz + 3) / 4 : 0);
   uint32_t* pos_sel = reinterpret_cast<uint32_t*>(keys + bsz);
   uint32_t* pos_next = pos_sel + bsz;
   double* st = stats + (size_t)img * WL_STATS;
@@ -2010,7 +2026,10 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
     double* kb = mcnt <= LDS_KEYS ? reinterpret_cast<double*>(hist + 2048) : keys;
     // the exact keys of the selected bin, recomputed from the input (u8: 8 positions' loads in
     // flight per thread; the recompute is latency-bound otherwise)
-    if (in64) {
+    if (BAND) {
+      for (uint32_t t = threadIdx.x; t < mcnt; t += WLM_WG)
+        kb[t] = __longlong_as_double((long long)absbits(band_dd[pos_sel[t]]));
+    } else if (in64) {
       for (uint32_t t = threadIdx.x; t < mcnt; t += WLM_WG)
         kb[t] = __longlong_as_double((long long)wl_dd1_key<MARK>(
             src, in64, img, Lt.h, Lt.w, row_stride, pos_sel[t], W1, c, mn, inv, rcp));
@@ -2076,8 +2095,10 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       } else {  // it is the smallest key of the next nonempty bin
         unsigned long long nmin = ~0ull;
         for (uint32_t t = threadIdx.x; t < ncnt; t += WLM_WG) {
-          const unsigned long long key = wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride,
-                                                          pos_next[t], W1, c, mn, inv, rcp);
+          const unsigned long long key =
+              BAND ? absbits(band_dd[pos_next[t]])
+                   : wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride, pos_next[t], W1, c,
+                                      mn, inv, rcp);
           nmin = key < nmin ? key : nmin;
         }
         for (int o = 32; o > 0; o >>= 1) {
@@ -2182,6 +2203,10 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
                        row_stride, stats);
   }
   double* part = (double*)((char*)ws + Lt.part_off);
+  // sigma from level-1 dd codes (wl_haar_median<.., true>) when the channel's input-plane slot
+  // holds codes + keys + positions (2.25 band sizes); else the radix select over the band
+  const size_t bsz1 = (size_t)Lt.H[1] * Lt.W[1];
+  const bool codes = env_int("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
@@ -2189,20 +2214,24 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[l]);
+                         Lt.part_tile0[l], 0);
     else if (in64)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1]);
+                         Lt.part_tile0[1], codes ? 1 : 0);
     else
       hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1]);
+                         Lt.part_tile0[1], codes ? 1 : 0);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
-  hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
+  if (codes)
+    hipLaunchKernelGGL((wl_haar_median<1, true>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64,
+                       row_stride, wsf, Lt.img_floats, stats, Lt);
+  else
+    hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   for (int l = Lt.L; l >= 2; --l) {
     // the level-(l-1) 'aa' slot (consumed by the analysis already) receives the reconstruction
