@@ -593,6 +593,10 @@ __global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const JpegDev* __res
 
 // stage 2a/2b: sync passes.  grid (max chunks per image, n).  PASS_A: start from the chunk's
 // own first bit; else from the predecessor's end state in `prev` (chunk 0: the true start).
+// chg_prev / chg_next: per chunk, did its end state change in the previous / this pass.  After
+// the first B pass (`all`) a chunk is decoded again only if its predecessor's end state -- its
+// start -- changed; otherwise its end state and counts are those of the previous pass.  Only the
+// chains still converging cost anything in the later passes.
 template <bool PASS_A>
 __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict__ imgs,
                                                        const uint8_t* __restrict__ ub,
@@ -600,14 +604,25 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
                                                        const uint64_t* __restrict__ prev,
                                                        uint64_t* __restrict__ next,
                                                        ChunkOut* __restrict__ cnt,
-                                                       uint32_t* __restrict__ changed) {
+                                                       uint32_t* __restrict__ changed,
+                                                       const uint8_t* __restrict__ chg_prev,
+                                                       uint8_t* __restrict__ chg_next, int all) {
   __shared__ JpegLds T;
   const JpegDev& D = imgs[blockIdx.y];
   if (D.restart || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  bool redo = true;
+  if (!PASS_A && !all) {
+    redo = t < D.nchunks && t > 0 && chg_prev[D.ch_off + t - 1];
+    if (t < D.nchunks && !redo) {
+      next[D.ch_off + t] = prev[D.ch_off + t];
+      chg_next[D.ch_off + t] = 0;
+    }
+    if (__ballot(redo) == 0) return;  // the whole workgroup (one wave) is settled
+  }
   jpg_load_tables(T, D);
   __syncthreads();
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= D.nchunks) return;
+  if (t >= D.nchunks || !redo) return;
   const uint32_t nbits = ublen[blockIdx.y] * 8u;
   const uint32_t b0 = min(t * D.chunk_bits, nbits), b1 = min(b0 + D.chunk_bits, nbits);
   uint64_t st;
@@ -621,9 +636,13 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
   const uint64_t e = ((uint32_t)st >= b1) ? st
                                          : jpg_run<false>(K, T, ub + D.ub_off, st, b1, &co, 0, pred, nullptr);
   next[D.ch_off + t] = e;
-  if (!PASS_A) {
+  if (PASS_A) {
+    chg_next[D.ch_off + t] = 1;
+  } else {
     cnt[D.ch_off + t] = co;
-    if (e != prev[D.ch_off + t]) changed[0] = 1u;
+    const bool ch = e != prev[D.ch_off + t];
+    chg_next[D.ch_off + t] = ch ? 1 : 0;
+    if (ch) changed[0] = 1u;
   }
 }
 
@@ -903,7 +922,7 @@ struct JpegPlan {
   bool any_chunked = false;
   size_t off_imgs = 0, off_blkend = 0, off_scan = 0, off_coef = 0, off_planes = 0;
   size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_s0 = 0, off_s1 = 0, off_cnt = 0,
-         off_start = 0, off_flag = 0, total = 0;
+         off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, total = 0;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1012,7 +1031,9 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
   P.off_cnt = align256(P.off_s1 + sizeof(uint64_t) * (size_t)P.nchunks);
   P.off_start = align256(P.off_cnt + sizeof(ChunkOut) * (size_t)P.nchunks);
   P.off_flag = align256(P.off_start + sizeof(ChunkOut) * (size_t)P.nchunks);
-  P.total = align256(P.off_flag + 256);
+  P.off_chg0 = align256(P.off_flag + 256);
+  P.off_chg1 = align256(P.off_chg0 + (size_t)P.nchunks);
+  P.total = align256(P.off_chg1 + (size_t)P.nchunks);
   return IDN_OK;
 }
 
@@ -1097,6 +1118,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   ChunkOut* cnt = reinterpret_cast<ChunkOut*>(ws + P.off_cnt);
   ChunkOut* cstart = reinterpret_cast<ChunkOut*>(ws + P.off_start);
   uint32_t* flag = reinterpret_cast<uint32_t*>(ws + P.off_flag);
+  uint8_t* chg[2] = {reinterpret_cast<uint8_t*>(ws + P.off_chg0),
+                     reinterpret_cast<uint8_t*>(ws + P.off_chg1)};
   hipLaunchKernelGGL(jpeg_unstuff_kernel, dim3(n), dim3(1024), 0, st, dimg, ws + P.off_scan, ub,
                      ivs, ublen);
   const dim3 gitems((P.max_items + 63) / 64, n);
@@ -1104,12 +1127,12 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   if (P.any_chunked) {
     // pass A, then pass B until no chunk's end state changes (typically twice)
     hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
-                       S[0], cnt, flag);
+                       S[0], cnt, flag, chg[1], chg[0], 1);
     for (uint32_t it = 0;; ++it) {
       if (hipMemsetAsync(flag, 0, 4, st) != hipSuccess)
         return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
       hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
-                         S[cur], S[cur ^ 1], cnt, flag);
+                         S[cur], S[cur ^ 1], cnt, flag, chg[cur], chg[cur ^ 1], it == 0 ? 1 : 0);
       cur ^= 1;
       uint32_t changed = 0;
       if (hipMemcpyAsync(&changed, flag, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
