@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -1093,20 +1094,41 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   uint8_t* host = pin;
   memcpy(host + P.off_imgs, P.dev.data(), sizeof(JpegDev) * (size_t)n);
   memcpy(host + P.off_blkend, P.blk_end.data(), sizeof(uint64_t) * (size_t)n);
-  {  // the entropy segments, copied by a few host threads
+  bool copy_ok = hipMemcpyAsync(ws, host, P.off_scan, hipMemcpyHostToDevice, st) == hipSuccess;
+  {
+    // the entropy segments, gathered by a few host threads in NPART parts of the batch; each
+    // part's host-to-device copy is issued as soon as the part is complete, so the DMA of part
+    // k overlaps the gathering of part k + 1
     const int nt = std::max(1, std::min(8, n / 8));
-    auto part = [&](int k) {
-      for (int i = k; i < n; i += nt)
-        memcpy(host + P.off_scan + P.dev[i].scan_off, files[i] + P.scan_begin[i],
-               P.dev[i].scan_len);
+    const int npart = std::max(1, std::min(4, n / 16));
+    std::atomic<int> done[4];
+    for (int q = 0; q < 4; ++q) done[q].store(0);
+    auto first = [&](int q) { return (int)((int64_t)n * q / npart); };
+    auto worker = [&](int k) {
+      for (int q = 0; q < npart; ++q) {
+        for (int i = first(q) + k; i < first(q + 1); i += nt)
+          memcpy(host + P.off_scan + P.dev[i].scan_off, files[i] + P.scan_begin[i],
+                 P.dev[i].scan_len);
+        done[q].fetch_add(1, std::memory_order_release);
+      }
     };
     std::vector<std::thread> th;
-    for (int k = 1; k < nt; ++k) th.emplace_back(part, k);
-    part(0);
+    for (int k = 1; k < nt; ++k) th.emplace_back(worker, k);
+    for (int q = 0; q < npart; ++q) {  // the calling thread: its share, then the part's copy
+      for (int i = first(q); i < first(q + 1); i += nt)
+        memcpy(host + P.off_scan + P.dev[i].scan_off, files[i] + P.scan_begin[i],
+               P.dev[i].scan_len);
+      done[q].fetch_add(1, std::memory_order_release);
+      while (done[q].load(std::memory_order_acquire) < nt) std::this_thread::yield();
+      const size_t b0 = P.dev[first(q)].scan_off;
+      const size_t b1 = q + 1 < npart ? (size_t)P.dev[first(q + 1)].scan_off : P.scan_bytes;
+      if (b1 > b0)
+        copy_ok = copy_ok && hipMemcpyAsync(ws + P.off_scan + b0, host + P.off_scan + b0,
+                                            b1 - b0, hipMemcpyHostToDevice, st) == hipSuccess;
+    }
     for (auto& t : th) t.join();
   }
-  if (hipMemcpyAsync(ws, host, P.off_coef, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemsetAsync(ws + P.off_coef, 0, P.nblk * 128, st) != hipSuccess)
+  if (!copy_ok || hipMemsetAsync(ws + P.off_coef, 0, P.nblk * 128, st) != hipSuccess)
     return set_error(IDN_EHIP, "idn_jpeg_decode_u8: staging copy failed");
   const JpegDev* dimg = reinterpret_cast<const JpegDev*>(ws + P.off_imgs);
   int16_t* coef = reinterpret_cast<int16_t*>(ws + P.off_coef);
