@@ -648,19 +648,44 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
 }
 
 // stage 2c: per image, the first block index and DC predictors of every chunk
-__global__ void jpeg_prefix_kernel(const JpegDev* __restrict__ imgs,
-                                   const ChunkOut* __restrict__ cnt, ChunkOut* __restrict__ start,
-                                   int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const JpegDev& D = imgs[i];
+// one 256-thread workgroup per image: exclusive scan of the chunk counts (block counts and DC
+// sums add), 256 chunks per round (a serial walk per image was a ~300-step latency chain)
+__global__ __launch_bounds__(256) void jpeg_prefix_kernel(const JpegDev* __restrict__ imgs,
+                                                          const ChunkOut* __restrict__ cnt,
+                                                          ChunkOut* __restrict__ start, int n) {
+  const JpegDev& D = imgs[blockIdx.x];
   if (D.restart) return;
-  ChunkOut acc{0u, {0, 0, 0}};
-  for (uint32_t t = 0; t < D.nchunks; ++t) {
-    start[D.ch_off + t] = acc;
-    const ChunkOut c = cnt[D.ch_off + t];
-    acc.nblk += c.nblk;
-    for (int k = 0; k < 3; ++k) acc.dcsum[k] += c.dcsum[k];
+  __shared__ int32_t sv[4][256];
+  __shared__ int32_t carry[4];
+  if (threadIdx.x < 4) carry[threadIdx.x] = 0;
+  for (uint32_t t0 = 0; t0 < D.nchunks; t0 += 256) {
+    const uint32_t t = t0 + threadIdx.x;
+    ChunkOut c{0u, {0, 0, 0}};
+    if (t < D.nchunks) c = cnt[D.ch_off + t];
+    int32_t v[4] = {(int32_t)c.nblk, c.dcsum[0], c.dcsum[1], c.dcsum[2]};
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sv[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+      int32_t u[4] = {0, 0, 0, 0};
+      if (threadIdx.x >= (unsigned)o)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = sv[k][threadIdx.x - o];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sv[k][threadIdx.x] += u[k];
+      __syncthreads();
+    }
+    if (t < D.nchunks) {
+      ChunkOut e;  // exclusive = carry + inclusive - own
+      e.nblk = (uint32_t)(carry[0] + sv[0][threadIdx.x] - v[0]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) e.dcsum[k] = carry[k + 1] + sv[k + 1][threadIdx.x] - v[k + 1];
+      start[D.ch_off + t] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) carry[threadIdx.x] += sv[threadIdx.x][255];
   }
 }
 
@@ -910,6 +935,116 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDev* __restri
   } else {
     for (int k = 0; k < 4 && x0 + k < w; ++k)
       for (int c = 0; c < 3; ++c) o[3 * k + c] = (uint8_t)px[k][c];
+  }
+}
+
+// 8 consecutive pixels of a row per thread from dword loads: Y 2 dwords, each chroma row 3 dwords
+// (the samples the 8 outputs' fancy upsampling needs, columns x0/2 - 1 .. x0/2 + 4 for h2),
+// where jpeg_color_kernel issued 9 byte loads per pixel.  Same arithmetic (jpg_up's formulas on
+// the extracted samples, jdcolor.c's tables).
+__device__ __forceinline__ uint32_t ld_dw(const uint8_t* __restrict__ row, int col4, int pw) {
+  return (col4 >= 0 && col4 < pw) ? *reinterpret_cast<const uint32_t*>(row + col4) : 0u;
+}
+// the 12 samples of chroma row r at columns cb .. cb + 11 (cb = x0/2 - 4, dword aligned)
+struct C12 {
+  uint32_t d[3];
+  __device__ __forceinline__ int at(int k) const { return (int)((d[k >> 2] >> (8 * (k & 3))) & 0xFFu); }
+};
+template <int HS, int VS>  // chroma subsampling factors (1 or 2)
+__device__ __forceinline__ void jpg_chroma8(const uint8_t* __restrict__ P, int pw, int dw, int dh,
+                                            int x0, int y, int (&out)[8]) {
+  if constexpr (HS == 1) {  // 4:4:4
+    const uint8_t* r = P + (int64_t)y * pw;
+    const uint32_t a = ld_dw(r, x0, pw), b = ld_dw(r, x0 + 4, pw);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = (int)(((k < 4 ? a : b) >> (8 * (k & 3))) & 0xFFu);
+    return;
+  }
+  const int cb = x0 / 2 - 4;  // x0 % 8 == 0: dword aligned
+  const int inrow = VS == 2 ? y >> 1 : y;
+  C12 r0, r1;
+  const uint8_t* p0 = P + (int64_t)inrow * pw;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) r0.d[j] = ld_dw(p0, cb + 4 * j, pw);
+  if constexpr (VS == 2) {
+    const int other = min(max((y & 1) ? inrow + 1 : inrow - 1, 0), dh - 1);
+    const uint8_t* p1 = P + (int64_t)other * pw;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) r1.d[j] = ld_dw(p1, cb + 4 * j, pw);
+  }
+  // column sum of sample k (k = col - cb): h2v1 the sample, h2v2 3 * nearer + further row
+  auto cs = [&](int k) { return VS == 2 ? r0.at(k) * 3 + r1.at(k) : r0.at(k); };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int col = x0 / 2 + (i >> 1), k = 4 + (i >> 1);
+    const int t = cs(k);
+    if constexpr (VS == 2) {
+      if ((i & 1) == 0) out[i] = col == 0 ? (t * 4 + 8) >> 4 : (t * 3 + cs(k - 1) + 8) >> 4;
+      else out[i] = col == dw - 1 ? (t * 4 + 7) >> 4 : (t * 3 + cs(k + 1) + 7) >> 4;
+    } else {
+      if ((i & 1) == 0) out[i] = col == 0 ? t : (t * 3 + cs(k - 1) + 1) >> 2;
+      else out[i] = col == dw - 1 ? t : (t * 3 + cs(k + 1) + 2) >> 2;
+    }
+  }
+}
+
+template <int HS, int VS, bool GRAY>
+__device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __restrict__ planes,
+                                           int x0, int y, uint32_t (&o)[6]) {
+  const int pw0 = D.bw[0] * 8;
+  const uint8_t* yr = planes + D.pl_off[0] + (int64_t)y * pw0;
+  const uint32_t ya = ld_dw(yr, x0, pw0), yb = ld_dw(yr, x0 + 4, pw0);
+  int cbv[8], crv[8];
+  if constexpr (!GRAY) {
+    jpg_chroma8<HS, VS>(planes + D.pl_off[1], D.bw[1] * 8, D.dw[1], D.dh[1], x0, y, cbv);
+    jpg_chroma8<HS, VS>(planes + D.pl_off[2], D.bw[2] * 8, D.dw[2], D.dh[2], x0, y, crv);
+  }
+  uint32_t px[24];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int Y = (int)(((i < 4 ? ya : yb) >> (8 * (i & 3))) & 0xFFu);
+    if constexpr (GRAY) {
+      px[3 * i] = px[3 * i + 1] = px[3 * i + 2] = (uint32_t)Y;
+    } else {
+      const int xb = cbv[i] - 128, xr = crv[i] - 128;
+      px[3 * i + 0] = jpg_clamp(Y + ((116130 * xb + 32768) >> 16));                   // B
+      px[3 * i + 1] = jpg_clamp(Y + ((-46802 * xr + (-22554 * xb + 32768)) >> 16));  // G
+      px[3 * i + 2] = jpg_clamp(Y + ((91881 * xr + 32768) >> 16));                    // R
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    o[j] = px[4 * j] | px[4 * j + 1] << 8 | px[4 * j + 2] << 16 | px[4 * j + 3] << 24;
+}
+
+// grid (tiles of 256 x 8 pixels, n); images whose planes do not fit the 8-pixel form use
+// jpeg_color_kernel
+__global__ __launch_bounds__(256) void jpeg_color8_kernel(const JpegDev* __restrict__ imgs,
+                                                          const uint8_t* __restrict__ planes,
+                                                          uint8_t* __restrict__ dst, int h, int w,
+                                                          int64_t row_stride) {
+  const JpegDev& D = imgs[blockIdx.y];
+  const int ow = (w + 7) / 8;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)h * ow) return;
+  const int y = (int)(q / ow), x0 = 8 * (int)(q - (int64_t)y * ow);
+  uint32_t o[6];
+  if (D.ncomp == 1) jpg_color8<1, 1, true>(D, planes, x0, y, o);
+  else if (D.hmax == 1) jpg_color8<1, 1, false>(D, planes, x0, y, o);
+  else if (D.vmax == 1) jpg_color8<2, 1, false>(D, planes, x0, y, o);
+  else jpg_color8<2, 2, false>(D, planes, x0, y, o);
+  uint8_t* p = dst + (int64_t)blockIdx.y * h * row_stride + (int64_t)y * row_stride + (int64_t)x0 * 3;
+  if (x0 + 8 <= w && ((uintptr_t)p & 7) == 0) {
+    uint2* p2 = reinterpret_cast<uint2*>(p);
+    p2[0] = make_uint2(o[0], o[1]);
+    p2[1] = make_uint2(o[2], o[3]);
+    p2[2] = make_uint2(o[4], o[5]);
+  } else if (x0 + 8 <= w && ((uintptr_t)p & 3) == 0) {
+    uint32_t* p4 = reinterpret_cast<uint32_t*>(p);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) p4[j] = o[j];
+  } else {
+    for (int k = 0; k < 24 && x0 + k / 3 < w; ++k) p[k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
   }
 }
 
@@ -1164,8 +1299,7 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
       if (it > P.max_items + 2)
         return set_error(IDN_EHIP, "idn_jpeg_decode_u8: entropy decoding did not converge");
     }
-    hipLaunchKernelGGL(jpeg_prefix_kernel, dim3((n + 63) / 64), dim3(64), 0, st, dimg, cnt,
-                       cstart, n);
+    hipLaunchKernelGGL(jpeg_prefix_kernel, dim3(n), dim3(256), 0, st, dimg, cnt, cstart, n);
   }
   hipLaunchKernelGGL(jpeg_write_kernel, gitems, dim3(64), 0, st, dimg, ub, ublen, ivs, S[cur],
                      cstart, coef);
@@ -1174,9 +1308,15 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)gb), dim3(256), 0, st, dimg,
                      reinterpret_cast<const uint64_t*>(ws + P.off_blkend), n, P.nblk, coef,
                      ws + P.off_planes);
-  const int64_t gx = ((int64_t)h * ((w + 3) / 4) + 255) / 256;
-  hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
-                     ws + P.off_planes, dst, h, w, row_stride);
+  if (env_int("IDN_JPEG_COLOR8", 1)) {
+    const int64_t gx = ((int64_t)h * ((w + 7) / 8) + 255) / 256;
+    hipLaunchKernelGGL(jpeg_color8_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
+                       ws + P.off_planes, dst, h, w, row_stride);
+  } else {
+    const int64_t gx = ((int64_t)h * ((w + 3) / 4) + 255) / 256;
+    hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
+                       ws + P.off_planes, dst, h, w, row_stride);
+  }
   // the staging buffer is reused by the next call: finish here
   if (hipStreamSynchronize(st) != hipSuccess)
     return set_error(IDN_EHIP, "idn_jpeg_decode_u8: decode failed");
