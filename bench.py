@@ -262,7 +262,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         fn(img)
         n_img += nb
         el = time.perf_counter() - t0
-        if el >= budget_s or n_img >= 20000:
+        if el >= budget_s or n_img >= 1000000:
             break
     if op in ("noise_gaussian", "noise_sap", "noise_poisson", "wavelet_haar3", "cfg5",
               "wavelet_bior15"):
@@ -336,6 +336,11 @@ def parse_args(argv=None):
                     help="weak: every rank filters --batch images; strong: --batch images in "
                          "total, split into contiguous shards over the ranks")
     ap.add_argument("--op", default="gauss5", choices=sorted(OPS))
+    ap.add_argument("--settle-s", type=float, default=0.5,
+                    help="after the W warmup steps, keep stepping (untimed) until this many seconds "
+                         "of sustained load have passed: the GPU's power controller settles the "
+                         "clocks of a power-capped kernel over the first ~30-50 ms "
+                         "(profiles/r02/clock/), and the timed K steps should see that steady state")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-copy", action="store_true", help="skip the same-run copy ceiling")
     ap.add_argument("--gather", action="store_true",
@@ -424,6 +429,14 @@ def main():
     for _ in range(args.warmup):
         call(idn, x, y)
     torch.cuda.synchronize()
+    # sustained-load settle (untimed): chunks of launches until settle_s seconds have passed
+    settle_steps, ts0 = 0, time.perf_counter()
+    while time.perf_counter() - ts0 < args.settle_s:
+        for _ in range(16):
+            call(idn, x, y)
+        settle_steps += 16
+        torch.cuda.synchronize()
+    settle_s = time.perf_counter() - ts0
 
     stream = torch.cuda.current_stream()
     # kernel time: one HIP event pair around the K back-to-back launches on the launch stream
@@ -497,6 +510,9 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"seconds": round(settle_s, 3), "steps": settle_steps,
+                       "why": "untimed sustained load after the warmup steps so the timed steps "
+                              "run at the power controller's steady-state clocks"},
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,

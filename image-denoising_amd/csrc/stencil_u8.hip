@@ -265,8 +265,10 @@ __device__ __forceinline__ v4u ring_row(const uint32_t (&Rg)[Stencil<OP>::K][8],
   V.SO[1] = from_prev_lane(Vs[7]);
   V.SE[6] = from_next_lane(Vs[0]);
   V.SO[6] = from_next_lane(Vs[4]);
-  if (g.fix_t0) vwin_tail_fix<C>(V, 24);
-  if (g.fix_t8) vwin_tail_fix<C>(V, 16);
+  if (g.tail) {  // scalar branch: the other segments' waves skip the masked tail fix-ups
+    if (g.fix_t0) vwin_tail_fix<C>(V, 24);
+    if (g.fix_t8) vwin_tail_fix<C>(V, 16);
+  }
   uint32_t A[8];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -299,7 +301,7 @@ __device__ __forceinline__ void lds_take_row(const uint8_t* tile, uint32_t o, bo
 
 constexpr int RING_WGT = 192;
 enum RingPre { PRE_NONE = 0, PRE_GAUSSIAN = 1, PRE_SPECKLE = 2, PRE_SAP = 3 };
-enum RingEpi { EPI_U8 = 0, EPI_BLOB = 1 };
+enum RingEpi { EPI_U8 = 0, EPI_BLOB = 1, EPI_FLAT = 2 };
 
 struct RingArgs {
   const uint8_t* src;
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
   const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
   const rsrc_t rs = make_rsrc(src + (size_t)g.img * img_bytes, img_bytes);
-  const rsrc_t rd = EPI == EPI_U8 ? make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes)
+  const rsrc_t rd = EPI != EPI_BLOB ? make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes)
                                   : make_rsrc(blob + (size_t)g.img * img_bytes, 4u * img_bytes);
 
   const int y0 = g.band * NB;
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     }
   }
   __syncthreads();
-  if (wave >= nseg || item >= total_items || y0 >= y1) return;
+  const bool active = !(wave >= nseg || item >= total_items || y0 >= y1);  // wave-uniform
+  if (EPI != EPI_FLAT && !active) return;
 
   const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
   const int nin = (y1 - y0) + 2 * R;
@@ -419,6 +422,54 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
     lds_take_row<C>(tile, (uint32_t)(y - ys) * (uint32_t)rb + shift + ld_off, g.lead, Rg[r % K]);
   };
+  if constexpr (EPI == EPI_FLAT) {
+    // Flat epilogue: the band's NB output rows are contiguous in HBM too.  Each wave keeps its
+    // rows in registers until every wave has read the tile, stages them in LDS over the tile in
+    // image order, and the workgroup stores the band flat -- 16 B per lane, consecutive lanes on
+    // consecutive addresses, whole 128-B lines except the two a band shares with its neighbours
+    // -- where the row segments' own stores leave partial lines at every segment and row edge.
+    // The host takes this form when NB * rb, the image size and dst are 16-byte multiples.
+    v4u ov[NB];
+    if (active) {
+#pragma unroll
+      for (int r = 0; r < 2 * R; ++r) take_row(r);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int r = 2 * R + u;
+        take_row(r);
+        ov[u] = ring_row<C, OP>(Rg, r % K, g);
+        // one row at a time: without the fence the scheduler hoists every row's LDS reads and
+        // the held output rows push the kernel past 128 VGPRs (3 waves per SIMD)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();  // the tile is consumed: reuse it for the output band
+    if (active && g.kind != 0) {
+      const uint32_t lo = g.kind == 3 ? (uint32_t)g.q + 8u : (uint32_t)g.q;
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (y0 + u < y1) {
+          const uint32_t o = (uint32_t)u * (uint32_t)rb + lo;
+          const v2u a = g.kind == 3 ? v2u{ov[u].z, ov[u].w} : v2u{ov[u].x, ov[u].y};
+          *reinterpret_cast<v2u*>(&tile[o]) = a;
+          if (g.kind == 1) *reinterpret_cast<v2u*>(&tile[o + 8]) = v2u{ov[u].z, ov[u].w};
+        }
+      }
+    }
+    __syncthreads();
+    constexpr int NLO = (NB * TILE_RBMAX + 16 * TILE_WGT - 1) / (16 * TILE_WGT);
+    // bytes of the band (0 for a workgroup past the batch: it stores nothing)
+    const uint32_t nout = (item < total_items && y1 > y0) ? (uint32_t)(y1 - y0) * (uint32_t)rb : 0u;
+    const uint32_t gbase = (uint32_t)y0 * (uint32_t)rb;
+#pragma unroll
+    for (int i = 0; i < NLO; ++i) {
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
+      const v4u v = *reinterpret_cast<const v4u*>(&tile[o < nout ? o : 0u]);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rd, o < nout ? gbase + o : OOB_OFF, 0,
+                                             (NT & 2) ? 2 : 0);
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 2 * R; ++r) take_row(r);
 #pragma unroll
@@ -436,6 +487,108 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   }
 }
 
+
+// ---- persistent band-tile form with register prefetch ------------------------------------------
+// The tile form above stops fetching while its waves filter: a resident workgroup alternates a
+// burst of loads with a stretch of arithmetic, so the bytes in flight per CU dip whenever several
+// of its workgroups filter at once.  Here a resident workgroup walks a sequence of bands and
+// issues the NEXT band's tile loads into registers right after staging the current one, so its
+// loads are in flight for the whole filtering of the current band:
+//   prefetch(t0) -> [ barrier; registers -> LDS; barrier; prefetch(t + P); filter band t ] ...
+// Band order keeps neighbours together: XCD x (blockIdx & 7) owns the contiguous band range
+// [T x / 8, T (x + 1) / 8) of the flattened (image, band) list, and its P/8 workgroups take
+// consecutive bands at every step, so a band's halo rows were fetched by the band before it on
+// the same XCD moments earlier and come from that XCD's L2.
+template <int C, int OP, int NB, int NT>
+__global__ __launch_bounds__(TILE_WGT) void stencil_u8_pf(const uint8_t* __restrict__ src,
+                                                         uint8_t* __restrict__ dst, int h, int rb,
+                                                         int nseg, int seg_len, int bands,
+                                                         int total_bands) {
+  constexpr int K = Stencil<OP>::K;
+  constexpr int R = K / 2;
+  using TS = TileShape<NB, K>;
+  __shared__ __attribute__((aligned(16))) uint8_t tile[TS::LDS];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int xcd = blockIdx.x & 7, per = gridDim.x >> 3;  // gridDim.x % 8 == 0 (host)
+  const int t_lo = (int)(((int64_t)total_bands * xcd) >> 3);
+  const int t_hi = (int)(((int64_t)total_bands * (xcd + 1)) >> 3);
+  const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
+
+  // fetch geometry of band t (workgroup-uniform)
+  struct Fetch {
+    int img, y0, y1, ys;
+    uint32_t base_al, shift, nbytes;
+  };
+  auto fetch_geom = [&](int t) {
+    Fetch f;
+    f.img = t / bands;
+    const int band = t - f.img * bands;
+    f.y0 = band * NB;
+    f.y1 = min(f.y0 + NB, h);
+    f.ys = max(f.y0 - R, 0);
+    const int ye = min(f.y1 + R, h);
+    const uint32_t base = (uint32_t)f.ys * (uint32_t)rb;
+    f.base_al = base & ~15u;
+    f.shift = base - f.base_al;
+    f.nbytes = (uint32_t)ye * (uint32_t)rb - f.base_al;
+    return f;
+  };
+  v4u v[TS::NL];
+  auto prefetch = [&](const Fetch& f) {
+    const rsrc_t rs = make_rsrc(src + (size_t)f.img * img_bytes, img_bytes);
+#pragma unroll
+    for (int i = 0; i < TS::NL; ++i) {
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < f.nbytes ? f.base_al + o : OOB_OFF, 0,
+                                                    (NT & 1) ? 2 : 0);
+    }
+  };
+
+  int t = t_lo + (int)(blockIdx.x >> 3);
+  Fetch f = fetch_geom(t < t_hi ? t : t_lo);
+  if (t < t_hi) prefetch(f);
+#pragma unroll 1
+  for (; t < t_hi; t += per) {
+    __syncthreads();  // every wave has finished reading the previous band's tile
+#pragma unroll
+    for (int i = 0; i < TS::NL; ++i) {
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
+      if (o < f.nbytes) *reinterpret_cast<v4u*>(&tile[o]) = v[i];
+    }
+    __syncthreads();
+    const Fetch cur = f;
+    if (t + per < t_hi) {  // the next band's loads stay in flight while this band is filtered
+      f = fetch_geom(t + per);
+      prefetch(f);
+    }
+    if (wave >= nseg) continue;  // rows narrower than 3 segments: the spare wave only fetches
+    const int band = t - cur.img * bands;
+    const StripeGeom g = stripe_geom((cur.img * bands + band) * nseg + wave, lane, rb, nseg,
+                                     seg_len, bands);
+    const rsrc_t rd = make_rsrc(dst + (size_t)cur.img * img_bytes, img_bytes);
+    const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
+    const int nin = (cur.y1 - cur.y0) + 2 * R;
+    const StoreOffs so = store_offs(g);
+    uint32_t Rg[K][8];
+    auto take_row = [&](int r) {
+      const int y = reflect101_1(cur.y0 - R + min(r, nin - 1), h);
+      lds_take_row<C>(tile, (uint32_t)(y - cur.ys) * (uint32_t)rb + cur.shift + ld_off, g.lead,
+                      Rg[r % K]);
+    };
+#pragma unroll
+    for (int r = 0; r < 2 * R; ++r) take_row(r);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int r = 2 * R + u;
+      take_row(r);
+      const int y = cur.y0 + u;
+      ring_out_row<C, OP, NT>(Rg, r % K, g, rd, so,
+                              y < cur.y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF);
+    }
+  }
+}
 
 // ---- streaming ring form (+ fused noise prologue / blob epilogue) ------------------------------
 // One workgroup (3 waves) walks a STRIP of consecutive bands of one image top to bottom.  The
@@ -763,6 +916,27 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
       case 5: launch_ring<OP, 2, 3, 38, 0, 0, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 4, st); break;
       default: launch_ring<OP, 6, 1, 64, 0, 0, PRE_NONE, EPI_U8>(a, n, h, (int)rb, 2, st); break;
     }
+  } else if (env_int("IDN_STENCIL_PF", 0) && tile_mode && stripe_ok(c, rb, row_stride, h, src, dst) &&
+             row_stride == rb && rb <= TILE_RBMAX && h > 2 * R) {
+    // persistent register-prefetch form: as many 3-wave workgroups as are resident (LDS-bound),
+    // a multiple of 8 (one band range per XCD)
+    const int nseg = (int)((rb + 1007) / 1008);
+    const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
+    constexpr int NBP = 6;
+    const int bands = (h + NBP - 1) / NBP;
+    const int64_t total = (int64_t)n * bands;
+    IDN_CHECK_ARG(total * nseg < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
+    const int per_cu = 160 * 1024 / TileShape<NBP, K>::LDS;
+    int64_t grid = (int64_t)cu_count() * per_cu;
+    const int64_t want = (total + 7) / 8 * 8;
+    if (grid > want) grid = want;
+    grid = (grid + 7) / 8 * 8;
+    if (ntst)
+      hipLaunchKernelGGL((stencil_u8_pf<3, OP, NBP, 2>), dim3((unsigned)grid), dim3(TILE_WGT), 0,
+                         st, src, dst, h, (int)rb, nseg, seg_len, bands, (int)total);
+    else
+      hipLaunchKernelGGL((stencil_u8_pf<3, OP, NBP, 0>), dim3((unsigned)grid), dim3(TILE_WGT), 0,
+                         st, src, dst, h, (int)rb, nseg, seg_len, bands, (int)total);
   } else if (tile_mode && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
       rb <= TILE_RBMAX && h > 2 * R) {
     const int nseg = (int)((rb + 1007) / 1008);
@@ -774,20 +948,26 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
     const int64_t total = (int64_t)n * bands * nseg;
     IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
     const dim3 grid((unsigned)((int64_t)n * bands)), block(TILE_WGT);
+    // flat output epilogue (EPI_FLAT): band starts and image bases on 16-byte boundaries
+    const int flat_cfg = env_int("IDN_STENCIL_FLAT", 0);
+    const bool flat = flat_cfg != 0 && ((int64_t)nb * rb) % 16 == 0 &&
+                      ((int64_t)h * rb) % 16 == 0 && ((uintptr_t)dst & 15) == 0;
 #define IDN_LAUNCH_TILE_NT(NBX, NTV)                                                              \
-  hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, NTV>), grid, block, 0, st, src, dst, h, (int)rb,   \
-                     nseg, seg_len, bands, (int)total, map)
+  if (flat)                                                                                       \
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, NTV, EPI_FLAT>), grid, block, 0, st, src, dst, \
+                       h, (int)rb, nseg, seg_len, bands, (int)total, map);                        \
+  else                                                                                            \
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, NTV>), grid, block, 0, st, src, dst, h,         \
+                       (int)rb, nseg, seg_len, bands, (int)total, map)
 #define IDN_LAUNCH_TILE(NBX)                                                                      \
   if (ntmode == 1)                                                                                \
     IDN_LAUNCH_TILE_NT(NBX, 1);                                                                   \
   else if (ntmode == 3)                                                                           \
     IDN_LAUNCH_TILE_NT(NBX, 3);                                                                   \
   else if (ntst)                                                                                  \
-    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, 2>), grid, block, 0, st, src, dst, h, (int)rb, \
-                       nseg, seg_len, bands, (int)total, map);                                    \
+    IDN_LAUNCH_TILE_NT(NBX, 2);                                                                   \
   else                                                                                            \
-    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NBX, 0>), grid, block, 0, st, src, dst, h, (int)rb, \
-                       nseg, seg_len, bands, (int)total, map)
+    IDN_LAUNCH_TILE_NT(NBX, 0)
     if (tile_mode == 2) {
       IDN_LAUNCH_TILE(NB2);
     } else if (tile_mode == 3) {

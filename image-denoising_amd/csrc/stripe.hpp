@@ -202,6 +202,7 @@ struct StripeGeom {
   int seg, band, img;
   int seg_start, seg_end, q;
   bool lead, fix_t0, fix_t8;
+  bool tail;  // wave-uniform: the wave owns the row's last segment (the only one with fix lanes)
   int kind;  // 0 none, 1 full 16 B, 2 low 8 B, 3 high 8 B
 };
 
@@ -217,6 +218,7 @@ __device__ __forceinline__ StripeGeom stripe_geom(int item, int lane, int rb, in
   g.q = g.seg_start - 8 + 16 * lane;
   g.lead = (g.seg_start == 0) && (lane == 0);
   const bool last_seg = (g.seg_end == rb);
+  g.tail = last_seg;
   const int tail = (rb - g.seg_start + 8) & 15;
   g.fix_t0 = last_seg && tail == 0 && (g.q + 16 == rb);
   g.fix_t8 = last_seg && tail == 8 && (g.q + 8 == rb);
