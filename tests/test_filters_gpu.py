@@ -85,6 +85,9 @@ FORMS = [
     {"IDN_STENCIL_TILE": "3"},                 # LDS tile, 8 / 4-row bands
     {"IDN_STENCIL_TILE": "1", "IDN_STENCIL_MAP": "2", "IDN_STENCIL_NT": "2"},
     {"IDN_STENCIL_TILE": "0"},                 # stripe form, short bands from HBM
+    {"IDN_STENCIL_FLAT": "1"},                 # flat-output epilogue (16-B aligned bands only)
+    {"IDN_STENCIL_FLAT": "1", "IDN_STENCIL_TILE": "3", "IDN_STENCIL_NT": "2"},
+    {"IDN_STENCIL_PF": "1"},                   # persistent register-prefetch form
 ]
 
 
