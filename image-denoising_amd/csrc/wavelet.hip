@@ -1479,6 +1479,17 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
   __shared__ double red[3 * L * 3][WLH_WG / 64];
   __shared__ uint32_t xq[WLS_XCAP];  // queued uncertain codes: position * 4 + channel
   __shared__ uint32_t xq_n;
+  // levels 2..L moments in LDS, one private column per thread ([k][thread]: consecutive lanes on
+  // consecutive banks, ds_add_u32 without conflicts): 36 fewer VGPRs than register accumulators,
+  // which with the one-ahead prefetch brings the kernel from 2 to 3 waves per SIMD
+  // (level 3: one column per 8x8 block, written by its sub-block-0 lane only)
+  __shared__ int ml2[3 * 6][WLH_WG];
+  __shared__ int ml3[L == 3 ? 3 * 6 : 1][WLH_WG / 4];
+#pragma unroll
+  for (int k = 0; k < 3 * 6; ++k) ml2[k][threadIdx.x] = 0;
+  if (L == 3 && threadIdx.x < WLH_WG / 4)
+#pragma unroll
+    for (int k = 0; k < 3 * 6; ++k) ml3[k][threadIdx.x] = 0;
   if (threadIdx.x == 0) xq_n = 0u;
   __syncthreads();
   const size_t W1 = (size_t)(w / 2), bsz = (size_t)(h / 2) * W1;
@@ -1491,17 +1502,25 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
     wl_minmax64(st, c, mn, mx);
     sc[c] = uniform_f64(0.5 / (255000.0 * (mx - mn)));
   }
-  int mom[L][3][6];
+  int mom[3][6];  // level 1 (levels >= 2: mlds)
 #pragma unroll
-  for (int l = 0; l < L; ++l)
+  for (int b = 0; b < 3; ++b)
 #pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int k = 0; k < 6; ++k) mom[l][b][k] = 0;
+    for (int k = 0; k < 6; ++k) mom[b][k] = 0;
+  auto mom_lds = [&](int l, int b, int r, int g, int bl) {  // level l >= 1 (0-based)
+    const int ld = l == 1 ? WLH_WG : WLH_WG / 4;  // row pitch of the level's array
+    int* m = l == 1 ? &ml2[b * 6][threadIdx.x] : &ml3[(L == 3 ? b : 0) * 6][threadIdx.x >> 2];
+    atomicAdd(m + 0 * ld, __mul24(r, r));
+    atomicAdd(m + 1 * ld, __mul24(g, g));
+    atomicAdd(m + 2 * ld, __mul24(bl, bl));
+    atomicAdd(m + 3 * ld, __mul24(r, g));
+    atomicAdd(m + 4 * ld, __mul24(r, bl));
+    atomicAdd(m + 5 * ld, __mul24(g, bl));
+  };
   const uint8_t* ib = src + (int64_t)img * h * row_stride;
   uint16_t* cdp0 = reinterpret_cast<uint16_t*>(ws + img * img_floats + dd_off + 3 * bsz);
   // sub-block geometry of iteration `it`; its 4 rows x 12 bytes (dword aligned: checked on the
-  // host) are loaded two iterations ahead (two waves per SIMD at this register count)
+  // host) are loaded one iteration ahead
   auto geom = [&](int it, int& sub, int& y0, int& x0) -> bool {
     const int tid = (blockIdx.x * WLS_IT + it) * WLH_WG + threadIdx.x;
     const int blk = tid / HS::NS;
@@ -1522,9 +1541,8 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
       for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
     }
   };
-  uint32_t qn[4][3] = {}, qn2[4][3] = {};
+  uint32_t qn[4][3] = {};
   load_q(0, qn);
-  load_q(1, qn2);
 #pragma unroll 1
   for (int it = 0; it < WLS_IT; ++it) {
     int sub, y0, x0;
@@ -1533,11 +1551,8 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        q[r][k] = qn[r][k];
-        qn[r][k] = qn2[r][k];
-      }
-    if (it + 2 < WLS_IT) load_q(it + 2, qn2);
+      for (int k = 0; k < 3; ++k) q[r][k] = qn[r][k];
+    if (it + 1 < WLS_IT) load_q(it + 1, qn);
     int a2[3] = {0, 0, 0};
     if (act) {
       auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
@@ -1553,7 +1568,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
                      px(2 * gy + 1, 6 * gx + ch), px(2 * gy + 1, 6 * gx + 3 + ch),
                      a1[gy * 2 + gx][ch], D[0][ch], D[1][ch], D[2][ch]);
 #pragma unroll
-          for (int b = 0; b < 3; ++b) mom_add(mom[0][b], D[b][0], D[b][1], D[b][2]);
+          for (int b = 0; b < 3; ++b) mom_add(mom[b], D[b][0], D[b][1], D[b][2]);
           const size_t cpos = (size_t)(y0 / 2 + gy) * W1 + (size_t)(x0 / 2 + gx);
           uint32_t code[3], unsure = 0u;
 #pragma unroll
@@ -1591,7 +1606,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
         haar_int(a1[0][ch], a1[1][ch], a1[2][ch], a1[3][ch], a2[ch], D2[0][ch], D2[1][ch],
                  D2[2][ch]);
 #pragma unroll
-      for (int b = 0; b < 3; ++b) mom_add(mom[1][b], D2[b][0], D2[b][1], D2[b][2]);
+      for (int b = 0; b < 3; ++b) mom_lds(1, b, D2[b][0], D2[b][1], D2[b][2]);
     }
     if constexpr (L == 3) {  // level 3 across the block's 4 lanes (all lanes take part)
       const int base = (threadIdx.x & 63) & ~3;
@@ -1604,7 +1619,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
       }
       if (act && sub == 0)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) mom_add(mom[2][b], D3[b][0], D3[b][1], D3[b][2]);
+        for (int b = 0; b < 3; ++b) mom_lds(2, b, D3[b][0], D3[b][1], D3[b][2]);
     }
     // the queued uncertain codes, densely over the workgroup, once the queue could overflow in
     // the next iteration (and after the last one)
@@ -1636,7 +1651,12 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_stats(
       const double s = ldexp(sc[c], -l);  // 2^-(l+1) / (255000 inv)
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
-        const int* m = mom[l][b];
+        int m[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          m[k] = l == 0 ? mom[b][k]
+                 : l == 1 ? ml2[b * 6 + k][threadIdx.x]
+                          : ((threadIdx.x & 3) == 0 ? ml3[(L == 3 ? b : 0) * 6 + k][threadIdx.x >> 2] : 0);
         double v = w0 * w0 * (double)m[0] + w1 * w1 * (double)m[1] + w2 * w2 * (double)m[2] +
                    2.0 * (w0 * w1 * (double)m[3] + w0 * w2 * (double)m[4] + w1 * w2 * (double)m[5]);
         v *= s * s;
