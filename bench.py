@@ -549,6 +549,9 @@ def main():
             rec["copy_ceiling_GBps"] = ceiling["copy_ceiling_GBps"]
             rec["roofline"]["frac_of_copy_ceiling"] = round(
                 achieved_gbs / ceiling["copy_ceiling_GBps"], 4)
+            # the stencil's own cache policy (default loads / stores) against the same-policy copy
+            rec["roofline"]["frac_of_default_policy_copy"] = round(
+                achieved_gbs / ceiling["by_policy"]["default"], 4)
             rec["copy_ceiling"] = ceiling
         if args.op == "cfg5":  # the drawn noise mix (record it in the output)
             rec["config"]["mix"] = {k: len(v[0]) for k, v in call.state["groups"].items()}
