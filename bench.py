@@ -512,7 +512,9 @@ def main():
             "warmup": args.warmup,
             "settle": {"seconds": round(settle_s, 3), "steps": settle_steps,
                        "why": "untimed sustained load after the warmup steps so the timed steps "
-                              "run at the power controller's steady-state clocks"},
+                              "run at the power controller's steady-state clocks (the first "
+                              "~30-50 ms of load swing 160-200 us per launch; see "
+                              "profiles/r02/clock/README.md)"},
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
