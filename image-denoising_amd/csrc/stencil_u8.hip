@@ -31,12 +31,16 @@
 
 namespace idn {
 
-enum StencilOp { OP_GAUSS3 = 0, OP_GAUSS5 = 1, OP_BOX3 = 2 };
+// OP_IDENT5: tuning probe only (IDN_STENCIL_IDENT=1 on the 5x5 Gaussian entry point) -- the 5x5
+// kernels' memory structure (tile fetch, halo rows, stores) with the arithmetic reduced to a copy
+// of the centre byte, to separate what the data movement costs from what the taps cost
+enum StencilOp { OP_GAUSS3 = 0, OP_GAUSS5 = 1, OP_BOX3 = 2, OP_IDENT5 = 3 };
 
 template <int OP> struct Stencil;
 template <> struct Stencil<OP_GAUSS3> { static constexpr int K = 3; };
 template <> struct Stencil<OP_GAUSS5> { static constexpr int K = 5; };
 template <> struct Stencil<OP_BOX3> { static constexpr int K = 3; };
+template <> struct Stencil<OP_IDENT5> { static constexpr int K = 5; };
 
 // ---- vertical-first fast path --------------------------------------------------------------
 // Halo rows of a band cost only their unpack (8 ops); the horizontal pass runs per output row.
@@ -58,7 +62,9 @@ __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t k, uint32_t c) {
 template <int OP>
 __device__ __forceinline__ uint32_t vtap(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
                                          uint32_t r4) {
-  if constexpr (OP == OP_GAUSS5) {
+  if constexpr (OP == OP_IDENT5) {
+    return r2;
+  } else if constexpr (OP == OP_GAUSS5) {
     // [1 4 6 4 1] + 8 per lane (x16 horizontal weight = the +128 rounding bias): <= 4088
     const uint32_t t = ((r1 + r3) << 2) + 0x00080008u;
     return r0 + r4 + mad24(r2, 6u, t);
@@ -74,7 +80,9 @@ __device__ __forceinline__ uint32_t vtap(uint32_t r0, uint32_t r1, uint32_t r2, 
 // two dwords (lo lane, hi lane)
 template <int C, int OP>
 __device__ __forceinline__ uint32_t htap(const VWin& V, int P) {
-  if constexpr (OP == OP_GAUSS5) {
+  if constexpr (OP == OP_IDENT5) {
+    return V.at(P) << 8;  // the centre byte into the high byte of each u16 lane
+  } else if constexpr (OP == OP_GAUSS5) {
     const uint32_t t = (V.at(P - C) + V.at(P + C)) << 2;
     return V.at(P - 2 * C) + V.at(P + 2 * C) + pk_mad16(V.at(P), 0x00060006u, t);
   } else if constexpr (OP == OP_GAUSS3) {
@@ -1039,6 +1047,9 @@ extern "C" int idn_gaussian_blur_u8(const uint8_t* src, uint8_t* dst, int n, int
   if (n == 0) return IDN_OK;
   if (ksize == 3)
     return launch_stencil<OP_GAUSS3>(src, dst, n, h, w, c, row_stride, as_stream(stream),
+                                     "idn_gaussian_blur_u8");
+  if (ksize == 5 && env_int("IDN_STENCIL_IDENT", 0))  // tuning probe: copy through the 5x5 form
+    return launch_stencil<OP_IDENT5>(src, dst, n, h, w, c, row_stride, as_stream(stream),
                                      "idn_gaussian_blur_u8");
   if (ksize == 5)
     return launch_stencil<OP_GAUSS5>(src, dst, n, h, w, c, row_stride, as_stream(stream),
