@@ -406,11 +406,23 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   // flat fetch of the tile into LDS (out-of-image lanes read 0 and are not written)
   {
     v4u v[TS::NL];
+    // split policy (NT & 4): chunks inside the band's private rows [y0 + R, y1 - R) -- rows no
+    // neighbouring band fetches -- load nontemporal, the rest default; two loads per chunk, the
+    // unused one at an out-of-range offset (no memory access, returns 0)
+    const uint32_t p_lo = (uint32_t)(y0 + R) * (uint32_t)rb - base_al;
+    const uint32_t p_hi = y1 - R > y0 + R ? (uint32_t)(y1 - R) * (uint32_t)rb - base_al : p_lo;
 #pragma unroll
     for (int i = 0; i < TS::NL; ++i) {
       const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
-      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < nbytes ? base_al + o : OOB_OFF, 0,
-                                                    (NT & 1) ? 2 : 0);
+      const uint32_t off = o < nbytes ? base_al + o : OOB_OFF;
+      if constexpr ((NT & 4) != 0) {
+        const bool priv = o >= p_lo && o + 16u <= p_hi;
+        const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, priv ? OOB_OFF : off, 0, 0);
+        const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rs, priv ? off : OOB_OFF, 0, 2);
+        v[i] = a | b;
+      } else {
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, (NT & 1) ? 2 : 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < TS::NL; ++i) {
@@ -909,7 +921,10 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
   constexpr int R = K / 2;
   const int64_t rb = (int64_t)w * c;
   const int tile_mode = env_int("IDN_STENCIL_TILE", 1);
-  const int ntmode = env_int("IDN_STENCIL_NT", 0) & 3;  // cache-policy variants (tuning)
+  // cache-policy variants (tuning): bit 0 nontemporal loads, bit 1 nontemporal stores, bit 2
+  // split loads (nontemporal only for the band's private rows, default for the halo rows its
+  // neighbours read too)
+  const int ntmode = env_int("IDN_STENCIL_NT", 0) & 7;
   const bool ntst = (ntmode & 2) != 0;  // nontemporal stores
   const int map = env_int("IDN_STENCIL_MAP", 1) == 2 ? 2 : 1;
   const int ring_cfg = env_int("IDN_STENCIL_RING", 0);  // the band-tiled form is faster plain
@@ -970,6 +985,8 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
 #define IDN_LAUNCH_TILE(NBX)                                                                      \
   if (ntmode == 1)                                                                                \
     IDN_LAUNCH_TILE_NT(NBX, 1);                                                                   \
+  else if (ntmode == 6)                                                                           \
+    IDN_LAUNCH_TILE_NT(NBX, 6);                                                                   \
   else if (ntmode == 3)                                                                           \
     IDN_LAUNCH_TILE_NT(NBX, 3);                                                                   \
   else if (ntst)                                                                                  \
