@@ -1234,10 +1234,11 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     // the entropy segments, gathered by a few host threads in NPART parts of the batch; each
     // part's host-to-device copy is issued as soon as the part is complete, so the DMA of part
     // k overlaps the gathering of part k + 1
-    const int nt = std::max(1, std::min(8, n / 8));
-    const int npart = std::max(1, std::min(4, n / 16));
-    std::atomic<int> done[4];
-    for (int q = 0; q < 4; ++q) done[q].store(0);
+    constexpr int MAXPART = 16;
+    const int nt = std::max(1, std::min(env_int("IDN_JPEG_THREADS", 8), std::max(1, n / 8)));
+    const int npart = std::max(1, std::min(std::min(env_int("IDN_JPEG_PARTS", 4), MAXPART), n / 16));
+    std::atomic<int> done[MAXPART];
+    for (int q = 0; q < MAXPART; ++q) done[q].store(0);
     auto first = [&](int q) { return (int)((int64_t)n * q / npart); };
     auto worker = [&](int k) {
       for (int q = 0; q < npart; ++q) {
