@@ -764,35 +764,49 @@ __device__ __forceinline__ void synth_pair(const wreal (&c)[Wav<WV>::F / 2], wre
 
 // synthesise one channel's tile (bands at A, band size Nh x Nw, coefficient origin (m0, n0));
 // thread t receives the tile outputs (row 2 * (t / ST_O) + r, column t % ST_O) for the row pairs
-// of i (v[2 i + r])
+// of i (v[2 i + r]).  Split in two so a caller can keep the next channel's loads in flight while
+// this one is synthesised: synth_load issues the thread's staging loads, synth_run stages them
+// (details soft-thresholded) and runs the two passes.
 template <int WV>
-__device__ __forceinline__ void synth_tile(SynthTile<WV>& S, const wreal* __restrict__ A,
-                                           size_t bsz, int Nh, int Nw, int m0, int n0,
-                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256]) {
-  constexpr int HF = SynthTile<WV>::HF, CR = SynthTile<WV>::CR;
-  constexpr int RPT = 256 / CR;            // staging: band rows per pass (CR columns each)
-  constexpr int NRW = 4 * CR;              // band rows to stage
-  constexpr int NLD = (NRW + RPT - 1) / RPT;
-  const int cc = threadIdx.x % CR, rr0 = threadIdx.x / CR;
+struct SynthLoad {
+  static constexpr int CR = SynthTile<WV>::CR;
+  static constexpr int RPT = 256 / CR;            // staging: band rows per pass (CR columns each)
+  static constexpr int NRW = 4 * CR;              // band rows to stage
+  static constexpr int NLD = (NRW + RPT - 1) / RPT;
+  wreal x[NLD];
+};
+template <int WV>
+__device__ __forceinline__ void synth_load(SynthLoad<WV>& L, const wreal* __restrict__ A,
+                                           size_t bsz, int Nh, int Nw, int m0, int n0) {
+  using SL = SynthLoad<WV>;
+  const int cc = threadIdx.x % SL::CR, rr0 = threadIdx.x / SL::CR;
   // coefficients past the band's end feed only outputs past the level's valid length (pywt's
   // stage-2 valid convolution), which are never stored: clamped reads keep them finite
   const wreal* Ac = A + min(n0 + cc, Nw - 1);
-  wreal x[NLD];
 #pragma unroll
-  for (int u = 0; u < NLD; ++u) {  // all loads in flight before any use
-    const int br = min(rr0 + RPT * u, NRW - 1);  // band * CR + row
-    const int b = br / CR, r = br - b * CR;
-    x[u] = Ac[(size_t)b * bsz + (size_t)min(m0 + r, Nh - 1) * Nw];
+  for (int u = 0; u < SL::NLD; ++u) {  // all loads in flight before any use
+    const int br = min(rr0 + SL::RPT * u, SL::NRW - 1);  // band * CR + row
+    const int b = br / SL::CR, r = br - b * SL::CR;
+    L.x[u] = Ac[(size_t)b * bsz + (size_t)min(m0 + r, Nh - 1) * Nw];
   }
+}
+template <int WV, typename Between>
+__device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>& L,
+                                          const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256],
+                                          Between between) {
+  using SL = SynthLoad<WV>;
+  constexpr int HF = SynthTile<WV>::HF, CR = SL::CR;
+  const int cc = threadIdx.x % CR, rr0 = threadIdx.x / CR;
 #pragma unroll
-  for (int u = 0; u < NLD; ++u) {
-    const int br = rr0 + RPT * u;
-    if (rr0 < RPT && br < NRW) {
+  for (int u = 0; u < SL::NLD; ++u) {
+    const int br = rr0 + SL::RPT * u;
+    if (rr0 < SL::RPT && br < SL::NRW) {
       const int b = br / CR, r = br - b * CR;
-      S.co[b][r][cc] = b > 0 ? soft(x[u], thr[b - 1]) : x[u];
+      S.co[b][r][cc] = b > 0 ? soft(L.x[u], thr[b - 1]) : L.x[u];
     }
   }
   __syncthreads();
+  between();  // the staged registers are free: e.g. the next channel's loads
   for (int k = threadIdx.x; k < CR * (ST_O / 2); k += 256) {  // axis 1: column pairs
     const int r = k / (ST_O / 2), nn = k - r * (ST_O / 2);
     wreal c0[HF], c1[HF], c2[HF], c3[HF];
@@ -832,6 +846,14 @@ __device__ __forceinline__ void synth_tile(SynthTile<WV>& S, const wreal* __rest
     v[2 * i + 1] = __dadd_rn(lo, ho);
   }
   __syncthreads();  // S is restaged by the next call
+}
+template <int WV>
+__device__ __forceinline__ void synth_tile(SynthTile<WV>& S, const wreal* __restrict__ A,
+                                           size_t bsz, int Nh, int Nw, int m0, int n0,
+                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256]) {
+  SynthLoad<WV> L;
+  synth_load<WV>(L, A, bsz, Nh, Nw, m0, n0);
+  synth_run<WV>(S, L, thr, v, [] {});
 }
 // output position of v[e] of thread t: (row, column) inside the tile
 __device__ __forceinline__ int synth_row(int e) {
@@ -885,7 +907,12 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
   const int ti = blockIdx.x / tiles_x, tj = blockIdx.x - ti * tiles_x;
   const int p0 = ti * ST_O, q0 = tj * ST_O;
   double ych[3][NV];
-#pragma unroll 1
+  // channel c + 1's coefficient loads are issued as soon as channel c is staged in LDS, so they
+  // are in flight while channel c is synthesised (the level-1 synthesis is bound by these fp64
+  // reads: 37.5 B per output pixel)
+  SynthLoad<WV> ld;
+  synth_load<WV>(ld, base, bsz, Nh, Nw, p0 / 2, q0 / 2);
+#pragma unroll
   for (int c = 0; c < 3; ++c) {
     wreal mn, mx;
     wl_minmax64(st, c, mn, mx);
@@ -893,7 +920,9 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
     const wreal thr[3] = {st[WlStats::thr(c, 0, 0, L)], st[WlStats::thr(c, 0, 1, L)],
                           st[WlStats::thr(c, 0, 2, L)]};
     wreal v[NV];
-    synth_tile<WV>(S, base + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v);
+    synth_run<WV>(S, ld, thr, v, [&] {
+      if (c < 2) synth_load<WV>(ld, base + (size_t)(c + 1) * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2);
+    });
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       // inner denoise_wavelet clip (0.14.2), then * (max - min) + min
