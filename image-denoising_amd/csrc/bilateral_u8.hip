@@ -247,7 +247,8 @@ static void launch_bl_pre_rpt(const uint8_t* src, uint8_t* dst, int n, int h, in
                      dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
 }
 
-// RPT output rows per thread: each converted pixel feeds up to RPT outputs (RPT = 8 measured
+// RPT output rows per thread: each converted pixel feeds up to RPT outputs (RPT = 5 / 6 measured
+// 1.87 / 2.27 ms against 1.71 in steady state, though 5 % / 8 % fewer VALU per output; RPT = 8
 // worse: the compiler spills the 16 accumulators around the pins; 2 columns x 4 rows per thread,
 // 15 instead of 27 conversions per output, measured 2.18 / 1.95 ms at 3 / 2 workgroups per CU
 // against 1.74)
