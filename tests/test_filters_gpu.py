@@ -204,7 +204,8 @@ def test_bilateral_gray(dev):
 
 @pytest.mark.parametrize("form", [{"IDN_MEDIAN_MAP": "0", "IDN_MEDIAN_ROWS": "32"},
                                   {"IDN_MEDIAN_MAP": "1", "IDN_MEDIAN_ROWS": "16"},
-                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"}],
+                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"},
+                                  {"IDN_MEDIAN_TILE": "1"}],  # LDS band-tile form
                          ids=lambda f: "-".join(f"{k[11:]}{v}" for k, v in f.items()))
 @pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (1, 601, 1000), (2, 13, 104)])
 def test_median_forms_agree(dev, monkeypatch, form, shape):
