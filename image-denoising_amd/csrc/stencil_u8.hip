@@ -387,7 +387,8 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int blk = map == 1 ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // map: bits 0-1 block order (1 XCD-contiguous, 2 plain), bit 2 the full-band fast fetch
+  const int blk = (map & 3) == 1 ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   // waves beyond nseg (rows narrower than 3 segments) only help fetch the tile
   const int item = blk * nseg + min(wave, nseg - 1);
   const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
@@ -411,6 +412,25 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     // unused one at an out-of-range offset (no memory access, returns 0)
     const uint32_t p_lo = (uint32_t)(y0 + R) * (uint32_t)rb - base_al;
     const uint32_t p_hi = y1 - R > y0 + R ? (uint32_t)(y1 - R) * (uint32_t)rb - base_al : p_lo;
+    // full bands (every chunk but the last round's inside the tile): one lane offset, the round
+    // in the scalar offset, no per-load compare / select and no guarded LDS stores but the last
+    // round's (~30 fewer VALU per band: the filter runs at the power cap, so VALU is time)
+    const bool full = (NT & 4) == 0 && (map & 4) != 0 &&
+                      __builtin_amdgcn_readfirstlane(
+                          (int)(nbytes >= (uint32_t)(16 * TILE_WGT * (TS::NL - 1))));
+    if (full) {
+      const uint32_t vo = base_al + 16u * threadIdx.x;
+#pragma unroll
+      for (int i = 0; i < TS::NL - 1; ++i)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 16 * TILE_WGT * i, (NT & 1) ? 2 : 0);
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * (TS::NL - 1) + threadIdx.x);
+      v[TS::NL - 1] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < nbytes ? base_al + o : OOB_OFF,
+                                                            0, (NT & 1) ? 2 : 0);
+#pragma unroll
+      for (int i = 0; i < TS::NL - 1; ++i)
+        *reinterpret_cast<v4u*>(&tile[16u * (uint32_t)(TILE_WGT * i + threadIdx.x)]) = v[i];
+      if (o < nbytes) *reinterpret_cast<v4u*>(&tile[o]) = v[TS::NL - 1];
+    } else {
 #pragma unroll
     for (int i = 0; i < TS::NL; ++i) {
       const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
@@ -428,6 +448,7 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     for (int i = 0; i < TS::NL; ++i) {
       const uint32_t o = 16u * (uint32_t)(TILE_WGT * i + threadIdx.x);
       if (o < nbytes) *reinterpret_cast<v4u*>(&tile[o]) = v[i];
+    }
     }
   }
   __syncthreads();
@@ -926,7 +947,8 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
   // neighbours read too)
   const int ntmode = env_int("IDN_STENCIL_NT", 0) & 7;
   const bool ntst = (ntmode & 2) != 0;  // nontemporal stores
-  const int map = env_int("IDN_STENCIL_MAP", 1) == 2 ? 2 : 1;
+  const int map = (env_int("IDN_STENCIL_MAP", 1) == 2 ? 2 : 1) |
+                  (env_int("IDN_STENCIL_FASTFETCH", 1) ? 4 : 0);  // stencil_u8_lds only
   const int ring_cfg = env_int("IDN_STENCIL_RING", 0);  // the band-tiled form is faster plain
   if (ring_cfg > 0 && ring_ok(c, rb, row_stride, h, src, dst, n, K)) {
     RingArgs a{};
