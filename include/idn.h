@@ -178,7 +178,8 @@ int idn_copy_slots_u8(const uint8_t* src, uint8_t* dst, int n, int64_t per_img,
  * lib/roi_data_layer/minibatch.py:492-667.  C = 3 (BGR), 1 <= k <= 16, h*w >= k.
  *   centers_in == NULL: device fit -- greedy k-means++ seeding + Lloyd to a fixed point on up to
  *     8192 Lab samples of the image (all pixels when h*w <= 8192, else Philox draws keyed by
- *     (seed, image id = offset + i or image_ids[i])).
+ *     (seed, image id = offset + i or image_ids[i])), best of 3 restarts by sample inertia
+ *     (sklearn's n_init = 3; the restarts run as separate workgroups).
  *   centers_in != NULL: replay -- the caller's fitted centres (double [n][k][3], e.g. sklearn's
  *     cluster_centers_): labels = argmin_j ||c_j||^2 - 2 x.c_j in float64 (sklearn's
  *     _labels_inertia), bit-exact given the centres.
