@@ -1,5 +1,6 @@
 #!/bin/bash
-# bilateral rows-per-thread A/B: parity tests with each RPT forced, then bench lines
+# bilateral rows-per-thread A/B (round 2; the IDN_BILATERAL_RPT knob it sets was removed after
+# this measurement: RPT 5 / 6 were slower, profiles/r02/bilateral_rpt/): parity tests, bench lines
 set -u
 mkdir -p gpurun_out/blr
 for r in 5 6; do
