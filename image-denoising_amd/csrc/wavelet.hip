@@ -333,6 +333,11 @@ static_assert(3 * RB_TY * (RB_TX / RB_R) == 192, "axis-1 items: one per thread o
 static_assert(2 * 3 * RB_TY * (2 * RB_TX + 1 - 2 + 1) >= 3 * 4 * RB_TY * RB_TX,
               "the band staging buffer fits in vl + vh (F >= 2)");
 
+// fp32 detail storage (IDN_WAVELET_FDET, default on): the 'ad' and 'da' bands (1, 2) round trip
+// through HBM as fp32 (relative 6e-8; the thresholds come from the fp64 sums of squares taken
+// before the store, and 'dd' stays fp64 for the sigma median's exact keys), 25 % fewer band bytes
+__host__ __device__ __forceinline__ bool wl_fdet_band(int b) { return b == 1 || b == 2; }
+
 // SRC: 0 = u8 image, 1 = f64 image (level 1, normalised per channel), 2 = the 'aa' planes of the
 // level above (levels >= 2).  Grid (tiles, 1, n).
 template <int WV, int SRC>
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
                                                  const double* __restrict__ in64,
                                                  int64_t row_stride, double* __restrict__ part,
                                                  size_t part_per_img, size_t part_tile0,
-                                                 int emit_codes) {
+                                                 int emit_codes, int fdet) {
   using Wv = Wav<WV>;
   constexpr int F = Wv::F, NX = DwtRB<WV>::NX, NY = DwtRB<WV>::NY;
   __shared__ DwtRB<WV> S;
@@ -471,18 +476,25 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
   }
   }
   __syncthreads();
-  // coalesced band stores: rows of RB_TX coefficients, 16 lanes x 16 bytes per row
+  // coalesced band stores: rows of RB_TX coefficients, 16 lanes x 16 bytes per row; with fdet
+  // the ad / da bands are stored as fp32 in the first half of their slot (wl_fdet_band)
   const size_t bsz = (size_t)Ho * Wo;
   constexpr int PR = RB_TX / 2;  // coefficient pairs per row
   for (int k = t; k < 3 * 4 * RB_TY * PR; k += 256) {
     const int row = k / PR, pr = k - row * PR;  // row = (c * 4 + band) * RB_TY + ii
-    const int cb = row / RB_TY, iy = row - cb * RB_TY;
+    const int cb = row / RB_TY, iy = row - cb * RB_TY;  // wave-uniform (4 rows of one band)
     const int oi = i0 + iy, oj = j0 + 2 * pr;
     if (oi >= Ho || oj >= Wo) continue;
     const wreal* sv = &ob[0][0][0][0] + (size_t)row * RB_TX + 2 * pr;
-    wreal* dst = base + out_off + (size_t)cb * bsz + (size_t)oi * Wo + oj;
-    dst[0] = sv[0];
-    if (oj + 1 < Wo) dst[1] = sv[1];
+    if (fdet && wl_fdet_band(cb & 3)) {
+      float* dst = reinterpret_cast<float*>(base + out_off + (size_t)cb * bsz) + (size_t)oi * Wo + oj;
+      dst[0] = (float)sv[0];
+      if (oj + 1 < Wo) dst[1] = (float)sv[1];
+    } else {
+      wreal* dst = base + out_off + (size_t)cb * bsz + (size_t)oi * Wo + oj;
+      dst[0] = sv[0];
+      if (oj + 1 < Wo) dst[1] = sv[1];
+    }
   }
 }
 
@@ -773,27 +785,35 @@ struct SynthLoad {
   static constexpr int RPT = 256 / CR;            // staging: band rows per pass (CR columns each)
   static constexpr int NRW = 4 * CR;              // band rows to stage
   static constexpr int NLD = (NRW + RPT - 1) / RPT;
+  static_assert(NLD <= 32, "odd-index bits");
   wreal x[NLD];
+  uint32_t odd;  // fdet: bit u set when x[u] holds an fp32 band pair whose odd element is wanted
 };
 template <int WV>
 __device__ __forceinline__ void synth_load(SynthLoad<WV>& L, const wreal* __restrict__ A,
-                                           size_t bsz, int Nh, int Nw, int m0, int n0) {
+                                           size_t bsz, int Nh, int Nw, int m0, int n0, int fdet) {
   using SL = SynthLoad<WV>;
   const int cc = threadIdx.x % SL::CR, rr0 = threadIdx.x / SL::CR;
   // coefficients past the band's end feed only outputs past the level's valid length (pywt's
   // stage-2 valid convolution), which are never stored: clamped reads keep them finite
-  const wreal* Ac = A + min(n0 + cc, Nw - 1);
+  const int col = min(n0 + cc, Nw - 1);
+  L.odd = 0;
 #pragma unroll
   for (int u = 0; u < SL::NLD; ++u) {  // all loads in flight before any use
     const int br = min(rr0 + SL::RPT * u, SL::NRW - 1);  // band * CR + row
     const int b = br / SL::CR, r = br - b * SL::CR;
-    L.x[u] = Ac[(size_t)b * bsz + (size_t)min(m0 + r, Nh - 1) * Nw];
+    const size_t e = (size_t)min(m0 + r, Nh - 1) * Nw + col;
+    // an fp32 band is read as the 8-byte pair holding element e (the same dwordx2 load for every
+    // lane; the band's unique bytes halve), the half is picked in synth_run
+    const bool f = fdet && wl_fdet_band(b);
+    L.x[u] = A[(size_t)b * bsz + (f ? e >> 1 : e)];
+    if (f) L.odd |= (uint32_t)(e & 1) << u;
   }
 }
 template <int WV, typename Between>
 __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>& L,
                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256],
-                                          Between between) {
+                                          int fdet, Between between) {
   using SL = SynthLoad<WV>;
   constexpr int HF = SynthTile<WV>::HF, CR = SL::CR;
   const int cc = threadIdx.x % CR, rr0 = threadIdx.x / CR;
@@ -802,7 +822,12 @@ __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>&
     const int br = rr0 + SL::RPT * u;
     if (rr0 < SL::RPT && br < SL::NRW) {
       const int b = br / CR, r = br - b * CR;
-      S.co[b][r][cc] = b > 0 ? soft(L.x[u], thr[b - 1]) : L.x[u];
+      wreal x = L.x[u];
+      if (fdet && wl_fdet_band(b)) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+        x = (wreal)__uint_as_float((uint32_t)(((L.odd >> u) & 1u) ? bits >> 32 : bits));
+      }
+      S.co[b][r][cc] = b > 0 ? soft(x, thr[b - 1]) : x;
     }
   }
   __syncthreads();
@@ -850,10 +875,11 @@ __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>&
 template <int WV>
 __device__ __forceinline__ void synth_tile(SynthTile<WV>& S, const wreal* __restrict__ A,
                                            size_t bsz, int Nh, int Nw, int m0, int n0,
-                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256]) {
+                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256],
+                                           int fdet) {
   SynthLoad<WV> L;
-  synth_load<WV>(L, A, bsz, Nh, Nw, m0, n0);
-  synth_run<WV>(S, L, thr, v, [] {});
+  synth_load<WV>(L, A, bsz, Nh, Nw, m0, n0, fdet);
+  synth_run<WV>(S, L, thr, v, fdet, [] {});
 }
 // output position of v[e] of thread t: (row, column) inside the tile
 __device__ __forceinline__ int synth_row(int e) {
@@ -867,7 +893,7 @@ __global__ __launch_bounds__(256) void wl_synth(wreal* __restrict__ ws, size_t i
                                                 const double* __restrict__ stats, int level, int L,
                                                 size_t in_off, int Nh, int Nw, size_t out_off,
                                                 int Hout, int Wout, size_t out_chan_stride,
-                                                int tiles_x) {
+                                                int tiles_x, int fdet) {
   __shared__ SynthTile<WV> S;
   const int img = blockIdx.y / 3, c = blockIdx.y % 3;
   wreal* base = ws + img * img_floats;
@@ -878,7 +904,7 @@ __global__ __launch_bounds__(256) void wl_synth(wreal* __restrict__ ws, size_t i
   const int ti = blockIdx.x / tiles_x, tj = blockIdx.x - ti * tiles_x;
   const int p0 = ti * ST_O, q0 = tj * ST_O;
   wreal v[ST_O * ST_O / 256];
-  synth_tile<WV>(S, base + in_off + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v);
+  synth_tile<WV>(S, base + in_off + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v, fdet);
   wreal* out = base + out_off + (size_t)c * out_chan_stride;
 #pragma unroll
   for (int i = 0; i < ST_O * ST_O / 256; ++i) {
@@ -895,7 +921,7 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
                                                       size_t in_off, int Nh, int Nw, int h, int w,
                                                       int tiles_x, uint8_t* __restrict__ out_u8,
                                                       int64_t row_stride,
-                                                      float* __restrict__ out_f32) {
+                                                      float* __restrict__ out_f32, int fdet) {
   __shared__ SynthTile<WV> S;
   __shared__ uint32_t obuf[ST_O][ST_O * 3 / 4];  // the tile's U8 BGR rows
   constexpr int NV = ST_O * ST_O / 256;
@@ -911,7 +937,7 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
   // are in flight while channel c is synthesised (the level-1 synthesis is bound by these fp64
   // reads: 37.5 B per output pixel)
   SynthLoad<WV> ld;
-  synth_load<WV>(ld, base, bsz, Nh, Nw, p0 / 2, q0 / 2);
+  synth_load<WV>(ld, base, bsz, Nh, Nw, p0 / 2, q0 / 2, fdet);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     wreal mn, mx;
@@ -920,8 +946,9 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
     const wreal thr[3] = {st[WlStats::thr(c, 0, 0, L)], st[WlStats::thr(c, 0, 1, L)],
                           st[WlStats::thr(c, 0, 2, L)]};
     wreal v[NV];
-    synth_run<WV>(S, ld, thr, v, [&] {
-      if (c < 2) synth_load<WV>(ld, base + (size_t)(c + 1) * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2);
+    synth_run<WV>(S, ld, thr, v, fdet, [&] {
+      if (c < 2)
+        synth_load<WV>(ld, base + (size_t)(c + 1) * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, fdet);
     });
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -2256,6 +2283,7 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   // holds codes + keys + positions (2.25 band sizes); else the radix select over the band
   const size_t bsz1 = (size_t)Lt.H[1] * Lt.W[1];
   const bool codes = env_int("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
+  const int fdet = env_int("IDN_WAVELET_FDET", 1) ? 1 : 0;
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
@@ -2263,17 +2291,17 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[l], 0);
+                         Lt.part_tile0[l], 0, fdet);
     else if (in64)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0);
+                         Lt.part_tile0[1], codes ? 1 : 0, fdet);
     else
       hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0);
+                         Lt.part_tile0[1], codes ? 1 : 0, fdet);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   if (codes)
@@ -2287,13 +2315,13 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
     const int tx = (Lt.W[l - 1] + ST_O - 1) / ST_O, ty = (Lt.H[l - 1] + ST_O - 1) / ST_O;
     hipLaunchKernelGGL((wl_synth<WV>), dim3(tx * ty, n * 3), dim3(256), 0, st, wsf, Lt.img_floats,
                        stats, l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1],
-                       Lt.H[l - 1], Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1], tx);
+                       Lt.H[l - 1], Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1], tx, fdet);
   }
   {
     const int tx = (Lt.w + ST_O - 1) / ST_O, ty = (Lt.h + ST_O - 1) / ST_O;
     hipLaunchKernelGGL((wl_synth_final<WV>), dim3(tx * ty, n), dim3(256), 0, st, wsf,
                        Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h, Lt.w,
-                       tx, out_u8, row_stride, out_f32);
+                       tx, out_u8, row_stride, out_f32, fdet);
   }
   return IDN_OK;
 }
