@@ -178,3 +178,22 @@ def test_wavelet_haar_fused_matches_general(dev, monkeypatch, shape, levels, f64
     if shape[0] * shape[1] <= 24000:
         ref = oracle.wavelet.denoise_wavelet(img, "db1", levels)
         assert np.abs(fa - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("shape,wavelet,levels", [((600, 1000), "bior1.5", None),
+                                                  ((37, 53), "bior1.5", None),
+                                                  ((90, 70), "db1", 3)])
+def test_wavelet_fp32_details_vs_fp64(dev, monkeypatch, shape, wavelet, levels):
+    """IDN_WAVELET_FDET: ad / da bands through HBM as fp32 (default) against the all-fp64 form
+    (IDN_WAVELET_FDET=0); both within TOL of the oracle, and within 1e-6 of each other"""
+    import oracle
+    img = make_img(*shape, 17)
+    u8a, fa = run(img, wavelet, levels)
+    monkeypatch.setenv("IDN_WAVELET_FDET", "0")
+    u8b, fb = run(img, wavelet, levels)
+    assert np.abs(fa - fb).max() <= 1e-6
+    d = u8a.astype(int) - u8b.astype(int)
+    assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-4
+    ref = oracle.wavelet.denoise_wavelet(img, wavelet, levels)
+    assert np.abs(fb - ref).max() <= TOL
+    check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
