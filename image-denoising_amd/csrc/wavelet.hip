@@ -327,11 +327,14 @@ struct DwtRB {
   static constexpr int F = Wav<WV>::F;
   static constexpr int NX = 2 * RB_TX + F - 2;  // staged input columns
   static constexpr int NY = 2 * RB_TY + F - 2;  // input rows per column
-  wreal vl[3][RB_TY][NX + 1], vh[3][RB_TY][NX + 1];
+  // row stride: odd (the 8 rows of a 32-lane read fall on distinct banks) and large enough for
+  // vl + vh to hold the band staging buffer
+  static constexpr int NXP = (NX + 1 > 2 * (RB_TX + 1) ? NX + 1 : 2 * (RB_TX + 1)) | 1;
+  wreal vl[3][RB_TY][NXP], vh[3][RB_TY][NXP];
 };
 static_assert(3 * RB_TY * (RB_TX / RB_R) == 192, "axis-1 items: one per thread of waves 0-2");
-static_assert(2 * 3 * RB_TY * (2 * RB_TX + 1 - 2 + 1) >= 3 * 4 * RB_TY * RB_TX,
-              "the band staging buffer fits in vl + vh (F >= 2)");
+constexpr int RB_OBS = RB_TX + 1;  // band staging row stride (doubles): conflict-free b64 stores
+
 
 // fp32 detail storage (IDN_WAVELET_FDET, default on): the 'ad' and 'da' bands (1, 2) round trip
 // through HBM as fp32 (relative 6e-8; the thresholds come from the fp64 sums of squares taken
@@ -417,7 +420,10 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     }
   }
   __syncthreads();
-  const int c = t >> 6, ii = (t >> 3) & 7, g = t & 7;  // wave = channel (waves 0-2)
+  // wave = channel (waves 0-2); lane bits [5] g / 4, [4:2] ii, [1:0] g % 4: a 32-lane half reads
+  // 8 rows x 4 column groups, whose ds_read_b64 addresses (row stride NX + 1, 8 doubles per
+  // group) fall on distinct bank pairs (lanes g / g + 4 of one row were 2-way conflicts)
+  const int c = t >> 6, ii = (t >> 2) & 7, g = ((t >> 5) & 1) * 4 + (t & 3);
   const int i = i0 + ii, jl = g * RB_R;
   constexpr int NC = 2 * RB_R + F - 2;  // staged columns one thread reads
   wreal l[NC], h[NC];
@@ -429,7 +435,10 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     }
   }
   __syncthreads();  // vl / vh become the output staging buffer
-  wreal(*ob)[4][RB_TY][RB_TX] = reinterpret_cast<wreal(*)[4][RB_TY][RB_TX]>(&S.vl[0][0][0]);
+  // rows padded to RB_OBS = RB_TX + 1 doubles: the 16 lanes of a ds_write_b64 group (4 rows x 4
+  // column groups) hit distinct bank pairs (an unpadded stride made them 4-way conflicts)
+  static_assert(sizeof(S) >= sizeof(wreal) * 3 * 4 * RB_TY * RB_OBS, "band staging fits");
+  wreal(*ob)[4][RB_TY][RB_OBS] = reinterpret_cast<wreal(*)[4][RB_TY][RB_OBS]>(&S.vl[0][0][0]);
   double sq[3] = {0.0, 0.0, 0.0};
   if (t < 192) {
 #pragma unroll
@@ -485,7 +494,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     const int cb = row / RB_TY, iy = row - cb * RB_TY;  // wave-uniform (4 rows of one band)
     const int oi = i0 + iy, oj = j0 + 2 * pr;
     if (oi >= Ho || oj >= Wo) continue;
-    const wreal* sv = &ob[0][0][0][0] + (size_t)row * RB_TX + 2 * pr;
+    const wreal* sv = &ob[0][0][0][0] + (size_t)row * RB_OBS + 2 * pr;
     if (fdet && wl_fdet_band(cb & 3)) {
       float* dst = reinterpret_cast<float*>(base + out_off + (size_t)cb * bsz) + (size_t)oi * Wo + oj;
       dst[0] = (float)sv[0];
