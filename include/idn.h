@@ -228,7 +228,9 @@ int idn_copy_u8(const uint8_t* src, uint8_t* dst, int64_t nbytes, int policy, vo
  * c = 3.  levels <= 0 selects skimage's default max(dwt_max_level - 3, 1).  in_f64 (nullable)
  * replaces src when the caller holds a float image in [0,1] (the reference's f64 branches, dense
  * n*h*w*3).  out_f32 (nullable) receives the float result before the U8 cast (dense n*h*w*3).
- * Computed in fp64 throughout (out_f32 is only a rounded side output):
+ * Computed in fp64 (out_f32 is only a rounded side output); the general (non-Haar-fused) path
+ * keeps its 'ad' / 'da' detail bands in the workspace as fp32 (IDN_WAVELET_FDET=0: fp64), the
+ * sums of squares and sigma being taken from the fp64 values:
  * |out - reference| <= 1e-5 before the cast.
  * Replaces lib/model/test.py:197-201,1807-1810, minibatch.py:1653-1656,
  * minibatch_before_curvelet.py:85-87. */
