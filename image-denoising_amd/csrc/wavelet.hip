@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
                                                  const double* __restrict__ in64,
                                                  int64_t row_stride, double* __restrict__ part,
                                                  size_t part_per_img, size_t part_tile0,
-                                                 int emit_codes, int fdet) {
+                                                 int emit_codes, int fdet, int coop) {
   using Wv = Wav<WV>;
   constexpr int F = Wv::F, NX = DwtRB<WV>::NX, NY = DwtRB<WV>::NY;
   __shared__ DwtRB<WV> S;
@@ -361,11 +361,71 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
   const int i0 = ti * RB_TY, j0 = tj * RB_TX;
   const int r0 = 2 * i0 + 2 - F, q0 = 2 * j0 + 2 - F;  // input coordinate of staged [0][0]
   const int t = threadIdx.x;
+  wreal x[NY];
+  // u8 input, cooperative form (IDN_WAVELET_COOP, default on): every staged pixel is loaded and
+  // normalised once for its three channels by one of the 256 threads, through LDS in two halves
+  // of rows (aliasing vl / vh), instead of once per channel by the three (channel, column)
+  // threads -- the same fp64 operations per sample, a third of the u8 -> fp64 conversions
+  const bool coop_u8 = SRC == 0 && coop;
+  if (coop_u8) {
+    constexpr int HR = NY / 2;  // NY = 2 RB_TY + F - 2 is even
+    constexpr int IT = (HR * NX + 255) / 256;
+    static_assert(sizeof(S) >= sizeof(wreal) * 3 * HR * NX, "normalised half fits in vl + vh");
+    wreal(*nz)[HR][NX] = reinterpret_cast<wreal(*)[HR][NX]>(&S.vl[0][0][0]);
+    const double* st = stats + (size_t)img * WL_STATS;
+    wreal mn[3], inv[3], rcp[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      wreal mx;
+      wl_minmax64(st, c, mn[c], mx);
+      inv[c] = mx - mn[c];
+      rcp[c] = 1.0 / inv[c];
+    }
+    const uint8_t* im = src + (int64_t)img * Hin * row_stride;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      uint32_t raw[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {  // all loads in flight before any use
+        const int k = t + 256 * it, rr = k / NX, q = k - rr * NX;
+        raw[it] = 0;
+        if (k < HR * NX) {
+          const uint8_t* p = im + (int64_t)sym_idx(r0 + hf * HR + rr, Hin) * row_stride +
+                             (int64_t)sym_idx(q0 + q, Win) * 3;
+          raw[it] = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16;
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int k = t + 256 * it, rr = k / NX, q = k - rr * NX;
+        if (k < HR * NX) {
+          double px[3];
+#pragma unroll
+          for (int kk = 0; kk < 3; ++kk)
+            px[kk] = (double)((raw[it] >> (8 * kk)) & 0xFFu) * (1.0 / 255.0);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {  // as the per-channel form below, op for op
+            const wreal a = ycbcr_c(px, c) - mn[c];
+            const wreal qq = a * rcp[c];
+            nz[c][rr][q] = __fma_rn(__fma_rn(-qq, inv[c], a), rcp[c], qq);
+          }
+        }
+      }
+      __syncthreads();
+      if (t < 3 * NX) {
+        const int c = t / NX, q = t - c * NX;
+#pragma unroll
+        for (int rr = 0; rr < HR; ++rr) x[hf * HR + rr] = nz[c][rr][q];
+      }
+      __syncthreads();  // nz is rewritten by the next half / becomes vl / vh
+    }
+  }
   if (t < 3 * NX) {
     const int c = t / NX, q = t - c * NX;
     const int xx = sym_idx(q0 + q, Win);
-    wreal x[NY];
-    if (SRC == 2) {
+    if (coop_u8) {
+      // x holds the column already
+    } else if (SRC == 2) {
       const wreal* X = base + in_off + (size_t)c * 4 * Hin * Win + xx;
 #pragma unroll
       for (int r = 0; r < NY; ++r) x[r] = X[(size_t)sym_idx(r0 + r, Hin) * Win];
@@ -2293,6 +2353,7 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   const size_t bsz1 = (size_t)Lt.H[1] * Lt.W[1];
   const bool codes = env_int("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
   const int fdet = env_int("IDN_WAVELET_FDET", 1) ? 1 : 0;
+  const int coop = env_int("IDN_WAVELET_COOP", 1) ? 1 : 0;
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
@@ -2300,17 +2361,17 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[l], 0, fdet);
+                         Lt.part_tile0[l], 0, fdet, coop);
     else if (in64)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0, fdet);
+                         Lt.part_tile0[1], codes ? 1 : 0, fdet, coop);
     else
       hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0, fdet);
+                         Lt.part_tile0[1], codes ? 1 : 0, fdet, coop);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   if (codes)
