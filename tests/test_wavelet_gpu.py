@@ -197,3 +197,15 @@ def test_wavelet_fp32_details_vs_fp64(dev, monkeypatch, shape, wavelet, levels):
     ref = oracle.wavelet.denoise_wavelet(img, wavelet, levels)
     assert np.abs(fb - ref).max() <= TOL
     check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
+
+
+@pytest.mark.parametrize("shape", [(600, 1000), (37, 53), (9, 11)])
+def test_wavelet_coop_normalisation_bitwise(dev, monkeypatch, shape):
+    """IDN_WAVELET_COOP: the analysis normalising each staged pixel once (default) against the
+    per-channel form (=0): the same fp64 operations per sample, so bit-identical outputs"""
+    img = make_img(*shape, 23)
+    u8a, fa = run(img, "bior1.5", None)
+    monkeypatch.setenv("IDN_WAVELET_COOP", "0")
+    u8b, fb = run(img, "bior1.5", None)
+    np.testing.assert_array_equal(u8a, u8b)
+    np.testing.assert_array_equal(fa, fb)
