@@ -338,7 +338,9 @@ constexpr int RB_OBS = RB_TX + 1;  // band staging row stride (doubles): conflic
 
 // fp32 detail storage (IDN_WAVELET_FDET, default on): the 'ad' and 'da' bands (1, 2) round trip
 // through HBM as fp32 (relative 6e-8; the thresholds come from the fp64 sums of squares taken
-// before the store, and 'dd' stays fp64 for the sigma median's exact keys), 25 % fewer band bytes
+// before the store, and 'dd' stays fp64 for the sigma median's exact keys), 25 % fewer band bytes.
+// wl_dwt_rb's fdet bits: 1 ad / da stored fp32, 2 'aa' stored fp32 (levels < L: it is read only
+// by the next analysis; the coarsest 'aa' feeds the synthesis and stays fp64), 4 'aa' input fp32
 __host__ __device__ __forceinline__ bool wl_fdet_band(int b) { return b == 1 || b == 2; }
 
 // SRC: 0 = u8 image, 1 = f64 image (level 1, normalised per channel), 2 = the 'aa' planes of the
@@ -426,9 +428,15 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     if (coop_u8) {
       // x holds the column already
     } else if (SRC == 2) {
-      const wreal* X = base + in_off + (size_t)c * 4 * Hin * Win + xx;
+      if (fdet & 4) {  // the level above stored its 'aa' as fp32
+        const float* X = reinterpret_cast<const float*>(base + in_off + (size_t)c * 4 * Hin * Win) + xx;
 #pragma unroll
-      for (int r = 0; r < NY; ++r) x[r] = X[(size_t)sym_idx(r0 + r, Hin) * Win];
+        for (int r = 0; r < NY; ++r) x[r] = (wreal)X[(size_t)sym_idx(r0 + r, Hin) * Win];
+      } else {
+        const wreal* X = base + in_off + (size_t)c * 4 * Hin * Win + xx;
+#pragma unroll
+        for (int r = 0; r < NY; ++r) x[r] = X[(size_t)sym_idx(r0 + r, Hin) * Win];
+      }
     } else {
       const double* st = stats + (size_t)img * WL_STATS;
       wreal mn, mx;
@@ -555,7 +563,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     const int oi = i0 + iy, oj = j0 + 2 * pr;
     if (oi >= Ho || oj >= Wo) continue;
     const wreal* sv = &ob[0][0][0][0] + (size_t)row * RB_OBS + 2 * pr;
-    if (fdet && wl_fdet_band(cb & 3)) {
+    if (((fdet & 1) && wl_fdet_band(cb & 3)) || ((fdet & 2) && (cb & 3) == 0)) {
       float* dst = reinterpret_cast<float*>(base + out_off + (size_t)cb * bsz) + (size_t)oi * Wo + oj;
       dst[0] = (float)sv[0];
       if (oj + 1 < Wo) dst[1] = (float)sv[1];
@@ -2361,17 +2369,17 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[l], 0, fdet, coop);
+                         Lt.part_tile0[l], 0, fdet | (fdet && l < Lt.L ? 2 : 0) | (fdet ? 4 : 0), coop);
     else if (in64)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0, fdet, coop);
+                         Lt.part_tile0[1], codes ? 1 : 0, fdet | (fdet && Lt.L > 1 ? 2 : 0), coop);
     else
       hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0, fdet, coop);
+                         Lt.part_tile0[1], codes ? 1 : 0, fdet | (fdet && Lt.L > 1 ? 2 : 0), coop);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   if (codes)
