@@ -336,12 +336,15 @@ static_assert(3 * RB_TY * (RB_TX / RB_R) == 192, "axis-1 items: one per thread o
 constexpr int RB_OBS = RB_TX + 1;  // band staging row stride (doubles): conflict-free b64 stores
 
 
-// fp32 detail storage (IDN_WAVELET_FDET, default on): the 'ad' and 'da' bands (1, 2) round trip
-// through HBM as fp32 (relative 6e-8; the thresholds come from the fp64 sums of squares taken
-// before the store, and 'dd' stays fp64 for the sigma median's exact keys), 25 % fewer band bytes.
-// wl_dwt_rb's fdet bits: 1 ad / da stored fp32, 2 'aa' stored fp32 (levels < L: it is read only
-// by the next analysis; the coarsest 'aa' feeds the synthesis and stays fp64), 4 'aa' input fp32
-__host__ __device__ __forceinline__ bool wl_fdet_band(int b) { return b == 1 || b == 2; }
+// fp32 band storage (IDN_WAVELET_FDET, default on): bands that only the synthesis (or the next
+// analysis) reads round-trip through HBM as fp32 (relative 6e-8; the thresholds come from the fp64
+// sums of squares taken before the store).  Band mask fmask: bit b (0 aa, 1 ad, 2 da, 3 dd) = band
+// b of the level is fp32, bit 4 = the analysis's input 'aa' (level above) is fp32.
+//   level 1: ad, da (dd stays fp64 for the sigma median's exact keys), aa when L > 1;
+//   levels >= 2: ad, da, dd, aa when l < L (the coarsest 'aa' and the synthesis's reconstructions
+//   in the 'aa' slots stay fp64)
+constexpr int WL_FB_AIN = 16;
+__host__ __device__ __forceinline__ bool wl_fband(int fmask, int b) { return (fmask >> b) & 1; }
 
 // SRC: 0 = u8 image, 1 = f64 image (level 1, normalised per channel), 2 = the 'aa' planes of the
 // level above (levels >= 2).  Grid (tiles, 1, n).
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
                                                  const double* __restrict__ in64,
                                                  int64_t row_stride, double* __restrict__ part,
                                                  size_t part_per_img, size_t part_tile0,
-                                                 int emit_codes, int fdet, int coop) {
+                                                 int emit_codes, int fmask, int coop) {
   using Wv = Wav<WV>;
   constexpr int F = Wv::F, NX = DwtRB<WV>::NX, NY = DwtRB<WV>::NY;
   __shared__ DwtRB<WV> S;
@@ -428,7 +431,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     if (coop_u8) {
       // x holds the column already
     } else if (SRC == 2) {
-      if (fdet & 4) {  // the level above stored its 'aa' as fp32
+      if (fmask & WL_FB_AIN) {  // the level above stored its 'aa' as fp32
         const float* X = reinterpret_cast<const float*>(base + in_off + (size_t)c * 4 * Hin * Win) + xx;
 #pragma unroll
         for (int r = 0; r < NY; ++r) x[r] = (wreal)X[(size_t)sym_idx(r0 + r, Hin) * Win];
@@ -553,8 +556,8 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
   }
   }
   __syncthreads();
-  // coalesced band stores: rows of RB_TX coefficients, 16 lanes x 16 bytes per row; with fdet
-  // the ad / da bands are stored as fp32 in the first half of their slot (wl_fdet_band)
+  // coalesced band stores: rows of RB_TX coefficients, 16 lanes x 16 bytes per row; fp32 bands
+  // (fmask) in the first half of their slot
   const size_t bsz = (size_t)Ho * Wo;
   constexpr int PR = RB_TX / 2;  // coefficient pairs per row
   for (int k = t; k < 3 * 4 * RB_TY * PR; k += 256) {
@@ -563,7 +566,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
     const int oi = i0 + iy, oj = j0 + 2 * pr;
     if (oi >= Ho || oj >= Wo) continue;
     const wreal* sv = &ob[0][0][0][0] + (size_t)row * RB_OBS + 2 * pr;
-    if (((fdet & 1) && wl_fdet_band(cb & 3)) || ((fdet & 2) && (cb & 3) == 0)) {
+    if (wl_fband(fmask, cb & 3)) {
       float* dst = reinterpret_cast<float*>(base + out_off + (size_t)cb * bsz) + (size_t)oi * Wo + oj;
       dst[0] = (float)sv[0];
       if (oj + 1 < Wo) dst[1] = (float)sv[1];
@@ -864,11 +867,11 @@ struct SynthLoad {
   static constexpr int NLD = (NRW + RPT - 1) / RPT;
   static_assert(NLD <= 32, "odd-index bits");
   wreal x[NLD];
-  uint32_t odd;  // fdet: bit u set when x[u] holds an fp32 band pair whose odd element is wanted
+  uint32_t odd;  // bit u set when x[u] holds an fp32 band pair whose odd element is wanted
 };
 template <int WV>
 __device__ __forceinline__ void synth_load(SynthLoad<WV>& L, const wreal* __restrict__ A,
-                                           size_t bsz, int Nh, int Nw, int m0, int n0, int fdet) {
+                                           size_t bsz, int Nh, int Nw, int m0, int n0, int fmask) {
   using SL = SynthLoad<WV>;
   const int cc = threadIdx.x % SL::CR, rr0 = threadIdx.x / SL::CR;
   // coefficients past the band's end feed only outputs past the level's valid length (pywt's
@@ -882,7 +885,7 @@ __device__ __forceinline__ void synth_load(SynthLoad<WV>& L, const wreal* __rest
     const size_t e = (size_t)min(m0 + r, Nh - 1) * Nw + col;
     // an fp32 band is read as the 8-byte pair holding element e (the same dwordx2 load for every
     // lane; the band's unique bytes halve), the half is picked in synth_run
-    const bool f = fdet && wl_fdet_band(b);
+    const bool f = wl_fband(fmask, b);
     L.x[u] = A[(size_t)b * bsz + (f ? e >> 1 : e)];
     if (f) L.odd |= (uint32_t)(e & 1) << u;
   }
@@ -890,7 +893,7 @@ __device__ __forceinline__ void synth_load(SynthLoad<WV>& L, const wreal* __rest
 template <int WV, typename Between>
 __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>& L,
                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256],
-                                          int fdet, Between between) {
+                                          int fmask, Between between) {
   using SL = SynthLoad<WV>;
   constexpr int HF = SynthTile<WV>::HF, CR = SL::CR;
   const int cc = threadIdx.x % CR, rr0 = threadIdx.x / CR;
@@ -900,7 +903,7 @@ __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>&
     if (rr0 < SL::RPT && br < SL::NRW) {
       const int b = br / CR, r = br - b * CR;
       wreal x = L.x[u];
-      if (fdet && wl_fdet_band(b)) {
+      if (wl_fband(fmask, b)) {
         const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
         x = (wreal)__uint_as_float((uint32_t)(((L.odd >> u) & 1u) ? bits >> 32 : bits));
       }
@@ -953,10 +956,10 @@ template <int WV>
 __device__ __forceinline__ void synth_tile(SynthTile<WV>& S, const wreal* __restrict__ A,
                                            size_t bsz, int Nh, int Nw, int m0, int n0,
                                            const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256],
-                                           int fdet) {
+                                           int fmask) {
   SynthLoad<WV> L;
-  synth_load<WV>(L, A, bsz, Nh, Nw, m0, n0, fdet);
-  synth_run<WV>(S, L, thr, v, fdet, [] {});
+  synth_load<WV>(L, A, bsz, Nh, Nw, m0, n0, fmask);
+  synth_run<WV>(S, L, thr, v, fmask, [] {});
 }
 // output position of v[e] of thread t: (row, column) inside the tile
 __device__ __forceinline__ int synth_row(int e) {
@@ -970,7 +973,7 @@ __global__ __launch_bounds__(256) void wl_synth(wreal* __restrict__ ws, size_t i
                                                 const double* __restrict__ stats, int level, int L,
                                                 size_t in_off, int Nh, int Nw, size_t out_off,
                                                 int Hout, int Wout, size_t out_chan_stride,
-                                                int tiles_x, int fdet) {
+                                                int tiles_x, int fmask) {
   __shared__ SynthTile<WV> S;
   const int img = blockIdx.y / 3, c = blockIdx.y % 3;
   wreal* base = ws + img * img_floats;
@@ -981,7 +984,7 @@ __global__ __launch_bounds__(256) void wl_synth(wreal* __restrict__ ws, size_t i
   const int ti = blockIdx.x / tiles_x, tj = blockIdx.x - ti * tiles_x;
   const int p0 = ti * ST_O, q0 = tj * ST_O;
   wreal v[ST_O * ST_O / 256];
-  synth_tile<WV>(S, base + in_off + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v, fdet);
+  synth_tile<WV>(S, base + in_off + (size_t)c * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, thr, v, fmask);
   wreal* out = base + out_off + (size_t)c * out_chan_stride;
 #pragma unroll
   for (int i = 0; i < ST_O * ST_O / 256; ++i) {
@@ -998,7 +1001,7 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
                                                       size_t in_off, int Nh, int Nw, int h, int w,
                                                       int tiles_x, uint8_t* __restrict__ out_u8,
                                                       int64_t row_stride,
-                                                      float* __restrict__ out_f32, int fdet) {
+                                                      float* __restrict__ out_f32, int fmask) {
   __shared__ SynthTile<WV> S;
   __shared__ uint32_t obuf[ST_O][ST_O * 3 / 4];  // the tile's U8 BGR rows
   constexpr int NV = ST_O * ST_O / 256;
@@ -1014,7 +1017,7 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
   // are in flight while channel c is synthesised (the level-1 synthesis is bound by these fp64
   // reads: 37.5 B per output pixel)
   SynthLoad<WV> ld;
-  synth_load<WV>(ld, base, bsz, Nh, Nw, p0 / 2, q0 / 2, fdet);
+  synth_load<WV>(ld, base, bsz, Nh, Nw, p0 / 2, q0 / 2, fmask);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     wreal mn, mx;
@@ -1023,9 +1026,9 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
     const wreal thr[3] = {st[WlStats::thr(c, 0, 0, L)], st[WlStats::thr(c, 0, 1, L)],
                           st[WlStats::thr(c, 0, 2, L)]};
     wreal v[NV];
-    synth_run<WV>(S, ld, thr, v, fdet, [&] {
+    synth_run<WV>(S, ld, thr, v, fmask, [&] {
       if (c < 2)
-        synth_load<WV>(ld, base + (size_t)(c + 1) * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, fdet);
+        synth_load<WV>(ld, base + (size_t)(c + 1) * 4 * bsz, bsz, Nh, Nw, p0 / 2, q0 / 2, fmask);
     });
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -2360,7 +2363,13 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   // holds codes + keys + positions (2.25 band sizes); else the radix select over the band
   const size_t bsz1 = (size_t)Lt.H[1] * Lt.W[1];
   const bool codes = env_int("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
-  const int fdet = env_int("IDN_WAVELET_FDET", 1) ? 1 : 0;
+  const bool fdet = env_int("IDN_WAVELET_FDET", 1) != 0;
+  // band masks (wl_fband): level 1 / deeper levels, analysis stores and synthesis loads
+  auto fm_an = [&](int l) {
+    if (!fdet) return 0;
+    return (l == 1 ? 0b0110 : 0b1110 | WL_FB_AIN) | (l < Lt.L ? 0b0001 : 0);
+  };
+  auto fm_syn = [&](int l) { return !fdet ? 0 : (l == 1 ? 0b0110 : 0b1110); };
   const int coop = env_int("IDN_WAVELET_COOP", 1) ? 1 : 0;
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
@@ -2369,17 +2378,17 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[l], 0, fdet | (fdet && l < Lt.L ? 2 : 0) | (fdet ? 4 : 0), coop);
+                         Lt.part_tile0[l], 0, fm_an(l), coop);
     else if (in64)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0, fdet | (fdet && Lt.L > 1 ? 2 : 0), coop);
+                         Lt.part_tile0[1], codes ? 1 : 0, fm_an(1), coop);
     else
       hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
-                         Lt.part_tile0[1], codes ? 1 : 0, fdet | (fdet && Lt.L > 1 ? 2 : 0), coop);
+                         Lt.part_tile0[1], codes ? 1 : 0, fm_an(1), coop);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   if (codes)
@@ -2393,13 +2402,13 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
     const int tx = (Lt.W[l - 1] + ST_O - 1) / ST_O, ty = (Lt.H[l - 1] + ST_O - 1) / ST_O;
     hipLaunchKernelGGL((wl_synth<WV>), dim3(tx * ty, n * 3), dim3(256), 0, st, wsf, Lt.img_floats,
                        stats, l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1],
-                       Lt.H[l - 1], Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1], tx, fdet);
+                       Lt.H[l - 1], Lt.W[l - 1], (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1], tx, fm_syn(l));
   }
   {
     const int tx = (Lt.w + ST_O - 1) / ST_O, ty = (Lt.h + ST_O - 1) / ST_O;
     hipLaunchKernelGGL((wl_synth_final<WV>), dim3(tx * ty, n), dim3(256), 0, st, wsf,
                        Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h, Lt.w,
-                       tx, out_u8, row_stride, out_f32, fdet);
+                       tx, out_u8, row_stride, out_f32, fm_syn(1));
   }
   return IDN_OK;
 }
