@@ -209,3 +209,31 @@ def test_wavelet_coop_normalisation_bitwise(dev, monkeypatch, shape):
     u8b, fb = run(img, "bior1.5", None)
     np.testing.assert_array_equal(u8a, u8b)
     np.testing.assert_array_equal(fa, fb)
+
+
+def _key_to_f64(k):
+    k = k.astype(np.uint64)
+    neg = (k >> np.uint64(63)) == 0
+    bits = np.where(neg, ~k, k & np.uint64(0x7FFFFFFFFFFFFFFF))
+    return bits.view(np.float64)
+
+
+def test_wavelet_color_minmax_exact(dev):
+    """wl_color_minmax: the per-channel YCbCr min / max in the stats block equal numpy's fp64
+    rgb2ycbcr min / max bit for bit, on images whose triples tie in exact value but not in fp64
+    (gray ramps: Cb / Cr), binary channels, saturated noise and uniform noise"""
+    import torch
+    import oracle
+    from oracle.cv import matmul3_fma
+    imgs = _stat_images(96, 160)
+    rs = np.random.RandomState(5)
+    sat = np.clip(rs.normal(128, 200, imgs.shape[1:]), 0, 255).astype(np.uint8)  # many 0 / 255
+    imgs = np.concatenate([imgs, sat[None]])
+    _, _, st = _stats_after(torch.from_numpy(imgs).cuda(), 2)
+    for i, img in enumerate(imgs):
+        ycc = matmul3_fma(img.astype(np.float64) * (1.0 / 255.0), oracle.wavelet.YCBCR_FROM_RGB,
+                          post=oracle.wavelet.YCBCR_OFFSET)
+        mn = _key_to_f64(st[i, 200:203].view(np.uint64))
+        mx = _key_to_f64(st[i, 203:206].view(np.uint64))
+        np.testing.assert_array_equal(mn.view(np.uint64), ycc.min(axis=(0, 1)).view(np.uint64))
+        np.testing.assert_array_equal(mx.view(np.uint64), ycc.max(axis=(0, 1)).view(np.uint64))
