@@ -1,10 +1,16 @@
 // Baseline JPEG decode front-end: cv2.imread(path) (IMREAD_COLOR, BGR u8) for the reference's
 // images (lib/model/test.py:191, lib/roi_data_layer/minibatch.py:85), decoded on the GPU.
 //
-// Output = what libjpeg(-turbo) with its defaults produces (the decoder behind both cv2.imread and
-// PIL): the ISLOW integer IDCT (jidctint.c), "fancy" triangular chroma upsampling for 4:2:0 / 4:2:2
-// (jdsample.c h2v2 / h2v1), the integer YCbCr -> RGB tables (jdcolor.c), all restated here from
-// the published algorithms; tests check bit-exactness against PIL's decode.
+// Output = what the reference's pinned decoder produces with its defaults: IJG libjpeg 9d
+// (requirements.txt:74, under OpenCV 3.4.2) -- the ISLOW integer IDCT (jidctint.c) for full-size
+// components and, since libjpeg 7, a scaled IDCT for subsampled chroma (jdmaster.c: with fancy
+// upsampling a component sampled at half the maximum rate gets jpeg_idct_16x16 (4:2:0) or
+// jpeg_idct_16x8 (4:2:2), decoding straight to full resolution, no upsampling pass), then the
+// integer YCbCr -> RGB tables of libjpeg 9's jdcolor.c (FIX(0.344136286) for Cb -> G).
+// IDN_JPEG_TURBO selects libjpeg-turbo's decode instead (8x8 IDCT everywhere, "fancy" triangular
+// h2v1 / h2v2 upsampling from jdsample.c, FIX(0.34414)): what PIL 9+ / turbo-linked OpenCV make.
+// All restated from the published algorithms; tests check bit-exactness against the real libjpeg
+// 9d decode (committed fixtures) and the GPU box's turbo-linked PIL.
 //
 // Host: the marker parser (SOI .. SOS, DQT / DHT / SOF0 / DRI / APPn), Huffman lookup tables per
 // image, one packed host->device copy of the images' entropy-coded segments and tables.
@@ -12,9 +18,10 @@
 //   1 jpeg_huff_kernel   one wave per image; lane r decodes restart interval r, r + 64, ... (lane 0
 //                        decodes the whole scan when the image has no restart markers): Huffman +
 //                        byte unstuffing + DC prediction into int16 coefficient blocks (natural order)
-//   2 jpeg_idct_kernel   one thread per 8x8 block: dequantise + ISLOW IDCT into u8 component planes
-//   3 jpeg_color_kernel  one thread per output pixel: chroma upsampling + YCbCr -> BGR (or gray ->
-//                        BGR), written into the caller's NHWC batch
+//   2 jpeg_idct_kernel   one thread per coefficient block: dequantise + ISLOW IDCT (8x8, or
+//                        16x16 / 16x8 for libjpeg 9's scaled chroma) into u8 component planes
+//   3 jpeg_color8_kernel 8 output pixels per thread: chroma upsampling (turbo only) + YCbCr -> BGR
+//                        (or gray -> BGR), written into the caller's NHWC batch
 // Supported: 8-bit baseline sequential (SOF0/SOF1) Huffman, one interleaved scan, 1 or 3
 // components, sampling 4:4:4 / 4:2:2 (h2v1) / 4:2:0 (h2v2), optional restart intervals.  Anything
 // else (progressive, arithmetic, 12-bit, CMYK, multi-scan) is IDN_EUNSUPPORTED.
@@ -39,7 +46,11 @@ struct JpegDev {
   int hmax, vmax, nintervals;
   int ch[3], cv[3], tq[3], td[3], ta[3];
   int bw[3], bh[3];         // blocks per row / column of each component plane (MCU-padded)
-  int dw[3], dh[3];         // downsampled component size (libjpeg downsampled_width / _height)
+  int sh[3], sv[3];         // IDCT output scale per component: 1 (8 samples) or 2 (16 samples)
+  int pw[3];                // component plane row pitch in bytes (bw * 8 * sh)
+  int dw[3], dh[3];         // component plane size after the IDCT (libjpeg downsampled_width)
+  int up;                   // chroma upsampling: 0 none (full-size planes), 1 h2v1, 2 h2v2 fancy
+  int cb_g;                 // jdcolor.c Cb -> G multiplier: libjpeg 9 22553, turbo 22554
   uint64_t blk_off[3];      // first block of each component in the batch coefficient buffer
   uint64_t pl_off[3];       // component plane byte offset in the batch plane buffer
   uint64_t ub_off;          // unstuffed entropy bytes (workspace), capacity scan_len + 64
@@ -172,6 +183,7 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         break;
       case 0xDA: {  // SOS
         if (!sof) return jpg_fail(err, "SOS before SOF");
+        if (sl < 1) return jpg_fail(err, "bad SOS");
         const int ns = s[0];
         if (ns != J.ncomp) return jpg_fail(err, "multi-scan (non-interleaved) JPEG not supported");
         if (sl < 1 + 2 * (size_t)ns + 3) return jpg_fail(err, "bad SOS");
@@ -218,6 +230,9 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
   int code = 0, k = 0;
   memset(lut, 0, sizeof(uint16_t) << JPG_LUTB);
   for (int l = 1; l <= 16; ++l) {
+    // jdhuff.c jpeg_make_d_derived_tbl: the codes of length l must fit in l bits and none may be
+    // all ones (code after the last >= 2^l is JERR_BAD_HUFF_TABLE); checked before any LUT write
+    if (code + (int)H.bits[l] >= (1 << l)) return jpg_fail(err, "bad Huffman table");
     if (H.bits[l]) {
       valoff[l] = k - code;
       for (int t = 0; t < H.bits[l]; ++t, ++k, ++code) {
@@ -231,7 +246,6 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
       valoff[l] = 0;
       maxcode[l] = -1;
     }
-    if (code > (1 << l)) return jpg_fail(err, "bad Huffman table");
     code <<= 1;
   }
   maxcode[0] = -1;
@@ -261,7 +275,7 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 //   prefix   per image: each chunk's first block index and DC predictors
 //   write    every chunk again from its exact start state, writing coefficient blocks
 // Images with restart markers: one thread per restart interval (true start state known).
-constexpr int JPG_CHUNK = 4096;  // default bits per chunk (IDN_JPEG_CHUNK overrides; measured
+constexpr int JPG_CHUNK = 4096;  // default bits per chunk (the ABI's flags may set another; measured
                                  // 256 x 600x1000 q90: 2048 11.9, 4096 10.4, 8192 11.8 ms)
 
 __device__ __forceinline__ uint32_t jpg_be32(const uint8_t* __restrict__ p) {
@@ -517,6 +531,9 @@ __global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const JpegDev* __res
     rst_s = 0;
     ivstart[D.iv_off] = 0;
   }
+  // intervals whose RST marker is missing (truncated / corrupt file) must not start at garbage:
+  // marked here, set to the end of the data below
+  for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x) ivstart[D.iv_off + k] = ~0u;
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (uint32_t base = 0; base < n; base += 1024 * 16) {
@@ -590,6 +607,8 @@ __global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const JpegDev* __res
   const uint32_t len = carry_s;
   if (threadIdx.x < 64) out[len + threadIdx.x] = 0;
   if (threadIdx.x == 0) ublen[blockIdx.x] = len;
+  for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x)
+    if (ivstart[D.iv_off + k] == ~0u) ivstart[D.iv_off + k] = len * 8u;
 }
 
 // stage 2a/2b: sync passes.  grid (max chunks per image, n).  PASS_A: start from the chunk's
@@ -712,8 +731,8 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
   uint32_t b1, dc_limit = 0xFFFFFFFFu;
   int32_t blk;
   if (D.restart) {  // interval t: restart MCUs from its first bit, DC predictors reset
-    const uint32_t b0 = ivstart[D.iv_off + t];
-    b1 = t + 1 < nitems ? ivstart[D.iv_off + t + 1] : nbits;
+    const uint32_t b0 = min(ivstart[D.iv_off + t], nbits);
+    b1 = t + 1 < nitems ? min(ivstart[D.iv_off + t + 1], nbits) : nbits;
     // stop after the interval's MCUs: the bits behind them are the encoder's padding (1s)
     const uint32_t mcu0 = t * (uint32_t)D.restart;
     dc_limit = min((uint32_t)D.restart, (uint32_t)(D.mcux * D.mcuy) - mcu0) * D.bpm;
@@ -790,7 +809,86 @@ __device__ __forceinline__ void jpg_idct1(int i0, int i1, int i2, int i3, int i4
   o[4] = jpg_descale(tmp13 - tmp0, SH);
 }
 
-// one thread per block; blocks of all components of all images in one flat index space
+// 16-point IDCT kernel of jidctint.c's jpeg_idct_16x16 / jpeg_idct_16x8 (libjpeg 9, cK =
+// sqrt(2) cos(K pi / 32)): 8 coefficients -> 16 samples.  Pass 1 (columns) descales by
+// CONST_BITS - PASS1_BITS, pass 2 (ROW) by CONST_BITS + PASS1_BITS + 3; libjpeg 9 folds the
+// rounding fudge (and the range centre) into the DC term, which equals rounding at the end.
+template <bool ROW>
+__device__ __forceinline__ void jpg_idct16(const int (&x)[8], int (&o)[16]) {
+  // even part
+  int tmp0 = x[0] * (1 << JCB);
+  int z1 = x[4];
+  int tmp1 = z1 * 10703;   // FIX(1.306562965)   c4[16] = c2[8]
+  int tmp2 = z1 * 4433;    // FIX_0_541196100    c12[16] = c6[8]
+  int tmp10 = tmp0 + tmp1, tmp11 = tmp0 - tmp1, tmp12 = tmp0 + tmp2, tmp13 = tmp0 - tmp2;
+  z1 = x[2];
+  int z2 = x[6];
+  int z3 = z1 - z2;
+  int z4 = z3 * 2260;      // FIX(0.275899379)   c14[16] = c7[8]
+  z3 = z3 * 11363;         // FIX(1.387039845)   c2[16] = c1[8]
+  tmp0 = z3 + z2 * 20995;  // FIX_2_562915447    (c6+c2)[16]
+  tmp1 = z4 + z1 * 7373;   // FIX_0_899976223    (c6-c14)[16]
+  tmp2 = z3 - z1 * 4926;   // FIX(0.601344887)   (c2-c10)[16]
+  int tmp3 = z4 - z2 * 4176;  // FIX(0.509795579) (c10-c14)[16]
+  const int tmp20 = tmp10 + tmp0, tmp27 = tmp10 - tmp0;
+  const int tmp21 = tmp12 + tmp1, tmp26 = tmp12 - tmp1;
+  const int tmp22 = tmp13 + tmp2, tmp25 = tmp13 - tmp2;
+  const int tmp23 = tmp11 + tmp3, tmp24 = tmp11 - tmp3;
+  // odd part
+  z1 = x[1];
+  z2 = x[3];
+  z3 = x[5];
+  z4 = x[7];
+  tmp11 = z1 + z3;
+  tmp1 = (z1 + z2) * 11086;  // FIX(1.353318001) c3
+  tmp2 = tmp11 * 10217;      // FIX(1.247225013) c5
+  tmp3 = (z1 + z4) * 8956;   // FIX(1.093201867) c7
+  tmp10 = (z1 - z4) * 7350;  // FIX(0.897167586) c9
+  tmp11 = tmp11 * 5461;      // FIX(0.666655658) c11
+  tmp12 = (z1 - z2) * 3363;  // FIX(0.410524528) c13
+  tmp0 = tmp1 + tmp2 + tmp3 - z1 * 18730;     // FIX(2.286341144) c7+c5+c3-c1
+  tmp13 = tmp10 + tmp11 + tmp12 - z1 * 15038; // FIX(1.835730603) c9+c11+c13-c15
+  z1 = (z2 + z3) * 1136;                      // FIX(0.138617169) c15
+  tmp1 += z1 + z2 * 589;                      // FIX(0.071888074) c9+c11-c3-c15
+  tmp2 += z1 - z3 * 9222;                     // FIX(1.125726048) c5+c7+c15-c3
+  z1 = (z3 - z2) * 11529;                     // FIX(1.407403738) c1
+  tmp11 += z1 - z3 * 6278;                    // FIX(0.766367282) c1+c11-c9-c13
+  tmp12 += z1 + z2 * 16154;                   // FIX(1.971951411) c1+c5+c13-c7
+  z2 += z4;
+  z1 = z2 * -5461;                            // -c11
+  tmp1 += z1;
+  tmp3 += z1 + z4 * 8728;                     // FIX(1.065388962) c3+c11+c15-c7
+  z2 = z2 * -10217;                           // -c5
+  tmp10 += z2 + z4 * 25733;                   // FIX(3.141271809) c1+c5+c9-c13
+  tmp12 += z2;
+  z2 = (z3 + z4) * -11086;                    // -c3
+  tmp2 += z2;
+  tmp3 += z2;
+  z2 = (z4 - z3) * 3363;                      // c13
+  tmp10 += z2;
+  tmp11 += z2;
+  constexpr int SH = ROW ? JCB + JP1 + 3 : JCB - JP1;
+  o[0] = jpg_descale(tmp20 + tmp0, SH);
+  o[15] = jpg_descale(tmp20 - tmp0, SH);
+  o[1] = jpg_descale(tmp21 + tmp1, SH);
+  o[14] = jpg_descale(tmp21 - tmp1, SH);
+  o[2] = jpg_descale(tmp22 + tmp2, SH);
+  o[13] = jpg_descale(tmp22 - tmp2, SH);
+  o[3] = jpg_descale(tmp23 + tmp3, SH);
+  o[12] = jpg_descale(tmp23 - tmp3, SH);
+  o[4] = jpg_descale(tmp24 + tmp10, SH);
+  o[11] = jpg_descale(tmp24 - tmp10, SH);
+  o[5] = jpg_descale(tmp25 + tmp11, SH);
+  o[10] = jpg_descale(tmp25 - tmp11, SH);
+  o[6] = jpg_descale(tmp26 + tmp12, SH);
+  o[9] = jpg_descale(tmp26 - tmp12, SH);
+  o[7] = jpg_descale(tmp27 + tmp13, SH);
+  o[8] = jpg_descale(tmp27 - tmp13, SH);
+}
+
+// one thread per coefficient block of components whose IDCT output is (8 SV) x (8 SH) samples;
+// blocks of all components of all images in one flat index space (blocks of other scales exit)
+template <int SV, int SH>
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDev* __restrict__ imgs,
                                                         const uint64_t* __restrict__ blk_end,
                                                         int n, uint64_t nblk,
@@ -811,6 +909,7 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDev* __restric
   const JpegDev& D = imgs[img];
   int c = D.ncomp - 1;
   while (c > 0 && b < D.blk_off[c]) --c;
+  if (D.sv[c] != SV || D.sh[c] != SH) return;
   const uint64_t lb = b - D.blk_off[c];
   const int by = (int)(lb / D.bw[c]), bx = (int)(lb - (uint64_t)by * D.bw[c]);
   const uint16_t* q = D.q[D.tq[c]];
@@ -826,122 +925,59 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDev* __restric
       x[8 * k + 2 * j + 1] = (int)(int16_t)((uint32_t)w4[j] >> 16) * (int)q[8 * k + 2 * j + 1];
     }
   }
-  int ws[64];
+  constexpr int R = 8 * SV, C = 8 * SH;  // output rows, columns
+  int ws[R * 8];
 #pragma unroll
   for (int col = 0; col < 8; ++col) {  // pass 1: columns (the all-zero-AC shortcut is exact)
-    int o[8];
-    jpg_idct1<false>(x[col], x[8 + col], x[16 + col], x[24 + col], x[32 + col], x[40 + col],
-                     x[48 + col], x[56 + col], o);
+    if constexpr (SV == 1) {
+      int o[8];
+      jpg_idct1<false>(x[col], x[8 + col], x[16 + col], x[24 + col], x[32 + col], x[40 + col],
+                       x[48 + col], x[56 + col], o);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) ws[8 * r + col] = o[r];
-  }
-  uint8_t* out = planes + D.pl_off[c] + (uint64_t)(by * 8) * (D.bw[c] * 8) + bx * 8;
+      for (int r = 0; r < 8; ++r) ws[8 * r + col] = o[r];
+    } else {
+      const int xi[8] = {x[col], x[8 + col], x[16 + col], x[24 + col], x[32 + col], x[40 + col],
+                         x[48 + col], x[56 + col]};
+      int o[16];
+      jpg_idct16<false>(xi, o);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {  // pass 2: rows
-    int o[8];
-    jpg_idct1<true>(ws[8 * r], ws[8 * r + 1], ws[8 * r + 2], ws[8 * r + 3], ws[8 * r + 4],
-                    ws[8 * r + 5], ws[8 * r + 6], ws[8 * r + 7], o);
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lo |= jpg_range(o[j]) << (8 * j);
-      hi |= jpg_range(o[4 + j]) << (8 * j);
+      for (int r = 0; r < 16; ++r) ws[8 * r + col] = o[r];
     }
-    reinterpret_cast<uint2*>(out + (uint64_t)r * (D.bw[c] * 8))[0] = make_uint2(lo, hi);
+  }
+  const int pw = D.pw[c];
+  uint8_t* out = planes + D.pl_off[c] + (uint64_t)(by * R) * pw + bx * C;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {  // pass 2: rows
+    int o[C];
+    if constexpr (SH == 1) {
+      jpg_idct1<true>(ws[8 * r], ws[8 * r + 1], ws[8 * r + 2], ws[8 * r + 3], ws[8 * r + 4],
+                      ws[8 * r + 5], ws[8 * r + 6], ws[8 * r + 7], o);
+    } else {
+      const int xi[8] = {ws[8 * r], ws[8 * r + 1], ws[8 * r + 2], ws[8 * r + 3], ws[8 * r + 4],
+                         ws[8 * r + 5], ws[8 * r + 6], ws[8 * r + 7]};
+      jpg_idct16<true>(xi, o);
+    }
+    uint32_t wd[C / 4];
+#pragma unroll
+    for (int j = 0; j < C / 4; ++j)
+      wd[j] = jpg_range(o[4 * j]) | jpg_range(o[4 * j + 1]) << 8 | jpg_range(o[4 * j + 2]) << 16 |
+              jpg_range(o[4 * j + 3]) << 24;
+    uint8_t* orow = out + (uint64_t)r * pw;
+    if constexpr (SH == 1) {
+      reinterpret_cast<uint2*>(orow)[0] = make_uint2(wd[0], wd[1]);
+    } else {
+      reinterpret_cast<uint4*>(orow)[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
   }
 }
 
 // ---- device: upsampling + colour ---------------------------------------------------------------
-// h2v1 / h2v2 "fancy" upsampling (jdsample.c) of chroma plane P (dw x dh real samples, row pitch
-// pw) at output (x, y)
-template <int V>
-__device__ __forceinline__ int jpg_up(const uint8_t* __restrict__ P, int pw, int dw, int dh,
-                                      int x, int y) {
-  const int col = x >> 1, s = x & 1;
-  if (V == 1) {  // h2v1: 3/4 nearer + 1/4 further sample of the row
-    const uint8_t* r = P + (int64_t)y * pw;
-    const int in = r[col];
-    if (s == 0) return col == 0 ? in : (in * 3 + r[col - 1] + 1) >> 2;
-    return col == dw - 1 ? in : (in * 3 + r[col + 1] + 2) >> 2;
-  }
-  // h2v2: column sums 3 * nearer row + further row (rows replicated at the top and bottom)
-  const int inrow = y >> 1;
-  const int other = min(max((y & 1) ? inrow + 1 : inrow - 1, 0), dh - 1);
-  const uint8_t* r0 = P + (int64_t)inrow * pw;
-  const uint8_t* r1 = P + (int64_t)other * pw;
-  auto cs = [&](int k) { return r0[k] * 3 + r1[k]; };
-  const int t = cs(col);
-  if (s == 0) return col == 0 ? (t * 4 + 8) >> 4 : (t * 3 + cs(col - 1) + 8) >> 4;
-  return col == dw - 1 ? (t * 4 + 7) >> 4 : (t * 3 + cs(col + 1) + 7) >> 4;
-}
-
 __device__ __forceinline__ uint32_t jpg_clamp(int v) { return (uint32_t)min(max(v, 0), 255); }
 
-__device__ __forceinline__ void jpg_pixel(const JpegDev& D, const uint8_t* __restrict__ planes,
-                                          int x, int y, uint32_t (&bgr)[3]) {
-  const int pw0 = D.bw[0] * 8;
-  const int Y = planes[D.pl_off[0] + (int64_t)y * pw0 + x];
-  if (D.ncomp == 1) {
-    bgr[0] = bgr[1] = bgr[2] = (uint32_t)Y;
-    return;
-  }
-  int cb, cr;
-  const int pw1 = D.bw[1] * 8, pw2 = D.bw[2] * 8;
-  const uint8_t* P1 = planes + D.pl_off[1];
-  const uint8_t* P2 = planes + D.pl_off[2];
-  if (D.hmax == 1) {
-    cb = P1[(int64_t)y * pw1 + x];
-    cr = P2[(int64_t)y * pw2 + x];
-  } else if (D.vmax == 1) {
-    cb = jpg_up<1>(P1, pw1, D.dw[1], D.dh[1], x, y);
-    cr = jpg_up<1>(P2, pw2, D.dw[2], D.dh[2], x, y);
-  } else {
-    cb = jpg_up<2>(P1, pw1, D.dw[1], D.dh[1], x, y);
-    cr = jpg_up<2>(P2, pw2, D.dw[2], D.dh[2], x, y);
-  }
-  // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert (SCALEBITS 16)
-  const int xb = cb - 128, xr = cr - 128;
-  const int r = Y + ((91881 * xr + 32768) >> 16);                   // FIX(1.40200)
-  const int g = Y + ((-46802 * xr + (-22554 * xb + 32768)) >> 16);  // FIX(0.71414), FIX(0.34414)
-  const int b = Y + ((116130 * xb + 32768) >> 16);                  // FIX(1.77200)
-  bgr[0] = jpg_clamp(b);  // BGR, as cv2.imread
-  bgr[1] = jpg_clamp(g);
-  bgr[2] = jpg_clamp(r);
-}
-
-// grid (tiles of 256 x 4 pixels, n): each thread 4 consecutive pixels of a row, stored as three
-// dwords when the row is dword aligned (else byte by byte)
-__global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDev* __restrict__ imgs,
-                                                         const uint8_t* __restrict__ planes,
-                                                         uint8_t* __restrict__ dst, int h, int w,
-                                                         int64_t row_stride) {
-  const JpegDev& D = imgs[blockIdx.y];
-  const int qw = (w + 3) / 4;
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= (int64_t)h * qw) return;
-  const int y = (int)(q / qw), x0 = 4 * (int)(q - (int64_t)y * qw);
-  uint8_t* o = dst + (int64_t)blockIdx.y * h * row_stride + (int64_t)y * row_stride + (int64_t)x0 * 3;
-  uint32_t px[4][3];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (x0 + k < w) jpg_pixel(D, planes, x0 + k, y, px[k]);
-    else px[k][0] = px[k][1] = px[k][2] = 0u;
-  }
-  if (x0 + 4 <= w && ((uintptr_t)o & 3) == 0) {
-    uint32_t* o4 = reinterpret_cast<uint32_t*>(o);
-    o4[0] = px[0][0] | px[0][1] << 8 | px[0][2] << 16 | px[1][0] << 24;
-    o4[1] = px[1][1] | px[1][2] << 8 | px[2][0] << 16 | px[2][1] << 24;
-    o4[2] = px[2][2] | px[3][0] << 8 | px[3][1] << 16 | px[3][2] << 24;
-  } else {
-    for (int k = 0; k < 4 && x0 + k < w; ++k)
-      for (int c = 0; c < 3; ++c) o[3 * k + c] = (uint8_t)px[k][c];
-  }
-}
-
-// 8 consecutive pixels of a row per thread from dword loads: Y 2 dwords, each chroma row 3 dwords
-// (the samples the 8 outputs' fancy upsampling needs, columns x0/2 - 1 .. x0/2 + 4 for h2),
-// where jpeg_color_kernel issued 9 byte loads per pixel.  Same arithmetic (jpg_up's formulas on
-// the extracted samples, jdcolor.c's tables).
+// 8 consecutive pixels of a row per thread from dword loads: Y 2 dwords, each chroma row 2 dwords
+// (full-size planes) or 3 dwords (the samples the 8 outputs' fancy upsampling needs, columns
+// x0/2 - 1 .. x0/2 + 4 for turbo's h2 forms); jdsample.c's h2v1 / h2v2 formulas on the extracted
+// samples, jdcolor.c's integer tables.
 __device__ __forceinline__ uint32_t ld_dw(const uint8_t* __restrict__ row, int col4, int pw) {
   return (col4 >= 0 && col4 < pw) ? *reinterpret_cast<const uint32_t*>(row + col4) : 0u;
 }
@@ -991,15 +1027,16 @@ __device__ __forceinline__ void jpg_chroma8(const uint8_t* __restrict__ P, int p
 template <int HS, int VS, bool GRAY>
 __device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __restrict__ planes,
                                            int x0, int y, uint32_t (&o)[6]) {
-  const int pw0 = D.bw[0] * 8;
+  const int pw0 = D.pw[0];
   const uint8_t* yr = planes + D.pl_off[0] + (int64_t)y * pw0;
   const uint32_t ya = ld_dw(yr, x0, pw0), yb = ld_dw(yr, x0 + 4, pw0);
   int cbv[8], crv[8];
   if constexpr (!GRAY) {
-    jpg_chroma8<HS, VS>(planes + D.pl_off[1], D.bw[1] * 8, D.dw[1], D.dh[1], x0, y, cbv);
-    jpg_chroma8<HS, VS>(planes + D.pl_off[2], D.bw[2] * 8, D.dw[2], D.dh[2], x0, y, crv);
+    jpg_chroma8<HS, VS>(planes + D.pl_off[1], D.pw[1], D.dw[1], D.dh[1], x0, y, cbv);
+    jpg_chroma8<HS, VS>(planes + D.pl_off[2], D.pw[2], D.dw[2], D.dh[2], x0, y, crv);
   }
   uint32_t px[24];
+  const int cbg = D.cb_g;  // jdcolor.c build_ycc_rgb_table (SCALEBITS 16)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int Y = (int)(((i < 4 ? ya : yb) >> (8 * (i & 3))) & 0xFFu);
@@ -1007,9 +1044,9 @@ __device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __re
       px[3 * i] = px[3 * i + 1] = px[3 * i + 2] = (uint32_t)Y;
     } else {
       const int xb = cbv[i] - 128, xr = crv[i] - 128;
-      px[3 * i + 0] = jpg_clamp(Y + ((116130 * xb + 32768) >> 16));                   // B
-      px[3 * i + 1] = jpg_clamp(Y + ((-46802 * xr + (-22554 * xb + 32768)) >> 16));  // G
-      px[3 * i + 2] = jpg_clamp(Y + ((91881 * xr + 32768) >> 16));                    // R
+      px[3 * i + 0] = jpg_clamp(Y + ((116130 * xb + 32768) >> 16));                  // FIX(1.772)
+      px[3 * i + 1] = jpg_clamp(Y + ((-46802 * xr + (-cbg * xb + 32768)) >> 16));  // FIX(0.714136286)
+      px[3 * i + 2] = jpg_clamp(Y + ((91881 * xr + 32768) >> 16));                   // FIX(1.402)
     }
   }
 #pragma unroll
@@ -1017,8 +1054,7 @@ __device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __re
     o[j] = px[4 * j] | px[4 * j + 1] << 8 | px[4 * j + 2] << 16 | px[4 * j + 3] << 24;
 }
 
-// grid (tiles of 256 x 8 pixels, n); images whose planes do not fit the 8-pixel form use
-// jpeg_color_kernel
+// grid (tiles of 256 x 8 pixels, n)
 __global__ __launch_bounds__(256) void jpeg_color8_kernel(const JpegDev* __restrict__ imgs,
                                                           const uint8_t* __restrict__ planes,
                                                           uint8_t* __restrict__ dst, int h, int w,
@@ -1030,8 +1066,8 @@ __global__ __launch_bounds__(256) void jpeg_color8_kernel(const JpegDev* __restr
   const int y = (int)(q / ow), x0 = 8 * (int)(q - (int64_t)y * ow);
   uint32_t o[6];
   if (D.ncomp == 1) jpg_color8<1, 1, true>(D, planes, x0, y, o);
-  else if (D.hmax == 1) jpg_color8<1, 1, false>(D, planes, x0, y, o);
-  else if (D.vmax == 1) jpg_color8<2, 1, false>(D, planes, x0, y, o);
+  else if (D.up == 0) jpg_color8<1, 1, false>(D, planes, x0, y, o);
+  else if (D.up == 1) jpg_color8<2, 1, false>(D, planes, x0, y, o);
   else jpg_color8<2, 2, false>(D, planes, x0, y, o);
   uint8_t* p = dst + (int64_t)blockIdx.y * h * row_stride + (int64_t)y * row_stride + (int64_t)x0 * 3;
   if (x0 + 8 <= w && ((uintptr_t)p & 7) == 0) {
@@ -1056,6 +1092,7 @@ struct JpegPlan {
   uint64_t scan_bytes = 0, nblk = 0, plane_bytes = 0, ub_bytes = 0;
   uint32_t nintervals = 0, nchunks = 0, max_items = 1;
   bool any_chunked = false;
+  bool scales[2][2] = {};  // IDCT output scales present: [sv - 1][sh - 1]
   size_t off_imgs = 0, off_blkend = 0, off_scan = 0, off_coef = 0, off_planes = 0;
   size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_s0 = 0, off_s1 = 0, off_cnt = 0,
          off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, total = 0;
@@ -1063,8 +1100,18 @@ struct JpegPlan {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// flags: IDN_JPEG_TURBO selects libjpeg-turbo's decode (else libjpeg 9d's); bits 8..23 = entropy
+// chunk size in bits (0: the default JPG_CHUNK; else a multiple of 64, >= 512)
 static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int h, int w,
-                     JpegPlan& P, std::string* err, bool tables = true) {
+                     int flags, JpegPlan& P, std::string* err, bool tables = true) {
+  const bool turbo = (flags & IDN_JPEG_TURBO) != 0;
+  const uint32_t chunk_req = (uint32_t)(flags >> 8) & 0xFFFFu;
+  if ((flags & ~(IDN_JPEG_TURBO | (0xFFFF << 8))) != 0 ||
+      (chunk_req != 0 && (chunk_req < 512 || chunk_req % 64 != 0))) {
+    if (err) *err = "bad flags";
+    return IDN_EINVAL;
+  }
+  const uint32_t chunk_bits = chunk_req ? chunk_req : (uint32_t)JPG_CHUNK;
   P.dev.assign(n, JpegDev{});
   P.blk_end.assign(n, 0);
   P.scan_begin.assign(n, 0);
@@ -1109,14 +1156,34 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       D.ta[c] = J.ta[c];
       D.bw[c] = D.mcux * D.ch[c];
       D.bh[c] = D.mcuy * D.cv[c];
-      // libjpeg: downsampled size = ceil(image size * samp / max samp)
-      D.dw[c] = (J.width * D.ch[c] + D.hmax - 1) / D.hmax;
-      D.dh[c] = (J.height * D.cv[c] + D.vmax - 1) / D.vmax;
+      // jdmaster.c (libjpeg >= 7, do_fancy_upsampling): the IDCT size doubles while the doubled
+      // component still divides the maximum sampling factor (at most 16 = 2 x DCTSIZE); the two
+      // directions never differ by more than 2x, which holds for factors 1 and 2
+      D.sh[c] = (!turbo && D.hmax % (2 * D.ch[c]) == 0) ? 2 : 1;
+      D.sv[c] = (!turbo && D.vmax % (2 * D.cv[c]) == 0) ? 2 : 1;
+      D.pw[c] = D.bw[c] * 8 * D.sh[c];
+      // libjpeg: downsampled size = ceil(image size * samp * idct size / (max samp * 8))
+      D.dw[c] = (J.width * D.ch[c] * D.sh[c] + D.hmax - 1) / D.hmax;
+      D.dh[c] = (J.height * D.cv[c] * D.sv[c] + D.vmax - 1) / D.vmax;
+      P.scales[D.sv[c] - 1][D.sh[c] - 1] = true;
       D.blk_off[c] = P.nblk;
       P.nblk += (uint64_t)D.bw[c] * D.bh[c];
       D.pl_off[c] = P.plane_bytes;
-      P.plane_bytes += (uint64_t)D.bw[c] * 8 * D.bh[c] * 8;
+      P.plane_bytes += (uint64_t)D.pw[c] * D.bh[c] * 8 * D.sv[c];
     }
+    // what the colour pass still has to upsample (the chroma planes' remaining factor)
+    D.up = 0;
+    if (J.ncomp == 3) {
+      const int fh = D.hmax / (D.ch[1] * D.sh[1]), fv = D.vmax / (D.cv[1] * D.sv[1]);
+      if (fh != D.hmax / (D.ch[2] * D.sh[2]) || fv != D.vmax / (D.cv[2] * D.sv[2]) ||
+          D.ch[0] * D.sh[0] != D.hmax || D.cv[0] * D.sv[0] != D.vmax)
+        return jpg_fail(err, "unsupported chroma sampling");
+      if (fh == 1 && fv == 1) D.up = 0;
+      else if (fh == 2 && fv == 1) D.up = 1;
+      else if (fh == 2 && fv == 2) D.up = 2;
+      else return jpg_fail(err, "unsupported chroma sampling");
+    }
+    D.cb_g = turbo ? 22554 : 22553;  // FIX(0.34414) / FIX(0.344136286), SCALEBITS 16
     P.blk_end[i] = P.nblk;
     D.bpm = 0;
     for (int c = 0; c < J.ncomp; ++c)
@@ -1146,7 +1213,7 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     D.iv_off = P.nintervals;
     P.nintervals += (uint32_t)D.nintervals;
     D.ch_off = P.nchunks;
-    D.chunk_bits = (uint32_t)std::max(512, env_int("IDN_JPEG_CHUNK", JPG_CHUNK));
+    D.chunk_bits = chunk_bits;
     D.nchunks = D.restart ? 0u
                           : (uint32_t)(((uint64_t)D.scan_len * 8 + D.chunk_bits - 1) / D.chunk_bits);
     if (D.nchunks == 0 && !D.restart) D.nchunks = 1;
@@ -1190,16 +1257,17 @@ extern "C" int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* 
   return IDN_OK;
 }
 
-extern "C" size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n) {
+extern "C" size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n,
+                                          int flags) {
   if (!files || !lens || n <= 0) return 0;
   JpegPlan P;
-  if (jpeg_plan(files, lens, n, 0, 0, P, nullptr, false) != IDN_OK) return 0;
+  if (jpeg_plan(files, lens, n, 0, 0, flags, P, nullptr) != IDN_OK) return 0;  // tables checked
   return P.total;
 }
 
 extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* lens, int n,
-                                  uint8_t* dst, int h, int w, int64_t row_stride, void* workspace,
-                                  size_t ws_bytes, void* stream) {
+                                  uint8_t* dst, int h, int w, int64_t row_stride, int flags,
+                                  void* workspace, size_t ws_bytes, void* stream) {
   IDN_CHECK_ARG(n >= 0 && (n == 0 || (files && lens && dst)), "idn_jpeg_decode_u8: null pointer");
   IDN_CHECK_ARG(h > 0 && w > 0 && row_stride >= (int64_t)w * 3,
                 "idn_jpeg_decode_u8: bad output shape");
@@ -1207,7 +1275,7 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   if (n == 0) return IDN_OK;
   JpegPlan P;
   std::string err;
-  const int rc = jpeg_plan(files, lens, n, h, w, P, &err);
+  const int rc = jpeg_plan(files, lens, n, h, w, flags, P, &err);
   if (rc != IDN_OK) return set_error(rc, "idn_jpeg_decode_u8: %s", err.c_str());
   if (!workspace || ws_bytes < P.total)
     return set_error(IDN_EWORKSPACE, "idn_jpeg_decode_u8: needs %zu workspace bytes (got %zu)",
@@ -1235,8 +1303,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     // part's host-to-device copy is issued as soon as the part is complete, so the DMA of part
     // k overlaps the gathering of part k + 1
     constexpr int MAXPART = 16;
-    const int nt = std::max(1, std::min(env_int("IDN_JPEG_THREADS", 8), std::max(1, n / 8)));
-    const int npart = std::max(1, std::min(std::min(env_int("IDN_JPEG_PARTS", 4), MAXPART), n / 16));
+    const int nt = std::max(1, std::min(8, n / 8));
+    const int npart = std::max(1, std::min(std::min(4, MAXPART), n / 16));
     std::atomic<int> done[MAXPART];
     for (int q = 0; q < MAXPART; ++q) done[q].store(0);
     auto first = [&](int q) { return (int)((int64_t)n * q / npart); };
@@ -1306,16 +1374,19 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
                      cstart, coef);
   const uint64_t gb = (P.nblk + 255) / 256;
   IDN_CHECK_ARG(gb < 0x7FFFFFFF, "idn_jpeg_decode_u8: batch too large");
-  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)gb), dim3(256), 0, st, dimg,
-                     reinterpret_cast<const uint64_t*>(ws + P.off_blkend), n, P.nblk, coef,
-                     ws + P.off_planes);
-  if (env_int("IDN_JPEG_COLOR8", 1)) {
+  const uint64_t* bend = reinterpret_cast<const uint64_t*>(ws + P.off_blkend);
+  if (P.scales[0][0])
+    hipLaunchKernelGGL((jpeg_idct_kernel<1, 1>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
+                       n, P.nblk, coef, ws + P.off_planes);
+  if (P.scales[0][1])
+    hipLaunchKernelGGL((jpeg_idct_kernel<1, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
+                       n, P.nblk, coef, ws + P.off_planes);
+  if (P.scales[1][1])
+    hipLaunchKernelGGL((jpeg_idct_kernel<2, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
+                       n, P.nblk, coef, ws + P.off_planes);
+  {
     const int64_t gx = ((int64_t)h * ((w + 7) / 8) + 255) / 256;
     hipLaunchKernelGGL(jpeg_color8_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
-                       ws + P.off_planes, dst, h, w, row_stride);
-  } else {
-    const int64_t gx = ((int64_t)h * ((w + 3) / 4) + 255) / 256;
-    hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
                        ws + P.off_planes, dst, h, w, row_stride);
   }
   // the staging buffer is reused by the next call: finish here

@@ -33,9 +33,9 @@ SIGNATURES = {
     "idn_noise_workspace_size": (_c_size, [_c_int, _c_int]),
     "idn_poisson_levels": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "idn_jpeg_info": (_c_int, [_c_vp, _c_size, _c_vp, _c_vp, _c_vp]),
-    "idn_jpeg_workspace_size": (_c_size, [_c_vp, _c_vp, _c_int]),
-    "idn_jpeg_decode_u8": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_int, _c_i64, _c_vp,
-                                    _c_size, _c_vp]),
+    "idn_jpeg_workspace_size": (_c_size, [_c_vp, _c_vp, _c_int, _c_int]),
+    "idn_jpeg_decode_u8": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_int, _c_i64, _c_int,
+                                    _c_vp, _c_size, _c_vp]),
     "idn_noise_ids_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64,
                                   _c_int, _c_dbl, _c_dbl, _c_u64, _c_vp, _c_vp, _c_size, _c_vp]),
     "idn_noise_slots_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64,

@@ -6,7 +6,8 @@ decoded with PIL and flipped to BGR (libjpeg builds can differ by a few LSB betw
 decoders; parity tests therefore feed both sides the same decoded pixels).
 
 `imread_gpu` is the GPU decode front-end: baseline JPEG files are decoded on
-the device (idn_jpeg_decode_u8), bit-exact with libjpeg's default decode, images of one size in one
+the device (idn_jpeg_decode_u8), bit-exact with the reference's pinned IJG libjpeg 9d
+(requirements.txt:74) by default or with libjpeg-turbo (mode="turbo"), images of one size in one
 launch; files the decoder does not take raise IdnError (no CPU fallback inside the product).
 """
 from __future__ import annotations
@@ -30,7 +31,7 @@ def imread(path) -> np.ndarray:
     return np.ascontiguousarray(rgb[..., ::-1])
 
 
-def imread_gpu(paths):
+def imread_gpu(paths, mode: str = "libjpeg9"):
     """cv2.imread for a list of JPEG paths, decoded on the GPU: a list of (h, w, 3) uint8 BGR
     device tensors in input order; same-size files share one decode launch."""
     from . import ops
@@ -43,7 +44,7 @@ def imread_gpu(paths):
         groups.setdefault(ops.jpeg_info(d)[:2], []).append(i)
     out = [None] * len(datas)
     for idx in groups.values():
-        dec = ops.jpeg_decode([datas[i] for i in idx])
+        dec = ops.jpeg_decode([datas[i] for i in idx], mode=mode)
         for k, i in enumerate(idx):
             out[i] = dec[k]
     return out

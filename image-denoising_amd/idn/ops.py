@@ -726,12 +726,22 @@ def jpeg_info(data: bytes) -> Tuple[int, int, int]:
     return h.value, w.value, c.value
 
 
-def jpeg_decode(files, out: Optional[torch.Tensor] = None, device=None) -> torch.Tensor:
+JPEG_MODES = {"libjpeg9": 0, "turbo": 1}  # include/idn.h IDN_JPEG_TURBO
+
+
+def jpeg_decode(files, out: Optional[torch.Tensor] = None, device=None, mode: str = "libjpeg9",
+                chunk_bits: int = 0) -> torch.Tensor:
     """cv2.imread(path) for a batch of same-size baseline JPEG files (bytes in host memory):
-    (n, h, w, 3) uint8 BGR on the GPU, bit-exact with libjpeg's default decode."""
+    (n, h, w, 3) uint8 BGR on the GPU.  mode "libjpeg9" (default) is bit-exact with the
+    reference's pinned IJG libjpeg 9d (requirements.txt:74, under OpenCV 3.4.2: scaled 16x16 /
+    16x8 chroma IDCT); "turbo" with libjpeg-turbo (fancy upsampling).  chunk_bits (0 = default)
+    sets the entropy decoder's chunk size; it does not change the output."""
     files = list(files)
     if not files:
         raise ValueError("jpeg_decode: no files")
+    if mode not in JPEG_MODES:
+        raise ValueError(f"jpeg_decode: mode must be one of {sorted(JPEG_MODES)}")
+    flags = JPEG_MODES[mode] | (int(chunk_bits) << 8)
     h, w, _ = jpeg_info(files[0])
     n = len(files)
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -742,13 +752,13 @@ def jpeg_decode(files, out: Optional[torch.Tensor] = None, device=None) -> torch
         raise ValueError("jpeg_decode: out must be a contiguous (n, h, w, 3) uint8 CUDA tensor")
     lib = _lib.load()
     bufs, ptrs, lens = _file_ptrs(files)
-    ws_bytes = lib.idn_jpeg_workspace_size(ptrs, lens, n)
+    ws_bytes = lib.idn_jpeg_workspace_size(ptrs, lens, n, flags)
     if ws_bytes == 0:
-        raise _lib.IdnError("jpeg_decode: unsupported or corrupt JPEG in the batch")
+        raise _lib.IdnError("jpeg_decode: unsupported or corrupt JPEG in the batch (or bad flags)")
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=out.device)
     with torch.cuda.device(out.device):
-        rc = lib.idn_jpeg_decode_u8(ptrs, lens, n, out.data_ptr(), h, w, w * 3, ws.data_ptr(),
-                                    ws_bytes, _stream())
+        rc = lib.idn_jpeg_decode_u8(ptrs, lens, n, out.data_ptr(), h, w, w * 3, flags,
+                                    ws.data_ptr(), ws_bytes, _stream())
     _lib.check(rc, "idn_jpeg_decode_u8")
     del bufs
     return out

@@ -294,15 +294,25 @@ int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int
  * IDN_EUNSUPPORTED for anything the decoder does not take (progressive, arithmetic, 12-bit,
  * CMYK / Adobe RGB, multi-scan, chroma sampling other than 4:4:4 / 4:2:2 / 4:2:0). */
 int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
-/* device workspace for decoding these files (0 if any is unsupported) */
-size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n);
+
+/* idn_jpeg_decode_u8 flags.  Default (0): the decode of the reference's pinned libjpeg 9d
+ * (requirements.txt:74, linked by its OpenCV 3.4.2): 8x8 ISLOW IDCT for full-size components,
+ * libjpeg 9's scaled 16x16 / 16x8 IDCT for 4:2:0 / 4:2:2 chroma (no upsampling pass), libjpeg 9's
+ * YCbCr tables.  IDN_JPEG_TURBO: libjpeg-turbo's decode (8x8 IDCT, fancy h2v1 / h2v2
+ * upsampling), what a turbo-linked OpenCV or PIL produce.  Bits 8..23: entropy chunk size in bits
+ * for the self-synchronising decoder (0 = default 4096; else a multiple of 64, >= 512; does not
+ * change the output). */
+#define IDN_JPEG_TURBO 1
+/* device workspace for decoding these files with these flags (0 if any is unsupported) */
+size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n, int flags);
 /* cv2.imread(path) (IMREAD_COLOR) of n baseline JPEG files held in host memory, all h x w, into
- * the device u8 BGR NHWC batch dst (row_stride bytes per row): libjpeg's default decode (ISLOW
- * IDCT, fancy upsampling, integer YCbCr tables) -- bit-exact with PIL / libjpeg-turbo.  The
- * entropy-coded segments are copied to the workspace in one transfer; synchronous on `stream`. */
+ * the device u8 BGR NHWC batch dst (row_stride bytes per row), bit-exact with the library the
+ * flags name (replaces cv2.imread at lib/model/test.py:191, lib/roi_data_layer/minibatch.py:85).
+ * The entropy-coded segments are copied to the workspace in one transfer; synchronous on
+ * `stream`. */
 int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* lens, int n, uint8_t* dst,
-                       int h, int w, int64_t row_stride, void* workspace, size_t ws_bytes,
-                       void* stream);
+                       int h, int w, int64_t row_stride, int flags, void* workspace,
+                       size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

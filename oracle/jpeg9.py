@@ -1,0 +1,374 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (never imported by the product path).
+
+CPU restatement of `cv2.imread(path)` (IMREAD_COLOR -> uint8 BGR) for baseline JPEG files, as the
+reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
+(`/root/reference/requirements.txt:74,89`; call sites `lib/model/test.py:191`,
+`lib/roi_data_layer/minibatch.py:85`).  libjpeg 9d is a third-party library absent from
+/root/reference; its published algorithm is restated here:
+
+  jdhuff.c     baseline Huffman decoding (DC prediction, AC run/size, restart intervals)
+  jdmaster.c   IDCT scaling: with do_fancy_upsampling (the default) a component whose sampling
+               factor divides the maximum by 2 gets a scaled IDCT of twice the size in that
+               direction (libjpeg >= 7), so 4:2:0 chroma is decoded by jpeg_idct_16x16 and
+               4:2:2 chroma by jpeg_idct_16x8 straight to full resolution; no upsampling pass
+  jidctint.c   jpeg_idct_islow (8x8), jpeg_idct_16x16, jpeg_idct_16x8 (integer, CONST_BITS 13,
+               PASS1_BITS 2, range centre folded into the DC term, 10-bit wrap range limit)
+  jdcolor.c    ycc_rgb_convert with libjpeg 9's tables (FIX(1.402), FIX(1.772),
+               FIX(0.714136286), FIX(0.344136286); SCALEBITS 16)
+OpenCV then swaps RGB -> BGR (grfmt_jpeg.cpp, no JCS_EXT_BGR in IJG libjpeg).
+
+mode="turbo" instead restates libjpeg-turbo (the system Pillow's decoder): 8x8 IDCT for every
+component, "fancy" triangular h2v1 / h2v2 upsampling (jdsample.c) and FIX(0.34414) for Cb->G.
+
+Pinned by tests/golden/jpeg9.npz / jpeg9.json: the real libjpeg 9d decode of every fixture file
+(tests/golden/make_jpeg9_fixtures.py, conda Pillow 8.4.0); tests/test_jpeg.py checks this
+restatement against it (and mode="turbo" against the system Pillow).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ZIGZAG = np.array([
+    0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27,
+    20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58,
+    59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63])
+
+CB, P1 = 13, 2  # CONST_BITS, PASS1_BITS
+
+
+def FIX(x: float) -> int:
+    return int(x * (1 << CB) + 0.5)
+
+
+# ---- parsing + entropy decoding (jdmarker.c / jdhuff.c) ----------------------------------------
+def _segments(data: bytes):
+    i = 2
+    assert data[:2] == b"\xff\xd8", "no SOI"
+    while i + 4 <= len(data):
+        assert data[i] == 0xFF
+        m = data[i + 1]
+        if m == 0xFF:
+            i += 1
+            continue
+        i += 2
+        if m == 0xD8 or 0xD0 <= m <= 0xD7 or m == 0x01:
+            continue
+        ln = (data[i] << 8) | data[i + 1]
+        yield m, data[i + 2:i + ln], i + ln
+        if m == 0xDA:
+            return
+        i += ln
+
+
+def _huff_lut(bits, vals):
+    """16-bit peek -> (length, symbol)"""
+    lut = [(0, 0)] * 65536
+    code, k = 0, 0
+    for ln in range(1, 17):
+        for _ in range(bits[ln]):
+            lo = code << (16 - ln)
+            for x in range(lo, lo + (1 << (16 - ln))):
+                lut[x] = (ln, vals[k])
+            code += 1
+            k += 1
+        code <<= 1
+    return lut
+
+
+def _extend(v, s):
+    return v - (1 << s) + 1 if v < (1 << (s - 1)) else v
+
+
+def parse_and_decode(data: bytes):
+    """-> dict(width, height, comps=[(h, v, q[64] natural)], coef=[int32 (bh, bw, 64) natural])"""
+    q, dc, ac, comps, restart = {}, {}, {}, [], 0
+    W = H = 0
+    scan_start = None
+    sel = []
+    for m, s, end in _segments(data):
+        if m in (0xC0, 0xC1):
+            assert s[0] == 8
+            H, W, nc = (s[1] << 8) | s[2], (s[3] << 8) | s[4], s[5]
+            comps = [dict(id=s[6 + 3 * c], h=s[7 + 3 * c] >> 4, v=s[7 + 3 * c] & 15,
+                          tq=s[8 + 3 * c]) for c in range(nc)]
+        elif m == 0xC4:
+            k = 0
+            while k < len(s):
+                tc, th = s[k] >> 4, s[k] & 15
+                bits = [0] + list(s[k + 1:k + 17])
+                n = sum(bits)
+                tbl = _huff_lut(bits, list(s[k + 17:k + 17 + n]))
+                (ac if tc else dc)[th] = tbl
+                k += 17 + n
+        elif m == 0xDB:
+            k = 0
+            while k < len(s):
+                pq, tq = s[k] >> 4, s[k] & 15
+                if pq:
+                    z = [(s[k + 1 + 2 * i] << 8) | s[k + 2 + 2 * i] for i in range(64)]
+                else:
+                    z = list(s[k + 1:k + 65])
+                nat = np.zeros(64, np.int64)
+                nat[ZIGZAG] = z
+                q[tq] = nat
+                k += 1 + 64 * (2 if pq else 1)
+        elif m == 0xDD:
+            restart = (s[0] << 8) | s[1]
+        elif m == 0xDA:
+            ns = s[0]
+            for k in range(ns):
+                c = [cc["id"] for cc in comps].index(s[1 + 2 * k])
+                sel.append((c, s[2 + 2 * k] >> 4, s[2 + 2 * k] & 15))
+            scan_start = end
+        elif 0xC2 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
+            raise ValueError("not a baseline sequential JPEG")
+    assert scan_start is not None and len(sel) == len(comps)
+    nc = len(comps)
+    if nc == 1:
+        comps[0]["h"] = comps[0]["v"] = 1
+    hmax = max(c["h"] for c in comps)
+    vmax = max(c["v"] for c in comps)
+    mcux = -(-W // (8 * hmax))
+    mcuy = -(-H // (8 * vmax))
+    coef = [np.zeros((mcuy * c["v"], mcux * c["h"], 64), np.int64) for c in comps]
+    # entropy-coded data -> restart intervals of unstuffed bytes
+    seg = data[scan_start:]
+    intervals, cur, i = [], bytearray(), 0
+    while i < len(seg):
+        b = seg[i]
+        if b == 0xFF and i + 1 < len(seg):
+            nb = seg[i + 1]
+            if nb == 0x00:
+                cur.append(0xFF)
+                i += 2
+                continue
+            if 0xD0 <= nb <= 0xD7:
+                intervals.append(bytes(cur))
+                cur = bytearray()
+                i += 2
+                continue
+            if nb == 0xFF:
+                i += 1
+                continue
+            break  # EOI or another marker
+        cur.append(b)
+        i += 1
+    intervals.append(bytes(cur))
+    order = [(ci, dv, dh) for ci, c in enumerate(comps) for dv in range(c["v"])
+             for dh in range(c["h"])]
+    nmcu = mcux * mcuy
+    per = restart if restart else nmcu
+    mcu = 0
+    for iv in intervals:
+        if mcu >= nmcu:
+            break
+        bits = "".join(f"{b:08b}" for b in iv) + "0" * 64
+        pos = 0
+        pred = [0] * nc
+        for _ in range(min(per, nmcu - mcu)):
+            my, mx = divmod(mcu, mcux)
+            for ci, dv, dh in order:
+                c, td, ta = sel[ci]
+                blk = coef[ci][my * comps[ci]["v"] + dv, mx * comps[ci]["h"] + dh]
+                ln, s = dc[td][int(bits[pos:pos + 16], 2)]
+                pos += ln
+                diff = _extend(int(bits[pos:pos + s], 2), s) if s else 0
+                pos += s
+                pred[ci] += diff
+                blk[0] = pred[ci]
+                k = 1
+                tbl = ac[ta]
+                while k < 64:
+                    ln, rs = tbl[int(bits[pos:pos + 16], 2)]
+                    pos += ln
+                    r, s = rs >> 4, rs & 15
+                    if s:
+                        k += r
+                        blk[ZIGZAG[min(k, 63)]] = _extend(int(bits[pos:pos + s], 2), s)
+                        pos += s
+                        k += 1
+                    elif r == 15:
+                        k += 16
+                    else:
+                        break
+            mcu += 1
+    return dict(width=W, height=H, hmax=hmax, vmax=vmax,
+                comps=[(c["h"], c["v"], q[c["tq"]]) for c in comps], coef=coef)
+
+
+# ---- IDCT kernels (jidctint.c) -------------------------------------------------------------------
+# 1-D kernels over the last axis (8 inputs).  `first`: pass 1 (x0 << CONST_BITS plus the pass-1
+# fudge; outputs >> CONST_BITS - PASS1_BITS); else pass 2 (range centre + fudge added to the DC
+# workspace value, outputs >> CONST_BITS + PASS1_BITS + 3).
+def _dc_term(x0, first):
+    if first:
+        return (x0 << CB) + (1 << (CB - P1 - 1))
+    return (x0 + ((512 << (P1 + 3)) + (1 << (P1 + 2)))) << CB
+
+
+def _idct8(x, first):
+    x = [x[..., k] for k in range(8)]
+    z2, z3 = x[2], x[6]
+    z1 = (z2 + z3) * FIX(0.541196100)
+    tmp2 = z1 + z2 * FIX(0.765366865)
+    tmp3 = z1 - z3 * FIX(1.847759065)
+    z2 = _dc_term(x[0], first)
+    z3 = x[4] << CB
+    tmp0, tmp1 = z2 + z3, z2 - z3
+    tmp10, tmp13, tmp11, tmp12 = tmp0 + tmp2, tmp0 - tmp2, tmp1 + tmp3, tmp1 - tmp3
+    tmp0, tmp1, tmp2, tmp3 = x[7], x[5], x[3], x[1]
+    z2, z3 = tmp0 + tmp2, tmp1 + tmp3
+    z1 = (z2 + z3) * FIX(1.175875602)
+    z2 = z2 * -FIX(1.961570560) + z1
+    z3 = z3 * -FIX(0.390180644) + z1
+    z1 = (tmp0 + tmp3) * -FIX(0.899976223)
+    tmp0 = tmp0 * FIX(0.298631336) + z1 + z2
+    tmp3 = tmp3 * FIX(1.501321110) + z1 + z3
+    z1 = (tmp1 + tmp2) * -FIX(2.562915447)
+    tmp1 = tmp1 * FIX(2.053119869) + z1 + z3
+    tmp2 = tmp2 * FIX(3.072711026) + z1 + z2
+    sh = CB - P1 if first else CB + P1 + 3
+    o = [tmp10 + tmp3, tmp11 + tmp2, tmp12 + tmp1, tmp13 + tmp0,
+         tmp13 - tmp0, tmp12 - tmp1, tmp11 - tmp2, tmp10 - tmp3]
+    return np.stack([v >> sh for v in o], -1)
+
+
+def _idct16(x, first):
+    x = [x[..., k] for k in range(8)]
+    tmp0 = _dc_term(x[0], first)
+    z1 = x[4]
+    tmp1, tmp2 = z1 * FIX(1.306562965), z1 * FIX(0.541196100)
+    tmp10, tmp11, tmp12, tmp13 = tmp0 + tmp1, tmp0 - tmp1, tmp0 + tmp2, tmp0 - tmp2
+    z1, z2 = x[2], x[6]
+    z3 = z1 - z2
+    z4 = z3 * FIX(0.275899379)
+    z3 = z3 * FIX(1.387039845)
+    tmp0 = z3 + z2 * FIX(2.562915447)
+    tmp1 = z4 + z1 * FIX(0.899976223)
+    tmp2 = z3 - z1 * FIX(0.601344887)
+    tmp3 = z4 - z2 * FIX(0.509795579)
+    tmp20, tmp27 = tmp10 + tmp0, tmp10 - tmp0
+    tmp21, tmp26 = tmp12 + tmp1, tmp12 - tmp1
+    tmp22, tmp25 = tmp13 + tmp2, tmp13 - tmp2
+    tmp23, tmp24 = tmp11 + tmp3, tmp11 - tmp3
+    z1, z2, z3, z4 = x[1], x[3], x[5], x[7]
+    tmp11 = z1 + z3
+    tmp1 = (z1 + z2) * FIX(1.353318001)
+    tmp2 = tmp11 * FIX(1.247225013)
+    tmp3 = (z1 + z4) * FIX(1.093201867)
+    tmp10 = (z1 - z4) * FIX(0.897167586)
+    tmp11 = tmp11 * FIX(0.666655658)
+    tmp12 = (z1 - z2) * FIX(0.410524528)
+    tmp0 = tmp1 + tmp2 + tmp3 - z1 * FIX(2.286341144)
+    tmp13 = tmp10 + tmp11 + tmp12 - z1 * FIX(1.835730603)
+    z1 = (z2 + z3) * FIX(0.138617169)
+    tmp1 = tmp1 + z1 + z2 * FIX(0.071888074)
+    tmp2 = tmp2 + z1 - z3 * FIX(1.125726048)
+    z1 = (z3 - z2) * FIX(1.407403738)
+    tmp11 = tmp11 + z1 - z3 * FIX(0.766367282)
+    tmp12 = tmp12 + z1 + z2 * FIX(1.971951411)
+    z2 = z2 + z4
+    z1 = z2 * -FIX(0.666655658)
+    tmp1 = tmp1 + z1
+    tmp3 = tmp3 + z1 + z4 * FIX(1.065388962)
+    z2 = z2 * -FIX(1.247225013)
+    tmp10 = tmp10 + z2 + z4 * FIX(3.141271809)
+    tmp12 = tmp12 + z2
+    z2 = (z3 + z4) * -FIX(1.353318001)
+    tmp2 = tmp2 + z2
+    tmp3 = tmp3 + z2
+    z2 = (z4 - z3) * FIX(0.410524528)
+    tmp10 = tmp10 + z2
+    tmp11 = tmp11 + z2
+    sh = CB - P1 if first else CB + P1 + 3
+    lo = [tmp20 + tmp0, tmp21 + tmp1, tmp22 + tmp2, tmp23 + tmp3,
+          tmp24 + tmp10, tmp25 + tmp11, tmp26 + tmp12, tmp27 + tmp13]
+    hi = [tmp27 - tmp13, tmp26 - tmp12, tmp25 - tmp11, tmp24 - tmp10,
+          tmp23 - tmp3, tmp22 - tmp2, tmp21 - tmp1, tmp20 - tmp0]
+    return np.stack([v >> sh for v in lo + hi], -1)
+
+
+def _range_limit(v):
+    """IDCT_range_limit[(x) & RANGE_MASK]: (x + 512) & 1023, minus RANGE_SUBSET 384, clamped"""
+    return np.clip((v & 1023) - 384, 0, 255).astype(np.uint8)
+
+
+def idct_blocks(coef, q, rows: int, cols: int):
+    """coef (..., 64) natural order, q (64,) -> (..., rows, cols) u8; rows, cols in {8, 16}"""
+    x = (coef * q).reshape(coef.shape[:-1] + (8, 8))
+    col = _idct16 if rows == 16 else _idct8
+    row = _idct16 if cols == 16 else _idct8
+    ws = col(np.swapaxes(x, -1, -2), True)   # (..., 8 cols, rows) — pass 1 down each column
+    ws = np.swapaxes(ws, -1, -2)             # (..., rows, 8)
+    return _range_limit(row(ws, False))      # (..., rows, cols)
+
+
+def _fancy_h2v1(p, dw):
+    p = p.astype(np.int64)
+    out = np.empty(p.shape[:-1] + (2 * p.shape[-1],), np.int64)
+    left = np.concatenate([p[..., :1], p[..., :-1]], -1)
+    right = np.concatenate([p[..., 1:], p[..., -1:]], -1)
+    out[..., 0::2] = (p * 3 + left + 1) >> 2
+    out[..., 1::2] = (p * 3 + right + 2) >> 2
+    out[..., 0] = p[..., 0]
+    out[..., 2 * dw - 1] = p[..., dw - 1]
+    return out
+
+
+def _fancy_h2v2(p, dw, dh):
+    p = p.astype(np.int64)
+    above = np.concatenate([p[:1], p[:-1]], 0)
+    below = np.concatenate([p[1:dh], p[dh - 1:dh], p[dh:]], 0)[:p.shape[0]]
+    out = np.empty((2 * p.shape[0], 2 * p.shape[1]), np.int64)
+    for par, nb in ((0, above), (1, below)):
+        cs = p * 3 + nb
+        left = np.concatenate([cs[:, :1], cs[:, :-1]], 1)
+        right = np.concatenate([cs[:, 1:], cs[:, -1:]], 1)
+        ev = (cs * 3 + left + 8) >> 4
+        od = (cs * 3 + right + 7) >> 4
+        ev[:, 0] = (cs[:, 0] * 4 + 8) >> 4
+        od[:, dw - 1] = (cs[:, dw - 1] * 4 + 7) >> 4
+        out[par::2, 0::2] = ev
+        out[par::2, 1::2] = od
+    return out
+
+
+def imread(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
+    """cv2.imread(..., IMREAD_COLOR) of a baseline JPEG: (H, W, 3) uint8 BGR"""
+    d = parse_and_decode(data)
+    W, H, hmax, vmax = d["width"], d["height"], d["hmax"], d["vmax"]
+    planes = []
+    for (h, v, q), cf in zip(d["comps"], d["coef"]):
+        sh = 2 if (mode == "libjpeg9" and hmax % (2 * h) == 0 and h * 2 <= hmax) else 1
+        sv = 2 if (mode == "libjpeg9" and vmax % (2 * v) == 0 and v * 2 <= vmax) else 1
+        # IDCT sizes never differ by more than 2x between the directions (jdmaster.c)
+        blk = idct_blocks(cf, q, 8 * sv, 8 * sh)
+        bh, bw = cf.shape[:2]
+        p = blk.transpose(0, 2, 1, 3).reshape(bh * 8 * sv, bw * 8 * sh)
+        fh, fv = hmax // (h * sh), vmax // (v * sv)
+        if fh == 1 and fv == 1:
+            planes.append(p[:H, :W].astype(np.int64))
+        elif fh == 2 and fv == 1:
+            dw = -(-W * h // hmax)
+            planes.append(_fancy_h2v1(p, dw)[:H, :W])
+        elif fh == 2 and fv == 2:
+            dw, dh = -(-W * h // hmax), -(-H * v // vmax)
+            planes.append(_fancy_h2v2(p, dw, dh)[:H, :W])
+        else:
+            raise ValueError("unsupported sampling")
+    if len(planes) == 1:
+        y = planes[0].astype(np.uint8)
+        return np.repeat(y[..., None], 3, -1)
+    Y, Cb, Cr = planes
+    xb, xr = Cb - 128, Cr - 128
+    one_half = 1 << 15
+    cb_g = FIXS(0.344136286 if mode == "libjpeg9" else 0.34414)
+    cr_g = FIXS(0.714136286 if mode == "libjpeg9" else 0.71414)
+    r = Y + ((FIXS(1.402) * xr + one_half) >> 16)
+    g = Y + ((-cb_g * xb + one_half - cr_g * xr) >> 16)
+    b = Y + ((FIXS(1.772) * xb + one_half) >> 16)
+    return np.clip(np.stack([b, g, r], -1), 0, 255).astype(np.uint8)
+
+
+def FIXS(x: float) -> int:  # jdcolor.c FIX with SCALEBITS 16
+    return int(x * (1 << 16) + 0.5)

@@ -6,8 +6,9 @@
   takes: 4:2:0 / 4:2:2 / 4:4:4, grayscale, restart intervals (per row and every 3 MCUs), odd sizes,
   quality 10 .. 100, optimised Huffman tables, and a progressive file the decoder must reject.
 
-The expected pixels are PIL's own decode of each file, made at test time (same library on the GPU
-box): cv2.imread and PIL both decode with libjpeg(-turbo) defaults (ISLOW IDCT, fancy upsampling).
+Expected pixels: the reference's pinned IJG libjpeg 9d decode, committed as data by
+tests/golden/make_jpeg9_fixtures.py (run under /opt/conda/bin/python3.9); the libjpeg-turbo mode
+is compared with the GPU box's own Pillow (turbo) at test time.
 
   python tests/golden/make_jpeg_fixtures.py
 """
@@ -54,6 +55,9 @@ def main():
          restart_marker_blocks=3)
     save("gray_q80_91x77.jpg", textured(91, 77, 10)[..., 0], quality=80)
     save("gray_rst2_48x64.jpg", textured(48, 64, 11)[..., 0], quality=70, restart_marker_blocks=2)
+    save("s422_q100_odd_45x67.jpg", textured(45, 67, 13), quality=100, subsampling=1)
+    save("s422_rst2_77x130.jpg", textured(77, 130, 14), quality=60, subsampling=1,
+         restart_marker_blocks=2)
     save("progressive_64x64.jpg", textured(64, 64, 12), quality=80, progressive=True)
 
 

@@ -1,20 +1,72 @@
-"""CPU tests of the JPEG decode front-end's host side: the marker parser
-through the C-ABI (no GPU needed), on the fixture files of tests/golden/make_jpeg_fixtures.py."""
+"""CPU tests of the JPEG decode front-end (cv2.imread at lib/model/test.py:191,
+lib/roi_data_layer/minibatch.py:85).
+
+* the oracle (oracle/jpeg9.py, a restatement of IJG libjpeg 9d's baseline decode) against the
+  real libjpeg 9d decode of every fixture (tests/golden/jpeg9.*, made by
+  tests/golden/make_jpeg9_fixtures.py from conda Pillow 8.4.0 linked with libjpeg.so.9), and its
+  libjpeg-turbo mode against this container's Pillow (turbo);
+* the host side of the HIP library through the C-ABI (marker parser, table validation, workspace
+  sizing; no GPU needed)."""
+import hashlib
+import json
 from pathlib import Path
 
+import numpy as np
 import pytest
 
-JPEG = Path(__file__).resolve().parent / "golden" / "jpeg"
+GOLD = Path(__file__).resolve().parent / "golden"
+JPEG = GOLD / "jpeg"
 
 
 def _files():
     return sorted(p for p in JPEG.glob("*.jpg") if not p.name.startswith("progressive"))
 
 
+def _meta():
+    return json.loads((GOLD / "jpeg9.json").read_text())
+
+
+def test_fixture_set_is_complete():
+    meta = _meta()
+    assert meta["libjpeg"].startswith("9")
+    assert sorted(meta["files"]) == [p.name for p in _files()]
+    assert len(meta["files"]) >= 18
+
+
+@pytest.mark.parametrize("name", [p.name for p in _files()
+                                  if p.stat().st_size < 20000 or p.name.startswith("demo_0004")])
+def test_oracle_libjpeg9_matches_real_libjpeg9(name):
+    from oracle import jpeg9
+    rec = _meta()["files"][name]
+    got = jpeg9.imread((JPEG / name).read_bytes())
+    assert list(got.shape) == rec["shape"]
+    if rec.get("full"):
+        ref = np.load(GOLD / "jpeg9.npz")[name]
+        d = np.abs(got.astype(int) - ref.astype(int))
+        assert d.max() == 0, (name, d.max(), np.argwhere(d > 0)[:5])
+    assert hashlib.sha256(got.tobytes()).hexdigest() == rec["sha256"]
+
+
+@pytest.mark.parametrize("name", ["s420_q100_64x80.jpg", "s422_q85_120x200.jpg",
+                                  "s444_q95_96x128.jpg", "s420_q75_odd_37x53.jpg"])
+def test_oracle_turbo_mode_matches_system_pil(name):
+    from PIL import Image
+    from oracle import jpeg9
+    with Image.open(JPEG / name) as im:
+        ref = np.asarray(im.convert("RGB"))[..., ::-1]
+    assert np.array_equal(jpeg9.imread((JPEG / name).read_bytes(), mode="turbo"), ref)
+
+
+def test_libjpeg9_and_turbo_differ_on_subsampled_files():
+    """the reason for the re-pin: the two libraries disagree on every 4:2:x file"""
+    from oracle import jpeg9
+    data = (JPEG / "s420_q75_odd_37x53.jpg").read_bytes()
+    assert not np.array_equal(jpeg9.imread(data), jpeg9.imread(data, mode="turbo"))
+
+
 def test_info_matches_pil():
     from PIL import Image
     from idn import ops
-    assert len(_files()) >= 16
     for p in _files():
         with Image.open(p) as im:
             w, h = im.size
@@ -34,13 +86,60 @@ def test_unsupported_and_corrupt_raise():
         ops.jpeg_info(data[:40])  # truncated inside the headers
 
 
-def test_workspace_size():
-    import ctypes
+def _ws(datas, flags=0):
     from idn import _lib, ops
-    lib = _lib.load()
-    datas = [p.read_bytes() for p in _files()[:3]]
     bufs, ptrs, lens = ops._file_ptrs(datas)
-    assert lib.idn_jpeg_workspace_size(ptrs, lens, 3) > sum(lens)
-    bufs, ptrs, lens = ops._file_ptrs([(JPEG / "progressive_64x64.jpg").read_bytes()])
-    assert lib.idn_jpeg_workspace_size(ptrs, lens, 1) == 0
-    del ctypes
+    return _lib.load().idn_jpeg_workspace_size(ptrs, lens, len(datas), flags)
+
+
+def test_workspace_size():
+    datas = [p.read_bytes() for p in _files()[:3]]
+    assert _ws(datas) > sum(map(len, datas))
+    assert _ws([(JPEG / "progressive_64x64.jpg").read_bytes()]) == 0
+    # libjpeg 9's full-size chroma planes need more room than turbo's subsampled ones
+    d = [(JPEG / "s420_q90_600x1000.jpg").read_bytes()]
+    assert _ws(d, 0) > _ws(d, 1) > 0
+    assert _ws(d, 1 | (512 << 8)) > 0
+    assert _ws(d, 4) == 0 and _ws(d, 100 << 8) == 0  # unknown flag bit, chunk < 512
+
+
+def _dht_segments(data):
+    i, out = 2, []
+    while i + 4 <= len(data):
+        m, ln = data[i + 1], (data[i + 2] << 8) | data[i + 3]
+        if m == 0xC4:
+            out.append(i + 4)
+        if m == 0xDA:
+            break
+        i += 2 + ln
+    return out
+
+
+def test_malformed_huffman_table_is_rejected_before_use():
+    """jdhuff.c: a code length whose codes do not fit (or end all ones) is JERR_BAD_HUFF_TABLE.
+    Counts moved to length 1 keep the segment's size valid, so only the table check catches it
+    (before the fix the fast-lookup fill ran past its 512 entries)."""
+    data = bytearray((JPEG / "s444_q95_96x128.jpg").read_bytes())
+    k = _dht_segments(data)[0]
+    bits = data[k + 1:k + 17]
+    total = sum(bits)
+    assert total >= 3
+    new = [3] + [0] * 15
+    rest = total - 3
+    for ln in range(15, 0, -1):  # put the rest at the longest length, keeping the sum
+        if rest:
+            new[ln] = rest
+            rest = 0
+    data[k + 1:k + 17] = bytes(new)
+    assert _ws([bytes(data)]) == 0
+    from idn import ops
+    assert ops.jpeg_info(bytes(data))[0] == 96  # headers still parse
+
+
+def test_sos_length_checked_before_reading():
+    data = (JPEG / "s444_q95_96x128.jpg").read_bytes()
+    k = data.index(b"\xff\xda")
+    from idn import ops
+    from idn._lib import IdnError
+    with pytest.raises(IdnError):
+        ops.jpeg_info(data[:k] + b"\xff\xda\x00\x02")
