@@ -62,16 +62,23 @@ OPS = {
     "quant7": ("quant k=7", lambda idn, x, y: idn.ops.quantize(x, 7, seed=3, out=y), 6, "quant_"),
 }
 # arithmetic type each op computes in (the filters are integer SWAR / fixed point)
-DTYPE = {"noise_gaussian": "f64", "noise_sap": "f64", "noise_poisson": "f64", "wavelet_haar3": "f64", "bilateral": "f32", "cfg2": "f64",
-         "cfg2f": "f64", "cfg2p": "f64", "wavelet_bior15": "f64", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
-         "cfg3": "f64", "cfg4": "f64", "cfg5": "f64", "jpeg_decode": "i32 (integer IDCT)"}
-PARITY = {"noise_gaussian": "skimage random_noise semantics (bit-exact under replay)",
+# (the Philox u8 noise streams: fp32 Box-Muller on 16-bit uniforms, fp32 apply on the 0..255
+# scale; s&p integer thresholds on 16-bit uniforms; Poisson integer CDF thresholds)
+_U8NOISE = "f32 apply, 16-bit-uniform Box-Muller (32-bit tail refinement)"
+DTYPE = {"noise_gaussian": _U8NOISE, "noise_sap": "u32 (16-bit uniform thresholds)",
+         "noise_poisson": "u32 (CDF thresholds)", "wavelet_haar3": "f64", "bilateral": "f32",
+         "cfg2": _U8NOISE + " + u16 SWAR filter", "cfg2p": _U8NOISE + " + u16 SWAR filter",
+         "wavelet_bior15": "f64", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
+         "cfg3": "u32 noise + f16-lane median", "cfg4": _U8NOISE + " + f32 bilateral",
+         "cfg5": "f32/u32 noise + f64 wavelet", "jpeg_decode": "i32 (integer IDCT)"}
+PARITY = {"noise_gaussian": "skimage random_noise('gaussian') U8 law (chi-square tested at the "
+                            "reference's levels; bit-exact under replay)",
           "noise_poisson": "skimage random_noise('poisson') law (bit-exact under replay)",
           "noise_sap": "skimage random_noise('s&p') law (bit-exact under replay)",
           "wavelet_haar3": "skimage 0.14 denoise_wavelet within 1e-5",
           "bilateral": "cv2.bilateralFilter within 1 LSB",
           "cfg2": "Philox noise + cv2.blur bit-exact", "cfg3": "Philox s&p + cv2.medianBlur bit-exact",
-          "cfg2f": "Philox noise + cv2.blur bit-exact", "cfg2p": "Philox noise + cv2.blur bit-exact",
+"cfg2p": "Philox noise + cv2.blur bit-exact",
           "wavelet_bior15": "skimage 0.14 denoise_wavelet within 1e-5",
           "gauss5_blob": "cv2.GaussianBlur + blob.py float32 LUT, bit-exact",
           "quant7": "OpenCV 8-bit Lab + k-means (sklearn-replay bit-exact; device fit within 5% "
@@ -98,8 +105,6 @@ def _pipeline(kind):
         if kind == "cfg2":    # gaussian_var1.0 + mean 3x3: noise launch, then the filter
             ops.random_noise(x, "gaussian", var=1.0, seed=3, out="u8", out_u8=t)
             idn.blur(t, 3, out=y)
-        elif kind == "cfg2f":  # the same in one fused pass (LDS ring)
-            ops.noise_filter(x, "gaussian", "mean", 3, var=1.0, seed=3, out=y, form="fused")
         elif kind == "cfg2p":  # chunked: noise of chunk k+1 beside the filter of chunk k
             ops.noise_filter(x, "gaussian", "mean", 3, var=1.0, seed=3, out=y, form="pipelined")
         elif kind == "cfg3":  # sap_var0.4 + median 5x5
@@ -143,7 +148,6 @@ def _pipeline(kind):
 
 PIPELINES = {
     "cfg2": ("gaussian_var1.0 + 3x3 mean (config 2)", 256),
-    "cfg2f": ("gaussian_var1.0 + 3x3 mean (config 2, fused one-pass form)", 256),
     "cfg2p": ("gaussian_var1.0 + 3x3 mean (config 2, chunk-pipelined on two streams)", 256),
     "cfg3": ("sap_var0.4 + 5x5 median (config 3)", 1024),
     "cfg4": ("speckle_var1.0 + bilateral d=9 s=75/75 (config 4)", 512),
@@ -240,7 +244,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
             255 * oracle.wavelet.denoise_wavelet(a[0], "bior1.5", None)),
         "gauss5_blob": lambda a: oracle.sk.blob_f32(oracle.cv.gaussian_blur_fast(a, 5)),
     }
-    table["cfg2f"] = table["cfg2p"] = table["cfg2"]
+    table["cfg2p"] = table["cfg2"]
     if op == "jpeg_decode":  # Pillow's libjpeg-turbo decode of the same kind of file
         import io
         from PIL import Image
@@ -273,7 +277,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         threads, src = 1, "numpy, single thread"
     elif op == "jpeg_decode":
         threads, src = 1, "PIL (libjpeg-turbo) decode, single thread"
-    elif op in ("cfg2", "cfg2f", "cfg2p", "cfg3", "cfg4"):
+    elif op in ("cfg2", "cfg2p", "cfg3", "cfg4"):
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
         src = "numpy noise (1 thread) + oracle/filters.c OpenMP"
     elif op in ("gauss5", "gauss3", "gauss5_blob"):

@@ -297,7 +297,6 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
       taps.sw[(i + radius) * (2 * radius + 1) + (j + radius)] = (float)exp(r * r * gsc);  // OpenCV's
       taps.swq[i * i + j * j] = (float)exp(r * r * gsc);
     }
-  const bool pre = env_int("IDN_BILATERAL_PRE", 1) != 0;
   hipStream_t st = as_stream(stream);
 #define IDN_BL(CC)                                                          \
   switch (radius) {                                                         \
@@ -310,7 +309,7 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
     case 7: launch_bl<CC, 7>(src, dst, n, h, w, row_stride, taps, st); break; \
     default: launch_bl<CC, 8>(src, dst, n, h, w, row_stride, taps, st); break; \
   }
-  if (c == 3 && pre && radius <= 5) {
+  if (c == 3 && radius <= 5) {
     switch (radius) {
       case 1: launch_bl_pre<1>(src, dst, n, h, w, row_stride, taps, st); break;
       case 2: launch_bl_pre<2>(src, dst, n, h, w, row_stride, taps, st); break;

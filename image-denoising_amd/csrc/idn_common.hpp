@@ -46,11 +46,19 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(q, 0, nb, 0x00020000);
 }
 
-// tuning knobs read at launch time (host)
-inline int env_int(const char* name, int dflt) {
+// Tuning knobs (host).  The product library (idn/libidn_hip.so) is built without
+// IDN_TUNING_BUILD: every knob is its compile-time default and the library reads no environment
+// variable (tests/test_abi.py checks its undefined symbols).  The tools-only variant
+// (idn/libidn_hip_tuning.so, idn._build.build(tuning=True)) reads them from the environment for
+// A/B measurements and the cross-form tests, which load it explicitly (idn._lib.variant).
+#ifdef IDN_TUNING_BUILD
+inline int knob(const char* name, int dflt) {
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }
+#else
+constexpr int knob(const char*, int dflt) { return dflt; }
+#endif
 
 // compute units of the current device (host; cached per device)
 inline int cu_count() {

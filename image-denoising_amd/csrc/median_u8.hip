@@ -221,89 +221,6 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
   }
 }
 
-// LDS band-tile form (compact rows <= 3024 bytes), the stencils' stencil_u8_lds structure: one
-// 3-wave workgroup per NB-row band of one image fetches the band's NB + K - 1 input rows flat into
-// LDS (16 B per lane, consecutive lanes on consecutive addresses, all loads in flight), then each
-// wave walks its row segment out of LDS through the same median row functions.  Rows outside the
-// image are the replicated edge rows (BORDER_REPLICATE), which the tile always holds.
-constexpr int MT_WGT = 192;
-constexpr int MT_RBMAX = 3024;
-template <int C, int K, int NB>
-__global__ __launch_bounds__(MT_WGT) void median_u8_lds(const uint8_t* __restrict__ src,
-                                                       uint8_t* __restrict__ dst, int h, int rb,
-                                                       int nseg, int seg_len, int bands,
-                                                       int total_items) {
-  constexpr int R = K / 2;
-  constexpr int BYTES = (NB + K - 1) * MT_RBMAX + 16;  // + alignment shift
-  constexpr int NL = (BYTES + 16 * MT_WGT - 1) / (16 * MT_WGT);
-  __shared__ __attribute__((aligned(16))) uint8_t tile[(BYTES + 15) / 16 * 16];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
-  const int item = blk * nseg + min(wave, nseg - 1);  // waves beyond nseg only help fetch
-  const StripeGeom g = stripe_geom(item, lane, rb, nseg, seg_len, bands);
-  const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
-  const rsrc_t rs = make_rsrc(src + (size_t)g.img * img_bytes, img_bytes);
-  const rsrc_t rd = make_rsrc(dst + (size_t)g.img * img_bytes, img_bytes);
-  const int y0 = g.band * NB;
-  const int y1 = min(y0 + NB, h);
-  const int ys = max(y0 - R, 0), ye = min(y1 + R, h);
-  const uint32_t base = (uint32_t)ys * (uint32_t)rb;
-  const uint32_t base_al = base & ~15u, shift = base - base_al;
-  const uint32_t nbytes = (uint32_t)ye * (uint32_t)rb - base_al;
-  {
-    v4u v[NL];
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const uint32_t o = 16u * (uint32_t)(MT_WGT * i + threadIdx.x);
-      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < nbytes ? base_al + o : OOB_OFF, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const uint32_t o = 16u * (uint32_t)(MT_WGT * i + threadIdx.x);
-      if (o < nbytes) *reinterpret_cast<v4u*>(&tile[o]) = v[i];
-    }
-  }
-  __syncthreads();
-  if (wave >= nseg || item >= total_items || y0 >= y1) return;
-
-  const uint32_t ld_off = g.lead ? 0u : (uint32_t)g.q;
-  const int nin = (y1 - y0) + 2 * R;
-  uint32_t Wr[K][8];  // unpacked rows (float16 1024 + v lanes)
-  auto take_row = [&](int r) {
-    const int y = clampi(y0 - R + min(r, nin - 1), 0, h - 1);  // BORDER_REPLICATE, in the tile
-    const uint32_t o = (uint32_t)(y - ys) * (uint32_t)rb + shift + ld_off;
-    const v2u a = *reinterpret_cast<const v2u*>(&tile[o]);
-    const v2u b = *reinterpret_cast<const v2u*>(&tile[o + 8]);
-    v4u Lv = v4u{a.x, a.y, b.x, b.y};
-    if (g.lead) {  // chunk = row bytes -8..7: rebuild the replicated 8 bytes
-      const uint32_t L[4] = {Lv.x, Lv.y, Lv.z, Lv.w};
-      Lv = v4u{lead_fix<C, BORDER_REPLICATE>(L, -8), lead_fix<C, BORDER_REPLICATE>(L, -4), L[0],
-               L[1]};
-    }
-    unpack_row_f16(Lv, Wr[r % K]);
-  };
-#pragma unroll
-  for (int r = 0; r < 2 * R; ++r) take_row(r);
-#pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const int r = 2 * R + u;
-    take_row(r);
-    const int y = y0 + u;
-    if (y < y1) {
-      v4u o;
-      if constexpr (K == 3) {
-        o = median3_cols_out<C>(Wr[(r + 1) % K], Wr[(r + 2) % K], Wr[r % K], g.fix_t0, g.fix_t8);
-      } else {
-        o = median5_cols_out<C>(Wr[(r + 1) % K], Wr[(r + 2) % K], Wr[(r + 3) % K],
-                                Wr[(r + 4) % K], Wr[r % K], g.fix_t0, g.fix_t8);
-      }
-      stripe_store<0>(o, rd, (uint32_t)y * (uint32_t)rb + (uint32_t)g.q, g.kind);
-    }
-  }
-}
-
 // generic path: one thread per pixel, exact median by counting (any C, any alignment)
 template <int K>
 __global__ __launch_bounds__(256) void median_u8_generic(const uint8_t* __restrict__ src,
@@ -348,25 +265,13 @@ template <int K>
 static int launch_median(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
                          int64_t row_stride, hipStream_t st) {
   const int64_t rb = (int64_t)w * c;
-  // LDS band-tile form for compact rows (IDN_MEDIAN_TILE=1): bit-exact, measured no faster for
-  // 3x3 (0.203-0.216 vs 0.206-0.207 ms per 256 images) and slower for 5x5 (config 3 3.86-3.93 vs
-  // 3.70 ms) in steady state (profiles/r02/median_tile/), so the stripe form stays the default
-  const int tile = env_int("IDN_MEDIAN_TILE", 0);
-  if (tile && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb && rb <= MT_RBMAX &&
-      h > 2 * (K / 2)) {
-    constexpr int NB = 6;
-    const int nseg = (int)((rb + 1007) / 1008);
-    const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
-    const int bands = (h + NB - 1) / NB;
-    const int64_t total = (int64_t)n * bands * nseg;
-    IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
-    hipLaunchKernelGGL((median_u8_lds<3, K, NB>), dim3((unsigned)((int64_t)n * bands)), dim3(MT_WGT),
-                       0, st, src, dst, h, (int)rb, nseg, seg_len, bands, (int)total);
-  } else if (stripe_ok(c, rb, row_stride, h, src, dst)) {
+  // (an LDS band-tile form like the stencils' was bit-exact but measured no faster for 3x3 and
+  // 4-6 % slower for 5x5 in steady state, profiles/r02/median_tile/; removed in round 3)
+  if (stripe_ok(c, rb, row_stride, h, src, dst)) {
     // measured (tools/sweep_stencil.py): 3x3 is near the memory side -> whole-row workgroups over
     // 16-row bands with XCD-contiguous band order; 5x5 is VALU-bound -> independent waves
-    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096, env_int("IDN_MEDIAN_MAP", K == 3 ? 1 : 0),
-                                     env_int("IDN_MEDIAN_ROWS", K == 3 ? 16 : 32));
+    const StripePlan p = plan_stripe(n, h, rb, K, K, 4096, knob("IDN_MEDIAN_MAP", K == 3 ? 1 : 0),
+                                     knob("IDN_MEDIAN_ROWS", K == 3 ? 16 : 32));
     IDN_CHECK_ARG(p.total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
     hipLaunchKernelGGL((median_u8_fast<3, K, 0>), dim3(p.grid), dim3(p.block), 0, st, src, dst, h,
                        (int)rb, (uint32_t)row_stride, p.nseg, p.seg_len, p.bands, p.band_rows,

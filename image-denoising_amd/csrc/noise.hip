@@ -8,10 +8,14 @@
 // with a replayed random field (numpy's own draws) the outputs are bit-exact; with the Philox
 // stream they are statistically equivalent (tests/test_noise_gpu.py).
 //
-// RNG: Philox4x32 keyed by (seed ^ kind tag); counter = (element group / draw, image id)
-// (the flat Gaussian / speckle stream: Philox4x32-7 and 16-bit uniforms, noise_apply.hpp).
-// Image id = offset + image index, so a rank that owns images [a, b) of a batch draws exactly
-// what a single GPU would for those images.
+// RNG: Philox4x32 keyed by (seed ^ kind tag); counter = (element group, stream tag, image id).
+// Gaussian / speckle have two streams (noise_apply.hpp): u8-only outputs draw 16-bit uniforms
+// (fp32 Box-Muller, fp32 apply on the 0..255 scale, tag 0, refinement tag 3); float64 outputs
+// draw 53-bit uniforms with an fp64 Box-Muller (tag 2) and apply in numpy's float64 order, the
+// U8 then being trunc(255 * out) of that value.  s&p (tag 1) and Poisson have one stream each.
+// Every layout (flat 16-element kernels for compact rows, element kernels for strided ones) draws
+// the same values.  Image id = offset + image index (or an id array), so a rank that owns images
+// [a, b) of a batch draws exactly what a single GPU would for those images.
 //
 // Also: periodic noise pattern (add_periodic_noise, test.py:1128-1298) and cv2.add(u8, u8).
 #include "idn_common.hpp"
@@ -54,8 +58,25 @@ __device__ __forceinline__ void store_out(const NoiseArgs& a, int img, int64_t e
   if (a.out_u8) a.out_u8[boff] = u8_of(out);
 }
 
-// one thread per element pair (2 normals per Philox block)
-template <int KIND>
+// two standard normals in float64 from one Philox4x32-10 block (counter (pair, 2, image id)):
+// 53-bit uniforms u1 in (0, 1], u2 in [0, 1) (|z| <= 8.57), rad = sqrt(-2 ln u1), (cos, sin)
+// (2 pi u2) by sincospi
+__device__ __forceinline__ void normal2_f64(const u32x4& r, double& z0, double& z1) {
+  const uint64_t a = ((uint64_t)r.x << 21) | (r.y >> 11), b = ((uint64_t)r.z << 21) | (r.w >> 11);
+  const double u1 = (double)(a + 1) * 0x1p-53, u2 = (double)b * 0x1p-53;
+  const double rad = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);
+  z0 = rad * cs;
+  z1 = rad * sn;
+}
+
+// element form, one thread per element pair: the noise value n of each element is numpy's own
+// draw (SRC_REPLAY: N(mean, sd) field, bit-exact with the reference) or mean + sd * z from the
+// float64 stream (SRC_F64); out = clip(x + n) / clip(x + x n) in numpy's op order, U8 = trunc(255
+// out).  Any row stride and slot layout.
+enum NoiseSrc { SRC_REPLAY = 0, SRC_F64 = 1 };
+template <int KIND, int SRC>
 __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
   const int64_t pairs = (a.elems + 1) / 2;
   const int64_t total = pairs * a.n;
@@ -64,19 +85,20 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
     const int img = (int)(t / pairs);
     const int64_t pr = t - (int64_t)img * pairs;
     double nz[2];
-    if (a.replay) {
+    if constexpr (SRC == SRC_REPLAY) {
       const int64_t e0 = 2 * pr;
       nz[0] = a.replay[(int64_t)img * a.elems + e0];
       nz[1] = (e0 + 1 < a.elems) ? a.replay[(int64_t)img * a.elems + e0 + 1] : 0.0;
     } else {
       const uint64_t gimg = image_id(a, img);
-      const u32x4 r = philox4x32(u32x4{(uint32_t)pr, (uint32_t)(pr >> 32), (uint32_t)gimg,
-                                       (uint32_t)(gimg >> 32)},
+      const u32x4 r = philox4x32(u32x4{(uint32_t)pr, 2u ^ ((uint32_t)(pr >> 32) << 8),
+                                       (uint32_t)gimg, (uint32_t)(gimg >> 32)},
                                  a.key);
-      float z0, z1;
-      normal2(r, z0, z1);
-      nz[0] = __dadd_rn(a.p0, __dmul_rn(a.p1, (double)z0));
-      nz[1] = __dadd_rn(a.p0, __dmul_rn(a.p1, (double)z1));
+      double z0, z1;
+      normal2_f64(r, z0, z1);
+      // np.random.normal(mean, sd): loc + scale * gauss
+      nz[0] = __dadd_rn(a.p0, __dmul_rn(a.p1, z0));
+      nz[1] = __dadd_rn(a.p0, __dmul_rn(a.p1, z1));
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -96,10 +118,9 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
   }
 }
 
-// ---- flat form (compact rows, Philox stream): 16 consecutive elements per thread -------------
-// One 16-byte load / store per lane, image = blockIdx.y, no 64-bit index division; the stream and
-// the float64 apply are noise16_u8 (noise_apply.hpp), shared with the fused noise -> filter
-// kernel (stencil_u8.hip), so the fused and two-step results are identical.
+// ---- u8 stream, flat form (compact rows): 16 consecutive elements per thread ------------------
+// One 16-byte load / store per lane, image = blockIdx.y, no 64-bit index division; the stream is
+// noise16_u8 (noise_apply.hpp).
 template <int KIND, bool MEAN0 = false>
 __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t t_flip,
                                                            uint32_t t_salt) {
@@ -115,24 +136,55 @@ __global__ __launch_bounds__(256) void noise_flat16_kernel(NoiseArgs a, uint32_t
   if (a.out_u8) *reinterpret_cast<v4u*>(a.out_u8 + base) = o;
 }
 
-// salt & pepper: flipped = U1 < cdf0(amount), salted = U2 < cdf0(salt_vs_pepper)
+// ---- u8 stream, element form (any layout): the same 16-element chunks gathered byte by byte ---
+template <int KIND, bool MEAN0 = false>
+__global__ __launch_bounds__(256) void noise_elem16_kernel(NoiseArgs a, uint32_t t_flip,
+                                                           uint32_t t_salt) {
+  const int64_t chunks = (a.elems + 15) / 16;
+  const int64_t total = chunks * a.n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int img = (int)(t / chunks);
+    const uint32_t chunk = (uint32_t)(t - (int64_t)img * chunks);
+    const int64_t e0 = (int64_t)chunk * 16;
+    int64_t off[16];
+    uint32_t in[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t e = e0 + i;
+      off[i] = -1;
+      if (e < a.elems) {
+        const int64_t pix = e / a.c;
+        const int ch = (int)(e - pix * a.c);
+        const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
+        off[i] = slot_of(a, img) * a.h * a.row_stride + (int64_t)y * a.row_stride +
+                 (int64_t)x * a.c + ch;
+        in[i >> 2] |= (uint32_t)a.src[off[i]] << (8 * (i & 3));
+      }
+    }
+    double of[16];
+    const v4u o = noise16_u8<KIND, MEAN0>(v4u{in[0], in[1], in[2], in[3]}, chunk, image_id(a, img),
+                                          a.key, a.p0, a.p1, t_flip, t_salt,
+                                          (KIND == IDN_NOISE_SAP && a.out_f64) ? of : nullptr);
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (off[i] < 0) continue;
+      if (a.out_u8) a.out_u8[off[i]] = (uint8_t)(ow[i >> 2] >> (8 * (i & 3)));
+      if (KIND == IDN_NOISE_SAP && a.out_f64) a.out_f64[slot_of(a, img) * a.elems + e0 + i] = of[i];
+    }
+  }
+}
+
+// salt & pepper, replay: flipped = U1 < cdf0(amount), salted = U2 < cdf0(salt_vs_pepper) on
+// numpy's own random_sample fields
 __global__ __launch_bounds__(256) void noise_sap_kernel(NoiseArgs a) {
   const int64_t total = a.elems * a.n;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int img = (int)(t / a.elems);
     const int64_t e = t - (int64_t)img * a.elems;
-    double u1, u2;
-    if (a.replay) {
-      u1 = a.replay[t];
-      u2 = a.replay[total + t];
-    } else {
-      const uint64_t gimg = image_id(a, img);
-      const u32x4 r = philox4x32(
-          u32x4{(uint32_t)e, (uint32_t)(e >> 32), (uint32_t)gimg, (uint32_t)(gimg >> 32)}, a.key);
-      u1 = u01_closed_open(r.x, r.y);
-      u2 = u01_closed_open(r.z, r.w);
-    }
+    const double u1 = a.replay[t], u2 = a.replay[total + t];
     const int64_t pix = e / a.c;
     const int ch = (int)(e - pix * a.c);
     const int y = (int)(pix / a.w), x = (int)(pix - (int64_t)y * a.w);
@@ -655,8 +707,9 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
   // flat form: Philox stream, compact rows, 16-element chunks that never straddle images
   const bool flat = !replay && row_stride == (int64_t)w * c && a.elems % 16 == 0 &&
                     ((uintptr_t)src & 15) == 0 && ((uintptr_t)out_u8 & 15) == 0 &&
-                    ((uintptr_t)out_f64 & 7) == 0 && a.elems / 16 < ((int64_t)1 << 31) &&
-                    env_int("IDN_NOISE_FLAT", 1) != 0;
+                    ((uintptr_t)out_f64 & 7) == 0 && a.elems / 16 < ((int64_t)1 << 31);
+  IDN_CHECK_ARG((a.elems + 15) / 16 < ((int64_t)1 << 32), "idn_noise_u8: image too large");
+  const unsigned g16 = grid_for((a.elems + 15) / 16 * n);
   switch (kind) {
     case IDN_NOISE_GAUSSIAN:
     case IDN_NOISE_SPECKLE: {
@@ -664,21 +717,35 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       a.p0 = p0;             // mean
       a.p1 = pow(p1, 0.5);   // var ** 0.5 (random_noise)
       const int64_t work = (a.elems + 1) / 2 * n;
-      if (flat) {
+      const bool g = kind == IDN_NOISE_GAUSSIAN, m0 = a.p0 == 0.0;
+      if (replay || out_f64) {  // numpy's field, or the float64 stream: float64 apply
+        if (replay && g)
+          hipLaunchKernelGGL((noise_gauss_kernel<IDN_NOISE_GAUSSIAN, SRC_REPLAY>), dim3(grid_for(work)), dim3(256), 0, st, a);
+        else if (replay)
+          hipLaunchKernelGGL((noise_gauss_kernel<IDN_NOISE_SPECKLE, SRC_REPLAY>), dim3(grid_for(work)), dim3(256), 0, st, a);
+        else if (g)
+          hipLaunchKernelGGL((noise_gauss_kernel<IDN_NOISE_GAUSSIAN, SRC_F64>), dim3(grid_for(work)), dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((noise_gauss_kernel<IDN_NOISE_SPECKLE, SRC_F64>), dim3(grid_for(work)), dim3(256), 0, st, a);
+      } else if (flat) {
         const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
-        const bool m0 = a.p0 == 0.0;
-        if (kind == IDN_NOISE_GAUSSIAN && m0)
+        if (g && m0)
           hipLaunchKernelGGL((noise_flat16_kernel<IDN_NOISE_GAUSSIAN, true>), grid, dim3(256), 0, st, a, 0u, 0u);
-        else if (kind == IDN_NOISE_GAUSSIAN)
+        else if (g)
           hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_GAUSSIAN>, grid, dim3(256), 0, st, a, 0u, 0u);
         else if (m0)
           hipLaunchKernelGGL((noise_flat16_kernel<IDN_NOISE_SPECKLE, true>), grid, dim3(256), 0, st, a, 0u, 0u);
         else
           hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SPECKLE>, grid, dim3(256), 0, st, a, 0u, 0u);
-      } else if (kind == IDN_NOISE_GAUSSIAN)
-        hipLaunchKernelGGL(noise_gauss_kernel<IDN_NOISE_GAUSSIAN>, dim3(grid_for(work)), dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL(noise_gauss_kernel<IDN_NOISE_SPECKLE>, dim3(grid_for(work)), dim3(256), 0, st, a);
+      } else if (g && m0) {
+        hipLaunchKernelGGL((noise_elem16_kernel<IDN_NOISE_GAUSSIAN, true>), dim3(g16), dim3(256), 0, st, a, 0u, 0u);
+      } else if (g) {
+        hipLaunchKernelGGL(noise_elem16_kernel<IDN_NOISE_GAUSSIAN>, dim3(g16), dim3(256), 0, st, a, 0u, 0u);
+      } else if (m0) {
+        hipLaunchKernelGGL((noise_elem16_kernel<IDN_NOISE_SPECKLE, true>), dim3(g16), dim3(256), 0, st, a, 0u, 0u);
+      } else {
+        hipLaunchKernelGGL(noise_elem16_kernel<IDN_NOISE_SPECKLE>, dim3(g16), dim3(256), 0, st, a, 0u, 0u);
+      }
       break;
     }
     case IDN_NOISE_SAP: {
@@ -687,13 +754,15 @@ static int noise_u8_impl(const uint8_t* src, uint8_t* out_u8, double* out_f64, i
       // np.random.choice([True, False], p=[p, 1-p]): True iff random_sample < cdf[0]
       a.p0 = p0 / (p0 + (1.0 - p0));
       a.p1 = p1 / (p1 + (1.0 - p1));
-      if (flat) {
+      const uint32_t tf = sap_threshold(a.p0), ts = sap_threshold(a.p1);
+      if (replay) {
+        hipLaunchKernelGGL(noise_sap_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+      } else if (flat) {
         // 16-bit uniform thresholds: P(u < t / 2^16) within 2^-16 of cdf0
         const dim3 grid((unsigned)((a.elems / 16 + 255) / 256), (unsigned)n);
-        hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SAP>, grid, dim3(256), 0, st, a,
-                           sap_threshold(a.p0), sap_threshold(a.p1));
+        hipLaunchKernelGGL(noise_flat16_kernel<IDN_NOISE_SAP>, grid, dim3(256), 0, st, a, tf, ts);
       } else {
-        hipLaunchKernelGGL(noise_sap_kernel, dim3(grid_for(a.elems * n)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(noise_elem16_kernel<IDN_NOISE_SAP>, dim3(g16), dim3(256), 0, st, a, tf, ts);
       }
       break;
     }

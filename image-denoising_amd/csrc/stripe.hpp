@@ -307,9 +307,9 @@ inline StripePlan plan_stripe(int n, int h, int64_t rb, int K, int U, int64_t ca
   StripePlan p;
   p.nseg = (int)((rb + 1007) / 1008);
   p.seg_len = (int)(((rb + p.nseg - 1) / p.nseg + 7) / 8 * 8);
-  p.map = env_int("IDN_STRIPE_MAP", map_default);
+  p.map = knob("IDN_STRIPE_MAP", map_default);
   if (p.nseg > 4) p.map = 0;  // rows wider than 4 segments: independent waves
-  int band_rows = fixed_rows > 0 ? fixed_rows : env_int("IDN_BAND_ROWS", 0);
+  int band_rows = fixed_rows > 0 ? fixed_rows : knob("IDN_BAND_ROWS", 0);
   if (band_rows <= 0 && p.map != 0) {
     band_rows = short_rows < h ? short_rows : h;
     while ((band_rows + (K - 1)) % U != 0 && band_rows < h) ++band_rows;
@@ -338,7 +338,7 @@ inline bool stripe_ok(int c, int64_t rb, int64_t row_stride, int h, const void* 
                       const void* dst) {
   return c == 3 && rb % 8 == 0 && row_stride % 8 == 0 && rb >= 32 && h >= 5 &&
          (int64_t)h * row_stride < (int64_t)0x40000000 && ((uintptr_t)src & 7) == 0 &&
-         ((uintptr_t)dst & 7) == 0 && env_int("IDN_FORCE_GENERIC", 0) == 0;
+         ((uintptr_t)dst & 7) == 0 && knob("IDN_FORCE_GENERIC", 0) == 0;
 }
 
 }  // namespace idn

@@ -2294,7 +2294,7 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
   }
   int nwg_a;
   if constexpr (L >= 2) {
-    if (src && env_int("IDN_WAVELET_INTSTATS", 1)) {
+    if (src && knob("IDN_WAVELET_INTSTATS", 1)) {
       nwg_a = (nthr + WLH_WG * WLS_IT - 1) / (WLH_WG * WLS_IT);
       hipLaunchKernelGGL((wl_haar_stats<L>), dim3(nwg_a, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
                          row_stride, wsf, Lt.img_floats, Lt.off_band[1], stats, part,
@@ -2321,7 +2321,7 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
                      wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   if constexpr (L >= 2) {
-    if (src && env_int("IDN_WAVELET_INTSYNTH", 1)) {
+    if (src && knob("IDN_WAVELET_INTSYNTH", 1)) {
       hipLaunchKernelGGL((wl_haar_synth_int<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
                          row_stride, stats, out_u8, out_f32);
       return;
@@ -2333,7 +2333,7 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
 
 // the fused path applies: db1, 1 <= L <= 3, both sides divisible by 2^L, room for its partials
 static bool wl_haar_ok(int wavelet, const WlLayout& Lt, const uint8_t* src, int64_t row_stride) {
-  if (wavelet != IDN_WAVELET_DB1 || Lt.L < 1 || Lt.L > 3 || env_int("IDN_WAVELET_FUSED", 1) == 0)
+  if (wavelet != IDN_WAVELET_DB1 || Lt.L < 1 || Lt.L > 3 || knob("IDN_WAVELET_FUSED", 1) == 0)
     return false;
   const int B = 1 << Lt.L;
   if (Lt.h % B || Lt.w % B) return false;
@@ -2362,15 +2362,15 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   // sigma from level-1 dd codes (wl_haar_median<.., true>) when the channel's input-plane slot
   // holds codes + keys + positions (2.25 band sizes); else the radix select over the band
   const size_t bsz1 = (size_t)Lt.H[1] * Lt.W[1];
-  const bool codes = env_int("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
-  const bool fdet = env_int("IDN_WAVELET_FDET", 1) != 0;
+  const bool codes = knob("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
+  const bool fdet = knob("IDN_WAVELET_FDET", 1) != 0;
   // band masks (wl_fband): level 1 / deeper levels, analysis stores and synthesis loads
   auto fm_an = [&](int l) {
     if (!fdet) return 0;
     return (l == 1 ? 0b0110 : 0b1110 | WL_FB_AIN) | (l < Lt.L ? 0b0001 : 0);
   };
   auto fm_syn = [&](int l) { return !fdet ? 0 : (l == 1 ? 0b0110 : 0b1110); };
-  const int coop = env_int("IDN_WAVELET_COOP", 1) ? 1 : 0;
+  const int coop = knob("IDN_WAVELET_COOP", 1) ? 1 : 0;
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];

@@ -1,5 +1,9 @@
 """Build the HIP C-ABI library in-tree: csrc/*.hip -> idn/libidn_hip.so (gfx950 only).
 
+build(tuning=True) builds the tools-only variant idn/libidn_hip_tuning.so (-DIDN_TUNING_BUILD:
+the kernels' tuning knobs read from the environment, for A/B runs and the cross-form tests that
+load it through idn._lib.variant("tuning")); the product library reads no environment variable.
+
 Driven by ``__graft_entry__.build()`` and by ``python -m idn._build``.  Every translation unit
 is compiled with ``hipcc --offload-arch=gfx950 -O3 -ffp-contract=off`` (no FMA contraction:
 the noise-apply and blob kernels restate numpy's float64 op order exactly) and linked into
@@ -17,7 +21,9 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 CSRC = PKG_DIR.parent / "csrc"
 LIB_PATH = PKG_DIR / "libidn_hip.so"
+TUNING_LIB_PATH = PKG_DIR / "libidn_hip_tuning.so"
 OBJ_DIR = PKG_DIR.parent / "build" / "obj"
+TUNING_OBJ_DIR = PKG_DIR.parent / "build" / "obj_tuning"
 ARCH = "gfx950"
 
 
@@ -43,40 +49,44 @@ def _flags() -> list[str]:
     ]
 
 
-def _compile_one(src: Path) -> Path:
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
-    obj = OBJ_DIR / (src.stem + ".o")
+def _compile_one(src: Path, tuning: bool = False) -> Path:
+    odir = TUNING_OBJ_DIR if tuning else OBJ_DIR
+    odir.mkdir(parents=True, exist_ok=True)
+    obj = odir / (src.stem + ".o")
     deps = [src] + sorted(CSRC.glob("*.hpp")) + [PKG_DIR.parent.parent / "include" / "idn.h"]
     if obj.exists() and obj.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
         return obj
-    cmd = [_hipcc(), *_flags(), "-c", str(src), "-o", str(obj)]
+    cmd = [_hipcc(), *_flags(), *(["-DIDN_TUNING_BUILD"] if tuning else []), "-c", str(src),
+           "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
     return obj
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> Path:
+def build(verbose: bool = False, jobs: int | None = None, tuning: bool = False) -> Path:
     sources = sorted(CSRC.glob("*.hip"))
     if not sources:
         raise RuntimeError(f"no HIP sources under {CSRC}")
     jobs = jobs or min(8, os.cpu_count() or 1, len(sources))
+    lib_path = TUNING_LIB_PATH if tuning else LIB_PATH
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(_compile_one, sources))
+        objs = list(ex.map(lambda s: _compile_one(s, tuning), sources))
     newest = max(o.stat().st_mtime for o in objs)
-    if not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
-        tmp = LIB_PATH.with_suffix(".so.tmp")
+    if not lib_path.exists() or lib_path.stat().st_mtime < newest:
+        tmp = lib_path.with_suffix(".so.tmp")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(tmp),
                *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
-        os.replace(tmp, LIB_PATH)
+        os.replace(tmp, lib_path)
     if verbose:
-        print(f"built {LIB_PATH}")
-    return LIB_PATH
+        print(f"built {lib_path}")
+    return lib_path
 
 
 if __name__ == "__main__":
     build(verbose=True)
+    build(verbose=True, tuning=True)
     sys.exit(0)

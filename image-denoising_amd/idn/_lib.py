@@ -2,14 +2,20 @@
 
 The library is the only compute path: there is no CPU fallback.  If the .so is missing (not
 built) or cannot be loaded, every op raises immediately.
+
+`variant("tuning")` swaps in the tools-only build idn/libidn_hip_tuning.so for the duration of a
+`with` block (tests that compare a kernel's alternative forms, selected by its tuning knobs); the
+product never loads it.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libidn_hip.so"
+VARIANTS = {"tuning": Path(__file__).resolve().parent / "libidn_hip_tuning.so"}
 
 _c_u8p = ctypes.c_void_p
 _c_f64p = ctypes.c_void_p
@@ -57,8 +63,6 @@ SIGNATURES = {
     "idn_quant_workspace_size": (_c_size, [_c_int, _c_int]),
     "idn_bgr2lab_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
     "idn_lab2bgr_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_i64, _c_vp]),
-    "idn_noise_filter_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
-                                     _c_dbl, _c_dbl, _c_u64, _c_u64, _c_vp, _c_int, _c_int, _c_vp]),
     "idn_gaussian_blob_f32": (_c_int, [_c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
                                        ctypes.POINTER(ctypes.c_double), _c_vp]),
     "idn_copy_u8": (_c_int, [_c_u8p, _c_u8p, _c_i64, _c_int, _c_vp]),
@@ -87,27 +91,49 @@ class IdnError(RuntimeError):
     """A C-ABI call returned a negative idn_status."""
 
 
+def _open(path: Path, required: bool):
+    if not path.exists():
+        raise IdnError(
+            f"{path} is missing: build it with `python -m idn._build` "
+            "(or __graft_entry__.build()); idn has no CPU fallback")
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if required:
+                raise IdnError(f"{path.name} does not export {name}")
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
 def load(required: bool = False):
     """Load libidn_hip.so and bind the declared symbols (raises if the library is missing;
     with required=True also if any symbol of include/idn.h is not exported)."""
     global _lib
     with _lock:
         if _lib is None:
-            if not LIB_PATH.exists():
-                raise IdnError(
-                    f"{LIB_PATH} is missing: build it with `python -m idn._build` "
-                    "(or __graft_entry__.build()); idn has no CPU fallback")
-            lib = ctypes.CDLL(str(LIB_PATH))
-            for name, (res, args) in SIGNATURES.items():
-                fn = getattr(lib, name, None)
-                if fn is None:
-                    if required:
-                        raise IdnError(f"{LIB_PATH.name} does not export {name}")
-                    continue
-                fn.restype = res
-                fn.argtypes = args
-            _lib = lib
+            _lib = _open(LIB_PATH, required)
     return _lib
+
+
+_variants: dict = {}
+
+
+@contextlib.contextmanager
+def variant(name: str):
+    """Route every op through a variant build of the library inside the block (tests only)."""
+    global _lib
+    with _lock:
+        if name not in _variants:
+            _variants[name] = _open(VARIANTS[name], True)
+        prev, _lib = _lib, _variants[name]
+    try:
+        yield _lib
+    finally:
+        with _lock:
+            _lib = prev
 
 
 def check(rc: int, what: str) -> None:

@@ -369,12 +369,10 @@ def noise_filter(x: torch.Tensor, mode: str, filter: str, ksize: int, *, var: fl
                  offset: int = 0, image_ids=None, out: Optional[torch.Tensor] = None,
                  form: str = "serial"):
     """random_noise(x, mode, ...) -> U8 -> cv2.GaussianBlur (filter 'gaus_blur') or cv2.blur
-    ('mean'); the result is identical in every form (Philox stream keyed by (seed, image id)).
+    ('mean'); the result is identical in every form (Philox u8 stream keyed by (seed, image id)).
       form 'serial'    the noise launch, then the filter launch (the default: fastest measured,
-                       profiles/r02/README.md -- the noise is VALU-bound and neither fused form
-                       overlaps it with the filter's memory traffic well enough to win)
-      form 'fused'     one pass (idn_noise_filter_u8: LDS ring, every byte fetched and noised
-                       once) when the layout allows, else 'serial'
+                       profiles/r02/README.md -- the noise is VALU-bound; a one-pass fused LDS-ring
+                       form measured slower and was removed in round 3)
       form 'pipelined' the batch in chunks: the noise of chunk k+1 (VALU-bound) runs on a side
                        stream beside the filter of chunk k (HBM-bound), whose input is still in
                        the 256 MB Infinity Cache"""
@@ -382,8 +380,8 @@ def noise_filter(x: torch.Tensor, mode: str, filter: str, ksize: int, *, var: fl
         return _noise_filter_pipelined(x, mode, filter, ksize, var=var, amount=amount,
                                        salt_vs_pepper=salt_vs_pepper, seed=seed, offset=offset,
                                        image_ids=image_ids, out=out)
-    if form not in ("fused", "serial"):
-        raise ValueError("noise_filter: form must be 'fused', 'serial' or 'pipelined'")
+    if form != "serial":
+        raise ValueError("noise_filter: form must be 'serial' or 'pipelined'")
     kind = NOISE_KINDS.get(mode.lower())
     if kind is None or kind == 3:
         raise ValueError(f"noise_filter: mode {mode!r} not supported (gaussian, speckle, s&p)")
@@ -392,19 +390,9 @@ def noise_filter(x: torch.Tensor, mode: str, filter: str, ksize: int, *, var: fl
     xb, sq = _u8_batch(x, "noise_filter")
     n, h, w, c = xb.shape
     y = torch.empty_like(xb) if out is None else out.view(n, h, w, c)
-    p0, p1 = (float(amount), float(salt_vs_pepper)) if kind == 2 else (0.0, float(var))
-    ids = _ids_tensor(image_ids, n, xb.device) if image_ids is not None else None
-    lib = _lib.load()
-    rc = -2 if form == "serial" else lib.idn_noise_filter_u8(xb.data_ptr(), y.data_ptr(), n, h, w, c, w * c, kind, p0, p1,
-                                 int(seed) & (2 ** 64 - 1), int(offset),
-                                 ids.data_ptr() if ids is not None else None, FILTERS[filter],
-                                 int(ksize), _stream())
-    if rc == -2:  # IDN_EUNSUPPORTED: not fusable for this layout -- run the two steps
-        kw = dict(amount=amount, salt_vs_pepper=salt_vs_pepper) if kind == 2 else dict(var=var)
-        t = random_noise(xb, mode, seed=seed, offset=offset, image_ids=image_ids, out="u8", **kw)
-        return _finish((gaussian_blur if filter == "gaus_blur" else blur)(t, ksize, out=y), sq)
-    _lib.check(rc, "idn_noise_filter_u8")
-    return _finish(y, sq)
+    kw = dict(amount=amount, salt_vs_pepper=salt_vs_pepper) if kind == 2 else dict(var=var)
+    t = random_noise(xb, mode, seed=seed, offset=offset, image_ids=image_ids, out="u8", **kw)
+    return _finish((gaussian_blur if filter == "gaus_blur" else blur)(t, ksize, out=y), sq)
 
 
 _PIPE_STREAMS: dict = {}

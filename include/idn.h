@@ -12,9 +12,23 @@
  *   - Pointers are DEVICE pointers owned by the caller; nothing is allocated inside a call.
  *     Calls that need scratch take (workspace, ws_bytes) and expose idn_*_workspace_size().
  *   - Every call is stream-ordered on `stream` (NULL = default stream) and capture-safe
- *     (no sync, no malloc).  The RNG position is explicit: (seed, offset) keys a Philox4x32-10
- *     stream; element e of image i draws counter (offset + i, e), so results do not depend on
- *     how a batch is split across launches or ranks.
+ *     (no sync, no malloc; idn_jpeg_decode_u8 and the one-time Poisson table build are the
+ *     documented exceptions).  The RNG position is explicit: Philox4x32 keyed by (seed ^ a per-
+ *     mode tag), counter = (element group, stream tag, image id) with image id = offset + i (or
+ *     an explicit id array), so results do not depend on how a batch is split across launches,
+ *     ranks or memory layouts.  Streams (csrc/noise.hip, noise_apply.hpp):
+ *       gaussian / speckle, u8-only output  Philox4x32-7, one block per 8 elements: 16-bit
+ *         uniforms, fp32 Box-Muller (the extreme radius cell refined to 32 bits from a second
+ *         block, |z| <= 6.66), U8 computed as floor(clip(v + 255 n)) / floor(clip(v + v n)) in
+ *         fp32 on the 0..255 scale
+ *       gaussian / speckle, float64 output  Philox4x32-10, one block per 2 elements: 53-bit
+ *         uniforms, fp64 Box-Muller, numpy's float64 apply; U8 = trunc(255 * out) of it
+ *       s&p      Philox4x32-7, one block per 4 elements: 16-bit `flipped` / `salted` uniforms
+ *                against integer thresholds (|P - p| < 2^-16)
+ *       poisson  Philox4x32-7, one block per 4 elements, 32-bit words inverted through the
+ *                exact CDF of Poisson(img_as_float(v) * vals)
+ *     The tuning knobs of the kernels are compile-time constants: this library reads no
+ *     environment variable.
  *   - Return IDN_OK (0) or a negative idn_status; idn_last_error() returns a thread-local
  *     message for the last failing call on the calling thread.
  *
@@ -199,16 +213,6 @@ int idn_lab2bgr_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_
 
 /* ---- fused steps (one pass over HBM instead of two) ------------------------------------------ */
 
-/* idn_noise_u8(kind, p0, p1, seed, offset | image_ids, U8 out) followed by
- * cv2.GaussianBlur(ksize) (filter 0) or cv2.blur(3) (filter 1), bit-exact with running the two
- * steps: the noise -> denoise branches of lib/model/test.py:220-241 / minibatch.py:115-146
- * (BASELINE config 2).  Each input byte is fetched and noised once.  Returns IDN_EUNSUPPORTED
- * (nothing launched) unless: C = 3, compact rows of 8k <= 3024 bytes, kind gaussian / speckle
- * with p0 (mean) == 0 or s&p.  image_ids (nullable) as for idn_noise_ids_u8. */
-int idn_noise_filter_u8(const uint8_t* src, uint8_t* dst, int n, int h, int w, int c,
-                        int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
-                        uint64_t offset, const uint64_t* image_ids, int filter, int ksize,
-                        void* stream);
 /* cv2.GaussianBlur(img, (ksize, ksize), 0) then prep_im_for_blob at scale 1.0
  * (lib/utils/blob.py:33-47): blob = float32(float64(v) - mean[ch]), dense (n, h, w, c) float32
  * written by the filter kernel (the filtered u8 image never reaches HBM).  mean: host double[3].

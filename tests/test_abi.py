@@ -70,3 +70,36 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(_lib.IdnError):
         _lib.load()
+
+
+def test_product_library_reads_no_environment():
+    """No environment variable can change an output byte of the product library: getenv is not
+    among its undefined dynamic symbols (the tuning knobs are compile-time defaults; only the
+    tools-only variant libidn_hip_tuning.so reads them), and in csrc/ getenv appears only inside
+    `#ifdef IDN_TUNING_BUILD`."""
+    import subprocess
+    p = _lib_path()
+    nm = "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not Path(nm).exists():
+        nm = "nm"
+    und = subprocess.run([nm, "-D", "--undefined-only", str(p)], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {line.split()[-1].split("@")[0] for line in und.splitlines() if line.strip()}
+    assert not ({"getenv", "secure_getenv", "__secure_getenv"} & syms)
+    for src in sorted((ROOT / "image-denoising_amd" / "csrc").glob("*")):
+        depth, tuning_depth = 0, None
+        for i, line in enumerate(src.read_text().splitlines(), 1):
+            t = line.strip()
+            if t.startswith("#if"):
+                depth += 1
+                if "IDN_TUNING_BUILD" in t and tuning_depth is None:
+                    tuning_depth = depth
+            elif t.startswith("#else") and tuning_depth == depth:
+                tuning_depth = -depth  # the #else branch is the product's
+            elif t.startswith("#endif"):
+                if tuning_depth is not None and abs(tuning_depth) == depth:
+                    tuning_depth = None
+                depth -= 1
+            code = t.split("//")[0]
+            if "getenv" in code:
+                assert tuning_depth is not None and tuning_depth > 0, f"{src.name}:{i}: {t}"

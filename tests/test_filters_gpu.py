@@ -71,39 +71,53 @@ def test_stencil_random_extremes(dev, k):
 
 
 def test_generic_path_forced(dev, monkeypatch):
+    """the per-pixel kernel (shapes the lane layout does not take), forced on a shape it would
+    not get by itself through the tools-only tuning build"""
     import idn
     import oracle
+    from idn import _lib
     monkeypatch.setenv("IDN_FORCE_GENERIC", "1")
     img = textured(2, 31, 200, seed=9)
-    assert np.array_equal(_run(idn.gaussian_blur, img, 5), oracle.cv.gaussian_blur(img, 5))
-    assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+    with _lib.variant("tuning"):
+        assert np.array_equal(_run(idn.gaussian_blur, img, 5), oracle.cv.gaussian_blur(img, 5))
+        assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+    # and without forcing: c = 2 and odd row lengths take it in the product library
+    img2 = textured(2, 17, 45, c=2, seed=4)
+    assert np.array_equal(_run(idn.gaussian_blur, img2, 5), oracle.cv.gaussian_blur(img2, 5))
 
 
-FORMS = [
-    {"IDN_STENCIL_TILE": "1"},                 # LDS tile, 6-row bands (default)
-    {"IDN_STENCIL_TILE": "2"},                 # LDS tile, 11 / 10-row bands
-    {"IDN_STENCIL_TILE": "3"},                 # LDS tile, 8 / 4-row bands
-    {"IDN_STENCIL_TILE": "1", "IDN_STENCIL_MAP": "2", "IDN_STENCIL_NT": "2"},
-    {"IDN_STENCIL_TILE": "0"},                 # stripe form, short bands from HBM
-    {"IDN_STENCIL_FLAT": "1"},                 # flat-output epilogue (16-B aligned bands only)
-    {"IDN_STENCIL_FLAT": "1", "IDN_STENCIL_TILE": "3", "IDN_STENCIL_NT": "2"},
-    {"IDN_STENCIL_PF": "1"},                   # persistent register-prefetch form
-]
+def _run_strided(fn_name, img, k, pad=8):
+    """the C-ABI on rows padded to W*C + pad bytes (the stripe form from HBM)"""
+    import torch
+    from idn import _lib
+    lib = _lib.load()
+    n, h, w, c = img.shape
+    rs = (w * c + pad + 7) // 8 * 8
+    buf = torch.zeros((n, h, rs), dtype=torch.uint8, device="cuda")
+    buf[:, :, : w * c] = torch.from_numpy(img.reshape(n, h, w * c)).cuda()
+    out = torch.full_like(buf, 77)
+    rc = getattr(lib, fn_name)(buf.data_ptr(), out.data_ptr(), n, h, w, c, rs, k, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert bool((out[:, :, w * c:] == 77).all())  # padding untouched
+    return out[:, :, : w * c].cpu().numpy().reshape(n, h, w, c)
 
 
-@pytest.mark.parametrize("form", FORMS, ids=lambda f: "-".join(f"{k[12:]}{v}" for k, v in f.items()))
+@pytest.mark.parametrize("layout", ["compact", "strided"])
 @pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (2, 13, 104), (1, 601, 1000),
                                    (1, 26, 1000), (1, 25, 664)])
-def test_stencil_forms_agree(dev, monkeypatch, form, shape):
-    """every memory form of the stencil gives cv2's bytes (band tails, 1-3 segments, odd heights)"""
+def test_stencil_forms_agree(dev, layout, shape):
+    """both memory forms of the stencil (the LDS band tile for compact rows, the stripe form for
+    strided rows) give cv2's bytes (band tails, 1-3 segments, odd heights)"""
     import idn
     import oracle
-    for k, v in form.items():
-        monkeypatch.setenv(k, v)
     img = textured(*shape, seed=sum(shape))
     for k in (3, 5):
-        assert np.array_equal(_run(idn.gaussian_blur, img, k), oracle.cv.gaussian_blur(img, k)), k
-    assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+        got = (_run(idn.gaussian_blur, img, k) if layout == "compact"
+               else _run_strided("idn_gaussian_blur_u8", img, k))
+        assert np.array_equal(got, oracle.cv.gaussian_blur(img, k)), k
+    got = _run(idn.blur, img, 3) if layout == "compact" else _run_strided("idn_box_blur_u8", img, 3)
+    assert np.array_equal(got, oracle.cv.blur(img, 3))
 
 
 @pytest.mark.parametrize("w,pad", [(1000, 8), (344, 16), (1400, 0)])
@@ -165,10 +179,12 @@ def test_median_saltpepper_extremes(dev, k):
 def test_median_generic_forced(dev, monkeypatch):
     import idn
     import oracle
+    from idn import _lib
     monkeypatch.setenv("IDN_FORCE_GENERIC", "1")
     img = textured(2, 23, 64, seed=5)
-    for k in (3, 5):
-        assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k))
+    with _lib.variant("tuning"):
+        for k in (3, 5):
+            assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k))
 
 
 BILATERAL_CASES = [(9, 20.0, 100.0), (9, 75.0, 75.0), (5, 30.0, 10.0), (3, 10.0, 10.0)]
@@ -202,18 +218,21 @@ def test_bilateral_gray(dev):
     assert np.abs(got.astype(int) - ref.astype(int)).max() <= 1
 
 
-@pytest.mark.parametrize("form", [{"IDN_MEDIAN_MAP": "0", "IDN_MEDIAN_ROWS": "32"},
+@pytest.mark.parametrize("form", [{}, {"IDN_MEDIAN_MAP": "0", "IDN_MEDIAN_ROWS": "32"},
                                   {"IDN_MEDIAN_MAP": "1", "IDN_MEDIAN_ROWS": "16"},
-                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"},
-                                  {"IDN_MEDIAN_TILE": "1"}],  # LDS band-tile form
-                         ids=lambda f: "-".join(f"{k[11:]}{v}" for k, v in f.items()))
+                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"}],
+                         ids=lambda f: "-".join(f"{k[11:]}{v}" for k, v in f.items()) or "product")
 @pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (1, 601, 1000), (2, 13, 104)])
 def test_median_forms_agree(dev, monkeypatch, form, shape):
-    """every band / workgroup mapping of the median gives cv2's bytes (band tails, 1-3 segments)"""
+    """every band / workgroup mapping of the median (the tuning build's knobs; {} = the product
+    library) gives cv2's bytes (band tails, 1-3 segments)"""
+    import contextlib
     import idn
     import oracle
+    from idn import _lib
     for k, v in form.items():
         monkeypatch.setenv(k, v)
     img = textured(*shape, seed=sum(shape) + 1)
-    for k in (3, 5):
-        assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k)), k
+    with (_lib.variant("tuning") if form else contextlib.nullcontext()):
+        for k in (3, 5):
+            assert np.array_equal(_run(idn.median_blur, img, k), oracle.cv.median_blur(img, k)), k

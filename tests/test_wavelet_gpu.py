@@ -136,10 +136,11 @@ def test_wavelet_haar_integer_stats_match_fp64(dev, monkeypatch, levels):
     squares to 1e-12 relative, outputs to rounding"""
     import torch
     x = torch.from_numpy(_stat_images(96, 160)).cuda()
-    monkeypatch.setenv("IDN_WAVELET_INTSTATS", "1")
-    u8a, fa, sa = _stats_after(x, levels)
+    from idn import _lib
+    u8a, fa, sa = _stats_after(x, levels)  # product library: integer statistics
     monkeypatch.setenv("IDN_WAVELET_INTSTATS", "0")
-    u8b, fb, sb = _stats_after(x, levels)
+    with _lib.variant("tuning"):
+        u8b, fb, sb = _stats_after(x, levels)
     L = levels
     med = slice(8 + 9 * L, 8 + 9 * L + 3)
     np.testing.assert_array_equal(sa[:, med].view(np.uint64), sb[:, med].view(np.uint64))
@@ -170,8 +171,10 @@ def test_wavelet_haar_fused_matches_general(dev, monkeypatch, shape, levels, f64
     if f64:
         img = np.clip(img / 255.0 + np.random.RandomState(1).normal(0, 0.1, img.shape), 0, 1)
     u8a, fa = run(img, "db1", levels)
+    from idn import _lib
     monkeypatch.setenv("IDN_WAVELET_FUSED", "0")
-    u8b, fb = run(img, "db1", levels)
+    with _lib.variant("tuning"):
+        u8b, fb = run(img, "db1", levels)
     assert np.abs(fa - fb).max() <= 1e-6
     d = u8a.astype(int) - u8b.astype(int)
     assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-4
@@ -189,8 +192,10 @@ def test_wavelet_fp32_details_vs_fp64(dev, monkeypatch, shape, wavelet, levels):
     import oracle
     img = make_img(*shape, 17)
     u8a, fa = run(img, wavelet, levels)
+    from idn import _lib
     monkeypatch.setenv("IDN_WAVELET_FDET", "0")
-    u8b, fb = run(img, wavelet, levels)
+    with _lib.variant("tuning"):
+        u8b, fb = run(img, wavelet, levels)
     assert np.abs(fa - fb).max() <= 1e-6
     d = u8a.astype(int) - u8b.astype(int)
     assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-4
@@ -205,8 +210,10 @@ def test_wavelet_coop_normalisation_bitwise(dev, monkeypatch, shape):
     per-channel form (=0): the same fp64 operations per sample, so bit-identical outputs"""
     img = make_img(*shape, 23)
     u8a, fa = run(img, "bior1.5", None)
+    from idn import _lib
     monkeypatch.setenv("IDN_WAVELET_COOP", "0")
-    u8b, fb = run(img, "bior1.5", None)
+    with _lib.variant("tuning"):
+        u8b, fb = run(img, "bior1.5", None)
     np.testing.assert_array_equal(u8a, u8b)
     np.testing.assert_array_equal(fa, fb)
 
