@@ -89,7 +89,7 @@ PARITY = {"noise_gaussian": "skimage random_noise('gaussian') U8 law (chi-square
                          "the reference's pinned library"}
 # ops that synchronise inside the call (host work, H2D copies, convergence polls): their event
 # time is the op's end-to-end duration, not a kernel's, so no HBM fraction is claimed for them
-END_TO_END = {"jpeg_decode"}
+END_TO_END = {"jpeg_decode", "detect_e2e"}
 
 def _pipeline(kind):
     """BASELINE.json configs 2-5 as one step = noise + denoise over the batch (intermediate u8
@@ -194,6 +194,29 @@ def _jpeg_decode(idn, x, y):
 OPS["jpeg_decode"] = ("JPEG decode (cv2.imread), q90 4:2:0 files in host memory", _jpeg_decode, 3,
                       "jpeg_")
 
+def _detect_e2e(idn, x, y):
+    """The reference's per-image test loop body as one step (lib/model/test.py:189-191,
+    1678-1684, 1787-1811, 85-90): a 600x1000 q90 4:2:0 JPEG file on disk -> GPU decode
+    (cv2.imread) -> apply_noise('gaussian_wavelet_var0.1', test_v0: random gaussian level, float64
+    plain branch, the live bior1.5 wavelet hook) -> _get_blobs -> the float32 blob in host memory
+    (numpy), as net.test_image is fed.  Batch 1 (IMS_PER_BATCH = 1): the figure is latency."""
+    st = _detect_e2e.__dict__
+    if "path" not in st:
+        import tempfile
+        from PIL import Image
+        d = tempfile.mkdtemp(prefix="idn_bench_")
+        st["path"] = os.path.join(d, "im.jpg")
+        Image.fromarray(x[0].cpu().numpy()[..., ::-1]).save(st["path"], "JPEG", quality=90,
+                                                             subsampling=2)
+    from idn import detect_blob
+    im = detect_blob.apply_noise(st["path"], "gaussian_wavelet_var0.1", mode="test_v0",
+                                 decode="gpu", as_tensor=True)
+    detect_blob._get_blobs(im)
+
+
+OPS["detect_e2e"] = ("per-image test_net body: JPEG -> gaussian_wavelet (test_v0) -> blob, numpy out",
+                     _detect_e2e, 6, "e2e")
+
 METRIC = "Mpix/s filtered (5\u00d75 Gaussian, 1000\u00d7600) at 1/2/4/8 GPUs; % HBM roofline"
 
 
@@ -243,6 +266,10 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "wavelet_bior15": lambda a: oracle.sk.to_u8(
             255 * oracle.wavelet.denoise_wavelet(a[0], "bior1.5", None)),
         "gauss5_blob": lambda a: oracle.sk.blob_f32(oracle.cv.gaussian_blur_fast(a, 5)),
+        # the per-image body on the host: decode, f64 gaussian noise, bior1.5 wavelet, blob
+        "detect_e2e": lambda a: oracle.sk.blob_f32([oracle.wavelet.denoise_wavelet(
+            oracle.sk.noise_gaussian(a[0], np.random.normal(0.0, 1.0, a[0].shape)),
+            "bior1.5", None)]),  # test_v0 quirk: the float64 [0, 1] image goes to the blob
     }
     table["cfg2p"] = table["cfg2"]
     if op == "jpeg_decode":  # Pillow's libjpeg-turbo decode of the same kind of file
@@ -273,7 +300,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         if el >= budget_s or n_img >= 1000000:
             break
     if op in ("noise_gaussian", "noise_sap", "noise_poisson", "wavelet_haar3", "cfg5",
-              "wavelet_bior15"):
+              "wavelet_bior15", "detect_e2e"):
         threads, src = 1, "numpy, single thread"
     elif op == "jpeg_decode":
         threads, src = 1, "PIL (libjpeg-turbo) decode, single thread"
@@ -393,7 +420,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.batch <= 0:
-        args.batch = PIPELINES[args.op][1] if args.op in PIPELINES else 256
+        args.batch = (PIPELINES[args.op][1] if args.op in PIPELINES else
+                      1 if args.op == "detect_e2e" else 256)
     if args.scaling == "strong":
         from idn.parallel import shard_range
         lo, hi = shard_range(args.batch, rank, world)
@@ -566,6 +594,10 @@ def main():
             rec["roofline"]["frac_of_default_policy_copy"] = round(
                 achieved_gbs / ceiling["by_policy"]["default"], 4)
             rec["copy_ceiling"] = ceiling
+        if args.op == "detect_e2e":  # the user-visible number: latency per image
+            rec["ms_per_image"] = round(wall / args.steps * 1e3 / my_batch, 3)
+            rec["reference_ms_per_image"] = "65-180 (skimage random_noise / denoise_wavelet on "\
+                                            "the host, BASELINE.md)"
         if args.op == "cfg5":  # the drawn noise mix (record it in the output)
             rec["config"]["mix"] = {k: len(v[0]) for k, v in call.state["groups"].items()}
         if gather is not None:

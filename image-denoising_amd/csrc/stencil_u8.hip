@@ -300,33 +300,43 @@ __device__ __forceinline__ void lds_take_row(const uint8_t* tile, uint32_t o, bo
 
 enum TileEpi { EPI_U8 = 0, EPI_BLOB = 1 };
 
-// the blob of one lane's 16 output bytes at row byte offset q: 16 floats, 4 (full chunk) or
-// 2 (half chunk) 16-byte stores; always 6 store instructions (unused ones out of range)
-__device__ __forceinline__ void blob_store16(const v4u& o, const double (&means)[3],
-                                             rsrc_t rb_rsrc, const StoreOffs& so,
-                                             uint32_t row_off, int m0) {
-  const uint32_t b[4] = {o.x, o.y, o.z, o.w};
-  float f[16];
+// Blob epilogue (EPI_BLOB): blob = float32(float64(v) - PIXEL_MEANS[ch]) (lib/utils/blob.py:35-36:
+// numpy's float64 subtract, then the float32 store) is a 3 x 256 table, held in LDS interleaved as
+// lut[3 v + ch] (lanes reading the same byte value of different channels hit different banks).
+// The filtered row segment is staged in LDS (one 16-byte write per lane) and re-read as dwords, so
+// store k of a lane writes the four floats of row bytes seg_start + 256 k + 4 lane .. + 3: every
+// 16-byte store instruction of a wave writes 1 KiB of contiguous blob (the last 960 B), with no
+// partial-chunk stores.
+constexpr int BLOB_LUT = 768;          // floats
+constexpr int BLOB_STAGE = 3 * 1024;   // bytes: one 1 KiB row-segment stage per wave
+__device__ __forceinline__ void blob_row_store(const v4u& o, uint32_t* __restrict__ stage,
+                                               const float* __restrict__ lut, int lane,
+                                               const StripeGeom& g, const uint32_t (&c4)[3],
+                                               rsrc_t rd, bool row_ok, uint32_t row_byte) {
+  // WAR: the previous row's reads of this wave's stage are issued before this write
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  reinterpret_cast<v4u*>(stage)[lane] = o;  // stage byte 16 lane = row byte q
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int ch = (m0 + i) % 3;
-    const double mean = ch == 0 ? means[0] : ch == 1 ? means[1] : means[2];
-    f[i] = (float)__dsub_rn((double)((b[i >> 2] >> (8 * (i & 3))) & 0xFFu), mean);
+  for (int k = 0; k < 4; ++k) {
+    const int e = g.seg_start + 256 * k + 4 * lane;  // row byte of the store's first float
+    const bool ok = row_ok && e < g.seg_end;         // seg_end - seg_start is a multiple of 8
+    const uint32_t w = stage[min(2 + 64 * k + lane, 255)];
+    float f[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t v = (w >> (8 * j)) & 0xFFu;
+      f[j] = *reinterpret_cast<const float*>(reinterpret_cast<const uint8_t*>(lut) +
+                                             (v * 12u + c4[(k + j) % 3]));
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(
+        v4u{__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]),
+            __float_as_uint(f[3])},
+        rd, ok ? 4u * (row_byte + (uint32_t)e) : OOB_OFF, 0, 0);
   }
-  auto v = [&](int k) {
-    return v4u{__float_as_uint(f[4 * k]), __float_as_uint(f[4 * k + 1]),
-               __float_as_uint(f[4 * k + 2]), __float_as_uint(f[4 * k + 3])};
-  };
-  const uint32_t full = so.full + row_off, half = so.half + row_off;  // byte offsets
-  // full chunk: bytes q..q+15 -> floats at 4*(q..q+15)
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    __builtin_amdgcn_raw_buffer_store_b128(v(k), rb_rsrc, full >= OOB_OFF ? OOB_OFF : 4u * full + 16u * k, 0, 0);
-  // half chunk: bytes 0..7 (at q) or 8..15 (at q + 8) of the chunk
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-    __builtin_amdgcn_raw_buffer_store_b128(so.hi ? v(2 + k) : v(k), rb_rsrc,
-                                           half >= OOB_OFF ? OOB_OFF : 4u * half + 16u * k, 0, 0);
 }
 
 // ---- LDS-tiled form --------------------------------------------------------------------------
@@ -360,7 +370,9 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   constexpr int K = Stencil<OP>::K;
   constexpr int R = K / 2;
   using TS = TileShape<NB, K>;
-  __shared__ __attribute__((aligned(16))) uint8_t tile[TS::LDS];
+  constexpr int EXTRA = EPI == EPI_BLOB ? BLOB_LUT * 4 + BLOB_STAGE : 0;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[TS::LDS + EXTRA];
+  uint8_t* const tile = smem;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -381,6 +393,13 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
   const uint32_t base = (uint32_t)ys * (uint32_t)rb;
   const uint32_t base_al = base & ~15u, shift = base - base_al;
   const uint32_t nbytes = (uint32_t)ye * (uint32_t)rb - base_al;
+  if constexpr (EPI == EPI_BLOB) {  // the blob table (published by the tile's barrier)
+    float* lut = reinterpret_cast<float*>(smem + TS::LDS);
+    for (int i = threadIdx.x; i < BLOB_LUT; i += TILE_WGT) {
+      const int v = i / 3, ch = i - 3 * v;
+      lut[i] = (float)__dsub_rn((double)v, ch == 0 ? mb : ch == 1 ? mg : mr);
+    }
+  }
 
   // flat fetch of the tile into LDS (out-of-image lanes read 0 and are not written).  Full bands
   // (every chunk but the last round's inside the tile): one lane offset, the round in the scalar
@@ -427,6 +446,14 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     const int y = reflect101_1(y0 - R + min(r, nin - 1), h);
     lds_take_row<C>(tile, (uint32_t)(y - ys) * (uint32_t)rb + shift + ld_off, g.lead, Rg[r % K]);
   };
+  // blob: byte offsets into lut[3 v + ch] of the channels of this lane's store bytes
+  // (row byte seg_start + 256 k + 4 lane + j has channel (c0 + k + j) % 3: 256 = 1 mod 3)
+  uint32_t c4[3] = {0u, 0u, 0u};
+  if constexpr (EPI == EPI_BLOB) {
+    const int c0 = (g.seg_start + 4 * lane) % 3;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) c4[t] = 4u * (uint32_t)((c0 + t) % 3);
+  }
 #pragma unroll
   for (int r = 0; r < 2 * R; ++r) take_row(r);
 #pragma unroll
@@ -436,8 +463,10 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     const int y = y0 + u;
     const uint32_t row_off = y < y1 ? (uint32_t)y * (uint32_t)rb : OOB_OFF;
     if constexpr (EPI == EPI_BLOB) {
-      const double means[3] = {mb, mg, mr};
-      blob_store16(ring_row<C, OP>(Rg, r % K, g), means, rd, so, row_off, ((g.q % 3) + 3) % 3);
+      blob_row_store(ring_row<C, OP>(Rg, r % K, g),
+                     reinterpret_cast<uint32_t*>(smem + TS::LDS + BLOB_LUT * 4 + 1024 * wave),
+                     reinterpret_cast<const float*>(smem + TS::LDS), lane, g, c4, rd, y < y1,
+                     (uint32_t)y * (uint32_t)rb);
     } else {
       ring_out_row<C, OP, 0>(Rg, r % K, g, rd, so, row_off);
     }

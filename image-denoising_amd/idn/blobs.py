@@ -29,12 +29,22 @@ def im_scale_for(shape, target_size: int, max_size: int) -> float:
 
 
 def prep_im_for_blob(im, pixel_means, target_size, max_size, flip: bool = False,
-                     as_tensor: bool = False):
+                     as_tensor: bool = False, gaussian_ksize=None):
     """im (uint8 BGR or float64) -> (float32 mean-subtracted, resized image, im_scale).
 
-    `flip` folds the roidb 'flipped' column reversal (minibatch.py:1675) into the same pass."""
+    `flip` folds the roidb 'flipped' column reversal (minibatch.py:1675) into the same pass.
+    gaussian_ksize: cv2.GaussianBlur(im, (k, k), 0) still to be applied to the uint8 image (a
+    recipe's last step, idn.pipeline.Preprocessor.run_for_blob): at scale 1.0 without a flip the
+    blur and the blob are one pass (idn_gaussian_blob_f32), else the blur runs first."""
     x = _to_device(im)
     means = np.asarray(pixel_means, np.float64).reshape(-1)
+    if gaussian_ksize:
+        if x.dtype != torch.uint8:
+            raise TypeError("prep_im_for_blob: a deferred GaussianBlur needs a uint8 image")
+        if not flip and im_scale_for(x.shape, target_size, max_size) == 1.0:
+            f = ops.gaussian_blob(x, int(gaussian_ksize), means)[0]
+            return (f if as_tensor else f.cpu().numpy()), 1.0
+        x = ops.gaussian_blur(x, int(gaussian_ksize))
     if x.dtype == torch.uint8:
         f = ops.blob(x, means, flip=flip)[0]
     elif x.dtype == torch.float64:

@@ -4,6 +4,10 @@ per-image loop (189-1831) and the blob builders _get_image_blob (49-83) / _get_b
     im = apply_noise(img, noise)          # replaces test.py:193-1831 for one image
     blobs, im_scales = _get_blobs(im)     # test.py:85, then net.test_image(...)
 
+or, with the decode front-end on the GPU too (cv2.imread at test.py:191):
+
+    im = apply_noise(path, noise, decode="gpu")
+
 mode='test_v0' (default) reproduces test.py as-is (sap/quant add no noise, gaussian picks a random
 level and returns float64, only the 'wavelet' post hook is live, unknown strings fall to
 gaussian_var0.1 + 3x3 mean on the float image).
@@ -15,7 +19,10 @@ from types import SimpleNamespace
 
 import numpy as np
 
+from pathlib import Path
+
 from . import blobs as _blob
+from . import io as _io
 from .pipeline import Preprocessor
 
 cfg = SimpleNamespace(
@@ -27,8 +34,16 @@ _PRE = {}
 
 
 def apply_noise(img, noise: str, mode: str = "test_v0", image_id: int = 0,
-                noise_rng: str = "philox", as_tensor: bool = False):
-    """One image through the reference's noise + denoise recipe on the GPU (uint8 or float64)."""
+                noise_rng: str = "philox", as_tensor: bool = False, decode: str = "host"):
+    """One image through the reference's noise + denoise recipe on the GPU (uint8 or float64).
+
+    img: the cv2.imread image (numpy / device tensor) or a file path, read by cv2.imread
+    semantics: decode="host" (PIL / cv2 on the host) or decode="gpu" (the GPU JPEG decoder,
+    bit-exact with the pinned libjpeg 9d; no CPU fallback: an unsupported file raises)."""
+    if decode not in ("host", "gpu"):
+        raise ValueError("decode must be 'host' or 'gpu'")
+    if isinstance(img, (str, Path)):
+        img = _io.imread_gpu([img])[0] if decode == "gpu" else _io.imread(img)
     key = (noise, mode, noise_rng)
     if key not in _PRE:
         _PRE[key] = Preprocessor(noise, mode, seed=cfg.RNG_SEED, rng=_random, noise_rng=noise_rng)

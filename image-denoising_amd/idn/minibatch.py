@@ -42,13 +42,17 @@ def _preprocessor(noise: str, mode: str, noise_rng: str):
     return p
 
 
-def get_minibatch(roidb, num_classes, mode: str = "train_v0", noise_rng: str = "philox"):
-    """Given a roidb, construct a minibatch sampled from it (minibatch.py:42)."""
+def get_minibatch(roidb, num_classes, mode: str = "train_v0", noise_rng: str = "philox",
+                  decode: str = "host"):
+    """Given a roidb, construct a minibatch sampled from it (minibatch.py:42).  decode="gpu"
+    reads the images with the GPU JPEG decoder (cv2.imread at minibatch.py:85 -> idn.io.imread_gpu,
+    bit-exact with the pinned libjpeg 9d); a file it does not take raises IdnError."""
     num_images = len(roidb)
     random_scale_inds = npr.randint(0, high=len(cfg.TRAIN.SCALES), size=num_images)
     assert cfg.TRAIN.BATCH_SIZE % num_images == 0, \
         "num_images ({}) must divide BATCH_SIZE ({})".format(num_images, cfg.TRAIN.BATCH_SIZE)
-    im_blob, im_scales = _get_image_blob(roidb, random_scale_inds, mode=mode, noise_rng=noise_rng)
+    im_blob, im_scales = _get_image_blob(roidb, random_scale_inds, mode=mode, noise_rng=noise_rng,
+                                         decode=decode)
     blobs = {"data": im_blob}
     assert len(im_scales) == 1, "Single batch only"
     assert len(roidb) == 1, "Single batch only"
@@ -66,20 +70,26 @@ def get_minibatch(roidb, num_classes, mode: str = "train_v0", noise_rng: str = "
 
 
 def _get_image_blob(roidb, scale_inds, mode: str = "train_v0", noise_rng: str = "philox",
-                    as_tensor: bool = False):
+                    as_tensor: bool = False, decode: str = "host"):
     """Builds an input blob from the images in the roidb at the specified scales."""
+    if decode not in ("host", "gpu"):
+        raise ValueError("decode must be 'host' or 'gpu'")
     processed_ims, im_scales = [], []
     for i in range(len(roidb)):
         img = roidb[i].get("im")
         if img is None:
-            img = _io.imread(roidb[i]["image"])
+            img = (_io.imread_gpu([roidb[i]["image"]])[0] if decode == "gpu"
+                   else _io.imread(roidb[i]["image"]))
         pre = _preprocessor(roidb[i]["noise_type"], mode, noise_rng)
-        outs, _plans = pre(_blob._to_device(img)[None], image_ids=[int(roidb[i].get("index", 0))])
+        # a recipe that ends in a uint8 GaussianBlur leaves that blur to the blob builder: at
+        # scale 1.0 without a flip the blur and prep_im_for_blob run as one pass
+        outs, ks, _plans = pre.run_for_blob(_blob._to_device(img)[None],
+                                            image_ids=[int(roidb[i].get("index", 0))])
         target_size = cfg.TRAIN.SCALES[scale_inds[i]]
+        flip = bool(roidb[i].get("flipped", False))
         im, im_scale = _blob.prep_im_for_blob(outs[0], cfg.PIXEL_MEANS, target_size,
-                                              cfg.TRAIN.MAX_SIZE,
-                                              flip=bool(roidb[i].get("flipped", False)),
-                                              as_tensor=True)
+                                              cfg.TRAIN.MAX_SIZE, flip=flip, as_tensor=True,
+                                              gaussian_ksize=ks[0])
         im_scales.append(im_scale)
         processed_ims.append(im)
     blob = _blob.im_list_to_blob(processed_ims, as_tensor=as_tensor)

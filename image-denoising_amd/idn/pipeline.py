@@ -62,6 +62,7 @@ class Preprocessor:
             key = (i,) if self.noise_rng == "numpy" else _group_key(p.steps)
             groups.setdefault(key, []).append(i)
         outs: List[Optional[torch.Tensor]] = [None] * n
+        self._deferred = [None] * n
         for _, idx in groups.items():
             steps = plans[idx[0]].steps
             if len(idx) == n:
@@ -70,10 +71,25 @@ class Preprocessor:
                 sub = batch.index_select(0, torch.as_tensor(idx, device=batch.device))
             self._bloom_draws = [next((st.args for st in plans[i].steps if st.op == "bloom"), ())
                                  for i in idx]
-            res = self._run_steps(sub, steps, [ids[i] for i in idx])
+            res, k_def = self._run_steps(sub, steps, [ids[i] for i in idx])
             for k, i in enumerate(idx):
                 outs[i] = res[k]
+                self._deferred[i] = k_def
         return outs, plans
+
+    def run_for_blob(self, batch: torch.Tensor, image_ids: Optional[Sequence[int]] = None,
+                     plans: Optional[Sequence[ns.Plan]] = None):
+        """Like __call__, but a plan that ends in a uint8 cv2.GaussianBlur stops before it:
+        returns (outputs, ksizes, plans) with ksizes[i] the deferred blur's ksize (None if
+        nothing was deferred), so the blob builder can run the blur and prep_im_for_blob as one
+        pass (idn_gaussian_blob_f32) -- the filtered uint8 image never reaches HBM."""
+        self._defer = True
+        try:
+            outs, plans = self(batch, image_ids, plans)
+        finally:
+            self._defer = False
+        ks = list(getattr(self, "_deferred", [None] * len(outs)))
+        return outs, ks, plans
 
     def run_batch(self, batch: torch.Tensor, image_ids=None, plans=None):
         """Like __call__ but stacks the outputs when they share dtype and shape."""
@@ -192,6 +208,9 @@ class Preprocessor:
         while i < len(steps):
             st = steps[i]
             nxt = steps[i + 1] if i + 1 < len(steps) else None
+            if (nxt is None and getattr(self, "_defer", False) and st.kind == "filter"
+                    and st.op == "gaus_blur" and cur.dtype == torch.uint8):
+                return list(cur.unbind(0)), int(st.args[0])  # left to the blob builder
             if st.kind == "noise":
                 cur = self._noise(cur, st, nxt, ids)
                 if nxt is not None and nxt.kind == "cast_u8":
@@ -201,7 +220,7 @@ class Preprocessor:
             else:
                 cur = self._filter(cur, st)
             i += 1
-        return list(cur.unbind(0))
+        return list(cur.unbind(0)), None
 
 
 def _group_key(steps: Tuple[ns.Step, ...]) -> tuple:

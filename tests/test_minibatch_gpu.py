@@ -100,3 +100,74 @@ def test_get_minibatch_matches_oracle(dev, tmp_path, spec, flip):
     assert np.array_equal(blobs["gt_boxes"][:, :4], boxes)
     assert blobs["gt_boxes"][:, 4].tolist() == [5, 12]
     assert blobs["im_info"].tolist() == [600.0, 800.0, 2.0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["s420_opt_130x170.jpg", "s422_q85_120x200.jpg"])
+def test_get_minibatch_gpu_decode_matches_libjpeg9_pixels(dev, tmp_path, name):
+    """decode="gpu" (cv2.imread at minibatch.py:85 on the GPU): the blob equals the one built from
+    the reference's pinned libjpeg 9d pixels of the same file (tests/golden/jpeg9.npz)"""
+    import shutil
+    from pathlib import Path
+    from idn import minibatch
+    from idn.roidb import prepare_roidb
+    gold = Path(__file__).resolve().parent / "golden"
+    px = np.load(gold / "jpeg9.npz")[name]
+    imdb = _imdb(tmp_path, [px])
+    shutil.copyfile(gold / "jpeg" / name, tmp_path / name)
+    imdb._paths = [tmp_path / name]
+    prepare_roidb(imdb, "gaussian_mean_var0.1")
+    entry = dict(imdb.roidb[0], flipped=True)
+    random.seed(5)
+    np.random.seed(6)
+    got = minibatch.get_minibatch([entry], 21, mode="train_v0", noise_rng="numpy", decode="gpu")
+    random.seed(5)
+    np.random.seed(6)
+    ref = minibatch.get_minibatch([dict(entry, im=px)], 21, mode="train_v0", noise_rng="numpy")
+    assert np.array_equal(got["data"], ref["data"])
+    assert np.array_equal(got["im_info"], ref["im_info"])
+
+
+@pytest.mark.gpu
+def test_apply_noise_gpu_decode(dev):
+    from pathlib import Path
+    from idn import detect_blob
+    from idn._lib import IdnError
+    gold = Path(__file__).resolve().parent / "golden"
+    name = "s420_q75_odd_37x53.jpg"
+    px = np.load(gold / "jpeg9.npz")[name]
+    random.seed(2)
+    a = detect_blob.apply_noise(gold / "jpeg" / name, "gaussian_wavelet_var0.1", decode="gpu",
+                                noise_rng="philox", image_id=4)
+    random.seed(2)
+    b = detect_blob.apply_noise(px, "gaussian_wavelet_var0.1", noise_rng="philox", image_id=4)
+    assert a.dtype == b.dtype and np.array_equal(a, b)
+    with pytest.raises(IdnError):  # no silent CPU fallback for files the decoder does not take
+        detect_blob.apply_noise(gold / "jpeg" / "progressive_64x64.jpg", "original", decode="gpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flip", [False, True])
+def test_minibatch_defers_final_gaussian_into_the_blob(dev, flip):
+    """a recipe ending in a uint8 GaussianBlur at scale 1.0: _get_image_blob runs the blur and
+    prep_im_for_blob as one pass (idn_gaussian_blob_f32); the blob equals the two-step result
+    (flipped entries take the two steps)"""
+    import torch
+    from idn import minibatch, ops
+    img = textured(1, 600, 1000, seed=8)[0]
+    spec = "speckle_gaus_blur_var0.5"
+    entry = {"im": img, "noise_type": spec, "flipped": flip, "index": 3}
+    pre = minibatch._preprocessor(spec, "canonical", "numpy")
+    random.seed(1)
+    np.random.seed(2)
+    _, ks, _ = pre.run_for_blob(torch.from_numpy(img).cuda()[None], image_ids=[3])
+    assert ks[0] in (3, 5)
+    random.seed(1)
+    np.random.seed(2)
+    blob, scales = minibatch._get_image_blob([entry], [0], mode="canonical", noise_rng="numpy")
+    assert scales == [1.0]
+    random.seed(1)
+    np.random.seed(2)
+    outs, _ = pre(torch.from_numpy(img).cuda()[None], image_ids=[3])
+    ref = ops.blob(outs[0][None], flip=flip).cpu().numpy()
+    assert np.array_equal(blob, ref)
