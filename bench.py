@@ -381,6 +381,8 @@ def parse_args(argv=None):
     ap.add_argument("--gather", action="store_true",
                     help="N>1: also time reassembling the filtered batch on every rank with one "
                          "RCCL all-gather over xGMI per step (reported as 'allgather')")
+    ap.add_argument("--lib", choices=("product", "tuning"), default="product",
+                    help="tools only: run through the tuning build (knobs from the environment)")
     ap.add_argument("--dry-run", action="store_true",
                     help="resolve ranks and shards and print them without touching a GPU (tests)")
     return ap.parse_args(argv)
@@ -453,6 +455,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
+    if args.lib == "tuning":  # A/B runs of the kernels' tuning knobs (never the driver's line)
+        from idn import _lib
+        _lib.variant("tuning").__enter__()
     label, call, bpp, kname = OPS[args.op]
     x = synth_batch(torch, my_batch, dev, seed=3 + rank)
     y = torch.empty_like(x)

@@ -359,7 +359,7 @@ struct TileShape {
   static constexpr int LDS = (BYTES + 15) / 16 * 16;
 };
 
-template <int C, int OP, int NB, int EPI = EPI_U8>
+template <int C, int OP, int NB, int EPI = EPI_U8, int NTS = 0>
 __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __restrict__ src,
                                                           uint8_t* __restrict__ dst, int h, int rb,
                                                           int nseg, int seg_len, int bands,
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
                      reinterpret_cast<const float*>(smem + TS::LDS), lane, g, c4, rd, y < y1,
                      (uint32_t)y * (uint32_t)rb);
     } else {
-      ring_out_row<C, OP, 0>(Rg, r % K, g, rd, so, row_off);
+      ring_out_row<C, OP, NTS ? 2 : 0>(Rg, r % K, g, rd, so, row_off);
     }
   }
 }
@@ -607,9 +607,15 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
     const int bands = (h + NB - 1) / NB;
     const int64_t total = (int64_t)n * bands * nseg;
     IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
-    hipLaunchKernelGGL((stencil_u8_lds<3, OP, NB>), dim3((unsigned)((int64_t)n * bands)),
-                       dim3(TILE_WGT), 0, st, src, dst, h, (int)rb, nseg, seg_len, bands,
-                       (int)total);
+    // nontemporal stores: a tuning-build A/B (IDN_STENCIL_NTS); the product keeps the default
+    if (knob("IDN_STENCIL_NTS", 0))
+      hipLaunchKernelGGL((stencil_u8_lds<3, OP, NB, EPI_U8, 1>), dim3((unsigned)((int64_t)n * bands)),
+                         dim3(TILE_WGT), 0, st, src, dst, h, (int)rb, nseg, seg_len, bands,
+                         (int)total);
+    else
+      hipLaunchKernelGGL((stencil_u8_lds<3, OP, NB>), dim3((unsigned)((int64_t)n * bands)),
+                         dim3(TILE_WGT), 0, st, src, dst, h, (int)rb, nseg, seg_len, bands,
+                         (int)total);
   } else if (stripe_ok(c, rb, row_stride, h, src, dst)) {
     // strided or wide rows: stripe form.  Rows of <= 4 segments: short bands, one workgroup per
     // band, all band rows loaded up front; wider rows: long bands of independent waves.

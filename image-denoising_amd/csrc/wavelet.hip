@@ -119,6 +119,8 @@ __device__ __forceinline__ int wl_fbin(unsigned long long key) {
   return e * 16 + (int)((key >> 48) & 15u);
 }
 
+inline int ws_strips(int Wo);
+inline int ws_bands(int n, int Ho, int strips);
 inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   WlLayout Lt;
   Lt.n = n;
@@ -143,8 +145,13 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   Lt.stats_off = (size_t)n * Lt.img_floats * sizeof(wreal);
   size_t tiles_tot = 0;
   for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
-    Lt.tiles_x[l] = (Lt.W[l] + RB_TX - 1) / RB_TX;  // wl_dwt_rb tiles
-    Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + RB_TY - 1) / RB_TY);
+    if (wv == IDN_WAVELET_BIOR15) {  // wl_dwt_stream: strips x row bands
+      Lt.tiles_x[l] = ws_strips(Lt.W[l]);
+      Lt.tiles[l] = Lt.tiles_x[l] * ws_bands(n, Lt.H[l], Lt.tiles_x[l]);
+    } else {
+      Lt.tiles_x[l] = (Lt.W[l] + RB_TX - 1) / RB_TX;  // wl_dwt_rb tiles
+      Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + RB_TY - 1) / RB_TY);
+    }
     Lt.part_tile0[l] = tiles_tot;
     tiles_tot += (size_t)Lt.tiles[l];
   }
@@ -347,7 +354,7 @@ constexpr int WL_FB_AIN = 16;
 __host__ __device__ __forceinline__ bool wl_fband(int fmask, int b) { return (fmask >> b) & 1; }
 
 // SRC: 0 = u8 image, 1 = f64 image (level 1, normalised per channel), 2 = the 'aa' planes of the
-// level above (levels >= 2).  Grid (tiles, 1, n).
+// level above (levels >= 2; wl_dwt_stream: 2 fp64, 3 fp32).  Grid (tiles, 1, n).
 template <int WV, int SRC>
 __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t img_floats,
                                                  const double* __restrict__ stats, size_t in_off,
@@ -575,6 +582,271 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
       dst[0] = sv[0];
       if (oj + 1 < Wo) dst[1] = sv[1];
     }
+  }
+}
+
+// ---- 2b: bior1.5 analysis, streaming form ------------------------------------------------------
+// pywt's bior1.5 decomposition pair in terms of input pairs: with s_k = x[2k] + x[2k+1] and
+// e_k = x[2k+1] - x[2k] over the symmetrically extended input (output i uses x[2i-8 .. 2i+1]),
+//   lo[i] = S2 s_{i-2} + B1 (e_i - e_{i-4}) + B2 (e_{i-3} - e_{i-1})     (10 taps -> 5 operations;
+//           rounding within a few ulps of pywt's sum: aa / ad / da only feed the thresholds and
+//           the synthesis, both checked within 1e-5)
+//   hi[i] = (-S2 x[2i-3]) + S2 x[2i-4]                                  (pywt's order, exact:
+//           the finest dd's exact zeros select the sigma median's population)
+// One workgroup per (image, strip of SW output columns, band of output rows) walks down the rows,
+// one input row pair per step.
+//   column phase: thread u = staged input column 2 j0 - 8 + u (all three channels) normalises its
+//     two new samples -- every sample once per strip (halo: 8 of 2 SW + 8 columns; the tiled
+//     wl_dwt_rb normalised each sample ~1.7 times) -- and adds the pair to five running lowpass
+//     accumulators (pair k contributes B1 e_k, -B2 e_k, S2 s_k, B2 e_k, -B1 e_k to outputs
+//     k .. k+4); output row i's column lowpass / highpass go to LDS (double-buffered: one barrier
+//     per step).  The raw samples of the next PF steps are in flight in a register ring.
+//   row phase: thread (c, jj) runs the pair form along the row for the two adjacent outputs jj,
+//     jj + 1: aa / da (lowpass of the column low / high), ad = S2 (v[2j-4] - v[2j-3]), dd in
+//     pywt's exact order; band stores (fp32 bands per fmask), level-1 dd codes, sums of squares
+// Row bands start four pairs early to fill the accumulators (4 / band height extra work).
+constexpr int WS_MAXT = 256;                 // threads = staged columns per workgroup (max)
+constexpr int WS_MAXSW = (WS_MAXT - 8) / 2;  // 124 output columns per strip (max)
+inline int ws_strips(int Wo) { return (Wo + WS_MAXSW - 1) / WS_MAXSW; }
+inline int ws_sw(int Wo) {
+  const int st = ws_strips(Wo);
+  return ((Wo + st - 1) / st + 1) & ~1;
+}
+inline int ws_bands(int n, int Ho, int strips) {  // >= ~6 workgroups per CU; bands >= 24 rows
+  const int want = (1536 + n * strips - 1) / (n * strips);
+  return std::max(1, std::min(want, Ho / 24));
+}
+
+template <int SRC>
+struct WsRaw;  // the raw input of one step (two rows) for one staged column
+template <> struct WsRaw<0> {  // u8 pixels: 3 bytes of each row
+  uint32_t p[2];
+};
+template <> struct WsRaw<1> {  // f64 pixels
+  double p[2][3];
+};
+template <> struct WsRaw<2> {  // the level above's 'aa', three channels, fp64
+  double p[2][3];
+};
+template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (WL_FB_AIN)
+  float p[2][3];
+};
+// prefetch depth (steps; divides 5): the u8 and fp32 rings are small, the fp64 ones are not
+template <int SRC> constexpr int ws_pf() { return SRC == 0 || SRC == 3 ? 5 : 1; }
+
+template <int SRC>
+__global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
+    wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
+    int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands,
+    const uint8_t* __restrict__ src, const double* __restrict__ in64, int64_t row_stride,
+    double* __restrict__ part, size_t part_per_img, size_t part_tile0, int emit_codes,
+    int fmask) {
+  constexpr int PF = ws_pf<SRC>();
+  __shared__ wreal VL[2][3][WS_MAXT], VH[2][3][WS_MAXT];
+  const int img = blockIdx.z;
+  const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
+  const int j0 = strip * SW;
+  const int ia = (int)((int64_t)band * Ho / bands), ib = (int)((int64_t)(band + 1) * Ho / bands);
+  const int t = threadIdx.x;
+  wreal* base = ws + img * img_floats;
+  // ---- column role
+  const int NXs = 2 * SW + 8;
+  const bool colt = t < NXs;
+  const int qc = sym_idx(2 * j0 - 8 + t, Win);  // this thread's input column
+  wreal mn[3] = {0, 0, 0}, inv[3] = {1, 1, 1}, rcp[3] = {1, 1, 1};
+  if (SRC < 2) {
+    const double* st = stats + (size_t)img * WL_STATS;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      wreal mx;
+      wl_minmax64(st, c, mn[c], mx);
+      inv[c] = mx - mn[c];
+      rcp[c] = 1.0 / inv[c];
+    }
+  }
+  rsrc_t rs;
+  if (SRC == 0)
+    rs = make_rsrc(src + (int64_t)img * Hin * row_stride, (uint32_t)((int64_t)Hin * row_stride));
+  else if (SRC == 1)
+    rs = make_rsrc(in64 + (int64_t)img * Hin * Win * 3, (uint32_t)((int64_t)Hin * Win * 24));
+  auto load = [&](int k, WsRaw<SRC>& R) {
+    const int rows[2] = {sym_idx(2 * k, Hin), sym_idx(2 * k + 1, Hin)};
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      if constexpr (SRC == 0) {
+        const uint32_t so = (uint32_t)((int64_t)rows[h2] * row_stride), vo = (uint32_t)qc * 3u;
+        const uint32_t b0 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo, so, 0);
+        const uint32_t b1 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo + 1u, so, 0);
+        const uint32_t b2 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo + 2u, so, 0);
+        R.p[h2] = b0 | b1 << 8 | b2 << 16;
+      } else if constexpr (SRC == 1) {
+        const uint32_t so = (uint32_t)rows[h2] * (uint32_t)Win * 24u;
+#pragma unroll
+        for (int k3 = 0; k3 < 3; ++k3)
+          R.p[h2][k3] = __longlong_as_double((long long)__builtin_amdgcn_raw_buffer_load_b64(
+              rs, (uint32_t)qc * 24u + 8u * k3, so, 0));
+      } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const wreal* X = base + in_off + (size_t)c * 4 * Hin * Win;
+          const size_t e = (size_t)rows[h2] * Win + qc;
+          if constexpr (SRC == 3) R.p[h2][c] = reinterpret_cast<const float*>(X)[e];
+          else R.p[h2][c] = X[e];
+        }
+      }
+    }
+  };
+  // channel c of row h2 of the raw step: normalised (SRC 0 / 1) or the aa sample (SRC 2)
+  auto norm = [&](const WsRaw<SRC>& R, int h2, int c) -> wreal {
+    if constexpr (SRC >= 2) {
+      return (wreal)R.p[h2][c];
+    } else {
+      double px[3];
+#pragma unroll
+      for (int k3 = 0; k3 < 3; ++k3) {
+        if constexpr (SRC == 0) px[k3] = (double)((R.p[h2] >> (8 * k3)) & 0xFFu) * (1.0 / 255.0);
+        else px[k3] = R.p[h2][k3];
+      }
+      const wreal a = ycbcr_c(px, c) - mn[c];
+      if constexpr (SRC == 1) {
+        return a / inv[c];
+      } else {
+        // skimage's (Y - min) / (max - min) as the IEEE quotient: reciprocal multiply + one
+        // Markstein correction, exact over every u8 triple (tools/check_div.c)
+        const wreal qq = a * rcp[c];
+        return __fma_rn(__fma_rn(-qq, inv[c], a), rcp[c], qq);
+      }
+    }
+  };
+  wreal acc[3][5];           // running column lowpass of outputs k .. k+4 (slot = output % 5)
+  wreal hd0[3], hd1[3];      // column highpass of pairs k-1, k-2 (hi[i] is pair i-2's)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    hd0[c] = hd1[c] = 0.0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) acc[c][r] = 0.0;
+  }
+  // ---- row role
+  const int half = SW / 2;
+  const bool rowt = t < 3 * half;
+  const int rc = rowt ? t / half : 0, jj = rowt ? 2 * (t - rc * half) : 0;
+  const int oj = j0 + jj;
+  const bool ok0 = rowt && oj < Wo, ok1 = rowt && oj + 1 < Wo;
+  const size_t bsz = (size_t)Ho * Wo;
+  double sq[3] = {0.0, 0.0, 0.0};
+
+  const int k0 = ia - 4, M = ib - ia + 4;  // steps m = 0 .. M-1 cover pairs k = k0 + m
+  WsRaw<SRC> rq[PF];                        // raw samples of steps m .. m + PF - 1 (slot m % PF)
+  if (colt) {
+#pragma unroll
+    for (int f = 0; f < PF; ++f)
+      if (f < M) load(k0 + f, rq[f]);
+  }
+  for (int m0 = 0; m0 < M; m0 += 5) {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      const int k = k0 + m;
+      const int buf = m & 1;
+      if (colt) {
+        const int slot = r % PF;  // PF divides 5 (compile-time after unrolling)
+        const WsRaw<SRC> cur = rq[slot];
+        if (m + PF < M) load(k + PF, rq[slot]);  // refill the slot PF steps ahead
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const wreal x0 = norm(cur, 0, c), x1 = norm(cur, 1, c);
+          const wreal sk = x0 + x1, ek = x1 - x0;
+          const wreal hk = __dadd_rn(__dmul_rn(-S2, x1), __dmul_rn(S2, x0));  // pywt: mul, add
+          // pair k's contributions; slot (k + j) % 5 == (r + j) % 5 for the unrolled r
+          acc[c][(r + 4) % 5] = -B1 * ek;
+          acc[c][(r + 3) % 5] = __fma_rn(B2, ek, acc[c][(r + 3) % 5]);
+          acc[c][(r + 2) % 5] = __fma_rn(S2, sk, acc[c][(r + 2) % 5]);
+          acc[c][(r + 1) % 5] = __fma_rn(-B2, ek, acc[c][(r + 1) % 5]);
+          const wreal lo = __fma_rn(B1, ek, acc[c][r]);  // output k complete
+          if (m >= 4) {
+            VL[buf][c][t] = lo;
+            VH[buf][c][t] = hd1[c];
+          }
+          hd1[c] = hd0[c];
+          hd0[c] = hk;
+        }
+      }
+      if (m < 4) continue;  // accumulator fill (wave-uniform)
+      __syncthreads();
+      const int i = k;  // output row
+      if (rowt) {
+        const wreal* vl = &VL[buf][rc][2 * jj];
+        const wreal* vh = &VH[buf][rc][2 * jj];
+        wreal o[2][4];  // [output][aa, ad, da, dd]
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {  // column low -> aa / ad, column high -> da / dd
+          const wreal* v = pass ? vh : vl;
+          wreal S[6], E[6];
+#pragma unroll
+          for (int nn = 0; nn < 6; ++nn) {
+            const wreal a0 = v[2 * nn], a1 = v[2 * nn + 1];
+            S[nn] = a0 + a1;
+            E[nn] = a1 - a0;
+          }
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            o[d][2 * pass] =
+                __fma_rn(S2, S[2 + d], __fma_rn(B1, E[4 + d] - E[d], B2 * (E[1 + d] - E[3 + d])));
+            if (pass == 0) o[d][1] = -S2 * E[2 + d];
+            else o[d][3] = __dadd_rn(__dmul_rn(-S2, v[2 * d + 5]), __dmul_rn(S2, v[2 * d + 4]));
+          }
+        }
+        const size_t e0 = (size_t)i * Wo + oj;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          if (!(d ? ok1 : ok0)) continue;
+          sq[0] += o[d][1] * o[d][1];
+          sq[1] += o[d][2] * o[d][2];
+          sq[2] += o[d][3] * o[d][3];
+          if (emit_codes) {
+            const unsigned long long key = absbits(o[d][3]);
+            reinterpret_cast<uint16_t*>(base + (size_t)rc * Hin * Win)[e0 + d] =
+                (uint16_t)(key ? wl_fbin(key) + 1 : 0);
+          }
+        }
+        wreal* ob = base + out_off + (size_t)rc * 4 * bsz;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (wl_fband(fmask, b)) {
+            float* f = reinterpret_cast<float*>(ob + (size_t)b * bsz) + e0;
+            if (ok1 && ((uintptr_t)f & 7) == 0) {  // both outputs, one aligned 8-byte store
+              *reinterpret_cast<float2*>(f) = make_float2((float)o[0][b], (float)o[1][b]);
+            } else {
+              if (ok0) f[0] = (float)o[0][b];
+              if (ok1) f[1] = (float)o[1][b];
+            }
+          } else {
+            wreal* f = ob + (size_t)b * bsz + e0;
+            if (ok1 && ((uintptr_t)f & 15) == 0) {
+              *reinterpret_cast<double2*>(f) = make_double2(o[0][b], o[1][b]);
+            } else {
+              if (ok0) f[0] = o[0][b];
+              if (ok1) f[1] = o[1][b];
+            }
+          }
+        }
+      }
+    }
+  }
+  // per-workgroup sums of squares, channel by channel in thread order (deterministic)
+  __syncthreads();
+  wreal* red = &VL[0][0][0];
+  if (rowt) {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) red[b * WS_MAXT + t] = sq[b];
+  }
+  __syncthreads();
+  if (t < 9) {
+    const int c = t / 3, b = t - 3 * c;
+    double s2 = 0.0;
+    for (int g = 0; g < half; ++g) s2 += red[b * WS_MAXT + c * half + g];
+    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = s2;
   }
 }
 
@@ -890,6 +1162,30 @@ __device__ __forceinline__ void synth_load(SynthLoad<WV>& L, const wreal* __rest
     if (f) L.odd |= (uint32_t)(e & 1) << u;
   }
 }
+// one output pair of the full synthesis step, lowpass band coefficients cl[j] and highpass
+// cd[j] (c[j] = x[i - j]), written to (ev, od).  Haar / generic: pywt's sums (synth_pair).
+// bior1.5: rlo has the two taps S2 (even, odd) at j = 2, and rhi's even / odd taps are
+// B1, -B2, +-S2, B2, -B1, so with common = B1 (d0 - d4) + B2 (d3 - d1)
+//   ev = common + S2 (a + d2),  od = common + S2 (a - d2)      (a = cl[2], d = cd)
+// 8 operations for the pair instead of pywt's 26; the rounding differs from pywt's by a few ulps
+// (the synthesis is checked within 1e-5, and no exact zero depends on it).
+template <int WV>
+__device__ __forceinline__ void synth_full(const wreal (&cl)[Wav<WV>::F / 2],
+                                           const wreal (&cd)[Wav<WV>::F / 2], wreal& ev,
+                                           wreal& od) {
+  if constexpr (WV == IDN_WAVELET_BIOR15) {
+    const wreal common = __fma_rn(B1, cd[0] - cd[4], B2 * (cd[3] - cd[1]));
+    ev = __fma_rn(S2, cl[2] + cd[2], common);
+    od = __fma_rn(S2, cl[2] - cd[2], common);
+  } else {
+    wreal le, lo, he, ho;
+    synth_pair<WV, false>(cl, le, lo);
+    synth_pair<WV, true>(cd, he, ho);
+    ev = __dadd_rn(le, he);
+    od = __dadd_rn(lo, ho);
+  }
+}
+
 template <int WV, typename Between>
 __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>& L,
                                           const wreal (&thr)[3], wreal (&v)[ST_O * ST_O / 256],
@@ -923,15 +1219,8 @@ __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>&
       c2[j] = S.co[2][r][col];
       c3[j] = S.co[3][r][col];
     }
-    wreal le, lo, he, ho;
-    synth_pair<WV, false>(c0, le, lo);
-    synth_pair<WV, true>(c1, he, ho);
-    S.sa[r][2 * nn] = __dadd_rn(le, he);
-    S.sa[r][2 * nn + 1] = __dadd_rn(lo, ho);
-    synth_pair<WV, false>(c2, le, lo);
-    synth_pair<WV, true>(c3, he, ho);
-    S.sd[r][2 * nn] = __dadd_rn(le, he);
-    S.sd[r][2 * nn + 1] = __dadd_rn(lo, ho);
+    synth_full<WV>(c0, c1, S.sa[r][2 * nn], S.sa[r][2 * nn + 1]);
+    synth_full<WV>(c2, c3, S.sd[r][2 * nn], S.sd[r][2 * nn + 1]);
   }
   __syncthreads();
 #pragma unroll
@@ -944,11 +1233,7 @@ __device__ __forceinline__ void synth_run(SynthTile<WV>& S, const SynthLoad<WV>&
       ca[j] = S.sa[m + HF - 1 - j][q];
       cd[j] = S.sd[m + HF - 1 - j][q];
     }
-    wreal le, lo, he, ho;
-    synth_pair<WV, false>(ca, le, lo);
-    synth_pair<WV, true>(cd, he, ho);
-    v[2 * i] = __dadd_rn(le, he);
-    v[2 * i + 1] = __dadd_rn(lo, ho);
+    synth_full<WV>(ca, cd, v[2 * i], v[2 * i + 1]);
   }
   __syncthreads();  // S is restaged by the next call
 }
@@ -1073,6 +1358,245 @@ __global__ __launch_bounds__(256) void wl_synth_final(const wreal* __restrict__ 
       const int r = k / (ST_O * 3), b = k - r * (ST_O * 3);
       if (p0 + r < h && q0 + b / 3 < w) orow[(int64_t)(p0 + r) * row_stride + b] = ob[r * (ST_O * 3) + b];
     }
+  }
+}
+
+// ---- 6/7 (bior1.5): synthesis, streaming form -------------------------------------------------
+// One workgroup per (image, strip of SWo output columns, band of output row pairs) walks down the
+// band's coefficient rows; every coefficient is loaded and soft-thresholded once per strip (the
+// tiled form staged 1.56x with its halos).  Output pair (2m, 2m+1) x (2n, 2n+1) uses coefficient
+// rows m .. m+4 and columns n .. n+4 (pywt upsampling_convolution_valid_sf, c[j] = x[i - j]).
+// Per step, coefficient row r:
+//   stage    the row's 4 bands x 3 channels over columns [n0, n0 + SWo/2 + 4) into LDS (details
+//            soft-thresholded), from a register ring SS_PF rows ahead; every load is issued
+//            unconditionally (an fp32 band is read as the 8-byte pair holding its element, the
+//            half picked by a select) so no load sits behind a branch and its wait
+//   axis 1   thread (c, np): the pair form (synth_full) on row r for output columns 2np, 2np+1:
+//            sa = idwt(aa, ad), sd = idwt(da, dd) -> a five-row register ring (shifted by moves)
+//   axis 0   once five rows are in: output rows 2m, 2m+1 (m = r - 4) of both columns from the
+//            ring; levels >= 2 store the reconstruction (fp64) into the level above's 'aa' slot,
+//            level 1 (FINAL) clips, de-normalises and hands Y / Cb / Cr to LDS; there every pixel
+//            pair is converted to BGR (inverse YCbCr, clip, U8 / f32) into an LDS row image that
+//            the next step stores as whole dwords.
+constexpr int SS_MAXT = 256;
+constexpr int SS_MAXSW = 168;  // 3 x 84 column pairs <= 256 threads
+inline int ss_strips(int Wout) { return (Wout + SS_MAXSW - 1) / SS_MAXSW; }
+inline int ss_sw(int Wout) {
+  const int st = ss_strips(Wout);
+  return ((Wout + st - 1) / st + 3) & ~3;  // strips start on 4 pixels: 12-byte (dword) multiples
+}
+inline int ss_bands(int n, int Mo, int strips) {  // Mo output row pairs; bands >= 32 pairs
+  const int want = (4096 + n * strips - 1) / (n * strips);
+  return std::max(1, std::min(want, Mo / 32));
+}
+constexpr int SS_PF = 4;                   // coefficient rows in flight ahead of the one staged
+constexpr int SS_NCOL = SS_MAXSW / 2 + 4;  // staged coefficient columns (max)
+constexpr int SS_ITEMS = 5;                // staging items per thread: 12 x SS_NCOL <= 5 x 256
+constexpr int SS_OBW = SS_MAXSW * 3 / 4;   // dwords of one U8 BGR strip row
+
+template <bool FINAL>
+__global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
+    wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, int level, int L,
+    size_t in_off, int Nh, int Nw, size_t out_off, int Hout, int Wout, size_t out_chan_stride,
+    int fmask, int SWo, int strips, int bands, uint8_t* __restrict__ out_u8, int64_t row_stride,
+    float* __restrict__ out_f32) {
+  __shared__ wreal SB[2][12][SS_NCOL];  // staged row: [c * 4 + band][column]
+  __shared__ wreal YB[FINAL ? 3 : 1][2][FINAL ? SS_MAXSW : 1];
+  __shared__ uint32_t OB[FINAL ? 2 : 1][FINAL ? SS_OBW : 1];
+  __shared__ wreal TH[12];  // soft thresholds by [c * 4 + band] (0 for aa)
+  const int img = blockIdx.z;
+  const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
+  const int x0 = strip * SWo, n0 = x0 / 2;
+  const int Mo = (Hout + 1) / 2;  // output row pairs
+  const int ma = (int)((int64_t)band * Mo / bands), mb = (int)((int64_t)(band + 1) * Mo / bands);
+  const int t = threadIdx.x;
+  wreal* base = ws + img * img_floats;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const size_t bsz = (size_t)Nh * Nw;
+  const int ncol = SWo / 2 + 4;
+  const int nitems = 12 * ncol;
+  // staging items k = t + 256 u -> (band cb, column); items past the end load a valid address
+  const wreal* ip[SS_ITEMS];
+  int icb[SS_ITEMS], icl[SS_ITEMS];
+  uint32_t fb = 0;  // bit u: item u's band is stored fp32
+#pragma unroll
+  for (int u = 0; u < SS_ITEMS; ++u) {
+    const int k = t + SS_MAXT * u;
+    const bool ok = k < nitems;
+    const int cb = ok ? k / ncol : 0;
+    icb[u] = ok ? cb : -1;
+    icl[u] = ok ? k - cb * ncol : 0;
+    ip[u] = base + in_off + (size_t)cb * bsz;
+    fb |= (uint32_t)wl_fband(fmask, cb & 3) << u;
+  }
+  if (t < 12) TH[t] = (t & 3) ? st[WlStats::thr(t >> 2, level - 1, (t & 3) - 1, L)] : 0.0;
+  __syncthreads();
+  // coefficients past the band's end feed only outputs past the level's valid length (never
+  // stored): clamped reads keep them finite
+  auto load = [&](int r, double (&v)[SS_ITEMS], uint32_t& odd) {
+    const size_t rb = (size_t)min(r, Nh - 1) * Nw;
+    odd = 0;
+#pragma unroll
+    for (int u = 0; u < SS_ITEMS; ++u) {
+      const size_t e = rb + min(n0 + icl[u], Nw - 1);
+      const uint32_t f = (fb >> u) & 1u;
+      v[u] = ip[u][e >> f];
+      odd |= ((uint32_t)e & f) << u;
+    }
+  };
+  // ---- axis roles: thread (c, np)
+  const int half = SWo / 2;
+  const bool ct = t < 3 * half;
+  const int c = ct ? t / half : 0, np = ct ? t - c * half : 0;
+  wreal ring[5][4];  // coefficient rows r-4 .. r of (sa(2np), sa(2np+1), sd(2np), sd(2np+1))
+#pragma unroll
+  for (int s5 = 0; s5 < 5; ++s5)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ring[s5][q] = 0.0;
+  wreal mn = 0, sc = 0;
+  bool bad = false;
+  if (FINAL) {
+    wreal mx;
+    wl_minmax64(st, c, mn, mx);
+    sc = mx - mn;
+    bad = st[WlStats::FLAG] != 0.0;
+  }
+  // FINAL: the strip's U8 row bytes, stored whole dwords when the rows are dword aligned
+  const int nb = 3 * min(SWo, Wout - x0);
+  const bool al = ((uintptr_t)out_u8 & 3) == 0 && (row_stride & 3) == 0;
+  auto flush = [&](int m) {
+    if (!out_u8) return;
+    const int nw = SWo * 3 / 4;
+    for (int k = t; k < 2 * nw; k += SS_MAXT) {
+      const int rr2 = k >= nw, d = k - rr2 * nw;
+      const int y = 2 * m + rr2;
+      if (y >= Hout || 4 * d >= nb) continue;
+      uint8_t* orow = out_u8 + ((int64_t)img * Hout + y) * row_stride + (int64_t)x0 * 3;
+      const uint32_t wv = OB[rr2][d];
+      if (al && 4 * d + 4 <= nb) {
+        reinterpret_cast<uint32_t*>(orow)[d] = wv;
+      } else {
+        for (int bi = 4 * d; bi < min(4 * d + 4, nb); ++bi) orow[bi] = (uint8_t)(wv >> (8 * (bi & 3)));
+      }
+    }
+  };
+  const int r0 = ma, R = (mb - ma) + 4;  // coefficient rows r0 .. r0 + R - 1
+  double pf[SS_PF][SS_ITEMS];
+  uint32_t podd[SS_PF];
+#pragma unroll
+  for (int f = 0; f < SS_PF; ++f)
+    if (f < R) load(r0 + f, pf[f], podd[f]);
+  for (int s0 = 0; s0 < R; s0 += SS_PF) {
+#pragma unroll
+    for (int rs = 0; rs < SS_PF; ++rs) {
+      const int sidx = s0 + rs;
+      if (sidx >= R) break;
+      const int r = r0 + sidx, buf = sidx & 1;
+      // stage row r (details soft-thresholded; thr = 0 keeps aa), refill its prefetch slot
+#pragma unroll
+      for (int u = 0; u < SS_ITEMS; ++u) {
+        wreal x = pf[rs][u];
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+        const float h = __uint_as_float((uint32_t)(((podd[rs] >> u) & 1u) ? bits >> 32 : bits));
+        x = ((fb >> u) & 1u) ? (wreal)h : x;
+        if (icb[u] >= 0) SB[buf][icb[u]][icl[u]] = soft(x, TH[icb[u]]);
+      }
+      if (sidx + SS_PF < R) load(r + SS_PF, pf[rs], podd[rs]);
+      __syncthreads();
+      if (FINAL && sidx >= 5) flush(r - 5);  // the previous step's U8 rows
+      if (ct) {
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb) {  // sa: aa (lowpass) / ad (highpass); sd: da / dd
+          const wreal* lo = SB[buf][c * 4 + 2 * pb];
+          const wreal* hi = SB[buf][c * 4 + 2 * pb + 1];
+          wreal cl[5], cd[5];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {  // c[j] = column np + 4 - j
+            cl[j] = lo[np + 4 - j];
+            cd[j] = hi[np + 4 - j];
+          }
+          synth_full<IDN_WAVELET_BIOR15>(cl, cd, ring[4][2 * pb], ring[4][2 * pb + 1]);
+        }
+      }
+      if (sidx >= 4) {
+        const int m = r - 4;  // output row pair 2m, 2m+1
+        wreal v[2][2];        // [row][column]
+#pragma unroll
+        for (int col = 0; col < 2; ++col) {
+          wreal cl[5], cd[5];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {  // c[j] = coefficient row m + 4 - j
+            cl[j] = ring[4 - j][col];
+            cd[j] = ring[4 - j][2 + col];
+          }
+          synth_full<IDN_WAVELET_BIOR15>(cl, cd, v[0][col], v[1][col]);
+        }
+        if (!FINAL) {
+          wreal* out = base + out_off + (size_t)c * out_chan_stride;
+          const int x = x0 + 2 * np;
+#pragma unroll
+          for (int rr2 = 0; rr2 < 2; ++rr2) {
+            const int y = 2 * m + rr2;
+            if (!ct || y >= Hout || x >= Wout) continue;
+            wreal* o = out + (size_t)y * Wout + x;
+            if (x + 1 < Wout && ((uintptr_t)o & 15) == 0) {
+              *reinterpret_cast<double2*>(o) = make_double2(v[rr2][0], v[rr2][1]);
+            } else {
+              o[0] = v[rr2][0];
+              if (x + 1 < Wout) o[1] = v[rr2][1];
+            }
+          }
+        } else {
+          // inner clip (0.14.2) and de-normalisation
+          if (ct) {
+#pragma unroll
+            for (int rr2 = 0; rr2 < 2; ++rr2)
+#pragma unroll
+              for (int col = 0; col < 2; ++col)
+                YB[c][rr2][2 * np + col] = fmin(fmax(v[rr2][col], 0.0), 1.0) * sc + mn;
+          }
+          __syncthreads();
+          // pixel pairs: thread q -> row q / half, pixels 2 (q % half), +1
+          if (t < 2 * half) {
+            const int rr2 = t >= half, pp = t - rr2 * half;
+            const int y = 2 * m + rr2;
+            uint16_t* ob = reinterpret_cast<uint16_t*>(&OB[rr2][0]) + 3 * pp;
+            uint32_t b6[2] = {0u, 0u};  // the pair's 6 bytes
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+              const int xx = 2 * pp + p;
+              // ycbcr2rgb: (arr - [16,128,128]) @ inv(ycbcr_from_rgb).T (fma-chain dot), clip
+              const double Y = YB[0][rr2][xx] - 16.0, Cb = YB[1][rr2][xx] - 128.0,
+                           Cr = YB[2][rr2][xx] - 128.0;
+              double o3[3];
+              o3[0] = dot3(Y, Cb, Cr, 0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937);
+              o3[1] = dot3(Y, Cb, Cr, 0.004566210045662101, -0.0015363236860449021, -0.003188110949655707);
+              o3[2] = dot3(Y, Cb, Cr, 0.004566210045662101, 0.007910716233554741, 1.1977497040511743e-08);
+#pragma unroll
+              for (int k3 = 0; k3 < 3; ++k3) {
+                double vv = fmin(fmax(o3[k3], 0.0), 1.0);
+                if (bad) vv = 0.0;
+                const int bi = 3 * p + k3;
+                b6[bi >> 2] |= (uint32_t)(uint8_t)(int)(255.0 * vv) << (8 * (bi & 3));
+                if (out_f32 && y < Hout && x0 + xx < Wout)
+                  out_f32[(((int64_t)img * Hout + y) * Wout + x0 + xx) * 3 + k3] = (float)vv;
+              }
+            }
+            ob[0] = (uint16_t)b6[0];
+            ob[1] = (uint16_t)(b6[0] >> 16);
+            ob[2] = (uint16_t)b6[1];
+          }
+        }
+      }
+#pragma unroll
+      for (int s5 = 0; s5 < 4; ++s5)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ring[s5][q] = ring[s5 + 1][q];
+    }
+  }
+  if (FINAL && R >= 5) {
+    __syncthreads();
+    flush(r0 + R - 5);
   }
 }
 
@@ -2374,7 +2898,27 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
-    if (l > 1)
+    if (WV == IDN_WAVELET_BIOR15) {
+      const int strips = Lt.tiles_x[l], bands = Lt.tiles[l] / strips, sw = ws_sw(Lt.W[l]);
+      const dim3 blk((unsigned)((2 * sw + 8 + 63) / 64 * 64));
+      const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
+      if (l > 1 && (fm_an(l) & WL_FB_AIN))
+        hipLaunchKernelGGL((wl_dwt_stream<3>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
+                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
+                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], 0, fm_an(l));
+      else if (l > 1)
+        hipLaunchKernelGGL((wl_dwt_stream<2>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
+                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
+                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], 0, fm_an(l));
+      else if (in64)
+        hipLaunchKernelGGL((wl_dwt_stream<1>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
+                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
+                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], emit, fm_an(l));
+      else
+        hipLaunchKernelGGL((wl_dwt_stream<0>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
+                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
+                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], emit, fm_an(l));
+    } else if (l > 1)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
@@ -2397,6 +2941,24 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   else
     hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  if (WV == IDN_WAVELET_BIOR15) {  // streaming synthesis (wl_synth_stream)
+    for (int l = Lt.L; l >= 1; --l) {
+      const int Hout = Lt.H[l - 1], Wout = Lt.W[l - 1];
+      const int strips = ss_strips(Wout), sw = ss_sw(Wout);
+      const int bands = ss_bands(n, (Hout + 1) / 2, strips);
+      const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n), blk(SS_MAXT);
+      if (l >= 2)
+        hipLaunchKernelGGL((wl_synth_stream<false>), grid, blk, 0, st, wsf, Lt.img_floats, stats, l,
+                           Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Hout, Wout,
+                           (size_t)4 * Hout * Wout, fm_syn(l), sw, strips, bands, (uint8_t*)nullptr,
+                           row_stride, (float*)nullptr);
+      else
+        hipLaunchKernelGGL((wl_synth_stream<true>), grid, blk, 0, st, wsf, Lt.img_floats, stats, 1,
+                           Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], (size_t)0, Lt.h, Lt.w, (size_t)0,
+                           fm_syn(1), sw, strips, bands, out_u8, row_stride, out_f32);
+    }
+    return IDN_OK;
+  }
   for (int l = Lt.L; l >= 2; --l) {
     // the level-(l-1) 'aa' slot (consumed by the analysis already) receives the reconstruction
     const int tx = (Lt.W[l - 1] + ST_O - 1) / ST_O, ty = (Lt.H[l - 1] + ST_O - 1) / ST_O;
