@@ -15,6 +15,7 @@ duration) and the CPU baseline (oracle C restatement of the same filter, OpenMP,
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -68,7 +69,8 @@ _U8NOISE = "f32 apply, 16-bit-uniform Box-Muller (32-bit tail refinement)"
 DTYPE = {"noise_gaussian": _U8NOISE, "noise_sap": "u32 (16-bit uniform thresholds)",
          "noise_poisson": "u32 (CDF thresholds)", "wavelet_haar3": "f64", "bilateral": "f32",
          "cfg2": _U8NOISE + " + u16 SWAR filter", "cfg2p": _U8NOISE + " + u16 SWAR filter",
-         "wavelet_bior15": "f64", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
+         "wavelet_bior15": "f64 normalisation / finest-dd / sums of squares, f32 lowpass and "
+                           "synthesis", "gauss5_blob": "u8->f32", "quant7": "i32/f64",
          "cfg3": "u32 noise + f16-lane median", "cfg4": _U8NOISE + " + f32 bilateral",
          "cfg5": "f32/u32 noise + f64 wavelet", "jpeg_decode": "i32 (integer IDCT)"}
 PARITY = {"noise_gaussian": "skimage random_noise('gaussian') U8 law (chi-square tested at the "
@@ -320,8 +322,11 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         "cores": threads,
         "kind": "port",
         "sample": f"{n_img} x {H}x{W}x3 u8 images, {op}: {src}; {threads} threads, "
-                  f"{el:.1f} s (restatement -- cv2/skimage are not installed, so the "
-                  f"reference's own CPU path cannot run here)",
+                  f"{el:.1f} s; the same {nb}-image batch ({nb * H * W * C / 1e6:.1f} MB) "
+                  f"re-filtered each call, so it is cache-resident (a conservative, i.e. "
+                  f"favourable-to-CPU, baseline; the GPU line streams its batch from HBM) "
+                  f"(restatement -- cv2/skimage are not installed, so the reference's own CPU "
+                  f"path cannot run here)",
     }
 
 
@@ -455,9 +460,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
+    tuning = contextlib.ExitStack()
     if args.lib == "tuning":  # A/B runs of the kernels' tuning knobs (never the driver's line)
         from idn import _lib
-        _lib.variant("tuning").__enter__()
+        # held open for the whole run (a bare variant(...).__enter__() on a temporary reverts
+        # as soon as the context manager is collected)
+        tuning.enter_context(_lib.variant("tuning"))
     label, call, bpp, kname = OPS[args.op]
     x = synth_batch(torch, my_batch, dev, seed=3 + rank)
     y = torch.empty_like(x)

@@ -170,7 +170,9 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre_kernel(const uin
   }
 
   const int col = threadIdx.x & 63;
-  const int ly0 = (threadIdx.x >> 6) * RPT;  // first of the thread's RPT output rows
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ly0 = wave * RPT;  // first of the thread's RPT output rows
+  const uint32_t img_bytes = (uint32_t)((int64_t)h * row_stride);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int tx = t % tiles_x;
     const int ty = (t / tiles_x) % tiles_y;
@@ -178,10 +180,31 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre_kernel(const uin
     const uint8_t* s = src + (int64_t)img * h * row_stride;
     uint8_t* d = dst + (int64_t)img * h * row_stride;
     const int x0 = tx * BL_TW, y0 = ty * TH;
+    // staging: wave wv stages tile rows wv, wv + NW, ..., lane the columns lane and 64 + lane; one
+    // unaligned dword load per pixel, bytes 3x-1 .. 3x+2 (0 .. 3 at x = 0; the launcher requires
+    // w >= 2), so no load reaches past the image.  Rows / columns outside the image read 0
+    // (BORDER_CONSTANT) through the buffer's range check (offsets >= 2^30; the launcher requires
+    // images < 2^30 bytes).
+    const rsrc_t rs = make_rsrc(s, img_bytes);
+    uint32_t xo[2], sh[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int x = x0 + 64 * k + col - R;
+      const bool in = x >= 0 && x < w;
+      xo[k] = !in ? 0x40000000u : (x > 0 ? 3u * (uint32_t)x - 1u : 0u);
+      sh[k] = x > 0 ? 8u : 0u;
+    }
     __syncthreads();  // the previous tile is consumed (and the tables are built)
-    for (int i = threadIdx.x; i < LH * LW; i += NT) {
-      const int ly = i / LW, lx = i % LW;
-      tile[i] = load_px<3>(s, row_stride, h, w, y0 + ly - R, x0 + lx - R);
+    for (int ly = wave; ly < LH; ly += BLP_NW) {
+      const int y = y0 + ly - R;  // wave-uniform
+      const uint32_t so = (y >= 0 && y < h) ? (uint32_t)y * (uint32_t)row_stride : 0x40000000u;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (64 * k + col < LW) {
+          const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, xo[k], so, 0);
+          tile[ly * LW + 64 * k + col] = (v >> sh[k]) & 0xFFFFFFu;
+        }
+      }
     }
     __syncthreads();
 
@@ -309,7 +332,7 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
     case 7: launch_bl<CC, 7>(src, dst, n, h, w, row_stride, taps, st); break; \
     default: launch_bl<CC, 8>(src, dst, n, h, w, row_stride, taps, st); break; \
   }
-  if (c == 3 && radius <= 5) {
+  if (c == 3 && radius <= 5 && w >= 2 && (int64_t)h * row_stride < 0x3FFFFFFF) {
     switch (radius) {
       case 1: launch_bl_pre<1>(src, dst, n, h, w, row_stride, taps, st); break;
       case 2: launch_bl_pre<2>(src, dst, n, h, w, row_stride, taps, st); break;

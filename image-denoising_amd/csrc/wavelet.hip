@@ -41,6 +41,13 @@ constexpr wreal S2 = 0.7071067811865476;
 constexpr wreal B1 = 0.016572815184059706;
 constexpr wreal B2 = 0.12153397801643785;
 
+// fused multiply-add in the arithmetic type T (the build has -ffp-contract=off: no implicit fma)
+template <typename T>
+__device__ __forceinline__ T fma_t(T a, T b, T c) {
+  if constexpr (sizeof(T) == 4) return __fmaf_rn(a, b, c);
+  else return __fma_rn(a, b, c);
+}
+
 template <int WV> struct Wav;
 template <> struct Wav<IDN_WAVELET_DB1> {
   static constexpr int F = 2;
@@ -634,7 +641,12 @@ template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (
 // prefetch depth (steps; divides 5): the u8 and fp32 rings are small, the fp64 ones are not
 template <int SRC> constexpr int ws_pf() { return SRC == 0 || SRC == 3 ? 5 : 1; }
 
-template <int SRC>
+// TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the
+// product runs the lowpass outputs (aa, ad, da: continuous inputs of the thresholds' fp64 sums of
+// squares and of the synthesis) in fp32, and at level 1 keeps the normalisation, the column
+// highpass and dd in fp64 with pywt's op order (the finest dd's exact zeros select the sigma
+// median's population); deeper levels (no median) run both paths in fp32.
+template <int SRC, typename TL = wreal, typename TH = wreal>
 __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
     int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands,
@@ -642,7 +654,9 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
     double* __restrict__ part, size_t part_per_img, size_t part_tile0, int emit_codes,
     int fmask) {
   constexpr int PF = ws_pf<SRC>();
-  __shared__ wreal VL[2][3][WS_MAXT], VH[2][3][WS_MAXT];
+  __shared__ TL VL[2][3][WS_MAXT];
+  __shared__ TH VH[2][3][WS_MAXT];
+  __shared__ double RED[3][WS_MAXT];
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
   const int j0 = strip * SW;
@@ -674,6 +688,7 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       if constexpr (SRC == 0) {
+        // three byte loads (one unaligned dword per pixel measured 8 % slower for the kernel)
         const uint32_t so = (uint32_t)((int64_t)rows[h2] * row_stride), vo = (uint32_t)qc * 3u;
         const uint32_t b0 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo, so, 0);
         const uint32_t b1 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo + 1u, so, 0);
@@ -718,13 +733,13 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
       }
     }
   };
-  wreal acc[3][5];           // running column lowpass of outputs k .. k+4 (slot = output % 5)
-  wreal hd0[3], hd1[3];      // column highpass of pairs k-1, k-2 (hi[i] is pair i-2's)
+  TL acc[3][5];              // running column lowpass of outputs k .. k+4 (slot = output % 5)
+  TH hd0[3], hd1[3];         // column highpass of pairs k-1, k-2 (hi[i] is pair i-2's)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    hd0[c] = hd1[c] = 0.0;
+    hd0[c] = hd1[c] = (TH)0;
 #pragma unroll
-    for (int r = 0; r < 5; ++r) acc[c][r] = 0.0;
+    for (int r = 0; r < 5; ++r) acc[c][r] = (TL)0;
   }
   // ---- row role
   const int half = SW / 2;
@@ -755,15 +770,17 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
         if (m + PF < M) load(k + PF, rq[slot]);  // refill the slot PF steps ahead
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          const wreal x0 = norm(cur, 0, c), x1 = norm(cur, 1, c);
-          const wreal sk = x0 + x1, ek = x1 - x0;
-          const wreal hk = __dadd_rn(__dmul_rn(-S2, x1), __dmul_rn(S2, x0));  // pywt: mul, add
+          const auto x0 = norm(cur, 0, c), x1 = norm(cur, 1, c);
+          const TL l0 = (TL)x0, l1 = (TL)x1;
+          const TL sk = l0 + l1, ek = l1 - l0;
+          const TH h0 = (TH)x0, h1 = (TH)x1;
+          const TH hk = (TH)(-S2) * h1 + (TH)S2 * h0;  // pywt: mul, add (no contraction)
           // pair k's contributions; slot (k + j) % 5 == (r + j) % 5 for the unrolled r
-          acc[c][(r + 4) % 5] = -B1 * ek;
-          acc[c][(r + 3) % 5] = __fma_rn(B2, ek, acc[c][(r + 3) % 5]);
-          acc[c][(r + 2) % 5] = __fma_rn(S2, sk, acc[c][(r + 2) % 5]);
-          acc[c][(r + 1) % 5] = __fma_rn(-B2, ek, acc[c][(r + 1) % 5]);
-          const wreal lo = __fma_rn(B1, ek, acc[c][r]);  // output k complete
+          acc[c][(r + 4) % 5] = (TL)(-B1) * ek;
+          acc[c][(r + 3) % 5] = fma_t<TL>((TL)B2, ek, acc[c][(r + 3) % 5]);
+          acc[c][(r + 2) % 5] = fma_t<TL>((TL)S2, sk, acc[c][(r + 2) % 5]);
+          acc[c][(r + 1) % 5] = fma_t<TL>((TL)(-B2), ek, acc[c][(r + 1) % 5]);
+          const TL lo = fma_t<TL>((TL)B1, ek, acc[c][r]);  // output k complete
           if (m >= 4) {
             VL[buf][c][t] = lo;
             VH[buf][c][t] = hd1[c];
@@ -776,36 +793,38 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
       __syncthreads();
       const int i = k;  // output row
       if (rowt) {
-        const wreal* vl = &VL[buf][rc][2 * jj];
-        const wreal* vh = &VH[buf][rc][2 * jj];
-        wreal o[2][4];  // [output][aa, ad, da, dd]
+        const TL* vl = &VL[buf][rc][2 * jj];
+        const TH* vh = &VH[buf][rc][2 * jj];
+        TL o[2][3];  // [output][aa, ad, da]
+        TH odd[2];   // [output] dd
 #pragma unroll
         for (int pass = 0; pass < 2; ++pass) {  // column low -> aa / ad, column high -> da / dd
-          const wreal* v = pass ? vh : vl;
-          wreal S[6], E[6];
+          TL S[6], E[6];
 #pragma unroll
           for (int nn = 0; nn < 6; ++nn) {
-            const wreal a0 = v[2 * nn], a1 = v[2 * nn + 1];
+            const TL a0 = pass ? (TL)vh[2 * nn] : vl[2 * nn];
+            const TL a1 = pass ? (TL)vh[2 * nn + 1] : vl[2 * nn + 1];
             S[nn] = a0 + a1;
             E[nn] = a1 - a0;
           }
 #pragma unroll
           for (int d = 0; d < 2; ++d) {
-            o[d][2 * pass] =
-                __fma_rn(S2, S[2 + d], __fma_rn(B1, E[4 + d] - E[d], B2 * (E[1 + d] - E[3 + d])));
-            if (pass == 0) o[d][1] = -S2 * E[2 + d];
-            else o[d][3] = __dadd_rn(__dmul_rn(-S2, v[2 * d + 5]), __dmul_rn(S2, v[2 * d + 4]));
+            o[d][2 * pass] = fma_t<TL>((TL)S2, S[2 + d],
+                                       fma_t<TL>((TL)B1, E[4 + d] - E[d], (TL)B2 * (E[1 + d] - E[3 + d])));
+            if (pass == 0) o[d][1] = (TL)(-S2) * E[2 + d];
+            else odd[d] = (TH)(-S2) * vh[2 * d + 5] + (TH)S2 * vh[2 * d + 4];
           }
         }
         const size_t e0 = (size_t)i * Wo + oj;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
           if (!(d ? ok1 : ok0)) continue;
-          sq[0] += o[d][1] * o[d][1];
-          sq[1] += o[d][2] * o[d][2];
-          sq[2] += o[d][3] * o[d][3];
+          const double v1 = (double)o[d][1], v2 = (double)o[d][2], v3 = (double)odd[d];
+          sq[0] += v1 * v1;
+          sq[1] += v2 * v2;
+          sq[2] += v3 * v3;
           if (emit_codes) {
-            const unsigned long long key = absbits(o[d][3]);
+            const unsigned long long key = absbits((double)odd[d]);
             reinterpret_cast<uint16_t*>(base + (size_t)rc * Hin * Win)[e0 + d] =
                 (uint16_t)(key ? wl_fbin(key) + 1 : 0);
           }
@@ -813,21 +832,23 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
         wreal* ob = base + out_off + (size_t)rc * 4 * bsz;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
+          const double w0 = b < 3 ? (double)o[0][b] : (double)odd[0];
+          const double w1 = b < 3 ? (double)o[1][b] : (double)odd[1];
           if (wl_fband(fmask, b)) {
             float* f = reinterpret_cast<float*>(ob + (size_t)b * bsz) + e0;
             if (ok1 && ((uintptr_t)f & 7) == 0) {  // both outputs, one aligned 8-byte store
-              *reinterpret_cast<float2*>(f) = make_float2((float)o[0][b], (float)o[1][b]);
+              *reinterpret_cast<float2*>(f) = make_float2((float)w0, (float)w1);
             } else {
-              if (ok0) f[0] = (float)o[0][b];
-              if (ok1) f[1] = (float)o[1][b];
+              if (ok0) f[0] = (float)w0;
+              if (ok1) f[1] = (float)w1;
             }
           } else {
             wreal* f = ob + (size_t)b * bsz + e0;
             if (ok1 && ((uintptr_t)f & 15) == 0) {
-              *reinterpret_cast<double2*>(f) = make_double2(o[0][b], o[1][b]);
+              *reinterpret_cast<double2*>(f) = make_double2(w0, w1);
             } else {
-              if (ok0) f[0] = o[0][b];
-              if (ok1) f[1] = o[1][b];
+              if (ok0) f[0] = w0;
+              if (ok1) f[1] = w1;
             }
           }
         }
@@ -836,7 +857,7 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
   }
   // per-workgroup sums of squares, channel by channel in thread order (deterministic)
   __syncthreads();
-  wreal* red = &VL[0][0][0];
+  double* red = &RED[0][0];
   if (rowt) {
 #pragma unroll
     for (int b = 0; b < 3; ++b) red[b * WS_MAXT + t] = sq[b];
@@ -1394,16 +1415,37 @@ constexpr int SS_NCOL = SS_MAXSW / 2 + 4;  // staged coefficient columns (max)
 constexpr int SS_ITEMS = 5;                // staging items per thread: 12 x SS_NCOL <= 5 x 256
 constexpr int SS_OBW = SS_MAXSW * 3 / 4;   // dwords of one U8 BGR strip row
 
-template <bool FINAL>
+// T: the synthesis arithmetic.  double: pywt's fp64 (bit-identical to the tiled form's pair
+// arithmetic); float: fp32 coefficients, taps, de-normalisation and YCbCr -> RGB (the synthesis
+// is continuous in its inputs and no exact zero depends on it: ~3e-7 from the fp64 form on the
+// [0, 1] output scale, against the 1e-5 tolerance), with levels >= 2 storing their
+// reconstruction as fp32 (the level above reads its 'aa' through WL_FB bit 0).
+template <typename T>
+__device__ __forceinline__ void synth_bior(const T (&cl)[5], const T (&cd)[5], T& ev, T& od) {
+  const T common = fma_t<T>((T)B1, cd[0] - cd[4], (T)B2 * (cd[3] - cd[1]));
+  ev = fma_t<T>((T)S2, cl[2] + cd[2], common);
+  od = fma_t<T>((T)S2, cl[2] - cd[2], common);
+}
+template <typename T>
+__device__ __forceinline__ T soft_t(T d, T t) {
+  const T m = __builtin_fabs(d) - t;
+  return m > (T)0 ? __builtin_copysign(m, d) : (T)0;
+}
+template <typename T>
+__device__ __forceinline__ T dot3_t(T x0, T x1, T x2, T m0, T m1, T m2) {
+  return fma_t<T>(x2, m2, fma_t<T>(x1, m1, x0 * m0));
+}
+
+template <bool FINAL, typename T = wreal>
 __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, int level, int L,
     size_t in_off, int Nh, int Nw, size_t out_off, int Hout, int Wout, size_t out_chan_stride,
     int fmask, int SWo, int strips, int bands, uint8_t* __restrict__ out_u8, int64_t row_stride,
     float* __restrict__ out_f32) {
-  __shared__ wreal SB[2][12][SS_NCOL];  // staged row: [c * 4 + band][column]
-  __shared__ wreal YB[FINAL ? 3 : 1][2][FINAL ? SS_MAXSW : 1];
+  __shared__ T SB[2][12][SS_NCOL];  // staged row: [c * 4 + band][column]
+  __shared__ T YB[FINAL ? 3 : 1][2][FINAL ? SS_MAXSW : 1];
   __shared__ uint32_t OB[FINAL ? 2 : 1][FINAL ? SS_OBW : 1];
-  __shared__ wreal TH[12];  // soft thresholds by [c * 4 + band] (0 for aa)
+  __shared__ T TH[12];  // soft thresholds by [c * 4 + band] (0 for aa)
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
   const int x0 = strip * SWo, n0 = x0 / 2;
@@ -1429,7 +1471,7 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
     ip[u] = base + in_off + (size_t)cb * bsz;
     fb |= (uint32_t)wl_fband(fmask, cb & 3) << u;
   }
-  if (t < 12) TH[t] = (t & 3) ? st[WlStats::thr(t >> 2, level - 1, (t & 3) - 1, L)] : 0.0;
+  if (t < 12) TH[t] = (T)((t & 3) ? st[WlStats::thr(t >> 2, level - 1, (t & 3) - 1, L)] : 0.0);
   __syncthreads();
   // coefficients past the band's end feed only outputs past the level's valid length (never
   // stored): clamped reads keep them finite
@@ -1448,17 +1490,18 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
   const int half = SWo / 2;
   const bool ct = t < 3 * half;
   const int c = ct ? t / half : 0, np = ct ? t - c * half : 0;
-  wreal ring[5][4];  // coefficient rows r-4 .. r of (sa(2np), sa(2np+1), sd(2np), sd(2np+1))
+  T ring[5][4];  // coefficient rows r-4 .. r of (sa(2np), sa(2np+1), sd(2np), sd(2np+1))
 #pragma unroll
   for (int s5 = 0; s5 < 5; ++s5)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ring[s5][q] = 0.0;
-  wreal mn = 0, sc = 0;
+    for (int q = 0; q < 4; ++q) ring[s5][q] = (T)0;
+  T mn = 0, sc = 0;
   bool bad = false;
   if (FINAL) {
-    wreal mx;
-    wl_minmax64(st, c, mn, mx);
-    sc = mx - mn;
+    wreal mn64, mx64;
+    wl_minmax64(st, c, mn64, mx64);
+    sc = (T)(mx64 - mn64);
+    mn = (T)mn64;
     bad = st[WlStats::FLAG] != 0.0;
   }
   // FINAL: the strip's U8 row bytes, stored whole dwords when the rows are dword aligned
@@ -1495,11 +1538,11 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
       // stage row r (details soft-thresholded; thr = 0 keeps aa), refill its prefetch slot
 #pragma unroll
       for (int u = 0; u < SS_ITEMS; ++u) {
-        wreal x = pf[rs][u];
+        const wreal x = pf[rs][u];
         const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
         const float h = __uint_as_float((uint32_t)(((podd[rs] >> u) & 1u) ? bits >> 32 : bits));
-        x = ((fb >> u) & 1u) ? (wreal)h : x;
-        if (icb[u] >= 0) SB[buf][icb[u]][icl[u]] = soft(x, TH[icb[u]]);
+        const T xt = ((fb >> u) & 1u) ? (T)h : (T)x;
+        if (icb[u] >= 0) SB[buf][icb[u]][icl[u]] = soft_t<T>(xt, TH[icb[u]]);
       }
       if (sidx + SS_PF < R) load(r + SS_PF, pf[rs], podd[rs]);
       __syncthreads();
@@ -1507,40 +1550,41 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
       if (ct) {
 #pragma unroll
         for (int pb = 0; pb < 2; ++pb) {  // sa: aa (lowpass) / ad (highpass); sd: da / dd
-          const wreal* lo = SB[buf][c * 4 + 2 * pb];
-          const wreal* hi = SB[buf][c * 4 + 2 * pb + 1];
-          wreal cl[5], cd[5];
+          const T* lo = SB[buf][c * 4 + 2 * pb];
+          const T* hi = SB[buf][c * 4 + 2 * pb + 1];
+          T cl[5], cd[5];
 #pragma unroll
           for (int j = 0; j < 5; ++j) {  // c[j] = column np + 4 - j
             cl[j] = lo[np + 4 - j];
             cd[j] = hi[np + 4 - j];
           }
-          synth_full<IDN_WAVELET_BIOR15>(cl, cd, ring[4][2 * pb], ring[4][2 * pb + 1]);
+          synth_bior<T>(cl, cd, ring[4][2 * pb], ring[4][2 * pb + 1]);
         }
       }
       if (sidx >= 4) {
         const int m = r - 4;  // output row pair 2m, 2m+1
-        wreal v[2][2];        // [row][column]
+        T v[2][2];            // [row][column]
 #pragma unroll
         for (int col = 0; col < 2; ++col) {
-          wreal cl[5], cd[5];
+          T cl[5], cd[5];
 #pragma unroll
           for (int j = 0; j < 5; ++j) {  // c[j] = coefficient row m + 4 - j
             cl[j] = ring[4 - j][col];
             cd[j] = ring[4 - j][2 + col];
           }
-          synth_full<IDN_WAVELET_BIOR15>(cl, cd, v[0][col], v[1][col]);
+          synth_bior<T>(cl, cd, v[0][col], v[1][col]);
         }
         if (!FINAL) {
-          wreal* out = base + out_off + (size_t)c * out_chan_stride;
+          T* out = reinterpret_cast<T*>(base + out_off + (size_t)c * out_chan_stride);
           const int x = x0 + 2 * np;
 #pragma unroll
           for (int rr2 = 0; rr2 < 2; ++rr2) {
             const int y = 2 * m + rr2;
             if (!ct || y >= Hout || x >= Wout) continue;
-            wreal* o = out + (size_t)y * Wout + x;
-            if (x + 1 < Wout && ((uintptr_t)o & 15) == 0) {
-              *reinterpret_cast<double2*>(o) = make_double2(v[rr2][0], v[rr2][1]);
+            T* o = out + (size_t)y * Wout + x;
+            if (x + 1 < Wout && ((uintptr_t)o & (2 * sizeof(T) - 1)) == 0) {
+              if constexpr (sizeof(T) == 4) *reinterpret_cast<float2*>(o) = make_float2(v[rr2][0], v[rr2][1]);
+              else *reinterpret_cast<double2*>(o) = make_double2(v[rr2][0], v[rr2][1]);
             } else {
               o[0] = v[rr2][0];
               if (x + 1 < Wout) o[1] = v[rr2][1];
@@ -1553,7 +1597,8 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
             for (int rr2 = 0; rr2 < 2; ++rr2)
 #pragma unroll
               for (int col = 0; col < 2; ++col)
-                YB[c][rr2][2 * np + col] = fmin(fmax(v[rr2][col], 0.0), 1.0) * sc + mn;
+                YB[c][rr2][2 * np + col] =
+                    __builtin_fmin(__builtin_fmax(v[rr2][col], (T)0), (T)1) * sc + mn;
           }
           __syncthreads();
           // pixel pairs: thread q -> row q / half, pixels 2 (q % half), +1
@@ -1566,18 +1611,21 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
             for (int p = 0; p < 2; ++p) {
               const int xx = 2 * pp + p;
               // ycbcr2rgb: (arr - [16,128,128]) @ inv(ycbcr_from_rgb).T (fma-chain dot), clip
-              const double Y = YB[0][rr2][xx] - 16.0, Cb = YB[1][rr2][xx] - 128.0,
-                           Cr = YB[2][rr2][xx] - 128.0;
-              double o3[3];
-              o3[0] = dot3(Y, Cb, Cr, 0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937);
-              o3[1] = dot3(Y, Cb, Cr, 0.004566210045662101, -0.0015363236860449021, -0.003188110949655707);
-              o3[2] = dot3(Y, Cb, Cr, 0.004566210045662101, 0.007910716233554741, 1.1977497040511743e-08);
+              const T Y = YB[0][rr2][xx] - (T)16, Cb = YB[1][rr2][xx] - (T)128,
+                      Cr = YB[2][rr2][xx] - (T)128;
+              T o3[3];
+              o3[0] = dot3_t<T>(Y, Cb, Cr, (T)0.004566210045662101, (T)1.1808799897950177e-09,
+                                (T)0.006258928969943937);
+              o3[1] = dot3_t<T>(Y, Cb, Cr, (T)0.004566210045662101, (T)-0.0015363236860449021,
+                                (T)-0.003188110949655707);
+              o3[2] = dot3_t<T>(Y, Cb, Cr, (T)0.004566210045662101, (T)0.007910716233554741,
+                                (T)1.1977497040511743e-08);
 #pragma unroll
               for (int k3 = 0; k3 < 3; ++k3) {
-                double vv = fmin(fmax(o3[k3], 0.0), 1.0);
-                if (bad) vv = 0.0;
+                T vv = __builtin_fmin(__builtin_fmax(o3[k3], (T)0), (T)1);
+                if (bad) vv = (T)0;
                 const int bi = 3 * p + k3;
-                b6[bi >> 2] |= (uint32_t)(uint8_t)(int)(255.0 * vv) << (8 * (bi & 3));
+                b6[bi >> 2] |= (uint32_t)(uint8_t)(int)((T)255 * vv) << (8 * (bi & 3));
                 if (out_f32 && y < Hout && x0 + xx < Wout)
                   out_f32[(((int64_t)img * Hout + y) * Wout + x0 + xx) * 3 + k3] = (float)vv;
               }
@@ -2895,6 +2943,7 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   };
   auto fm_syn = [&](int l) { return !fdet ? 0 : (l == 1 ? 0b0110 : 0b1110); };
   const int coop = knob("IDN_WAVELET_COOP", 1) ? 1 : 0;
+  const int a32 = knob("IDN_WAVELET_A32", 3);
   for (int l = 1; l <= Lt.L; ++l) {
     const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
@@ -2902,22 +2951,26 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       const int strips = Lt.tiles_x[l], bands = Lt.tiles[l] / strips, sw = ws_sw(Lt.W[l]);
       const dim3 blk((unsigned)((2 * sw + 8 + 63) / 64 * 64));
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
-      if (l > 1 && (fm_an(l) & WL_FB_AIN))
-        hipLaunchKernelGGL((wl_dwt_stream<3>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
-                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
-                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], 0, fm_an(l));
-      else if (l > 1)
-        hipLaunchKernelGGL((wl_dwt_stream<2>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
-                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
-                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], 0, fm_an(l));
-      else if (in64)
-        hipLaunchKernelGGL((wl_dwt_stream<1>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
-                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
-                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], emit, fm_an(l));
-      else
-        hipLaunchKernelGGL((wl_dwt_stream<0>), grid, blk, 0, st, wsf, Lt.img_floats, stats, in_off,
-                           Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64,
-                           row_stride, part, Lt.part_per_img, Lt.part_tile0[l], emit, fm_an(l));
+      // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
+#define IDN_WS(SRC, TL, TH, EMIT)                                                                  \
+  hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH>), grid, blk, 0, st, wsf, Lt.img_floats, stats,    \
+                     in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64, \
+                     row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT, fm_an(l))
+      const bool f1 = (a32 & 1) != 0, fd = (a32 & 2) != 0;
+      if (l > 1 && (fm_an(l) & WL_FB_AIN)) {
+        if (fd) IDN_WS(3, float, float, 0);
+        else IDN_WS(3, wreal, wreal, 0);
+      } else if (l > 1) {
+        if (fd) IDN_WS(2, float, float, 0);
+        else IDN_WS(2, wreal, wreal, 0);
+      } else if (in64) {
+        if (f1) IDN_WS(1, float, wreal, emit);
+        else IDN_WS(1, wreal, wreal, emit);
+      } else {
+        if (f1) IDN_WS(0, float, wreal, emit);
+        else IDN_WS(0, wreal, wreal, emit);
+      }
+#undef IDN_WS
     } else if (l > 1)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
@@ -2941,21 +2994,55 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   else
     hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
-  if (WV == IDN_WAVELET_BIOR15) {  // streaming synthesis (wl_synth_stream)
+  // bior1.5 synthesis form per level (bit 0: level 1, bit 1: deeper levels): streaming
+  // (wl_synth_stream) or tiled (wl_synth / wl_synth_final)
+  const int sstream = WV == IDN_WAVELET_BIOR15 ? knob("IDN_WAVELET_SSTREAM", 3) : 0;
+  // streaming levels in fp32 arithmetic (wl_synth_stream<.., float>); a level >= 2 that is then
+  // stores its reconstruction as fp32, so the level below reads its 'aa' band as fp32 (bit 0)
+  const bool s32 = knob("IDN_WAVELET_S32", 1) != 0;
+  auto str = [&](int l) { return (sstream & (l == 1 ? 1 : 2)) != 0; };
+  auto fm_syn2 = [&](int l) { return fm_syn(l) | (l < Lt.L && str(l + 1) && s32 ? 0b0001 : 0); };
+  if (sstream) {
     for (int l = Lt.L; l >= 1; --l) {
+      if (!str(l)) {
+        if (l >= 2) {
+          const int tx = (Lt.W[l - 1] + ST_O - 1) / ST_O, ty = (Lt.H[l - 1] + ST_O - 1) / ST_O;
+          hipLaunchKernelGGL((wl_synth<WV>), dim3(tx * ty, n * 3), dim3(256), 0, st, wsf,
+                             Lt.img_floats, stats, l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l],
+                             Lt.off_band[l - 1], Lt.H[l - 1], Lt.W[l - 1],
+                             (size_t)4 * Lt.H[l - 1] * Lt.W[l - 1], tx, fm_syn2(l));
+        } else {
+          const int tx = (Lt.w + ST_O - 1) / ST_O, ty = (Lt.h + ST_O - 1) / ST_O;
+          hipLaunchKernelGGL((wl_synth_final<WV>), dim3(tx * ty, n), dim3(256), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h,
+                             Lt.w, tx, out_u8, row_stride, out_f32, fm_syn2(1));
+        }
+        continue;
+      }
       const int Hout = Lt.H[l - 1], Wout = Lt.W[l - 1];
       const int strips = ss_strips(Wout), sw = ss_sw(Wout);
       const int bands = ss_bands(n, (Hout + 1) / 2, strips);
       const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n), blk(SS_MAXT);
-      if (l >= 2)
-        hipLaunchKernelGGL((wl_synth_stream<false>), grid, blk, 0, st, wsf, Lt.img_floats, stats, l,
-                           Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Hout, Wout,
-                           (size_t)4 * Hout * Wout, fm_syn(l), sw, strips, bands, (uint8_t*)nullptr,
-                           row_stride, (float*)nullptr);
-      else
+      if (l >= 2) {
+        if (s32)
+          hipLaunchKernelGGL((wl_synth_stream<false, float>), grid, blk, 0, st, wsf, Lt.img_floats,
+                             stats, l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1],
+                             Hout, Wout, (size_t)4 * Hout * Wout, fm_syn2(l), sw, strips, bands,
+                             (uint8_t*)nullptr, row_stride, (float*)nullptr);
+        else
+          hipLaunchKernelGGL((wl_synth_stream<false>), grid, blk, 0, st, wsf, Lt.img_floats, stats,
+                             l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Hout,
+                             Wout, (size_t)4 * Hout * Wout, fm_syn2(l), sw, strips, bands,
+                             (uint8_t*)nullptr, row_stride, (float*)nullptr);
+      } else if (s32) {
+        hipLaunchKernelGGL((wl_synth_stream<true, float>), grid, blk, 0, st, wsf, Lt.img_floats,
+                           stats, 1, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], (size_t)0, Lt.h, Lt.w,
+                           (size_t)0, fm_syn2(1), sw, strips, bands, out_u8, row_stride, out_f32);
+      } else {
         hipLaunchKernelGGL((wl_synth_stream<true>), grid, blk, 0, st, wsf, Lt.img_floats, stats, 1,
                            Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], (size_t)0, Lt.h, Lt.w, (size_t)0,
-                           fm_syn(1), sw, strips, bands, out_u8, row_stride, out_f32);
+                           fm_syn2(1), sw, strips, bands, out_u8, row_stride, out_f32);
+      }
     }
     return IDN_OK;
   }

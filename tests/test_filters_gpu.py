@@ -190,7 +190,8 @@ def test_median_generic_forced(dev, monkeypatch):
 BILATERAL_CASES = [(9, 20.0, 100.0), (9, 75.0, 75.0), (5, 30.0, 10.0), (3, 10.0, 10.0)]
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 37, 53), (1, 600, 1000), (2, 5, 7)])
+@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 37, 53), (1, 600, 1000), (2, 5, 7), (1, 9, 1),
+                                   (2, 7, 2), (1, 70, 65)])
 @pytest.mark.parametrize("case", BILATERAL_CASES)
 def test_bilateral_within_1lsb(dev, shape, case):
     """<= 1 LSB vs OpenCV semantics (fp32 sum order / exp ulps); pre-round values within 1e-4 rel"""

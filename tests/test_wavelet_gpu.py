@@ -188,11 +188,14 @@ def test_wavelet_haar_fused_matches_general(dev, monkeypatch, shape, levels, f64
                                                   ((90, 70), "db1", 3)])
 def test_wavelet_fp32_details_vs_fp64(dev, monkeypatch, shape, wavelet, levels):
     """IDN_WAVELET_FDET: ad / da bands through HBM as fp32 (default) against the all-fp64 form
-    (IDN_WAVELET_FDET=0); both within TOL of the oracle, and within 1e-6 of each other"""
+    (IDN_WAVELET_FDET=0), both with the fp64 synthesis (IDN_WAVELET_S32=0) so that only the band
+    storage differs; both within TOL of the oracle, and within 1e-6 of each other"""
     import oracle
     img = make_img(*shape, 17)
-    u8a, fa = run(img, wavelet, levels)
     from idn import _lib
+    monkeypatch.setenv("IDN_WAVELET_S32", "0")
+    with _lib.variant("tuning"):
+        u8a, fa = run(img, wavelet, levels)
     monkeypatch.setenv("IDN_WAVELET_FDET", "0")
     with _lib.variant("tuning"):
         u8b, fb = run(img, wavelet, levels)
@@ -202,6 +205,98 @@ def test_wavelet_fp32_details_vs_fp64(dev, monkeypatch, shape, wavelet, levels):
     ref = oracle.wavelet.denoise_wavelet(img, wavelet, levels)
     assert np.abs(fb - ref).max() <= TOL
     check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
+
+
+def _run_env(monkeypatch, img, env):
+    from idn import _lib
+    with monkeypatch.context() as mp:
+        for k, v in env.items():
+            mp.setenv(k, v)
+        with _lib.variant("tuning"):
+            return run(img, "bior1.5", None)
+
+
+@pytest.mark.parametrize("shape", [(600, 1000), (37, 53), (9, 11), (130, 77)])
+@pytest.mark.parametrize("form", ["0", "1", "2"])
+def test_wavelet_bior15_synthesis_forms(dev, monkeypatch, shape, form):
+    """IDN_WAVELET_SSTREAM in fp64 (IDN_WAVELET_S32=0; bit 0 level 1, bit 1 deeper levels:
+    streaming wl_synth_stream vs tiled wl_synth / wl_synth_final): every mix within 1e-9 of the
+    all-streaming fp64 form (the same pair arithmetic, staged differently) and within TOL of the
+    oracle"""
+    import oracle
+    img = make_img(*shape, 29)
+    u8a, fa = _run_env(monkeypatch, img, {"IDN_WAVELET_S32": "0", "IDN_WAVELET_SSTREAM": "3"})
+    u8b, fb = _run_env(monkeypatch, img, {"IDN_WAVELET_S32": "0", "IDN_WAVELET_SSTREAM": form})
+    assert np.abs(fa - fb).max() <= 1e-9
+    d = u8a.astype(int) - u8b.astype(int)
+    assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-4
+    if shape[0] * shape[1] <= 24000:
+        ref = oracle.wavelet.denoise_wavelet(img, "bior1.5", None)
+        assert np.abs(fb - ref).max() <= TOL
+        check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
+
+
+@pytest.mark.parametrize("shape", [(600, 1000), (37, 53), (9, 11), (130, 77)])
+@pytest.mark.parametrize("env", [{"IDN_WAVELET_S32": "0"},
+                                 {"IDN_WAVELET_S32": "1", "IDN_WAVELET_SSTREAM": "2"},
+                                 {"IDN_WAVELET_S32": "1", "IDN_WAVELET_SSTREAM": "1"}],
+                         ids=["fp64", "f32-deeper", "f32-level1"])
+def test_wavelet_bior15_fp32_synthesis(dev, monkeypatch, shape, env):
+    """the product's fp32 streaming synthesis (IDN_WAVELET_S32 default on: taps, soft threshold,
+    de-normalisation and YCbCr -> RGB in fp32, levels >= 2 handing fp32 reconstructions down)
+    against the fp64 synthesis and against mixes with the tiled fp64 forms: within 2e-6 on the
+    [0, 1] scale, U8 one LSB only at integer boundaries; the product within TOL of the oracle"""
+    import oracle
+    img = make_img(*shape, 31)
+    u8a, fa = run(img, "bior1.5", None)
+    u8b, fb = _run_env(monkeypatch, img, env)
+    assert np.abs(fa - fb).max() <= 2e-6
+    check_u8(u8a, fb, u8b)
+    if shape[0] * shape[1] <= 24000:
+        ref = oracle.wavelet.denoise_wavelet(img, "bior1.5", None)
+        assert np.abs(fa - ref).max() <= TOL
+        check_u8(u8a, ref, oracle.sk.to_u8(255 * ref))
+
+
+def _bior_stats(monkeypatch, img, env):
+    """bior1.5 through the tuning build under env: (u8, f32, stats block of the image)"""
+    import torch
+    from idn import _lib, ops
+    x = torch.from_numpy(np.ascontiguousarray(img[None])).cuda()
+    with monkeypatch.context() as mp:
+        for k, v in env.items():
+            mp.setenv(k, v)
+        with _lib.variant("tuning"):
+            u8, f = ops.denoise_wavelet(x, "bior1.5", None, out="both")
+            off = _lib.load().idn_wavelet_stats_offset(1, img.shape[0], img.shape[1],
+                                                       ops.WAVELETS["bior1.5"], -1)
+    ws = ops._WS_CACHE[(str(x.device), torch.cuda.current_stream(x.device).cuda_stream)]
+    st = ws[off:off + 256 * 8].view(torch.float64).cpu().numpy().copy()
+    return u8[0].cpu().numpy(), f[0].cpu().numpy().astype(np.float64), st
+
+
+@pytest.mark.parametrize("shape", [(600, 1000), (130, 77), (37, 53), (9, 11)])
+@pytest.mark.parametrize("a32", ["1", "2", "3"])
+def test_wavelet_bior15_fp32_analysis(dev, monkeypatch, shape, a32):
+    """IDN_WAVELET_A32 (bit 0: level 1's lowpass path aa / ad / da in fp32, the normalisation,
+    column highpass and dd in fp64; bit 1: deeper levels in fp32) against the fp64 analysis:
+    the finest dd -- hence the sigma medians and the nonzero counts -- bit-identical, outputs
+    within 2e-6, small images within TOL of the oracle"""
+    import oracle
+    img = make_img(*shape, 37)
+    q = min(shape) // 9  # default levels (wl_layout): max(dwt_max_level - 3, 1)
+    lv = max((q.bit_length() - 1 if q >= 1 else 0) - 3, 1)
+    u8a, fa, sa = _bior_stats(monkeypatch, img, {"IDN_WAVELET_A32": "0"})
+    u8b, fb, sb = _bior_stats(monkeypatch, img, {"IDN_WAVELET_A32": a32})
+    med = slice(8 + 9 * lv, 8 + 9 * lv + 3)
+    np.testing.assert_array_equal(sa[med].view(np.uint64), sb[med].view(np.uint64))
+    np.testing.assert_array_equal(sa[248:251], sb[248:251])
+    assert np.abs(fa - fb).max() <= 2e-6
+    check_u8(u8b, fa, u8a)
+    if shape[0] * shape[1] <= 24000:
+        ref = oracle.wavelet.denoise_wavelet(img, "bior1.5", None)
+        assert np.abs(fb - ref).max() <= TOL
+        check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
 
 
 @pytest.mark.parametrize("shape", [(601, 999), (37, 53), (9, 11)])
