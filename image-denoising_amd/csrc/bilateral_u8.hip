@@ -256,6 +256,168 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre_kernel(const uin
   }
 }
 
+// ---- two adjacent columns x 4 rows per thread ---------------------------------------------------
+// A pixel is a tap of up to 8 of the thread's outputs, so it is read from LDS and converted to
+// float once per 8 outputs instead of once per 4 (~12.5 instead of 19 reads + 3 conversions per
+// output).  Lane l owns columns 2l, 2l+1 of a 128-wide tile; the staged rows keep even and odd
+// columns in separate halves (column x at (x & 1) * HW + x / 2), so for every tap the 64 lanes
+// read consecutive dwords (the plain layout would make every pixel read a 2-way bank conflict,
+// which is what sank the first two-column attempt).  The colour table is built straight into the
+// per-r^2 products (color_weight is never stored): 30 KB of tables per workgroup.
+constexpr int BL2_TW = 128;
+template <int R>
+__global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
+    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int h, int w, int64_t row_stride,
+    int tiles_x, int tiles_y, int ntiles, BilateralTaps taps) {
+  constexpr int RPT = 4;
+  constexpr int LWX = BL2_TW + 2 * R;  // staged columns
+  constexpr int HW = (LWX + 1) / 2;    // columns per parity half
+  constexpr int LW = 2 * HW;           // LDS row pitch (dwords)
+  constexpr int NT = 64 * BLP_NW;
+  constexpr int TH = BLP_NW * RPT;
+  constexpr int LH = TH + 2 * R;
+  constexpr Rsq<R> RS;
+  __shared__ uint32_t tile[LH * LW];
+  __shared__ float wt[RS.n * BL_LUT];
+
+  // wt[k][i] = space_weight(r^2 = q_k) * color_weight[i], OpenCV's float product
+  for (int i = threadIdx.x; i < BL_LUT; i += NT) {
+    const float cwv = (float)exp((double)(i * i) * taps.gcc);
+#pragma unroll
+    for (int k = 0; k < RS.n; ++k) wt[k * BL_LUT + i] = taps.swq[RS.q[k]] * cwv;
+  }
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ly0 = wave * RPT;
+  const uint32_t img_bytes = (uint32_t)((int64_t)h * row_stride);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tx = t % tiles_x;
+    const int ty = (t / tiles_x) % tiles_y;
+    const int img = t / (tiles_x * tiles_y);
+    const uint8_t* s = src + (int64_t)img * h * row_stride;
+    uint8_t* d = dst + (int64_t)img * h * row_stride;
+    const int x0 = tx * BL2_TW, y0 = ty * TH;
+    // staging as bilateral_u8_pre_kernel (one unaligned dword per pixel, zero outside the image),
+    // staged column sx = lane + 64 k at (sx & 1) * HW + sx / 2
+    const rsrc_t rs = make_rsrc(s, img_bytes);
+    constexpr int NK = (LWX + 63) / 64;
+    uint32_t xo[NK], sh[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int x = x0 + 64 * k + lane - R;
+      const bool in = x >= 0 && x < w;
+      xo[k] = !in ? 0x40000000u : (x > 0 ? 3u * (uint32_t)x - 1u : 0u);
+      sh[k] = x > 0 ? 8u : 0u;
+    }
+    __syncthreads();  // the previous tile is consumed (and the tables are built)
+    for (int ly = wave; ly < LH; ly += BLP_NW) {
+      const int y = y0 + ly - R;
+      const uint32_t so = (y >= 0 && y < h) ? (uint32_t)y * (uint32_t)row_stride : 0x40000000u;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const int sx = 64 * k + lane;
+        if (sx < LWX) {
+          const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, xo[k], so, 0);
+          tile[ly * LW + (sx & 1) * HW + (sx >> 1)] = (v >> sh[k]) & 0xFFFFFFu;
+        }
+      }
+    }
+    __syncthreads();
+
+    // staged column of output column 2 lane + cc, offset j: 2 lane + cc + R + j
+    auto at = [&](int row, int rel) -> uint32_t {  // rel = cc + R + j (compile time)
+      return tile[row * LW + (rel & 1) * HW + lane + (rel >> 1)];
+    };
+    uint32_t p0[RPT][2];
+#pragma unroll
+    for (int o = 0; o < RPT; ++o)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) p0[o][cc] = at(ly0 + o + R, cc + R);
+    f32x2 acc_bg[RPT][2], acc_rw[RPT][2];
+#pragma unroll
+    for (int o = 0; o < RPT; ++o)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) acc_bg[o][cc] = acc_rw[o][cc] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int dy = -R; dy < RPT + R; ++dy) {
+#pragma unroll
+      for (int rel = 0; rel <= 2 * R + 1; ++rel) {  // staged columns 2 lane .. 2 lane + 2R + 1
+        bool any = false;
+#pragma unroll
+        for (int o = 0; o < RPT; ++o)
+#pragma unroll
+          for (int cc = 0; cc < 2; ++cc) {
+            const int i = dy - o, j = rel - cc - R;
+            any |= (i >= -R && i <= R && j >= -R && j <= R && i * i + j * j <= R * R);
+          }
+        if (!any) continue;
+        const uint32_t p = at(ly0 + R + dy, rel);
+        const f32x2 bg = {(float)(p & 0xFFu), (float)((p >> 8) & 0xFFu)};
+        const f32x2 r1 = {(float)((p >> 16) & 0xFFu), 1.f};
+#pragma unroll
+        for (int o = 0; o < RPT; ++o)
+#pragma unroll
+          for (int cc = 0; cc < 2; ++cc) {
+            const int i = dy - o, j = rel - cc - R;
+            if (i < -R || i > R || j < -R || j > R || i * i + j * j > R * R) continue;
+            const uint32_t dist = __builtin_amdgcn_sad_u8(p, p0[o][cc], 0u);
+            const float wv = wt[RS.slot[i * i + j * j] * BL_LUT + dist];
+            const f32x2 w2 = {wv, wv};
+            acc_bg[o][cc] = __builtin_elementwise_fma(bg, w2, acc_bg[o][cc]);
+            acc_rw[o][cc] = __builtin_elementwise_fma(r1, w2, acc_rw[o][cc]);
+          }
+      }
+#pragma unroll
+      for (int o = 0; o < RPT; ++o)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) asm volatile("" : "+v"(acc_bg[o][cc]), "+v"(acc_rw[o][cc]));
+    }
+    auto cvt = [](float v) -> uint32_t {  // cvRound (half to even) + saturate
+      const float r = __builtin_rintf(v);
+      return (uint32_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+    };
+    const int x = x0 + 2 * lane;
+    if (x >= w) continue;
+#pragma unroll
+    for (int o = 0; o < RPT; ++o) {
+      const int y = y0 + ly0 + o;
+      if (y >= h) break;
+      uint32_t b[6];
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const float inv = 1.f / acc_rw[o][cc].y;
+        b[3 * cc + 0] = cvt(acc_bg[o][cc].x * inv);
+        b[3 * cc + 1] = cvt(acc_bg[o][cc].y * inv);
+        b[3 * cc + 2] = cvt(acc_rw[o][cc].x * inv);
+      }
+      uint8_t* op = d + (int64_t)y * row_stride + (int64_t)x * 3;
+      if (x + 1 < w && (((uintptr_t)op) & 1) == 0) {  // 6 bytes as three u16 stores
+        uint16_t* o16 = reinterpret_cast<uint16_t*>(op);
+        o16[0] = (uint16_t)(b[0] | b[1] << 8);
+        o16[1] = (uint16_t)(b[2] | b[3] << 8);
+        o16[2] = (uint16_t)(b[4] | b[5] << 8);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if (k < 3 || x + 1 < w) op[k] = (uint8_t)b[k];
+      }
+    }
+  }
+}
+
+template <int R>
+static void launch_bl_pre2(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
+                           const BilateralTaps& taps, hipStream_t st) {
+  const int tiles_x = (w + BL2_TW - 1) / BL2_TW;
+  const int tiles_y = (h + BLP_NW * 4 - 1) / (BLP_NW * 4);
+  const int64_t ntiles = (int64_t)n * tiles_x * tiles_y;
+  const int64_t res = (int64_t)cu_count() * knob("IDN_BL2_WG", 2);  // resident workgroups per CU
+  const int64_t grid = ntiles < res ? ntiles : res;
+  hipLaunchKernelGGL((bilateral_u8_pre2_kernel<R>), dim3((unsigned)grid), dim3(64 * BLP_NW), 0, st,
+                     src, dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
+}
+
 template <int R, int RPT>
 static void launch_bl_pre_rpt(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
                               const BilateralTaps& taps, hipStream_t st) {
@@ -278,7 +440,8 @@ static void launch_bl_pre_rpt(const uint8_t* src, uint8_t* dst, int n, int h, in
 template <int R>
 static void launch_bl_pre(const uint8_t* src, uint8_t* dst, int n, int h, int w, int64_t rs,
                           const BilateralTaps& taps, hipStream_t st) {
-  launch_bl_pre_rpt<R, 4>(src, dst, n, h, w, rs, taps, st);
+  if (knob("IDN_BL2", 1)) launch_bl_pre2<R>(src, dst, n, h, w, rs, taps, st);
+  else launch_bl_pre_rpt<R, 4>(src, dst, n, h, w, rs, taps, st);
 }
 
 template <int C, int R>

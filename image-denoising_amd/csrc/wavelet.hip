@@ -30,6 +30,9 @@
 // two equal samples is then exactly 0 (-S*x + S*x), which the "nonzero" median relies on.
 #include "idn_common.hpp"
 
+#include <cmath>
+#include <mutex>
+
 #include <math.h>
 
 #include <algorithm>
@@ -127,7 +130,42 @@ __device__ __forceinline__ int wl_fbin(unsigned long long key) {
 }
 
 inline int ws_strips(int Wo);
-inline int ws_bands(int n, int Ho, int strips);
+inline int ws_bands(int n, int Ho, int strips, int level);
+// Row bands per strip so that the grid fills whole rounds of resident workgroups: for each
+// candidate band count b the time is ~ rounds(b) x (rows per band + warm-up rows), rounds(b) =
+// ceil(units * b / resident).  (A grid of 2.5 rounds leaves the chip half idle for the last one.)
+inline int best_bands(int64_t units, int M, int warm, int64_t resident, int min_rows) {
+  const int bmax = std::max(1, std::min(64, M / std::max(min_rows, 1)));
+  int best = 1;
+  double bestc = 1e300;
+  for (int b = 1; b <= bmax; ++b) {
+    const double rounds = std::ceil((double)(units * b) / (double)std::max<int64_t>(resident, 1));
+    const double c = rounds * ((M + b - 1) / b + warm);
+    if (c < bestc * 0.999) {
+      bestc = c;
+      best = b;
+    }
+  }
+  return best;
+}
+// resident workgroups per CU of a kernel at a block size (cached; 1 if the query fails)
+inline int occ_wgs(const void* kernel, int block) {
+  static std::mutex mu;
+  static const void* keys[32];
+  static int blocks[32], vals[32], nk = 0;
+  std::lock_guard<std::mutex> g(mu);
+  for (int i = 0; i < nk; ++i)
+    if (keys[i] == kernel && blocks[i] == block) return vals[i];
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0) != hipSuccess || nb < 1)
+    nb = 1;
+  if (nk < 32) {
+    keys[nk] = kernel;
+    blocks[nk] = block;
+    vals[nk++] = nb;
+  }
+  return nb;
+}
 inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   WlLayout Lt;
   Lt.n = n;
@@ -154,7 +192,7 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
     if (wv == IDN_WAVELET_BIOR15) {  // wl_dwt_stream: strips x row bands
       Lt.tiles_x[l] = ws_strips(Lt.W[l]);
-      Lt.tiles[l] = Lt.tiles_x[l] * ws_bands(n, Lt.H[l], Lt.tiles_x[l]);
+      Lt.tiles[l] = Lt.tiles_x[l] * ws_bands(n, Lt.H[l], Lt.tiles_x[l], l);
     } else {
       Lt.tiles_x[l] = (Lt.W[l] + RB_TX - 1) / RB_TX;  // wl_dwt_rb tiles
       Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + RB_TY - 1) / RB_TY);
@@ -613,15 +651,19 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
 //     pywt's exact order; band stores (fp32 bands per fmask), level-1 dd codes, sums of squares
 // Row bands start four pairs early to fill the accumulators (4 / band height extra work).
 constexpr int WS_MAXT = 256;                 // threads = staged columns per workgroup (max)
-constexpr int WS_MAXSW = (WS_MAXT - 8) / 2;  // 124 output columns per strip (max)
-inline int ws_strips(int Wo) { return (Wo + WS_MAXSW - 1) / WS_MAXSW; }
+// output columns per strip (max): (threads - 8) / 2; tuning: IDN_WAVELET_WST threads (64..256)
+inline int ws_maxsw() {
+  const int t = std::min(std::max(knob("IDN_WAVELET_WST", WS_MAXT), 64), WS_MAXT) / 64 * 64;
+  return (t - 8) / 2;
+}
+inline int ws_strips(int Wo) { return (Wo + ws_maxsw() - 1) / ws_maxsw(); }
 inline int ws_sw(int Wo) {
   const int st = ws_strips(Wo);
   return ((Wo + st - 1) / st + 1) & ~1;
 }
-inline int ws_bands(int n, int Ho, int strips) {  // >= ~6 workgroups per CU; bands >= 24 rows
-  const int want = (1536 + n * strips - 1) / (n * strips);
-  return std::max(1, std::min(want, Ho / 24));
+int ws_resident(int level);  // resident analysis workgroups on the device (defined below)
+inline int ws_bands(int n, int Ho, int strips, int level) {  // bands >= 16 output rows
+  return best_bands((int64_t)n * strips, Ho, 4, ws_resident(level), 16);
 }
 
 template <int SRC>
@@ -646,13 +688,17 @@ template <int SRC> constexpr int ws_pf() { return SRC == 0 || SRC == 3 ? 5 : 1; 
 // squares and of the synthesis) in fp32, and at level 1 keeps the normalisation, the column
 // highpass and dd in fp64 with pywt's op order (the finest dd's exact zeros select the sigma
 // median's population); deeper levels (no median) run both paths in fp32.
-template <int SRC, typename TL = wreal, typename TH = wreal>
+// FM >= 0: the band storage mask (wl_fband) and CODES the level-1 code emission as compile-time
+// constants (the product's masks: no per-band branches); FM = -1 takes both from the arguments.
+template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1>
 __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
     int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands,
     const uint8_t* __restrict__ src, const double* __restrict__ in64, int64_t row_stride,
-    double* __restrict__ part, size_t part_per_img, size_t part_tile0, int emit_codes,
-    int fmask) {
+    double* __restrict__ part, size_t part_per_img, size_t part_tile0, int emit_codes_arg,
+    int fmask_arg) {
+  const int fmask = FM >= 0 ? FM : fmask_arg;
+  const int emit_codes = CODES >= 0 ? CODES : emit_codes_arg;
   constexpr int PF = ws_pf<SRC>();
   __shared__ TL VL[2][3][WS_MAXT];
   __shared__ TH VH[2][3][WS_MAXT];
@@ -869,6 +915,15 @@ __global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
     for (int g = 0; g < half; ++g) s2 += red[b * WS_MAXT + c * half + g];
     part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = s2;
   }
+}
+
+// resident workgroups of the product's streaming analysis of a level (level 1: u8 / fp32-lowpass;
+// deeper: fp32 'aa' input), used by wl_layout's band count for every form of that level
+int ws_resident(int level) {
+  const void* k = level == 1
+      ? reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1>)
+      : reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0>);
+  return cu_count() * occ_wgs(k, WS_MAXT);
 }
 
 // ---- 3: sum of squares per detail band ----------------------------------------------------------
@@ -1410,6 +1465,10 @@ inline int ss_bands(int n, int Mo, int strips) {  // Mo output row pairs; bands 
   const int want = (4096 + n * strips - 1) / (n * strips);
   return std::max(1, std::min(want, Mo / 32));
 }
+// the same on the measured residency of the launched kernel (>= 16 row pairs per band)
+inline int ss_bands_occ(int n, int Mo, int strips, const void* kernel, int block) {
+  return best_bands((int64_t)n * strips, Mo, 4, (int64_t)cu_count() * occ_wgs(kernel, block), 16);
+}
 constexpr int SS_PF = 4;                   // coefficient rows in flight ahead of the one staged
 constexpr int SS_NCOL = SS_MAXSW / 2 + 4;  // staged coefficient columns (max)
 constexpr int SS_ITEMS = 5;                // staging items per thread: 12 x SS_NCOL <= 5 x 256
@@ -1426,10 +1485,23 @@ __device__ __forceinline__ void synth_bior(const T (&cl)[5], const T (&cd)[5], T
   ev = fma_t<T>((T)S2, cl[2] + cd[2], common);
   od = fma_t<T>((T)S2, cl[2] - cd[2], common);
 }
+// type-exact helpers (the plain builtins are the double versions: a float argument would be
+// promoted and the arithmetic done in fp64)
+template <typename T>
+__device__ __forceinline__ T abs_t(T x) {
+  if constexpr (sizeof(T) == 4) return __builtin_fabsf(x);
+  else return __builtin_fabs(x);
+}
+template <typename T>
+__device__ __forceinline__ T clip01_t(T x) {
+  if constexpr (sizeof(T) == 4) return __builtin_fminf(__builtin_fmaxf(x, 0.f), 1.f);
+  else return __builtin_fmin(__builtin_fmax(x, 0.0), 1.0);
+}
 template <typename T>
 __device__ __forceinline__ T soft_t(T d, T t) {
-  const T m = __builtin_fabs(d) - t;
-  return m > (T)0 ? __builtin_copysign(m, d) : (T)0;
+  const T m = abs_t<T>(d) - t;
+  if constexpr (sizeof(T) == 4) return m > 0.f ? __builtin_copysignf(m, d) : 0.f;
+  else return m > 0.0 ? __builtin_copysign(m, d) : 0.0;
 }
 template <typename T>
 __device__ __forceinline__ T dot3_t(T x0, T x1, T x2, T m0, T m1, T m2) {
@@ -1597,8 +1669,7 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
             for (int rr2 = 0; rr2 < 2; ++rr2)
 #pragma unroll
               for (int col = 0; col < 2; ++col)
-                YB[c][rr2][2 * np + col] =
-                    __builtin_fmin(__builtin_fmax(v[rr2][col], (T)0), (T)1) * sc + mn;
+                YB[c][rr2][2 * np + col] = clip01_t<T>(v[rr2][col]) * sc + mn;
           }
           __syncthreads();
           // pixel pairs: thread q -> row q / half, pixels 2 (q % half), +1
@@ -1622,7 +1693,7 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
                                 (T)1.1977497040511743e-08);
 #pragma unroll
               for (int k3 = 0; k3 < 3; ++k3) {
-                T vv = __builtin_fmin(__builtin_fmax(o3[k3], (T)0), (T)1);
+                T vv = clip01_t<T>(o3[k3]);
                 if (bad) vv = (T)0;
                 const int bi = 3 * p + k3;
                 b6[bi >> 2] |= (uint32_t)(uint8_t)(int)((T)255 * vv) << (8 * (bi & 3));
@@ -1645,6 +1716,220 @@ __global__ __launch_bounds__(SS_MAXT) void wl_synth_stream(
   if (FINAL && R >= 5) {
     __syncthreads();
     flush(r0 + R - 5);
+  }
+}
+
+// ---- 7b (bior1.5): level-1 synthesis, fp32, three channels per thread ----------------------------
+// wl_synth_stream<true, float> splits a column pair's three channels over three threads, so the
+// YCbCr -> RGB step needs a second barrier per coefficient row (and 48 register moves shift its
+// ring).  Here thread np owns output columns 2np, 2np+1 of ALL three channels: one barrier per
+// coefficient row, and the five-row ring rotates by index (the loop is unrolled by 10 = lcm(5,
+// S3_PF)).  Thread t < SWo/2 + 4 stages coefficient column n0 + t of the 12 (channel, band) rows;
+// FM (compile time) says which bands are fp32 in HBM (aa / ad / da; the finest dd is fp64), so each
+// thread keeps S3_PF rows of raw loads in flight with no per-item selects.  The U8 rows go through
+// an LDS row image flushed as dwords after the next step's barrier.  Arithmetic as
+// wl_synth_stream<.., float>.
+constexpr int S3_T = 256;
+constexpr int S3_MAXSW = 2 * (S3_T - 4);  // 504 output columns per strip
+constexpr int S3_PF = 1;                  // coefficient rows in flight ahead of the one staged
+inline int s3_strips(int Wout) { return (Wout + S3_MAXSW - 1) / S3_MAXSW; }
+inline int s3_sw(int Wout) {
+  const int st = s3_strips(Wout);
+  return ((Wout + st - 1) / st + 3) & ~3;  // multiple of 4 pixels (12-byte strip starts)
+}
+template <int FM>
+struct S3Raw {  // one coefficient row of one staged column: the 12 (channel, band) values
+  float f[3][3];   // fp32 bands (slot b - (b > first fp64 band ...)): see s3_val
+  double d[3][2];  // fp64 bands
+};
+template <int FM>
+__device__ __forceinline__ constexpr int s3_slot(int b) {  // slot of band b in f (fp32) or d (fp64)
+  int k = 0;
+  for (int q = 0; q < b; ++q) k += (((FM >> q) & 1) == ((FM >> b) & 1)) ? 1 : 0;
+  return k;
+}
+template <int FM>
+__global__ __launch_bounds__(S3_T) void wl_synth_final3(
+    const wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, int L,
+    size_t in_off, int Nh, int Nw, int Hout, int Wout, int SWo, int strips, int bands,
+    uint8_t* __restrict__ out_u8, int64_t row_stride, float* __restrict__ out_f32) {
+  static_assert((FM & 0b1110) == 0b0110, "ad / da fp32, dd fp64");
+  __shared__ float SB[2][12][S3_T];                  // staged row: [c * 4 + band][column]
+  __shared__ uint32_t OB[2][2][S3_MAXSW * 3 / 4];     // U8 rows of the step's output row pair
+  __shared__ float TH[12];
+  const int img = blockIdx.z;
+  const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
+  const int x0 = strip * SWo, n0 = x0 / 2;
+  const int Mo = (Hout + 1) / 2;
+  const int ma = (int)((int64_t)band * Mo / bands), mb = (int)((int64_t)(band + 1) * Mo / bands);
+  const int t = threadIdx.x;
+  const wreal* base = ws + img * img_floats + in_off;
+  const double* st = stats + (size_t)img * WL_STATS;
+  const size_t bsz = (size_t)Nh * Nw;
+  const int half = SWo / 2, ncol = half + 4;
+  if (t < 12) TH[t] = (float)((t & 3) ? st[WlStats::thr(t >> 2, 0, (t & 3) - 1, L)] : 0.0);
+  float mn[3], sc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    wreal a, b;
+    wl_minmax64(st, c, a, b);
+    mn[c] = (float)a;
+    sc[c] = (float)(b - a);
+  }
+  const bool bad = st[WlStats::FLAG] != 0.0;
+  // staging role: coefficient column n0 + t (clamped: columns past the band's end feed only
+  // outputs past the valid width, never stored)
+  const bool stg = t < ncol;
+  const int scol = min(n0 + t, Nw - 1);
+  auto load = [&](int r, S3Raw<FM>& R) {
+    const size_t e = (size_t)min(r, Nh - 1) * Nw + scol;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const wreal* X = base + (size_t)(c * 4 + b) * bsz;
+        if ((FM >> b) & 1) R.f[c][s3_slot<FM>(b)] = reinterpret_cast<const float*>(X)[e];
+        else R.d[c][s3_slot<FM>(b)] = X[e];
+      }
+  };
+  // compute role: column pair np (outputs x0 + 2np, +1), all three channels
+  const bool cmp = t < half;
+  const int np = t;
+  float ring[3][5][4];  // [c][slot = coefficient row % 5][sa(2np), sa(2np+1), sd(2np), sd(2np+1)]
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int s5 = 0; s5 < 5; ++s5)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ring[c][s5][q] = 0.f;
+  const int nb = 3 * min(SWo, Wout - x0);  // U8 bytes of the strip's rows
+  const bool al = ((uintptr_t)out_u8 & 3) == 0 && (row_stride & 3) == 0;
+  auto flush = [&](int m, int ob) {  // output rows 2m, 2m+1 from OB[ob]
+    if (!out_u8) return;
+    const int nw = (nb + 3) / 4;
+    for (int k = t; k < 2 * nw; k += S3_T) {
+      const int rr2 = k >= nw, d = k - rr2 * nw;
+      const int y = 2 * m + rr2;
+      if (y >= Hout) continue;
+      uint8_t* orow = out_u8 + ((int64_t)img * Hout + y) * row_stride + (int64_t)x0 * 3;
+      const uint32_t wv = OB[ob][rr2][d];
+      if (al && 4 * d + 4 <= nb) {
+        reinterpret_cast<uint32_t*>(orow)[d] = wv;
+      } else {
+        for (int bi = 4 * d; bi < min(4 * d + 4, nb); ++bi) orow[bi] = (uint8_t)(wv >> (8 * (bi & 3)));
+      }
+    }
+  };
+  __syncthreads();  // TH
+  const int r0 = ma, R = (mb - ma) + 4;  // coefficient rows r0 .. r0 + R - 1
+  S3Raw<FM> pf[S3_PF];
+  if (stg) {
+#pragma unroll
+    for (int f = 0; f < S3_PF; ++f)
+      if (f < R) load(r0 + f, pf[f]);
+  }
+  for (int s0 = 0; s0 < R; s0 += 10) {
+#pragma unroll
+    for (int rs = 0; rs < 10; ++rs) {
+      const int sidx = s0 + rs;
+      if (sidx >= R) break;
+      const int r = r0 + sidx, buf = sidx & 1, slot = rs % 5;
+      if (stg) {  // stage row r (details soft-thresholded), refill its prefetch slot
+        const S3Raw<FM>& q = pf[rs % S3_PF];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const float x = ((FM >> b) & 1) ? q.f[c][s3_slot<FM>(b)] : (float)q.d[c][s3_slot<FM>(b)];
+            SB[buf][c * 4 + b][t] = b ? soft_t<float>(x, TH[c * 4 + b]) : x;
+          }
+        if (sidx + S3_PF < R) load(r + S3_PF, pf[rs % S3_PF]);
+      }
+      __syncthreads();
+      if (sidx >= 5) flush(r - 5, buf ^ 1);  // the previous step's U8 rows
+      if (cmp) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int pb = 0; pb < 2; ++pb) {  // sa: aa / ad; sd: da / dd
+            const float* lo = SB[buf][c * 4 + 2 * pb];
+            const float* hi = SB[buf][c * 4 + 2 * pb + 1];
+            float cl[5], cd[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {  // c[j] = column np + 4 - j
+              cl[j] = lo[np + 4 - j];
+              cd[j] = hi[np + 4 - j];
+            }
+            synth_bior<float>(cl, cd, ring[c][slot][2 * pb], ring[c][slot][2 * pb + 1]);
+          }
+      }
+      if (sidx >= 4 && cmp) {
+        const int m = r - 4;  // output row pair 2m, 2m+1
+        float Yv[3][2][2];    // [c][row][column], de-normalised
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int col = 0; col < 2; ++col) {
+            float cl[5], cd[5], v0, v1;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {  // c[j] = coefficient row m + 4 - j
+              cl[j] = ring[c][(rs + 5 - j) % 5][col];
+              cd[j] = ring[c][(rs + 5 - j) % 5][2 + col];
+            }
+            synth_bior<float>(cl, cd, v0, v1);
+            Yv[c][0][col] = clip01_t<float>(v0) * sc[c] + mn[c];
+            Yv[c][1][col] = clip01_t<float>(v1) * sc[c] + mn[c];
+          }
+#pragma unroll
+        for (int rr2 = 0; rr2 < 2; ++rr2) {
+          const int y = 2 * m + rr2;
+          uint32_t b6[2] = {0u, 0u};  // the pair's 6 bytes
+          float o6[6];
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const float Y = Yv[0][rr2][p] - 16.f, Cb = Yv[1][rr2][p] - 128.f, Cr = Yv[2][rr2][p] - 128.f;
+            float o3[3];
+            // (float) of the fp64 constants, as wl_synth_stream (a float literal of the decimal
+            // can round differently: double rounding)
+            o3[0] = dot3_t<float>(Y, Cb, Cr, (float)0.004566210045662101, (float)1.1808799897950177e-09,
+                                  (float)0.006258928969943937);
+            o3[1] = dot3_t<float>(Y, Cb, Cr, (float)0.004566210045662101, (float)-0.0015363236860449021,
+                                  (float)-0.003188110949655707);
+            o3[2] = dot3_t<float>(Y, Cb, Cr, (float)0.004566210045662101, (float)0.007910716233554741,
+                                  (float)1.1977497040511743e-08);
+#pragma unroll
+            for (int k3 = 0; k3 < 3; ++k3) {
+              float vv = clip01_t<float>(o3[k3]);
+              if (bad) vv = 0.f;
+              const int bi = 3 * p + k3;
+              o6[bi] = vv;
+              b6[bi >> 2] |= (uint32_t)(uint8_t)(int)(255.f * vv) << (8 * (bi & 3));
+            }
+          }
+          uint16_t* ob = reinterpret_cast<uint16_t*>(&OB[buf][rr2][0]) + 3 * np;
+          ob[0] = (uint16_t)b6[0];
+          ob[1] = (uint16_t)(b6[0] >> 16);
+          ob[2] = (uint16_t)b6[1];
+          const int x = x0 + 2 * np;
+          if (out_f32 && y < Hout && x < Wout) {
+            float* o = out_f32 + (((int64_t)img * Hout + y) * Wout + x) * 3;
+            if (x + 1 < Wout && ((uintptr_t)o & 7) == 0) {
+              reinterpret_cast<float2*>(o)[0] = make_float2(o6[0], o6[1]);
+              reinterpret_cast<float2*>(o)[1] = make_float2(o6[2], o6[3]);
+              reinterpret_cast<float2*>(o)[2] = make_float2(o6[4], o6[5]);
+            } else {
+#pragma unroll
+              for (int k = 0; k < 6; ++k)
+                if (k < 3 || x + 1 < Wout) o[k] = o6[k];
+            }
+          }
+        }
+      }
+    }
+  }
+  if (R >= 5) {
+    __syncthreads();
+    flush(r0 + R - 5, (R - 1) & 1);
   }
 }
 
@@ -2952,10 +3237,22 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       const dim3 blk((unsigned)((2 * sw + 8 + 63) / 64 * 64));
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
       // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
+#define IDN_WS_(SRC, TL, TH, FMC, CC, EMIT)                                                        \
+  hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC>), grid, blk, 0, st, wsf, Lt.img_floats,  \
+                     stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands,   \
+                     src, in64, row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT,         \
+                     fm_an(l))
+      // the product's band masks as compile-time constants (bit 4 = WL_FB_AIN is read by the
+      // launcher only); anything else (tuning forms) through the runtime-mask instance
 #define IDN_WS(SRC, TL, TH, EMIT)                                                                  \
-  hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH>), grid, blk, 0, st, wsf, Lt.img_floats, stats,    \
-                     in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands, src, in64, \
-                     row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT, fm_an(l))
+  do {                                                                                             \
+    const int fmb = fm_an(l) & 0b1111;                                                             \
+    if (SRC == 0 && fmb == 0b0111 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0111, 1, EMIT);           \
+    else if (SRC == 0 && fmb == 0b0110 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0110, 1, EMIT);      \
+    else if (SRC == 3 && fmb == 0b1111) IDN_WS_(SRC, TL, TH, 0b1111, 0, EMIT);                     \
+    else if (SRC == 3 && fmb == 0b1110) IDN_WS_(SRC, TL, TH, 0b1110, 0, EMIT);                     \
+    else IDN_WS_(SRC, TL, TH, -1, -1, EMIT);                                                       \
+  } while (0)
       const bool f1 = (a32 & 1) != 0, fd = (a32 & 2) != 0;
       if (l > 1 && (fm_an(l) & WL_FB_AIN)) {
         if (fd) IDN_WS(3, float, float, 0);
@@ -2971,6 +3268,7 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
         else IDN_WS(0, wreal, wreal, emit);
       }
 #undef IDN_WS
+#undef IDN_WS_
     } else if (l > 1)
       hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
@@ -3000,6 +3298,8 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   // streaming levels in fp32 arithmetic (wl_synth_stream<.., float>); a level >= 2 that is then
   // stores its reconstruction as fp32, so the level below reads its 'aa' band as fp32 (bit 0)
   const bool s32 = knob("IDN_WAVELET_S32", 1) != 0;
+  // fp32 level 1 with all three channels per thread (wl_synth_final3)
+  const bool s3 = knob("IDN_WAVELET_S3", 1) != 0;
   auto str = [&](int l) { return (sstream & (l == 1 ? 1 : 2)) != 0; };
   auto fm_syn2 = [&](int l) { return fm_syn(l) | (l < Lt.L && str(l + 1) && s32 ? 0b0001 : 0); };
   if (sstream) {
@@ -3021,7 +3321,9 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       }
       const int Hout = Lt.H[l - 1], Wout = Lt.W[l - 1];
       const int strips = ss_strips(Wout), sw = ss_sw(Wout);
-      const int bands = ss_bands(n, (Hout + 1) / 2, strips);
+      const int bands = ss_bands_occ(
+          n, (Hout + 1) / 2, strips,
+          reinterpret_cast<const void*>(&wl_synth_stream<false, float>), SS_MAXT);
       const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n), blk(SS_MAXT);
       if (l >= 2) {
         if (s32)
@@ -3034,6 +3336,19 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
                              l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Hout,
                              Wout, (size_t)4 * Hout * Wout, fm_syn2(l), sw, strips, bands,
                              (uint8_t*)nullptr, row_stride, (float*)nullptr);
+      } else if (s32 && s3 && (fm_syn2(1) == 0b0111 || fm_syn2(1) == 0b0110)) {
+        const int strips3 = s3_strips(Wout), sw3 = s3_sw(Wout);
+        const int bands3 = ss_bands_occ(n, (Hout + 1) / 2, strips3,
+                                        reinterpret_cast<const void*>(&wl_synth_final3<0b0111>), S3_T);
+        const dim3 grid3((unsigned)(strips3 * bands3), 1, (unsigned)n);
+        if (fm_syn2(1) == 0b0111)
+          hipLaunchKernelGGL((wl_synth_final3<0b0111>), grid3, dim3(S3_T), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h,
+                             Lt.w, sw3, strips3, bands3, out_u8, row_stride, out_f32);
+        else
+          hipLaunchKernelGGL((wl_synth_final3<0b0110>), grid3, dim3(S3_T), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h,
+                             Lt.w, sw3, strips3, bands3, out_u8, row_stride, out_f32);
       } else if (s32) {
         hipLaunchKernelGGL((wl_synth_stream<true, float>), grid, blk, 0, st, wsf, Lt.img_floats,
                            stats, 1, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], (size_t)0, Lt.h, Lt.w,

@@ -258,6 +258,23 @@ def test_wavelet_bior15_fp32_synthesis(dev, monkeypatch, shape, env):
         check_u8(u8a, ref, oracle.sk.to_u8(255 * ref))
 
 
+@pytest.mark.parametrize("shape", [(600, 1000), (601, 999), (130, 77), (37, 53), (9, 11), (40, 1100)])
+def test_wavelet_bior15_final3_bitwise(dev, monkeypatch, shape):
+    """wl_synth_final3 (level 1, all three channels per thread; product) against the per-channel
+    streaming kernel (IDN_WAVELET_S3=0): the same fp32 operations per output, so bit-identical U8
+    and float outputs (odd sizes, several strips, L = 1 with an fp64 coarsest aa)"""
+    img = make_img(*shape, 41)
+    u8a, fa = run(img, "bior1.5", None)
+    u8c, fc = run(img, "bior1.5", None)
+    np.testing.assert_array_equal(u8a, u8c)  # deterministic
+    np.testing.assert_array_equal(fa, fc)
+    u8b, fb = _run_env(monkeypatch, img, {"IDN_WAVELET_S3": "0"})
+    nd = int((fa != fb).sum())
+    print(f"final3 vs stream: {nd} float outputs differ, max {np.abs(fa - fb).max():.3g}")
+    np.testing.assert_array_equal(u8a, u8b)
+    np.testing.assert_array_equal(fa, fb)
+
+
 def _bior_stats(monkeypatch, img, env):
     """bior1.5 through the tuning build under env: (u8, f32, stats block of the image)"""
     import torch

@@ -21,7 +21,7 @@ def main():
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for p in args.paths:
         p = Path(p)
-        files = [p] if p.is_file() else sorted(p.rglob("*counter_collection.csv"))
+        files = ([p] if p.name.endswith(".csv") else []) if p.is_file() else sorted(p.rglob("*counter_collection.csv"))
         for f in files:
             for r in csv.DictReader(open(f)):
                 if args.match not in r["Kernel_Name"]:
