@@ -347,6 +347,9 @@ __device__ __forceinline__ void blob_row_store(const v4u& o, uint32_t* __restric
 // the vertical-first arithmetic above and store their output rows directly.  Measured on this
 // chip the flat tile fetch sustains ~5.8 TB/s copy-equivalent where per-segment row loads stop
 // near 5.2 (tools/membench3.hip).
+#ifndef IDN_STENCIL_NB  // band height of the u8 stencils' LDS tile (A/B builds set it)
+#define IDN_STENCIL_NB 6
+#endif
 constexpr int TILE_WGT = 192;     // 3 waves
 constexpr int TILE_RBMAX = 3024;  // 3 segments of 1008 bytes
 template <int NB, int K>
@@ -359,7 +362,7 @@ struct TileShape {
   static constexpr int LDS = (BYTES + 15) / 16 * 16;
 };
 
-template <int C, int OP, int NB, int EPI = EPI_U8, int NTS = 0>
+template <int C, int OP, int NB, int EPI = EPI_U8, int NTS = 0, int DMA = 0>
 __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __restrict__ src,
                                                           uint8_t* __restrict__ dst, int h, int rb,
                                                           int nseg, int seg_len, int bands,
@@ -409,7 +412,24 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     v4u v[TS::NL];
     const bool full = __builtin_amdgcn_readfirstlane(
         (int)(nbytes >= (uint32_t)(16 * TILE_WGT * (TS::NL - 1))));
-    if (full) {
+    if (DMA && full) {  // (full: every chunk but the last round's inside the tile)
+      // LDS-DMA: global_load_lds_dwordx4 writes each wave's 1 KiB straight into the tile (the
+      // destination is wave base + 16 lane, as the flat layout wants), no VGPR round trip and no
+      // ds_write; the barrier below waits for it (vmcnt)
+      const uint8_t* gsrc = src + (size_t)g.img * img_bytes + base_al + 16u * threadIdx.x;
+      const int wv64 = 64 * wave;
+#pragma unroll
+      for (int i = 0; i < TS::NL - 1; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(gsrc + 16 * TILE_WGT * i),
+            (__attribute__((address_space(3))) void*)(tile + 16 * (TILE_WGT * i + wv64)), 16, 0, 0);
+      const uint32_t o = 16u * (uint32_t)(TILE_WGT * (TS::NL - 1) + threadIdx.x);
+      if (o < nbytes)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(gsrc + 16 * TILE_WGT * (TS::NL - 1)),
+            (__attribute__((address_space(3))) void*)(tile + 16 * (TILE_WGT * (TS::NL - 1) + wv64)),
+            16, 0, 0);
+    } else if (full) {
       const uint32_t vo = base_al + 16u * threadIdx.x;
 #pragma unroll
       for (int i = 0; i < TS::NL - 1; ++i)
@@ -603,13 +623,19 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
       h > 2 * R) {
     const int nseg = (int)((rb + 1007) / 1008);
     const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
-    constexpr int NB = 6;
+    constexpr int NB = IDN_STENCIL_NB;
     const int bands = (h + NB - 1) / NB;
     const int64_t total = (int64_t)n * bands * nseg;
     IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
     // nontemporal stores: a tuning-build A/B (IDN_STENCIL_NTS); the product keeps the default
+    // tuning-build A/B: nontemporal stores (IDN_STENCIL_NTS, measured slower), register-staged
+    // tile fetch (IDN_STENCIL_GLDS=0; the product fetches the tile by LDS-DMA)
     if (knob("IDN_STENCIL_NTS", 0))
       hipLaunchKernelGGL((stencil_u8_lds<3, OP, NB, EPI_U8, 1>), dim3((unsigned)((int64_t)n * bands)),
+                         dim3(TILE_WGT), 0, st, src, dst, h, (int)rb, nseg, seg_len, bands,
+                         (int)total);
+    else if (knob("IDN_STENCIL_GLDS", 1))
+      hipLaunchKernelGGL((stencil_u8_lds<3, OP, NB, EPI_U8, 0, 1>), dim3((unsigned)((int64_t)n * bands)),
                          dim3(TILE_WGT), 0, st, src, dst, h, (int)rb, nseg, seg_len, bands,
                          (int)total);
     else
@@ -730,8 +756,16 @@ extern "C" int idn_gaussian_blob_f32(const uint8_t* src, float* blob, int n, int
   IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "idn_gaussian_blob_f32: batch too large");
   const dim3 grid((unsigned)((int64_t)n * bands)), block(TILE_WGT);
   hipStream_t st = as_stream(stream);
-  if (ksize == 5)
+  if (ksize == 5 && knob("IDN_STENCIL_GLDS", 1))  // LDS-DMA tile fetch (as the u8 filters)
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP_GAUSS5, NB, EPI_BLOB, 0, 1>), grid, block, 0, st, src,
+                       nullptr, h, (int)rb, nseg, seg_len, bands, (int)total, blob, mean[0],
+                       mean[1], mean[2]);
+  else if (ksize == 5)
     hipLaunchKernelGGL((stencil_u8_lds<3, OP_GAUSS5, NB, EPI_BLOB>), grid, block, 0, st, src,
+                       nullptr, h, (int)rb, nseg, seg_len, bands, (int)total, blob, mean[0],
+                       mean[1], mean[2]);
+  else if (knob("IDN_STENCIL_GLDS", 1))
+    hipLaunchKernelGGL((stencil_u8_lds<3, OP_GAUSS3, NB, EPI_BLOB, 0, 1>), grid, block, 0, st, src,
                        nullptr, h, (int)rb, nseg, seg_len, bands, (int)total, blob, mean[0],
                        mean[1], mean[2]);
   else

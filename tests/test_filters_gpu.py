@@ -70,6 +70,21 @@ def test_stencil_random_extremes(dev, k):
         assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
 
 
+@pytest.mark.parametrize("shape", SHAPES[:8] + [(3, 600, 1000)])
+def test_stencil_register_staged_form(dev, monkeypatch, shape):
+    """IDN_STENCIL_GLDS=0 (tuning build): the register-staged tile fetch (the product fetches the
+    tile by global_load_lds_dwordx4) -- bit-exact with the oracle like the product form"""
+    import idn
+    import oracle
+    from idn import _lib
+    monkeypatch.setenv("IDN_STENCIL_GLDS", "0")
+    img = textured(*shape, seed=sum(shape) + 7)
+    with _lib.variant("tuning"):
+        for k in (3, 5):
+            assert np.array_equal(_run(idn.gaussian_blur, img, k), oracle.cv.gaussian_blur(img, k))
+        assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
+
+
 def test_generic_path_forced(dev, monkeypatch):
     """the per-pixel kernel (shapes the lane layout does not take), forced on a shape it would
     not get by itself through the tools-only tuning build"""

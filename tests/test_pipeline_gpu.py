@@ -73,12 +73,14 @@ def test_plan_parity(dev, mode, spec):
         has_bil = any(s.op == "bilateral" for s in p.steps)
         has_bloom = any(s.op == "bloom" for s in p.steps)
         if wl:
-            # fp64 wavelet vs numpy: last-bit differences flip a U8 cast only where 255*x sits
-            # at an integer boundary (<= 1 LSB per wavelet step); train_v0's double filtering
-            # (closure wavelet + hook wavelet) feeds such a flipped pixel into the second
-            # wavelet, so the bound is one LSB per wavelet step in the plan
+            # wavelet vs numpy within the north-star 1e-5 (bior1.5 synthesises in fp32, ~3e-7):
+            # a U8 cast flips only where 255*x sits within 255e-5 of an integer, at most ~0.5 %
+            # of the values per wavelet step (<= 1 LSB); train_v0's double filtering (closure
+            # wavelet + hook wavelet) feeds such a flipped pixel into the second wavelet, whose
+            # output moves by a fraction of an LSB around it, so the bound is one LSB per wavelet
+            # step and the flip share 5e-3 per step
             n_wl = sum(s.op == "wavelet" for s in p.steps)
-            assert d.max() <= n_wl and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
+            assert d.max() <= n_wl and (d > 0).mean() < 5e-3 * n_wl, (p, d.max(), (d > 0).mean())
         elif has_bil or has_bloom:
             assert d.max() <= 1 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
         else:

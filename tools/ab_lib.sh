@@ -10,7 +10,7 @@ for v in "$@"; do
   timeout -k 10 120 python bench.py --op $OP --no-cpu --no-copy --steps 20 --warmup 3 > "$OUT/$v.json" || exit 1
   python3 -c "import json,sys; print(sys.argv[1], json.load(open(sys.argv[2]))['ms_per_step'])" $v "$OUT/$v.json"
 done
-for v in new old; do
+for v in new; do
   cp ab/$v.so $L || exit 1
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$v" -o k --output-format csv -- python3 bench.py --op $OP --no-cpu --no-copy --steps 10 --warmup 2 > /dev/null 2>&1 || exit 1
 done
