@@ -683,7 +683,16 @@ template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (
 // prefetch depth (steps; divides 5): the u8 and fp32 rings are small, the fp64 ones are not
 // (fp32 'aa' input: depth 1 keeps the deeper levels at 76 VGPRs, six waves per SIMD; depth 5
 // measured 1 % slower on the whole op)
-template <int SRC> constexpr int ws_pf() { return SRC == 0 ? 5 : 1; }
+#ifndef IDN_WS_PF0  // A/B builds set these
+#define IDN_WS_PF0 5
+#endif
+#ifndef IDN_WS_WPE
+#define IDN_WS_WPE 1
+#endif
+#ifndef IDN_S3_WPE
+#define IDN_S3_WPE 1
+#endif
+template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
 
 // TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the
 // product runs the lowpass outputs (aa, ad, da: continuous inputs of the thresholds' fp64 sums of
@@ -693,7 +702,7 @@ template <int SRC> constexpr int ws_pf() { return SRC == 0 ? 5 : 1; }
 // FM >= 0: the band storage mask (wl_fband) and CODES the level-1 code emission as compile-time
 // constants (the product's masks: no per-band branches); FM = -1 takes both from the arguments.
 template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1>
-__global__ __launch_bounds__(WS_MAXT) void wl_dwt_stream(
+__global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
     int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands,
     const uint8_t* __restrict__ src, const double* __restrict__ in64, int64_t row_stride,
@@ -1751,7 +1760,7 @@ __device__ __forceinline__ constexpr int s3_slot(int b) {  // slot of band b in 
   return k;
 }
 template <int FM>
-__global__ __launch_bounds__(S3_T) void wl_synth_final3(
+__global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
     const wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, int L,
     size_t in_off, int Nh, int Nw, int Hout, int Wout, int SWo, int strips, int bands,
     uint8_t* __restrict__ out_u8, int64_t row_stride, float* __restrict__ out_f32) {
