@@ -32,6 +32,7 @@
 
 #include <cmath>
 #include <mutex>
+#include <type_traits>
 
 #include <math.h>
 
@@ -711,7 +712,13 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
   const int fmask = FM >= 0 ? FM : fmask_arg;
   const int emit_codes = CODES >= 0 ? CODES : emit_codes_arg;
   constexpr int PF = ws_pf<SRC>();
+  // VL / VF: the column lowpass / highpass in the lowpass type (TL) at staged column u; VH: the
+  // column highpass in TH for dd, even and odd columns in separate halves (column u at
+  // (u & 1) * WS_MAXT / 2 + u / 2) so that the row threads' 16-byte reads (lane stride 4 columns)
+  // fill whole bank rows -- interleaved fp64 columns put two lanes on every 16-byte slot
+  constexpr bool SEPF = !std::is_same<TL, TH>::value;  // a separate TL copy of the highpass
   __shared__ TL VL[2][3][WS_MAXT];
+  __shared__ TL VF[SEPF ? 2 : 1][SEPF ? 3 : 1][SEPF ? WS_MAXT : 1];
   __shared__ TH VH[2][3][WS_MAXT];
   __shared__ double RED[3][WS_MAXT];
   const int img = blockIdx.z;
@@ -840,7 +847,8 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
           const TL lo = fma_t<TL>((TL)B1, ek, acc[c][r]);  // output k complete
           if (m >= 4) {
             VL[buf][c][t] = lo;
-            VH[buf][c][t] = hd1[c];
+            VH[buf][c][(t & 1) * (WS_MAXT / 2) + (t >> 1)] = hd1[c];
+            if constexpr (SEPF) VF[buf][c][t] = (TL)hd1[c];
           }
           hd1[c] = hd0[c];
           hd0[c] = hk;
@@ -851,7 +859,9 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
       const int i = k;  // output row
       if (rowt) {
         const TL* vl = &VL[buf][rc][2 * jj];
-        const TH* vh = &VH[buf][rc][2 * jj];
+        const TH* vhe = &VH[buf][rc][jj];                 // element 2 jj + m, m even: vhe[m / 2]
+        const TH* vho = &VH[buf][rc][WS_MAXT / 2 + jj];   //                   m odd:  vho[m / 2]
+        const TL* vf = SEPF ? &VF[buf][rc][2 * jj] : nullptr;
         TL o[2][3];  // [output][aa, ad, da]
         TH odd[2];   // [output] dd
 #pragma unroll
@@ -859,8 +869,17 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
           TL S[6], E[6];
 #pragma unroll
           for (int nn = 0; nn < 6; ++nn) {
-            const TL a0 = pass ? (TL)vh[2 * nn] : vl[2 * nn];
-            const TL a1 = pass ? (TL)vh[2 * nn + 1] : vl[2 * nn + 1];
+            TL a0, a1;
+            if (pass == 0) {
+              a0 = vl[2 * nn];
+              a1 = vl[2 * nn + 1];
+            } else if constexpr (SEPF) {
+              a0 = vf[2 * nn];
+              a1 = vf[2 * nn + 1];
+            } else {
+              a0 = (TL)vhe[nn];
+              a1 = (TL)vho[nn];
+            }
             S[nn] = a0 + a1;
             E[nn] = a1 - a0;
           }
@@ -869,7 +888,7 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
             o[d][2 * pass] = fma_t<TL>((TL)S2, S[2 + d],
                                        fma_t<TL>((TL)B1, E[4 + d] - E[d], (TL)B2 * (E[1 + d] - E[3 + d])));
             if (pass == 0) o[d][1] = (TL)(-S2) * E[2 + d];
-            else odd[d] = (TH)(-S2) * vh[2 * d + 5] + (TH)S2 * vh[2 * d + 4];
+            else odd[d] = (TH)(-S2) * vho[d + 2] + (TH)S2 * vhe[d + 2];  // elements 2d+5, 2d+4
           }
         }
         const size_t e0 = (size_t)i * Wo + oj;
@@ -877,9 +896,9 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
         for (int d = 0; d < 2; ++d) {
           if (!(d ? ok1 : ok0)) continue;
           const double v1 = (double)o[d][1], v2 = (double)o[d][2], v3 = (double)odd[d];
-          sq[0] += v1 * v1;
-          sq[1] += v2 * v2;
-          sq[2] += v3 * v3;
+          sq[0] = __fma_rn(v1, v1, sq[0]);  // (exact squares for the fp32 bands: = mul + add)
+          sq[1] = __fma_rn(v2, v2, sq[1]);
+          sq[2] = __fma_rn(v3, v3, sq[2]);
           if (emit_codes) {
             const unsigned long long key = absbits((double)odd[d]);
             reinterpret_cast<uint16_t*>(base + (size_t)rc * Hin * Win)[e0 + d] =
