@@ -71,13 +71,14 @@ def test_stencil_random_extremes(dev, k):
 
 
 @pytest.mark.parametrize("shape", SHAPES[:8] + [(3, 600, 1000)])
-def test_stencil_register_staged_form(dev, monkeypatch, shape):
+@pytest.mark.parametrize("form", ["0"])
+def test_stencil_tile_fetch_forms(dev, monkeypatch, shape, form):
     """IDN_STENCIL_GLDS=0 (tuning build): the register-staged tile fetch (the product fetches the
     tile by global_load_lds_dwordx4) -- bit-exact with the oracle like the product form"""
     import idn
     import oracle
     from idn import _lib
-    monkeypatch.setenv("IDN_STENCIL_GLDS", "0")
+    monkeypatch.setenv("IDN_STENCIL_GLDS", form)
     img = textured(*shape, seed=sum(shape) + 7)
     with _lib.variant("tuning"):
         for k in (3, 5):
