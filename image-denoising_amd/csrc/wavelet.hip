@@ -651,7 +651,10 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
 //     jj + 1: aa / da (lowpass of the column low / high), ad = S2 (v[2j-4] - v[2j-3]), dd in
 //     pywt's exact order; band stores (fp32 bands per fmask), level-1 dd codes, sums of squares
 // Row bands start four pairs early to fill the accumulators (4 / band height extra work).
-constexpr int WS_MAXT = 256;                 // threads = staged columns per workgroup (max)
+#ifndef IDN_WS_MAXT  // A/B builds set it
+#define IDN_WS_MAXT 512
+#endif
+constexpr int WS_MAXT = IDN_WS_MAXT;         // threads = staged columns per workgroup (max)
 // output columns per strip (max): (threads - 8) / 2; tuning: IDN_WAVELET_WST threads (64..256)
 inline int ws_maxsw() {
   const int t = std::min(std::max(knob("IDN_WAVELET_WST", WS_MAXT), 64), WS_MAXT) / 64 * 64;
