@@ -1772,7 +1772,7 @@ inline int s3_sw(int Wout) {
 }
 template <int FM>
 struct S3Raw {  // one coefficient row of one staged column: the 12 (channel, band) values
-  float f[3][3];   // fp32 bands (slot b - (b > first fp64 band ...)): see s3_val
+  float f[3][4];   // fp32 bands, by s3_slot (unused slots are never written)
   double d[3][2];  // fp64 bands
 };
 template <int FM>
@@ -1781,14 +1781,17 @@ __device__ __forceinline__ constexpr int s3_slot(int b) {  // slot of band b in 
   for (int q = 0; q < b; ++q) k += (((FM >> q) & 1) == ((FM >> b) & 1)) ? 1 : 0;
   return k;
 }
-template <int FM>
+// FINAL = false (levels >= 2): the same structure without the colour step; the three channels'
+// reconstructions go to the level below's 'aa' slots as fp32 (out_off + c * out_chan_stride).
+template <int FM, bool FINAL = true>
 __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
-    const wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, int L,
+    wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, int L,
     size_t in_off, int Nh, int Nw, int Hout, int Wout, int SWo, int strips, int bands,
-    uint8_t* __restrict__ out_u8, int64_t row_stride, float* __restrict__ out_f32) {
-  static_assert((FM & 0b1110) == 0b0110, "ad / da fp32, dd fp64");
+    uint8_t* __restrict__ out_u8, int64_t row_stride, float* __restrict__ out_f32, int level = 1,
+    size_t out_off = 0, size_t out_chan_stride = 0) {
+  static_assert(!FINAL || (FM & 0b1110) == 0b0110, "level 1: ad / da fp32, dd fp64");
   __shared__ float SB[2][12][S3_T];                  // staged row: [c * 4 + band][column]
-  __shared__ uint32_t OB[2][2][S3_MAXSW * 3 / 4];     // U8 rows of the step's output row pair
+  __shared__ uint32_t OB[FINAL ? 2 : 1][2][FINAL ? S3_MAXSW * 3 / 4 : 1];  // U8 rows (FINAL)
   __shared__ float TH[12];
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
@@ -1800,7 +1803,7 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
   const double* st = stats + (size_t)img * WL_STATS;
   const size_t bsz = (size_t)Nh * Nw;
   const int half = SWo / 2, ncol = half + 4;
-  if (t < 12) TH[t] = (float)((t & 3) ? st[WlStats::thr(t >> 2, 0, (t & 3) - 1, L)] : 0.0);
+  if (t < 12) TH[t] = (float)((t & 3) ? st[WlStats::thr(t >> 2, level - 1, (t & 3) - 1, L)] : 0.0);
   float mn[3], sc[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -1838,7 +1841,7 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
   const int nb = 3 * min(SWo, Wout - x0);  // U8 bytes of the strip's rows
   const bool al = ((uintptr_t)out_u8 & 3) == 0 && (row_stride & 3) == 0;
   auto flush = [&](int m, int ob) {  // output rows 2m, 2m+1 from OB[ob]
-    if (!out_u8) return;
+    if (!FINAL || !out_u8) return;
     const int nw = (nb + 3) / 4;
     for (int k = t; k < 2 * nw; k += S3_T) {
       const int rr2 = k >= nw, d = k - rr2 * nw;
@@ -1896,7 +1899,39 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
             synth_bior<float>(cl, cd, ring[c][slot][2 * pb], ring[c][slot][2 * pb + 1]);
           }
       }
-      if (sidx >= 4 && cmp) {
+      if (!FINAL && sidx >= 4 && cmp) {  // reconstruction of the level below, fp32
+        const int m = r - 4;
+        const int x = x0 + 2 * np;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float v[2][2];  // [row][column]
+#pragma unroll
+          for (int col = 0; col < 2; ++col) {
+            float cl[5], cd[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+              cl[j] = ring[c][(rs + 5 - j) % 5][col];
+              cd[j] = ring[c][(rs + 5 - j) % 5][2 + col];
+            }
+            synth_bior<float>(cl, cd, v[0][col], v[1][col]);
+          }
+          float* out = reinterpret_cast<float*>(ws + img * img_floats + out_off +
+                                                (size_t)c * out_chan_stride);
+#pragma unroll
+          for (int rr2 = 0; rr2 < 2; ++rr2) {
+            const int y = 2 * m + rr2;
+            if (y >= Hout || x >= Wout) continue;
+            float* o = out + (size_t)y * Wout + x;
+            if (x + 1 < Wout && ((uintptr_t)o & 7) == 0) {
+              *reinterpret_cast<float2*>(o) = make_float2(v[rr2][0], v[rr2][1]);
+            } else {
+              o[0] = v[rr2][0];
+              if (x + 1 < Wout) o[1] = v[rr2][1];
+            }
+          }
+        }
+      }
+      if (FINAL && sidx >= 4 && cmp) {
         const int m = r - 4;  // output row pair 2m, 2m+1
         float Yv[3][2][2];    // [c][row][column], de-normalised
 #pragma unroll
@@ -1960,7 +1995,7 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
       }
     }
   }
-  if (R >= 5) {
+  if (FINAL && R >= 5) {
     __syncthreads();
     flush(r0 + R - 5, (R - 1) & 1);
   }
@@ -3335,6 +3370,10 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   const bool s32 = knob("IDN_WAVELET_S32", 1) != 0;
   // fp32 level 1 with all three channels per thread (wl_synth_final3)
   const bool s3 = knob("IDN_WAVELET_S3", 1) != 0;
+  // ... and at the deeper levels whose output is at least this wide (0: every level; measured
+  // 2.93 -> 2.85 ms per 256 images against wl_synth_stream<false, float> at levels >= 2, and no
+  // better with a width floor of 200 or 384: profiles/r03/wavelet/s3d_ab.txt)
+  const int s3d = knob("IDN_WAVELET_S3D", 0);
   auto str = [&](int l) { return (sstream & (l == 1 ? 1 : 2)) != 0; };
   auto fm_syn2 = [&](int l) { return fm_syn(l) | (l < Lt.L && str(l + 1) && s32 ? 0b0001 : 0); };
   if (sstream) {
@@ -3360,7 +3399,24 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
           n, (Hout + 1) / 2, strips,
           reinterpret_cast<const void*>(&wl_synth_stream<false, float>), SS_MAXT);
       const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n), blk(SS_MAXT);
-      if (l >= 2) {
+      const int fm2 = fm_syn2(l);
+      if (l >= 2 && s32 && s3 && Wout >= s3d && (fm2 == 0b1111 || fm2 == 0b1110)) {
+        const int strips3 = s3_strips(Wout), sw3 = s3_sw(Wout);
+        const int bands3 = ss_bands_occ(
+            n, (Hout + 1) / 2, strips3,
+            reinterpret_cast<const void*>(&wl_synth_final3<0b1111, false>), S3_T);
+        const dim3 grid3((unsigned)(strips3 * bands3), 1, (unsigned)n);
+        if (fm2 == 0b1111)
+          hipLaunchKernelGGL((wl_synth_final3<0b1111, false>), grid3, dim3(S3_T), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Hout,
+                             Wout, sw3, strips3, bands3, (uint8_t*)nullptr, row_stride,
+                             (float*)nullptr, l, Lt.off_band[l - 1], (size_t)4 * Hout * Wout);
+        else
+          hipLaunchKernelGGL((wl_synth_final3<0b1110, false>), grid3, dim3(S3_T), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Hout,
+                             Wout, sw3, strips3, bands3, (uint8_t*)nullptr, row_stride,
+                             (float*)nullptr, l, Lt.off_band[l - 1], (size_t)4 * Hout * Wout);
+      } else if (l >= 2) {
         if (s32)
           hipLaunchKernelGGL((wl_synth_stream<false, float>), grid, blk, 0, st, wsf, Lt.img_floats,
                              stats, l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1],

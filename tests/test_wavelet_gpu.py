@@ -275,6 +275,20 @@ def test_wavelet_bior15_final3_bitwise(dev, monkeypatch, shape):
     np.testing.assert_array_equal(fa, fb)
 
 
+@pytest.mark.parametrize("shape", [(600, 1000), (1201, 2003), (130, 77), (40, 1100)])
+def test_wavelet_bior15_final3_deeper_bitwise(dev, monkeypatch, shape):
+    """wl_synth_final3<FM, false> at the deeper levels (IDN_WAVELET_S3D = 0: every level >= 2;
+    product) against wl_synth_stream<false, float> (a width floor above every level): the same
+    fp32 operations per reconstructed sample, so bit-identical outputs (one and several strips,
+    odd sizes)"""
+    img = make_img(*shape, 43)
+    u8a, fa = _run_env(monkeypatch, img, {"IDN_WAVELET_S3D": "0"})
+    u8b, fb = _run_env(monkeypatch, img, {"IDN_WAVELET_S3D": str(1 << 30)})
+    print(f"final3 deeper vs stream: {int((fa != fb).sum())} float outputs differ")
+    np.testing.assert_array_equal(u8a, u8b)
+    np.testing.assert_array_equal(fa, fb)
+
+
 def _bior_stats(monkeypatch, img, env):
     """bior1.5 through the tuning build under env: (u8, f32, stats block of the image)"""
     import torch
