@@ -265,7 +265,7 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre_kernel(const uin
 // which is what sank the first two-column attempt).  The colour table is built straight into the
 // per-r^2 products (color_weight is never stored): 30 KB of tables per workgroup.
 constexpr int BL2_TW = 128;
-template <int R>
+template <int R, bool SYM = true>
 __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int h, int w, int64_t row_stride,
     int tiles_x, int tiles_y, int ntiles, BilateralTaps taps) {
@@ -339,6 +339,12 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
     for (int o = 0; o < RPT; ++o)
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) acc_bg[o][cc] = acc_rw[o][cc] = f32x2{0.f, 0.f};
+    // weights shared by two of the thread's own outputs (w(A, B) = w(B, A): same r^2, same SAD),
+    // looked up at the first of the two visits in the walk order and kept in a register for the
+    // second; the centre tap's weight is the constant wt[slot(0)][0].  Each output's sum keeps
+    // its order, so the results are unchanged bit for bit.
+    const float w00 = wt[RS.slot[0] * BL_LUT];
+    float wsh[RPT * 2][RPT * 2];
 #pragma unroll
     for (int dy = -R; dy < RPT + R; ++dy) {
 #pragma unroll
@@ -361,8 +367,20 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
           for (int cc = 0; cc < 2; ++cc) {
             const int i = dy - o, j = rel - cc - R;
             if (i < -R || i > R || j < -R || j > R || i * i + j * j > R * R) continue;
-            const uint32_t dist = __builtin_amdgcn_sad_u8(p, p0[o][cc], 0u);
-            const float wv = wt[RS.slot[i * i + j * j] * BL_LUT + dist];
+            // walk positions of the tap (meaningful when it is one of the thread's own outputs)
+            // and of the output
+            const bool own = dy >= 0 && dy < RPT && rel - R >= 0 && rel - R < 2;
+            const int kx = dy * 2 + (rel - R), ky = o * 2 + cc;
+            float wv;
+            if (SYM && own && kx == ky) {
+              wv = w00;
+            } else if (SYM && own && kx > ky) {
+              wv = wsh[ky][kx];  // looked up when the walk passed the output's own position
+            } else {
+              const uint32_t dist = __builtin_amdgcn_sad_u8(p, p0[o][cc], 0u);
+              wv = wt[RS.slot[i * i + j * j] * BL_LUT + dist];
+              if (SYM && own) wsh[kx][ky] = wv;
+            }
             const f32x2 w2 = {wv, wv};
             acc_bg[o][cc] = __builtin_elementwise_fma(bg, w2, acc_bg[o][cc]);
             acc_rw[o][cc] = __builtin_elementwise_fma(r1, w2, acc_rw[o][cc]);
@@ -414,8 +432,12 @@ static void launch_bl_pre2(const uint8_t* src, uint8_t* dst, int n, int h, int w
   const int64_t ntiles = (int64_t)n * tiles_x * tiles_y;
   const int64_t res = (int64_t)cu_count() * knob("IDN_BL2_WG", 2);  // resident workgroups per CU
   const int64_t grid = ntiles < res ? ntiles : res;
-  hipLaunchKernelGGL((bilateral_u8_pre2_kernel<R>), dim3((unsigned)grid), dim3(64 * BLP_NW), 0, st,
-                     src, dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
+  if (knob("IDN_BL2_SYM", 1))
+    hipLaunchKernelGGL((bilateral_u8_pre2_kernel<R, true>), dim3((unsigned)grid), dim3(64 * BLP_NW),
+                       0, st, src, dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
+  else
+    hipLaunchKernelGGL((bilateral_u8_pre2_kernel<R, false>), dim3((unsigned)grid), dim3(64 * BLP_NW),
+                       0, st, src, dst, h, w, rs, tiles_x, tiles_y, (int)ntiles, taps);
 }
 
 template <int R, int RPT>

@@ -49,6 +49,12 @@ def _flags() -> list[str]:
     ]
 
 
+# per-source flags: the two-column bilateral walk (bilateral_u8_pre2_kernel) is one fully unrolled
+# loop nest whose pre-unroll body exceeds LLVM's default pragma-unroll size limit; left rolled, its
+# shared-weight registers would go to scratch
+_EXTRA = {"bilateral_u8.hip": ["-mllvm", "-pragma-unroll-threshold=131072"]}
+
+
 def _compile_one(src: Path, tuning: bool = False) -> Path:
     odir = TUNING_OBJ_DIR if tuning else OBJ_DIR
     odir.mkdir(parents=True, exist_ok=True)
@@ -56,8 +62,8 @@ def _compile_one(src: Path, tuning: bool = False) -> Path:
     deps = [src] + sorted(CSRC.glob("*.hpp")) + [PKG_DIR.parent.parent / "include" / "idn.h"]
     if obj.exists() and obj.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
         return obj
-    cmd = [_hipcc(), *_flags(), *(["-DIDN_TUNING_BUILD"] if tuning else []), "-c", str(src),
-           "-o", str(obj)]
+    cmd = [_hipcc(), *_flags(), *_EXTRA.get(src.name, []),
+           *(["-DIDN_TUNING_BUILD"] if tuning else []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")

@@ -226,6 +226,23 @@ def test_bilateral_within_1lsb(dev, shape, case):
     assert (diff > 0).mean() < 1e-3
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 300), (1, 37, 53), (1, 600, 1000), (2, 7, 2)])
+@pytest.mark.parametrize("case", BILATERAL_CASES)
+def test_bilateral_shared_weights_bitwise(dev, monkeypatch, shape, case):
+    """the two-column kernel's shared own-output weights and constant centre weight (product)
+    against looking every tap up (IDN_BL2_SYM=0, tuning build): each output's fp32 sum keeps its
+    order, so the bytes are identical"""
+    import idn
+    from idn import _lib
+    d, sc, ss = case
+    img = textured(*shape, seed=d + 7)
+    got = _run(idn.bilateral_filter, img, d, sc, ss)
+    monkeypatch.setenv("IDN_BL2_SYM", "0")
+    with _lib.variant("tuning"):
+        ref = _run(idn.bilateral_filter, img, d, sc, ss)
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_bilateral_gray(dev):
     import idn
     import oracle

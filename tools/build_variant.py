@@ -21,7 +21,7 @@ def main():
 
     def one(src):
         obj = odir / (src.stem + ".o")
-        r = subprocess.run([_build._hipcc(), *_build._flags(), *extra, "-c", str(src), "-o", str(obj)],
+        r = subprocess.run([_build._hipcc(), *_build._flags(), *_build._EXTRA.get(src.name, []), *extra, "-c", str(src), "-o", str(obj)],
                            capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError(r.stderr)
