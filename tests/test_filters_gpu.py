@@ -4,6 +4,8 @@ Integer filters must be bit-exact.  Shapes cover the fast path's segment tails (
 % 16 == 0 and == 8), multi-segment rows, the 600x1000 BASELINE shape, tiny images (vertical
 reflection of h < ksize) and shapes only the generic path accepts (W*C % 8 != 0).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -241,6 +243,16 @@ def test_bilateral_shared_weights_bitwise(dev, monkeypatch, shape, case):
     with _lib.variant("tuning"):
         ref = _run(idn.bilateral_filter, img, d, sc, ss)
     np.testing.assert_array_equal(got, ref)
+
+
+def test_bilateral_recip_exact(dev):
+    """the two-column kernel's 1 / wsum (v_rcp_f32 + one Newton step) equals the IEEE quotient
+    for every float in [1, 128), the range of its weight sums"""
+    import torch
+    from idn import _lib
+    lib = _lib.load()
+    bad = lib.idn_internal_bl_recip_check(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert bad == 0
 
 
 def test_bilateral_gray(dev):
