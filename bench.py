@@ -171,6 +171,23 @@ def _gauss5_blob(idn, x, y):
 OPS["gauss5_blob"] = (OPS["gauss5_blob"][0], _gauss5_blob, 15, "stencil_u8")
 
 
+def _wavelet_bior15_f64(idn, x, y):
+    """the live test path's denoiser input: random_noise's float64 image (lib/model/test.py:1678-1684
+    -> 1807-1810); the f64 copy (img_as_float of the batch) is made once, untimed"""
+    st = _wavelet_bior15_f64.__dict__
+    f = st.get("f64")
+    if f is None or f.shape != x.shape:
+        f = st["f64"] = x.double() * (1.0 / 255.0)
+    idn.ops.denoise_wavelet(f, "bior1.5", None, out_u8=y)
+
+
+# 24 B of float64 read + 3 B written per pixel
+OPS["wavelet_bior15_f64"] = ("bior1.5 wavelet on float64 input (live test path)", _wavelet_bior15_f64,
+                             27, "wl_")
+DTYPE["wavelet_bior15_f64"] = DTYPE["wavelet_bior15"]
+PARITY["wavelet_bior15_f64"] = PARITY["wavelet_bior15"]
+
+
 def _jpeg_files(x, quality=90):
     """the batch encoded once (untimed) by Pillow: baseline 4:2:0 JPEG files in host memory"""
     import io
@@ -267,6 +284,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
             255 * oracle.sk.noise_gaussian(a[0], np.random.normal(0.0, 1.0, a[0].shape))), "db1", 3)),
         "wavelet_bior15": lambda a: oracle.sk.to_u8(
             255 * oracle.wavelet.denoise_wavelet(a[0], "bior1.5", None)),
+        "wavelet_bior15_f64": lambda a: oracle.sk.to_u8(
+            255 * oracle.wavelet.denoise_wavelet(a[0] * (1.0 / 255.0), "bior1.5", None)),
         "gauss5_blob": lambda a: oracle.sk.blob_f32(oracle.cv.gaussian_blur_fast(a, 5)),
         # the per-image body on the host: decode, f64 gaussian noise, bior1.5 wavelet, blob
         "detect_e2e": lambda a: oracle.sk.blob_f32([oracle.wavelet.denoise_wavelet(
@@ -302,7 +321,7 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         if el >= budget_s or n_img >= 1000000:
             break
     if op in ("noise_gaussian", "noise_sap", "noise_poisson", "wavelet_haar3", "cfg5",
-              "wavelet_bior15", "detect_e2e"):
+              "wavelet_bior15", "wavelet_bior15_f64", "detect_e2e"):
         threads, src = 1, "numpy, single thread"
     elif op == "jpeg_decode":
         threads, src = 1, "PIL (libjpeg-turbo) decode, single thread"

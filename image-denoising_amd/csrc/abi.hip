@@ -17,6 +17,8 @@ int set_error(int status, const char* fmt, ...) {
 
 }  // namespace idn
 
-extern "C" const char* idn_version(void) { return "idn 0.1.0 gfx950"; }
+extern "C" int idn_abi_version(void) { return IDN_ABI_VERSION; }
+
+extern "C" const char* idn_version(void) { return "idn 0.4.0 gfx950"; }
 
 extern "C" const char* idn_last_error(void) { return idn::g_err; }

@@ -22,9 +22,11 @@
 //                        16x16 / 16x8 for libjpeg 9's scaled chroma) into u8 component planes
 //   3 jpeg_color8_kernel 8 output pixels per thread: chroma upsampling (turbo only) + YCbCr -> BGR
 //                        (or gray -> BGR), written into the caller's NHWC batch
-// Supported: 8-bit baseline sequential (SOF0/SOF1) Huffman, one interleaved scan, 1 or 3
-// components, sampling 4:4:4 / 4:2:2 (h2v1) / 4:2:0 (h2v2), optional restart intervals.  Anything
-// else (progressive, arithmetic, 12-bit, CMYK, multi-scan) is IDN_EUNSUPPORTED.
+// Supported: 8-bit Huffman JPEG, 1 or 3 components, sampling 4:4:4 / 4:2:2 (h2v1) / 4:2:0 (h2v2),
+// optional restart intervals: baseline / extended sequential (SOF0 / SOF1) with one interleaved
+// scan (the parallel path above), and progressive (SOF2) or multi-scan sequential files (the scan
+// path: jpeg_prog_kernel, one wave per image, scans in file order, restart intervals across the
+// lanes).  Anything else (arithmetic, lossless, 12-bit, CMYK) is IDN_EUNSUPPORTED.
 #include "idn_common.hpp"
 
 #include <string.h>
@@ -59,12 +61,31 @@ struct JpegDev {
   uint32_t chunk_bits;
   int bpm;                  // blocks per MCU (1 for a single-component scan)
   uint32_t total_blocks;    // MCUs x bpm
+  int wib[3], hib[3];       // blocks with data per component row / column (jdinput.c
+                            // width_in_blocks): what a non-interleaved scan codes
+  uint32_t scan0, nscan;    // scan path: the image's scans in the batch scan table (0: none)
   uint8_t ph_comp[10], ph_dv[10], ph_dh[10];  // block of the MCU -> component, block row, column
   uint16_t q[4][64];        // quantisation tables, natural order
   uint16_t lut[4][1 << JPG_LUTB];  // [DC0, DC1, AC0, AC1]: len << 8 | symbol, 0 = longer code
   int32_t maxcode[4][18];   // libjpeg jdhuff: largest code of each length (-1: none), [17] sentinel
   int32_t valoff[4][18];    // huffval index of the first code of each length, minus that code
   uint8_t huffval[4][256];
+};
+
+// one scan of the scan path (progressive / multi-scan files).  Table slots: k = the DC table of
+// scan component k, 3 + k = its AC table (only the slots the scan's kind reads are filled).
+enum { JPG_SEQ = 0, JPG_DC_FIRST = 1, JPG_DC_REFINE = 2, JPG_AC_FIRST = 3, JPG_AC_REFINE = 4 };
+struct JpegScanDev {
+  uint64_t scan_off;        // entropy-coded bytes in the batch buffer (unstuffed like JpegDev's)
+  uint32_t scan_len;
+  uint64_t ub_off;
+  uint32_t iv_off;
+  int nintervals;
+  int img, ns, comp[3], Ss, Se, Ah, Al, restart, kind;
+  uint32_t nunits;          // MCUs (interleaved) or the component's blocks (non-interleaved)
+  uint16_t lut[6][1 << JPG_LUTB];
+  int32_t maxcode[6][18], valoff[6][18];
+  uint8_t huffval[6][256];
 };
 
 // jpeg_natural_order: zigzag index -> natural (row-major) index
@@ -84,6 +105,13 @@ struct HuffSpec {
   uint8_t bits[17] = {};
   uint8_t val[256] = {};
 };
+// one scan of a progressive / multi-scan file: its components (frame indices), their tables as
+// defined when the scan starts, spectral band and successive-approximation bits, restart interval
+struct ScanHost {
+  int ns = 0, comp[3] = {}, Ss = 0, Se = 63, Ah = 0, Al = 0, restart = 0;
+  HuffSpec dc[3], ac[3];  // per scan component
+  size_t begin = 0, end = 0;
+};
 struct JpegHost {
   int width = 0, height = 0, ncomp = 0, restart = 0;
   int cid[3] = {}, ch[3] = {}, cv[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
@@ -92,11 +120,51 @@ struct JpegHost {
   HuffSpec dc[4], ac[4];
   size_t scan_begin = 0, scan_end = 0;
   bool adobe_rgb = false;
+  bool progressive = false;
+  std::vector<ScanHost> scans;  // the scan path (progressive or multi-scan); empty: one scan
 };
+
+// end of the entropy-coded segment starting at p[i]: the first marker that is not RSTn (stuffed
+// 0xFF00 and fill bytes skipped)
+static size_t jpg_segment_end(const uint8_t* p, size_t n, size_t i) {
+  while (i + 1 < n) {
+    if (p[i] != 0xFF) {
+      ++i;
+      continue;
+    }
+    const uint8_t nb = p[i + 1];
+    if (nb == 0x00 || (nb >= 0xD0 && nb <= 0xD7)) i += 2;
+    else if (nb == 0xFF) i += 1;
+    else return i;
+  }
+  return n;
+}
 
 static int jpg_fail(std::string* err, const char* msg) {
   if (err) *err = msg;
   return IDN_EUNSUPPORTED;
+}
+
+// the end of a scan-path file (EOI or end of data): at least one scan; a progressive file whose
+// last scans leave AC coefficients 1..5 of a component imprecise would be block-smoothed by
+// libjpeg (jdcoefct.c smoothing_ok): not restated, rejected
+static int jpg_scans_done(const JpegHost& J, std::string* err) {
+  if (J.scans.empty()) return jpg_fail(err, "no SOS");
+  if (J.progressive) {
+    int bits[3][6];
+    for (auto& b : bits)
+      for (int& v : b) v = -1;
+    for (const ScanHost& S : J.scans)
+      for (int k = 0; k < S.ns; ++k)
+        for (int z = S.Ss; z <= std::min(S.Se, 5); ++z) bits[S.comp[k]][z] = S.Al;
+    for (int c = 0; c < J.ncomp; ++c) {
+      if (bits[c][0] < 0) continue;
+      for (int z = 1; z <= 5; ++z)
+        if (bits[c][z] != 0)
+          return jpg_fail(err, "progressive file leaves AC 1..5 imprecise (libjpeg block smoothing)");
+    }
+  }
+  return IDN_OK;
 }
 
 static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err) {
@@ -112,15 +180,18 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
     }
     i += 2;
     if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;  // no length
-    if (m == 0xD9) return jpg_fail(err, "EOI before SOS");
+    if (m == 0xD9) return jpg_scans_done(J, err);
     const size_t len = ((size_t)p[i] << 8) | p[i + 1];
     if (len < 2 || i + len > n) return jpg_fail(err, "truncated segment");
     const uint8_t* s = p + i + 2;
     const size_t sl = len - 2;
     switch (m) {
       case 0xC0:
-      case 0xC1: {  // SOF0 / SOF1: baseline / extended sequential Huffman
-        if (sl < 6 || s[0] != 8) return jpg_fail(err, "only 8-bit sequential JPEG");
+      case 0xC1:
+      case 0xC2: {  // SOF0 / SOF1 / SOF2: baseline / extended sequential / progressive Huffman
+        if (sof) return jpg_fail(err, "second frame header");
+        if (sl < 6 || s[0] != 8) return jpg_fail(err, "only 8-bit JPEG");
+        J.progressive = m == 0xC2;
         J.height = (s[1] << 8) | s[2];
         J.width = (s[3] << 8) | s[4];
         J.ncomp = s[5];
@@ -137,9 +208,9 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         sof = true;
         break;
       }
-      case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB:
+      case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB:
       case 0xCD: case 0xCE: case 0xCF:
-        return jpg_fail(err, "progressive / lossless / arithmetic JPEG not supported");
+        return jpg_fail(err, "lossless / hierarchical / arithmetic JPEG not supported");
       case 0xC4: {  // DHT
         size_t k = 0;
         while (k < sl) {
@@ -185,26 +256,7 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         if (!sof) return jpg_fail(err, "SOS before SOF");
         if (sl < 1) return jpg_fail(err, "bad SOS");
         const int ns = s[0];
-        if (ns != J.ncomp) return jpg_fail(err, "multi-scan (non-interleaved) JPEG not supported");
-        if (sl < 1 + 2 * (size_t)ns + 3) return jpg_fail(err, "bad SOS");
-        for (int k = 0; k < ns; ++k) {
-          int c = 0;
-          while (c < J.ncomp && J.cid[c] != s[1 + 2 * k]) ++c;
-          if (c != k) return jpg_fail(err, "scan component order differs from the frame");
-          J.td[c] = s[2 + 2 * k] >> 4;
-          J.ta[c] = s[2 + 2 * k] & 15;
-          if (J.td[c] > 3 || J.ta[c] > 3) return jpg_fail(err, "bad SOS table");
-        }
-        const uint8_t* ss = s + 1 + 2 * ns;
-        if (ss[0] != 0 || ss[1] != 63 || ss[2] != 0) return jpg_fail(err, "not a sequential scan");
-        J.scan_begin = i + len;
-        // entropy-coded segment: up to the EOI (scanning back from the end) or the end of data
-        size_t e = n;
-        while (e >= J.scan_begin + 2 && !(p[e - 2] == 0xFF && p[e - 1] == 0xD9)) --e;
-        J.scan_end = (e >= J.scan_begin + 2) ? e - 2 : n;
-        for (int c = 0; c < J.ncomp; ++c)
-          if (!J.qpresent[J.tq[c]] || !J.dc[J.td[c]].present || !J.ac[J.ta[c]].present)
-            return jpg_fail(err, "missing quantisation / Huffman table");
+        if (ns < 1 || ns > J.ncomp || sl < 1 + 2 * (size_t)ns + 3) return jpg_fail(err, "bad SOS");
         if (J.adobe_rgb) return jpg_fail(err, "Adobe RGB / CMYK JPEG not supported");
         if (J.ncomp == 3) {
           const bool s444 = J.ch[0] == 1 && J.cv[0] == 1;
@@ -213,7 +265,60 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
           if (!(s444 || s422 || s420) || J.ch[1] != 1 || J.cv[1] != 1 || J.ch[2] != 1 || J.cv[2] != 1)
             return jpg_fail(err, "chroma sampling other than 4:4:4 / 4:2:2 / 4:2:0");
         }
-        return IDN_OK;
+        ScanHost S;
+        S.ns = ns;
+        S.restart = J.restart;
+        for (int k = 0; k < ns; ++k) {
+          int c = 0;
+          while (c < J.ncomp && J.cid[c] != s[1 + 2 * k]) ++c;
+          if (c == J.ncomp) return jpg_fail(err, "scan names an unknown component");
+          if (k > 0 && c <= S.comp[k - 1]) return jpg_fail(err, "scan component order differs from the frame");
+          S.comp[k] = c;
+          const int td = s[2 + 2 * k] >> 4, ta = s[2 + 2 * k] & 15;
+          if (td > 3 || ta > 3) return jpg_fail(err, "bad SOS table");
+          J.td[c] = td;
+          J.ta[c] = ta;
+          S.dc[k] = J.dc[td];
+          S.ac[k] = J.ac[ta];
+        }
+        const uint8_t* ss = s + 1 + 2 * ns;
+        S.Ss = ss[0];
+        S.Se = ss[1];
+        S.Ah = ss[2] >> 4;
+        S.Al = ss[2] & 15;
+        if (J.progressive) {  // jdinput.c / jdhuff.c start_pass_huff_decoder checks
+          const bool dc = S.Ss == 0;
+          if ((dc && S.Se != 0) || (!dc && (S.Se < S.Ss || S.Se > 63 || ns != 1)) || S.Ah > 13 ||
+              S.Al > 13 || (S.Ah != 0 && S.Al != S.Ah - 1))
+            return jpg_fail(err, "bad progressive scan parameters");
+        } else if (S.Ss != 0 || S.Se != 63 || ss[2] != 0) {
+          return jpg_fail(err, "not a sequential scan");
+        }
+        for (int k = 0; k < ns; ++k) {
+          const int c = S.comp[k];
+          if (!J.qpresent[J.tq[c]]) return jpg_fail(err, "missing quantisation table");
+          const bool need_dc = S.Ss == 0 && S.Ah == 0, need_ac = S.Se > 0 && !(J.progressive && S.Ah);
+          const bool need_ac_ref = J.progressive && S.Ss > 0 && S.Ah;
+          if ((need_dc && !S.dc[k].present) || ((need_ac || need_ac_ref) && !S.ac[k].present))
+            return jpg_fail(err, "missing Huffman table");
+        }
+        S.begin = i + len;
+        if (!J.progressive && J.scans.empty() && ns == J.ncomp) {
+          // one interleaved sequential scan: the parallel path.  Its segment runs up to the EOI
+          // (scanning back from the end) or the end of data
+          for (int c = 0; c < J.ncomp; ++c)
+            if (J.td[c] > 1 || J.ta[c] > 1) return jpg_fail(err, "Huffman table id > 1");
+          J.scan_begin = S.begin;
+          size_t e = n;
+          while (e >= J.scan_begin + 2 && !(p[e - 2] == 0xFF && p[e - 1] == 0xD9)) --e;
+          J.scan_end = (e >= J.scan_begin + 2) ? e - 2 : n;
+          return IDN_OK;
+        }
+        S.end = jpg_segment_end(p, n, S.begin);
+        J.scans.push_back(S);
+        if (J.scans.size() > 64) return jpg_fail(err, "too many scans");
+        i = S.end;
+        continue;  // the next marker
       }
       default:
         if (m < 0xC0) return jpg_fail(err, "corrupt marker");
@@ -221,7 +326,7 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
     }
     i += len;
   }
-  return jpg_fail(err, "no SOS");
+  return jpg_scans_done(J, err);
 }
 
 // jdhuff.c jpeg_make_d_derived_tbl: canonical codes -> fast lookup + maxcode / valoffset
@@ -343,8 +448,16 @@ struct JpegLds {
   uint8_t huffval[4][256];
 };
 
+// the scan path's tables (JpegScanDev slots)
+struct JpegLds6 {
+  uint16_t lut[6][1 << JPG_LUTB];
+  int32_t maxcode[6][18], valoff[6][18];
+  uint8_t huffval[6][256];
+};
+
 // one Huffman symbol (nb >= 32 on entry); returns the symbol and its code length in *len
-__device__ __forceinline__ int jpg_decode(const BitStream& br, const JpegLds& T, int t, int* len) {
+template <typename TT>
+__device__ __forceinline__ int jpg_decode(const BitStream& br, const TT& T, int t, int* len) {
   const uint32_t e = T.lut[t][br.acc >> (64 - JPG_LUTB)];
   if (e) {
     *len = (int)(e >> 8);
@@ -516,13 +629,15 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
 }
 
 // stage 1: unstuff (one 1024-thread workgroup per image, 16-byte tiles per thread)
-__global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const JpegDev* __restrict__ imgs,
+// (one workgroup per JpegDev, or per JpegScanDev of the scan path: the same fields)
+template <typename DESC>
+__global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const DESC* __restrict__ imgs,
                                                             const uint8_t* __restrict__ scans,
                                                             uint8_t* __restrict__ ub,
                                                             uint32_t* __restrict__ ivstart,
                                                             uint32_t* __restrict__ ublen) {
   __shared__ uint32_t wsum[16], carry_s, rst_s;
-  const JpegDev& D = imgs[blockIdx.x];
+  const DESC& D = imgs[blockIdx.x];
   const uint8_t* in = scans + D.scan_off;
   uint8_t* out = ub + D.ub_off;
   const uint32_t n = D.scan_len;
@@ -752,6 +867,175 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
   ChunkOut dummy{0u, {0, 0, 0}};
   const JpgConst K = jpg_const(D);
   jpg_run<true>(K, T, ub + D.ub_off, st, b1, &dummy, blk, pred, coef, dc_limit);
+}
+
+// ---- device: the scan path (progressive / multi-scan files) --------------------------------------
+// jdhuff.c's decode_mcu (sequential), decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine
+// (progressive: spectral selection, successive approximation, EOB runs), restated.  One wave per
+// image walks the image's scans in file order (a refinement scan reads what the earlier scans
+// left in the coefficient blocks); within a scan the lanes take the restart intervals (without
+// restart markers lane 0 decodes the scan).  Throughput is not the goal of this path: it makes
+// cv2.imread's progressive files decodable bit-exactly (the parallel path is the baseline one).
+__device__ __forceinline__ void jpg_load_scan_tables(JpegLds6& T, const JpegScanDev& S) {
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&S.lut[0][0]);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&T.lut[0][0]);
+  for (int k = threadIdx.x; k < (int)(sizeof(T.lut) / 4); k += blockDim.x) d[k] = s[k];
+  for (int k = threadIdx.x; k < 6 * 18; k += blockDim.x) {
+    (&T.maxcode[0][0])[k] = (&S.maxcode[0][0])[k];
+    (&T.valoff[0][0])[k] = (&S.valoff[0][0])[k];
+  }
+  for (int k = threadIdx.x; k < 6 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&S.huffval[0][0])[k];
+}
+
+__device__ __forceinline__ uint32_t jpg_get(BitStream& br, int s) {  // s <= 16
+  br.refill();
+  return br.bits(s);
+}
+__device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLds6& T, int t) {
+  br.refill();
+  int len;
+  const int sym = jpg_decode(br, T, t, &len);
+  br.bits(len);
+  return sym;
+}
+__device__ __forceinline__ int16_t jpg_lshift(int v, int al) { return (int16_t)(int)((uint32_t)v << al); }
+
+// one block of scan component k (slot k: DC table, 3 + k: AC table); eobrun / pred per interval
+__device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLds6& T, const JpegScanDev& S,
+                                               int k, int16_t* __restrict__ blk, int& pred,
+                                               uint32_t& eobrun) {
+  switch (S.kind) {
+    case JPG_SEQ: {
+      const int s = jpg_huff(br, T, k);
+      pred += s ? jpg_extend(jpg_get(br, s), s) : 0;
+      blk[0] = (int16_t)pred;
+      for (int z = 1; z < 64;) {
+        const int rs = jpg_huff(br, T, 3 + k);
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz) {
+          z += r;
+          blk[jpg_natural[min(z, 79)]] = (int16_t)jpg_extend(jpg_get(br, sz), sz);
+          ++z;
+        } else if (r == 15) {
+          z += 16;
+        } else {
+          break;
+        }
+      }
+      break;
+    }
+    case JPG_DC_FIRST: {
+      const int s = jpg_huff(br, T, k);
+      pred += s ? jpg_extend(jpg_get(br, s), s) : 0;
+      blk[0] = jpg_lshift(pred, S.Al);
+      break;
+    }
+    case JPG_DC_REFINE:
+      if (jpg_get(br, 1)) blk[0] = (int16_t)(blk[0] | (1 << S.Al));
+      break;
+    case JPG_AC_FIRST: {
+      if (eobrun) {
+        --eobrun;
+        break;
+      }
+      for (int z = S.Ss; z <= S.Se; ++z) {
+        const int rs = jpg_huff(br, T, 3);
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz) {
+          z += r;
+          blk[jpg_natural[min(z, 79)]] = jpg_lshift(jpg_extend(jpg_get(br, sz), sz), S.Al);
+        } else if (r != 15) {
+          eobrun = 1u << r;
+          if (r) eobrun += jpg_get(br, r);
+          --eobrun;
+          break;
+        } else {
+          z += 15;
+        }
+      }
+      break;
+    }
+    default: {  // JPG_AC_REFINE
+      const int p1 = 1 << S.Al, m1 = -(1 << S.Al);
+      int z = S.Ss;
+      if (eobrun == 0) {
+        for (; z <= S.Se; ++z) {
+          const int rs = jpg_huff(br, T, 3);
+          int r = rs >> 4, sz = rs & 15;
+          if (sz) {
+            sz = jpg_get(br, 1) ? p1 : m1;
+          } else if (r != 15) {
+            eobrun = 1u << r;
+            if (r) eobrun += jpg_get(br, r);
+            break;
+          }
+          do {  // refine the nonzero coefficients up to the target zero (r zeros skipped)
+            int16_t* c = blk + jpg_natural[min(z, 79)];
+            if (*c != 0) {
+              if (jpg_get(br, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+            } else if (--r < 0) {
+              break;
+            }
+            ++z;
+          } while (z <= S.Se);
+          if (sz) blk[jpg_natural[min(z, 79)]] = (int16_t)sz;
+        }
+      }
+      if (eobrun > 0) {  // the band of this block is in an EOB run: refine its nonzeros
+        for (; z <= S.Se; ++z) {
+          int16_t* c = blk + jpg_natural[min(z, 79)];
+          if (*c != 0 && jpg_get(br, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+        }
+        --eobrun;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict__ imgs,
+                                                       const JpegScanDev* __restrict__ scans,
+                                                       const uint8_t* __restrict__ ub,
+                                                       const uint32_t* __restrict__ ivstart,
+                                                       int16_t* __restrict__ coef) {
+  __shared__ JpegLds6 T;
+  const JpegDev& D = imgs[blockIdx.x];
+  const uint32_t nscan = D.nscan;
+  if (nscan == 0) return;  // uniform: a parallel-path image
+  for (uint32_t si = 0; si < nscan; ++si) {
+    const JpegScanDev& S = scans[D.scan0 + si];
+    // the previous scan's coefficient stores visible to every lane, its table reads done
+    __threadfence();
+    __syncthreads();
+    jpg_load_scan_tables(T, S);
+    __syncthreads();
+    for (int t = threadIdx.x; t < S.nintervals; t += 64) {
+      const uint32_t u0 = S.restart ? (uint32_t)t * (uint32_t)S.restart : 0u;
+      const uint32_t u1 = S.restart ? min(u0 + (uint32_t)S.restart, S.nunits) : S.nunits;
+      BitStream br;
+      br.start(ub + S.ub_off, ivstart[S.iv_off + t]);
+      int pred[3] = {0, 0, 0};
+      uint32_t eobrun = 0;
+      for (uint32_t u = u0; u < u1; ++u) {
+        if (S.ns == 1) {  // non-interleaved: the component's own blocks, raster order
+          const int c = S.comp[0];
+          const uint32_t by = u / (uint32_t)D.wib[c], bx = u - by * (uint32_t)D.wib[c];
+          int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
+          jpg_scan_block(br, T, S, 0, blk, pred[0], eobrun);
+        } else {  // interleaved MCU (sequential, or a progressive DC scan)
+          const uint32_t my = u / (uint32_t)D.mcux, mx = u - my * (uint32_t)D.mcux;
+          for (int k = 0; k < S.ns; ++k) {
+            const int c = S.comp[k];
+            for (int dv = 0; dv < D.cv[c]; ++dv)
+              for (int dh = 0; dh < D.ch[c]; ++dh) {
+                const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
+                int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
+                jpg_scan_block(br, T, S, k, blk, pred[k], eobrun);
+              }
+          }
+        }
+      }
+    }
+  }
 }
 
 // ---- device: ISLOW IDCT (jidctint.c) ------------------------------------------------------------
@@ -1089,13 +1373,15 @@ struct JpegPlan {
   std::vector<JpegDev> dev;
   std::vector<uint64_t> blk_end;
   std::vector<size_t> scan_begin;
+  std::vector<JpegScanDev> scans;   // the scan path's scans, image by image
+  std::vector<size_t> scan_src;     // their first byte in the file
   uint64_t scan_bytes = 0, nblk = 0, plane_bytes = 0, ub_bytes = 0;
   uint32_t nintervals = 0, nchunks = 0, max_items = 1;
   bool any_chunked = false;
   bool scales[2][2] = {};  // IDCT output scales present: [sv - 1][sh - 1]
-  size_t off_imgs = 0, off_blkend = 0, off_scan = 0, off_coef = 0, off_planes = 0;
-  size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_s0 = 0, off_s1 = 0, off_cnt = 0,
-         off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, total = 0;
+  size_t off_imgs = 0, off_blkend = 0, off_scans = 0, off_scan = 0, off_coef = 0, off_planes = 0;
+  size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_ublen_s = 0, off_s0 = 0, off_s1 = 0,
+         off_cnt = 0, off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, total = 0;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1195,7 +1481,76 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
           ++D.bpm;
         }
     D.total_blocks = (uint32_t)mcus * D.bpm;
+    for (int c = 0; c < J.ncomp; ++c) {  // jdinput.c: ceil(ceil(size * samp / max samp) / 8)
+      const int cw = (J.width * D.ch[c] + D.hmax - 1) / D.hmax;
+      const int chh = (J.height * D.cv[c] + D.vmax - 1) / D.vmax;
+      D.wib[c] = (cw + 7) / 8;
+      D.hib[c] = (chh + 7) / 8;
+    }
     for (int t = 0; t < 4; ++t) memcpy(D.q[t], J.q[t], sizeof(D.q[t]));
+    if (!J.scans.empty()) {  // the scan path: one descriptor per scan, its bytes in this image's
+                             // stretch of the batch scan buffer; the parallel path sees no data
+      D.scan_off = P.scan_bytes;
+      D.scan_len = 0;
+      P.scan_begin[i] = 0;
+      D.ub_off = P.ub_bytes;
+      P.ub_bytes += 64;
+      D.iv_off = P.nintervals;
+      D.nintervals = 1;
+      P.nintervals += 1;
+      D.restart = 0;
+      D.ch_off = P.nchunks;
+      D.chunk_bits = chunk_bits;
+      D.nchunks = 0;
+      D.scan0 = (uint32_t)P.scans.size();
+      D.nscan = (uint32_t)J.scans.size();
+      for (const ScanHost& S : J.scans) {
+        JpegScanDev SD;
+        memset(&SD, 0, sizeof(SD));
+        SD.img = i;
+        SD.ns = S.ns;
+        for (int k = 0; k < S.ns; ++k) SD.comp[k] = S.comp[k];
+        SD.Ss = S.Ss;
+        SD.Se = S.Se;
+        SD.Ah = S.Ah;
+        SD.Al = S.Al;
+        SD.restart = S.restart;
+        SD.kind = !J.progressive ? JPG_SEQ
+                  : S.Ss == 0     ? (S.Ah ? JPG_DC_REFINE : JPG_DC_FIRST)
+                                  : (S.Ah ? JPG_AC_REFINE : JPG_AC_FIRST);
+        SD.nunits = S.ns == 1 ? (uint32_t)D.wib[S.comp[0]] * (uint32_t)D.hib[S.comp[0]]
+                              : (uint32_t)mcus;
+        SD.nintervals = S.restart ? (int)((SD.nunits + S.restart - 1) / S.restart) : 1;
+        if (SD.nintervals < 1) SD.nintervals = 1;
+        for (int sl = 0; sl < 6; ++sl)
+          for (int k = 0; k < 18; ++k) SD.maxcode[sl][k] = -1;
+        for (int k = 0; k < S.ns && tables; ++k) {
+          const bool dc = SD.kind == JPG_SEQ || SD.kind == JPG_DC_FIRST;
+          const bool ac = SD.kind == JPG_SEQ || SD.kind == JPG_AC_FIRST || SD.kind == JPG_AC_REFINE;
+          if (dc) {
+            rc = jpeg_build_huff(S.dc[k], true, SD.lut[k], SD.maxcode[k], SD.valoff[k], SD.huffval[k], err);
+            if (rc != IDN_OK) return rc;
+          }
+          if (ac) {
+            rc = jpeg_build_huff(S.ac[k], false, SD.lut[3 + k], SD.maxcode[3 + k], SD.valoff[3 + k],
+                                 SD.huffval[3 + k], err);
+            if (rc != IDN_OK) return rc;
+          }
+        }
+        const size_t len = S.end - S.begin;
+        if ((uint64_t)len * 8 >= 0xFFFFFFF0ull) return jpg_fail(err, "scan too large");
+        SD.scan_off = P.scan_bytes;
+        SD.scan_len = (uint32_t)len;
+        P.scan_bytes += (len + 15) & ~(size_t)15;
+        SD.ub_off = P.ub_bytes;
+        P.ub_bytes += (len + 64 + 15) & ~(size_t)15;
+        SD.iv_off = P.nintervals;
+        P.nintervals += (uint32_t)SD.nintervals;
+        P.scans.push_back(SD);
+        P.scan_src.push_back(S.begin);
+      }
+      continue;
+    }
     for (int t = 0; t < 4 && tables; ++t) {
       for (int k = 0; k < 18; ++k) D.maxcode[t][k] = -1;
       const HuffSpec& H = t < 2 ? J.dc[t] : J.ac[t - 2];
@@ -1223,13 +1578,15 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
   }
   P.off_imgs = 0;
   P.off_blkend = align256(P.off_imgs + sizeof(JpegDev) * (size_t)n);
-  P.off_scan = align256(P.off_blkend + sizeof(uint64_t) * (size_t)n);
+  P.off_scans = align256(P.off_blkend + sizeof(uint64_t) * (size_t)n);
+  P.off_scan = align256(P.off_scans + sizeof(JpegScanDev) * P.scans.size());
   P.off_coef = align256(P.off_scan + P.scan_bytes + 16);
   P.off_planes = align256(P.off_coef + P.nblk * 128);
   P.off_ub = align256(P.off_planes + P.plane_bytes);
   P.off_iv = align256(P.off_ub + P.ub_bytes);
   P.off_ublen = align256(P.off_iv + sizeof(uint32_t) * (size_t)P.nintervals);
-  P.off_s0 = align256(P.off_ublen + sizeof(uint32_t) * (size_t)n);
+  P.off_ublen_s = align256(P.off_ublen + sizeof(uint32_t) * (size_t)n);
+  P.off_s0 = align256(P.off_ublen_s + sizeof(uint32_t) * (P.scans.size() + 1));
   P.off_s1 = align256(P.off_s0 + sizeof(uint64_t) * (size_t)P.nchunks);
   P.off_cnt = align256(P.off_s1 + sizeof(uint64_t) * (size_t)P.nchunks);
   P.off_start = align256(P.off_cnt + sizeof(ChunkOut) * (size_t)P.nchunks);
@@ -1297,6 +1654,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   uint8_t* host = pin;
   memcpy(host + P.off_imgs, P.dev.data(), sizeof(JpegDev) * (size_t)n);
   memcpy(host + P.off_blkend, P.blk_end.data(), sizeof(uint64_t) * (size_t)n);
+  if (!P.scans.empty())
+    memcpy(host + P.off_scans, P.scans.data(), sizeof(JpegScanDev) * P.scans.size());
   bool copy_ok = hipMemcpyAsync(ws, host, P.off_scan, hipMemcpyHostToDevice, st) == hipSuccess;
   {
     // the entropy segments, gathered by a few host threads in NPART parts of the batch; each
@@ -1308,20 +1667,27 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     std::atomic<int> done[MAXPART];
     for (int q = 0; q < MAXPART; ++q) done[q].store(0);
     auto first = [&](int q) { return (int)((int64_t)n * q / npart); };
+    // image i's entropy bytes: its one segment, or its scans' segments (the scan path)
+    auto gather = [&](int i) {
+      const JpegDev& D = P.dev[i];
+      if (D.nscan == 0) {
+        memcpy(host + P.off_scan + D.scan_off, files[i] + P.scan_begin[i], D.scan_len);
+        return;
+      }
+      for (uint32_t k = D.scan0; k < D.scan0 + D.nscan; ++k)
+        memcpy(host + P.off_scan + P.scans[k].scan_off, files[i] + P.scan_src[k],
+               P.scans[k].scan_len);
+    };
     auto worker = [&](int k) {
       for (int q = 0; q < npart; ++q) {
-        for (int i = first(q) + k; i < first(q + 1); i += nt)
-          memcpy(host + P.off_scan + P.dev[i].scan_off, files[i] + P.scan_begin[i],
-                 P.dev[i].scan_len);
+        for (int i = first(q) + k; i < first(q + 1); i += nt) gather(i);
         done[q].fetch_add(1, std::memory_order_release);
       }
     };
     std::vector<std::thread> th;
     for (int k = 1; k < nt; ++k) th.emplace_back(worker, k);
     for (int q = 0; q < npart; ++q) {  // the calling thread: its share, then the part's copy
-      for (int i = first(q); i < first(q + 1); i += nt)
-        memcpy(host + P.off_scan + P.dev[i].scan_off, files[i] + P.scan_begin[i],
-               P.dev[i].scan_len);
+      for (int i = first(q); i < first(q + 1); i += nt) gather(i);
       done[q].fetch_add(1, std::memory_order_release);
       while (done[q].load(std::memory_order_acquire) < nt) std::this_thread::yield();
       const size_t b0 = P.dev[first(q)].scan_off;
@@ -1346,8 +1712,13 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   uint32_t* flag = reinterpret_cast<uint32_t*>(ws + P.off_flag);
   uint8_t* chg[2] = {reinterpret_cast<uint8_t*>(ws + P.off_chg0),
                      reinterpret_cast<uint8_t*>(ws + P.off_chg1)};
-  hipLaunchKernelGGL(jpeg_unstuff_kernel, dim3(n), dim3(1024), 0, st, dimg, ws + P.off_scan, ub,
-                     ivs, ublen);
+  hipLaunchKernelGGL(jpeg_unstuff_kernel<JpegDev>, dim3(n), dim3(1024), 0, st, dimg,
+                     ws + P.off_scan, ub, ivs, ublen);
+  const JpegScanDev* dscan = reinterpret_cast<const JpegScanDev*>(ws + P.off_scans);
+  if (!P.scans.empty())
+    hipLaunchKernelGGL(jpeg_unstuff_kernel<JpegScanDev>, dim3((unsigned)P.scans.size()), dim3(1024),
+                       0, st, dscan, ws + P.off_scan, ub, ivs,
+                       reinterpret_cast<uint32_t*>(ws + P.off_ublen_s));
   const dim3 gitems((P.max_items + 63) / 64, n);
   int cur = 0;
   if (P.any_chunked) {
@@ -1372,6 +1743,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   }
   hipLaunchKernelGGL(jpeg_write_kernel, gitems, dim3(64), 0, st, dimg, ub, ublen, ivs, S[cur],
                      cstart, coef);
+  if (!P.scans.empty())
+    hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, coef);
   const uint64_t gb = (P.nblk + 255) / 256;
   IDN_CHECK_ARG(gb < 0x7FFFFFFF, "idn_jpeg_decode_u8: batch too large");
   const uint64_t* bend = reinterpret_cast<const uint64_t*>(ws + P.off_blkend);

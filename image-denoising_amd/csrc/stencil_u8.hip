@@ -415,7 +415,10 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
     if (DMA && full) {  // (full: every chunk but the last round's inside the tile)
       // LDS-DMA: global_load_lds_dwordx4 writes each wave's 1 KiB straight into the tile (the
       // destination is wave base + 16 lane, as the flat layout wants), no VGPR round trip and no
-      // ds_write; the barrier below waits for it (vmcnt)
+      // ds_write.  Every wave must see every other wave's rows after the barrier, so each wave
+      // waits for its own DMA (vmcnt(0)) before it: the workgroup fence does not promise that
+      // wait on gfx9 (LLVM emits it here today, s_waitcnt vmcnt(0) lgkmcnt(0) before s_barrier;
+      // stated explicitly so it cannot silently go away)
       const uint8_t* gsrc = src + (size_t)g.img * img_bytes + base_al + 16u * threadIdx.x;
       const int wv64 = 64 * wave;
 #pragma unroll
@@ -429,6 +432,7 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
             (const void*)(gsrc + 16 * TILE_WGT * (TS::NL - 1)),
             (__attribute__((address_space(3))) void*)(tile + 16 * (TILE_WGT * (TS::NL - 1) + wv64)),
             16, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (full) {
       const uint32_t vo = base_al + 16u * threadIdx.x;
 #pragma unroll

@@ -91,7 +91,8 @@ struct WlLayout {
   size_t off_band[WL_MAXL + 1];        // element offset of level l's 3x4 bands inside an image
   size_t img_floats;                   // wreal elements per image (planes + bands)
   size_t stats_off;                    // byte offset of the stats region (after all images)
-  int tiles_x[WL_MAXL + 1], tiles[WL_MAXL + 1];  // DWT tiles per level
+  int tiles_x[WL_MAXL + 1], tiles[WL_MAXL + 1];  // DWT tiles per level (partial-sum slots)
+  int bands[WL_MAXL + 1];              // bior1.5 streaming analysis: row bands per strip (launch)
   size_t part_tile0[WL_MAXL + 1];      // first tile index of level l in the partials array
   size_t part_per_img;                 // partial sums per image: 3 channels x 3 bands x tiles
   size_t part_off;                     // byte offset of the partial sums region
@@ -132,6 +133,7 @@ __device__ __forceinline__ int wl_fbin(unsigned long long key) {
 
 inline int ws_strips(int Wo);
 inline int ws_bands(int n, int Ho, int strips, int level);
+constexpr int WS_G = 16;  // rows per sum-of-squares group of the streaming analysis
 // Row bands per strip so that the grid fills whole rounds of resident workgroups: for each
 // candidate band count b the time is ~ rounds(b) x (rows per band + warm-up rows), rounds(b) =
 // ceil(units * b / resident).  (A grid of 2.5 rounds leaves the chip half idle for the last one.)
@@ -191,10 +193,16 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   Lt.stats_off = (size_t)n * Lt.img_floats * sizeof(wreal);
   size_t tiles_tot = 0;
   for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
-    if (wv == IDN_WAVELET_BIOR15) {  // wl_dwt_stream: strips x row bands
+    if (wv == IDN_WAVELET_BIOR15) {
+      // wl_dwt_stream: strips x row bands of whole WS_G-row groups; one partial sum per (strip,
+      // group), so the slots -- and the order wl_sumsq adds them in -- depend on the image size
+      // only, never on the batch size or the device (the band count does)
+      const int groups = (Lt.H[l] + WS_G - 1) / WS_G;
       Lt.tiles_x[l] = ws_strips(Lt.W[l]);
-      Lt.tiles[l] = Lt.tiles_x[l] * ws_bands(n, Lt.H[l], Lt.tiles_x[l], l);
+      Lt.tiles[l] = Lt.tiles_x[l] * groups * 2;  // two row waves per channel
+      Lt.bands[l] = std::min(ws_bands(n, Lt.H[l], Lt.tiles_x[l], l), groups);
     } else {
+      Lt.bands[l] = 0;
       Lt.tiles_x[l] = (Lt.W[l] + RB_TX - 1) / RB_TX;  // wl_dwt_rb tiles
       Lt.tiles[l] = Lt.tiles_x[l] * ((Lt.H[l] + RB_TY - 1) / RB_TY);
     }
@@ -655,6 +663,7 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
 #define IDN_WS_MAXT 512
 #endif
 constexpr int WS_MAXT = IDN_WS_MAXT;         // threads = staged columns per workgroup (max)
+static_assert(WS_MAXT >= 3 * 128, "the row role needs two whole waves per channel");
 // output columns per strip (max): (threads - 8) / 2; tuning: IDN_WAVELET_WST threads (64..256)
 inline int ws_maxsw() {
   const int t = std::min(std::max(knob("IDN_WAVELET_WST", WS_MAXT), 64), WS_MAXT) / 64 * 64;
@@ -697,6 +706,11 @@ template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (
 #define IDN_S3_WPE 1
 #endif
 template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
+// the fp32 deeper-level analyses at six waves per SIMD (<= 80 VGPRs: three 512-thread workgroups
+// per CU)
+#ifndef IDN_WS_DEEP_WPE
+#define IDN_WS_DEEP_WPE 6
+#endif
 
 // TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the
 // product runs the lowpass outputs (aa, ad, da: continuous inputs of the thresholds' fp64 sums of
@@ -706,9 +720,10 @@ template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
 // FM >= 0: the band storage mask (wl_fband) and CODES the level-1 code emission as compile-time
 // constants (the product's masks: no per-band branches); FM = -1 takes both from the arguments.
 template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1>
-__global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
+__global__ __launch_bounds__(WS_MAXT, SRC >= 2 && sizeof(TL) == 4 ? IDN_WS_DEEP_WPE : IDN_WS_WPE)
+void wl_dwt_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
-    int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands,
+    int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands, int groups,
     const uint8_t* __restrict__ src, const double* __restrict__ in64, int64_t row_stride,
     double* __restrict__ part, size_t part_per_img, size_t part_tile0, int emit_codes_arg,
     int fmask_arg) {
@@ -723,11 +738,12 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
   __shared__ TL VL[2][3][WS_MAXT];
   __shared__ TL VF[SEPF ? 2 : 1][SEPF ? 3 : 1][SEPF ? WS_MAXT : 1];
   __shared__ TH VH[2][3][WS_MAXT];
-  __shared__ double RED[3][WS_MAXT];
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
   const int j0 = strip * SW;
-  const int ia = (int)((int64_t)band * Ho / bands), ib = (int)((int64_t)(band + 1) * Ho / bands);
+  // the band: whole WS_G-row groups [ga, gb) (the last group of the image may be short)
+  const int ga = (int)((int64_t)band * groups / bands), gb = (int)((int64_t)(band + 1) * groups / bands);
+  const int ia = ga * WS_G, ib = min(gb * WS_G, Ho);
   const int t = threadIdx.x;
   wreal* base = ws + img * img_floats;
   // ---- column role
@@ -808,14 +824,21 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
 #pragma unroll
     for (int r = 0; r < 5; ++r) acc[c][r] = (TL)0;
   }
-  // ---- row role
+  // ---- row role: channel c's row threads are t = 128 c + jj / 2 (two whole waves per channel,
+  // so a wave's sums of squares are one channel's)
   const int half = SW / 2;
-  const bool rowt = t < 3 * half;
-  const int rc = rowt ? t / half : 0, jj = rowt ? 2 * (t - rc * half) : 0;
+  const int rl = t & 127;
+  const bool rowt = t < 3 * 128 && rl < half;
+  const int rc = rowt ? t >> 7 : 0, jj = rowt ? 2 * rl : 0;
   const int oj = j0 + jj;
   const bool ok0 = rowt && oj < Wo, ok1 = rowt && oj + 1 < Wo;
   const size_t bsz = (size_t)Ho * Wo;
   double sq[3] = {0.0, 0.0, 0.0};
+  // sums of squares per (strip, group, wave): each row thread sums its outputs of the group's
+  // rows in row order; at the group's last row every row wave adds its lanes by a fixed butterfly
+  // and lane 0 stores the partial -- the same operations whatever band holds the group, so the
+  // partials, and wl_sumsq's fixed-order total, do not depend on the band split
+  double* const part_img = part + img * part_per_img + part_tile0 + (size_t)strip * groups * 2;
 
   const int k0 = ia - 4, M = ib - ia + 4;  // steps m = 0 .. M-1 cover pairs k = k0 + m
   WsRaw<SRC> rq[PF];                        // raw samples of steps m .. m + PF - 1 (slot m % PF)
@@ -860,6 +883,7 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
       if (m < 4) continue;  // accumulator fill (wave-uniform)
       __syncthreads();
       const int i = k;  // output row
+      const bool gend = (i + 1) % WS_G == 0 || i + 1 == ib;
       if (rowt) {
         const TL* vl = &VL[buf][rc][2 * jj];
         const TH* vhe = &VH[buf][rc][jj];                 // element 2 jj + m, m even: vhe[m / 2]
@@ -932,21 +956,19 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
           }
         }
       }
-    }
-  }
-  // per-workgroup sums of squares, channel by channel in thread order (deterministic)
-  __syncthreads();
-  double* red = &RED[0][0];
-  if (rowt) {
+      if (gend && t < 3 * 128) {  // whole waves (wave-uniform): every lane takes part
+        const int g = i / WS_G;
 #pragma unroll
-    for (int b = 0; b < 3; ++b) red[b * WS_MAXT + t] = sq[b];
-  }
-  __syncthreads();
-  if (t < 9) {
-    const int c = t / 3, b = t - 3 * c;
-    double s2 = 0.0;
-    for (int g = 0; g < half; ++g) s2 += red[b * WS_MAXT + c * half + g];
-    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = s2;
+        for (int b = 0; b < 3; ++b) {
+          double v = rowt ? sq[b] : 0.0;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+          if ((t & 63) == 0)  // every row wave writes its slot (0 if none of its lanes has a row)
+            part_img[(size_t)((t >> 7) * 3 + b) * (part_per_img / 9) + (size_t)g * 2 + ((t >> 6) & 1)] = v;
+          sq[b] = 0.0;
+        }
+      }
+    }
   }
 }
 
@@ -3300,17 +3322,19 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   const int coop = knob("IDN_WAVELET_COOP", 1) ? 1 : 0;
   const int a32 = knob("IDN_WAVELET_A32", 3);
   for (int l = 1; l <= Lt.L; ++l) {
-    const dim3 grid(Lt.tiles[l], 1, n);
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
     if (WV == IDN_WAVELET_BIOR15) {
-      const int strips = Lt.tiles_x[l], bands = Lt.tiles[l] / strips, sw = ws_sw(Lt.W[l]);
-      const dim3 blk((unsigned)((2 * sw + 8 + 63) / 64 * 64));
+      const int strips = Lt.tiles_x[l], bands = Lt.bands[l], groups = Lt.tiles[l] / (2 * strips);
+      const int sw = ws_sw(Lt.W[l]);
+      const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n);
+      // threads: the staged columns (2 SW + 8), and at least the 3 x 128 of the row role
+      const dim3 blk((unsigned)std::max((2 * sw + 8 + 63) / 64 * 64, 3 * 128));
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
       // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
 #define IDN_WS_(SRC, TL, TH, FMC, CC, EMIT)                                                        \
   hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC>), grid, blk, 0, st, wsf, Lt.img_floats,  \
                      stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands,   \
-                     src, in64, row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT,         \
+                     groups, src, in64, row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT, \
                      fm_an(l))
       // the product's band masks as compile-time constants (bit 4 = WL_FB_AIN is read by the
       // launcher only); anything else (tuning forms) through the runtime-mask instance
@@ -3340,17 +3364,17 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
 #undef IDN_WS
 #undef IDN_WS_
     } else if (l > 1)
-      hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
+      hipLaunchKernelGGL((wl_dwt_rb<WV, 2>), dim3(Lt.tiles[l], 1, n), dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[l - 1], Lt.W[l - 1], Lt.off_band[l], Lt.H[l], Lt.W[l],
                          Lt.tiles_x[l], src, in64, row_stride, part, Lt.part_per_img,
                          Lt.part_tile0[l], 0, fm_an(l), coop);
     else if (in64)
-      hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
+      hipLaunchKernelGGL((wl_dwt_rb<WV, 1>), dim3(Lt.tiles[1], 1, n), dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
                          Lt.part_tile0[1], codes ? 1 : 0, fm_an(1), coop);
     else
-      hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), grid, dim3(256), 0, st, wsf, Lt.img_floats, stats,
+      hipLaunchKernelGGL((wl_dwt_rb<WV, 0>), dim3(Lt.tiles[1], 1, n), dim3(256), 0, st, wsf, Lt.img_floats, stats,
                          in_off, Lt.H[0], Lt.W[0], Lt.off_band[1], Lt.H[1], Lt.W[1],
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
                          Lt.part_tile0[1], codes ? 1 : 0, fm_an(1), coop);

@@ -15,6 +15,7 @@ import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libidn_hip.so"
+ABI_VERSION = 4  # IDN_ABI_VERSION of include/idn.h that SIGNATURES binds
 VARIANTS = {"tuning": Path(__file__).resolve().parent / "libidn_hip_tuning.so"}
 
 _c_u8p = ctypes.c_void_p
@@ -28,6 +29,7 @@ _c_vp = ctypes.c_void_p
 
 # name -> (restype, argtypes); must match include/idn.h exactly
 SIGNATURES = {
+    "idn_abi_version": (_c_int, []),
     "idn_version": (ctypes.c_char_p, []),
     "idn_last_error": (ctypes.c_char_p, []),
     "idn_gaussian_blur_u8": (_c_int, [_c_u8p, _c_u8p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp]),
@@ -97,6 +99,14 @@ def _open(path: Path, required: bool):
             f"{path} is missing: build it with `python -m idn._build` "
             "(or __graft_entry__.build()); idn has no CPU fallback")
     lib = ctypes.CDLL(str(path))
+    ver = getattr(lib, "idn_abi_version", None)
+    got = None
+    if ver is not None:
+        ver.restype, ver.argtypes = ctypes.c_int, []
+        got = ver()
+    if got != ABI_VERSION:
+        raise IdnError(f"{path.name} has C-ABI version {got}, this binding needs {ABI_VERSION}: "
+                       "rebuild it with `python -m idn._build`")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None:

@@ -1,14 +1,16 @@
 """Image loading for the drop-in path: cv2.imread semantics (BGR uint8 HxWx3).
 
 The reference reads every image with cv2.imread (lib/model/test.py:191,
-lib/roi_data_layer/minibatch.py:85).  OpenCV is used when importable; otherwise the file is
-decoded with PIL and flipped to BGR (libjpeg builds can differ by a few LSB between the two
-decoders; parity tests therefore feed both sides the same decoded pixels).
+lib/roi_data_layer/minibatch.py:85), i.e. OpenCV 3.4.2 over IJG libjpeg 9d (requirements.txt:74,
+89).  `imread` uses OpenCV when it is importable.  Without it, a JPEG is decoded by the GPU decoder
+(`imread_gpu`: bit-exact with libjpeg 9d) and returned as a host array -- never by PIL, whose
+libjpeg-turbo differs from 9d by up to tens of LSB on subsampled files; a JPEG the GPU decoder
+does not take raises IdnError.  Other (lossless) formats go through PIL, flipped to BGR.
 
-`imread_gpu` is the GPU decode front-end: baseline JPEG files are decoded on
-the device (idn_jpeg_decode_u8), bit-exact with the reference's pinned IJG libjpeg 9d
-(requirements.txt:74) by default or with libjpeg-turbo (mode="turbo"), images of one size in one
-launch; files the decoder does not take raise IdnError (no CPU fallback inside the product).
+`imread_gpu` is the GPU decode front-end: JPEG files are decoded on the
+device (idn_jpeg_decode_u8), bit-exact with the reference's pinned IJG libjpeg 9d by default or
+with libjpeg-turbo (mode="turbo"), images of one size in one launch; files the decoder does not
+take raise IdnError (no CPU fallback inside the product).
 """
 from __future__ import annotations
 
@@ -16,6 +18,7 @@ import numpy as np
 
 
 def imread(path) -> np.ndarray:
+    """cv2.imread(path) (IMREAD_COLOR) as a host uint8 BGR HxWx3 array."""
     try:
         import cv2
     except ImportError:
@@ -25,6 +28,10 @@ def imread(path) -> np.ndarray:
         if im is None:
             raise FileNotFoundError(path)
         return im
+    with open(path, "rb") as f:
+        head = f.read(3)
+    if head[:2] == b"\xff\xd8":  # JPEG: the libjpeg 9d decode, on the GPU
+        return imread_gpu([path])[0].cpu().numpy()
     from PIL import Image
     with Image.open(path) as im:
         rgb = np.asarray(im.convert("RGB"))

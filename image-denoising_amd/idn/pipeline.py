@@ -50,6 +50,20 @@ class Preprocessor:
     def __call__(self, batch: torch.Tensor, image_ids: Optional[Sequence[int]] = None,
                  plans: Optional[Sequence[ns.Plan]] = None):
         """Returns (outputs, plans): outputs[i] is a device tensor (H,W,3) uint8 or float64."""
+        outs, _, plans = self._execute(batch, image_ids, plans, defer=False)
+        return outs, plans
+
+    def run_for_blob(self, batch: torch.Tensor, image_ids: Optional[Sequence[int]] = None,
+                     plans: Optional[Sequence[ns.Plan]] = None):
+        """Like __call__, but a plan that ends in a uint8 cv2.GaussianBlur stops before it:
+        returns (outputs, ksizes, plans) with ksizes[i] the deferred blur's ksize (None if
+        nothing was deferred), so the blob builder can run the blur and prep_im_for_blob as one
+        pass (idn_gaussian_blob_f32) -- the filtered uint8 image never reaches HBM."""
+        return self._execute(batch, image_ids, plans, defer=True)
+
+    def _execute(self, batch, image_ids, plans, defer: bool):
+        # all per-call state lives in locals / arguments: a Preprocessor may be shared between
+        # threads (the drop-ins cache one per spec)
         if batch.dim() == 3:
             batch = batch.unsqueeze(0)
         n = batch.shape[0]
@@ -62,33 +76,18 @@ class Preprocessor:
             key = (i,) if self.noise_rng == "numpy" else _group_key(p.steps)
             groups.setdefault(key, []).append(i)
         outs: List[Optional[torch.Tensor]] = [None] * n
-        self._deferred = [None] * n
+        ks: List[Optional[int]] = [None] * n
         for _, idx in groups.items():
             steps = plans[idx[0]].steps
             if len(idx) == n:
                 sub = batch
             else:
                 sub = batch.index_select(0, torch.as_tensor(idx, device=batch.device))
-            self._bloom_draws = [next((st.args for st in plans[i].steps if st.op == "bloom"), ())
-                                 for i in idx]
-            res, k_def = self._run_steps(sub, steps, [ids[i] for i in idx])
+            bloom = [next((st.args for st in plans[i].steps if st.op == "bloom"), ()) for i in idx]
+            res, k_def = self._run_steps(sub, steps, [ids[i] for i in idx], bloom, defer)
             for k, i in enumerate(idx):
                 outs[i] = res[k]
-                self._deferred[i] = k_def
-        return outs, plans
-
-    def run_for_blob(self, batch: torch.Tensor, image_ids: Optional[Sequence[int]] = None,
-                     plans: Optional[Sequence[ns.Plan]] = None):
-        """Like __call__, but a plan that ends in a uint8 cv2.GaussianBlur stops before it:
-        returns (outputs, ksizes, plans) with ksizes[i] the deferred blur's ksize (None if
-        nothing was deferred), so the blob builder can run the blur and prep_im_for_blob as one
-        pass (idn_gaussian_blob_f32) -- the filtered uint8 image never reaches HBM."""
-        self._defer = True
-        try:
-            outs, plans = self(batch, image_ids, plans)
-        finally:
-            self._defer = False
-        ks = list(getattr(self, "_deferred", [None] * len(outs)))
+                ks[i] = k_def
         return outs, ks, plans
 
     def run_batch(self, batch: torch.Tensor, image_ids=None, plans=None):
@@ -98,7 +97,8 @@ class Preprocessor:
             return torch.stack(outs), plans
         return outs, plans
 
-    def _noise(self, x: torch.Tensor, step: ns.Step, nxt: Optional[ns.Step], ids: List[int]):
+    def _noise(self, x: torch.Tensor, step: ns.Step, nxt: Optional[ns.Step], ids: List[int],
+               bloom=()):
         op = step.op
         if op == "original":
             return x
@@ -112,7 +112,7 @@ class Preprocessor:
                 return ops.quantize(x, int(step.args[0]), seed=self.seed, image_ids=ids)
             return ops.quantize(x, int(step.args[0]), seed=self.seed, offset=int(ids[0]))
         if op == "bloom":
-            draws = getattr(self, "_bloom_draws", None) or []
+            draws = list(bloom)
             if len(draws) == x.shape[0] and all(draws):
                 return ops.bloom(x, circles=[(np.asarray(c, np.int32), np.asarray(w, np.float32))
                                              for c, w in draws])
@@ -202,17 +202,18 @@ class Preprocessor:
             return ops.denoise_wavelet(x, a[0], a[1])
         raise ValueError(f"unknown filter step {op!r}")
 
-    def _run_steps(self, x: torch.Tensor, steps: Tuple[ns.Step, ...], ids: List[int]):
+    def _run_steps(self, x: torch.Tensor, steps: Tuple[ns.Step, ...], ids: List[int],
+                   bloom=(), defer: bool = False):
         cur = x
         i = 0
         while i < len(steps):
             st = steps[i]
             nxt = steps[i + 1] if i + 1 < len(steps) else None
-            if (nxt is None and getattr(self, "_defer", False) and st.kind == "filter"
+            if (nxt is None and defer and st.kind == "filter"
                     and st.op == "gaus_blur" and cur.dtype == torch.uint8):
                 return list(cur.unbind(0)), int(st.args[0])  # left to the blob builder
             if st.kind == "noise":
-                cur = self._noise(cur, st, nxt, ids)
+                cur = self._noise(cur, st, nxt, ids, bloom)
                 if nxt is not None and nxt.kind == "cast_u8":
                     i += 1  # fused into the noise kernel's U8 output
             elif st.kind == "cast_u8":

@@ -71,8 +71,18 @@ typedef enum idn_wavelet {
 } idn_wavelet;
 
 /* ---- library ------------------------------------------------------------------------- */
+/* ABI version of this header; idn_abi_version() returns the library's.  A caller (the ctypes
+ * binding idn/_lib.py) refuses a library whose number differs.  History:
+ *   3  idn_jpeg_workspace_size / idn_jpeg_decode_u8 gained `flags` before `workspace`
+ *      (IDN_JPEG_TURBO); the default decode became IJG libjpeg 9d's; idn_noise_filter_u8
+ *      (the fused noise -> 3x3 / 5x5 filter) was removed: compose idn_noise_u8 and the filter
+ *   4  idn_abi_version added (no signature changed) */
+#define IDN_ABI_VERSION 4
+int idn_abi_version(void);
 const char* idn_version(void);
 const char* idn_last_error(void);
+/* Test hook, not part of the ABI (exported, deliberately undeclared): the bilateral output
+ * step's reciprocal, idn_internal_bl_recip_check, used by tests/test_filters_gpu.py only. */
 
 /* ---- denoising filters (u8 -> u8, src != dst) ------------------------------------------ */
 

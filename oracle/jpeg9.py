@@ -1,12 +1,20 @@
 """ORACLE — TEST INFRASTRUCTURE ONLY (never imported by the product path).
 
-CPU restatement of `cv2.imread(path)` (IMREAD_COLOR -> uint8 BGR) for baseline JPEG files, as the
+CPU restatement of `cv2.imread(path)` (IMREAD_COLOR -> uint8 BGR) for JPEG files, as the
 reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
 (`/root/reference/requirements.txt:74,89`; call sites `lib/model/test.py:191`,
 `lib/roi_data_layer/minibatch.py:85`).  libjpeg 9d is a third-party library absent from
 /root/reference; its published algorithm is restated here:
 
-  jdhuff.c     baseline Huffman decoding (DC prediction, AC run/size, restart intervals)
+  jdhuff.c     Huffman decoding: sequential (DC prediction, AC run/size, restart intervals) and
+               progressive (decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine: spectral
+               selection, successive approximation, EOB runs), one or several scans; a
+               non-interleaved scan codes only the component's own blocks (width_in_blocks)
+  jdcoefct.c   progressive files are decoded into the whole coefficient buffer first; block
+               smoothing (do_block_smoothing, smoothing_ok) then applies only if a component's AC
+               coefficients 1..5 are not all known to full precision after the last scan (coef_bits
+               != 0).  Encoders' standard scripts (jpeg_simple_progression) refine every one to
+               Al = 0; a file that does not is rejected here (not restated)
   jdmaster.c   IDCT scaling: with do_fancy_upsampling (the default) a component whose sampling
                factor divides the maximum by 2 gets a scaled IDCT of twice the size in that
                direction (libjpeg >= 7), so 4:2:0 chroma is decoded by jpeg_idct_16x16 and
@@ -41,25 +49,6 @@ def FIX(x: float) -> int:
 
 
 # ---- parsing + entropy decoding (jdmarker.c / jdhuff.c) ----------------------------------------
-def _segments(data: bytes):
-    i = 2
-    assert data[:2] == b"\xff\xd8", "no SOI"
-    while i + 4 <= len(data):
-        assert data[i] == 0xFF
-        m = data[i + 1]
-        if m == 0xFF:
-            i += 1
-            continue
-        i += 2
-        if m == 0xD8 or 0xD0 <= m <= 0xD7 or m == 0x01:
-            continue
-        ln = (data[i] << 8) | data[i + 1]
-        yield m, data[i + 2:i + ln], i + ln
-        if m == 0xDA:
-            return
-        i += ln
-
-
 def _huff_lut(bits, vals):
     """16-bit peek -> (length, symbol)"""
     lut = [(0, 0)] * 65536
@@ -79,65 +68,15 @@ def _extend(v, s):
     return v - (1 << s) + 1 if v < (1 << (s - 1)) else v
 
 
-def parse_and_decode(data: bytes):
-    """-> dict(width, height, comps=[(h, v, q[64] natural)], coef=[int32 (bh, bw, 64) natural])"""
-    q, dc, ac, comps, restart = {}, {}, {}, [], 0
-    W = H = 0
-    scan_start = None
-    sel = []
-    for m, s, end in _segments(data):
-        if m in (0xC0, 0xC1):
-            assert s[0] == 8
-            H, W, nc = (s[1] << 8) | s[2], (s[3] << 8) | s[4], s[5]
-            comps = [dict(id=s[6 + 3 * c], h=s[7 + 3 * c] >> 4, v=s[7 + 3 * c] & 15,
-                          tq=s[8 + 3 * c]) for c in range(nc)]
-        elif m == 0xC4:
-            k = 0
-            while k < len(s):
-                tc, th = s[k] >> 4, s[k] & 15
-                bits = [0] + list(s[k + 1:k + 17])
-                n = sum(bits)
-                tbl = _huff_lut(bits, list(s[k + 17:k + 17 + n]))
-                (ac if tc else dc)[th] = tbl
-                k += 17 + n
-        elif m == 0xDB:
-            k = 0
-            while k < len(s):
-                pq, tq = s[k] >> 4, s[k] & 15
-                if pq:
-                    z = [(s[k + 1 + 2 * i] << 8) | s[k + 2 + 2 * i] for i in range(64)]
-                else:
-                    z = list(s[k + 1:k + 65])
-                nat = np.zeros(64, np.int64)
-                nat[ZIGZAG] = z
-                q[tq] = nat
-                k += 1 + 64 * (2 if pq else 1)
-        elif m == 0xDD:
-            restart = (s[0] << 8) | s[1]
-        elif m == 0xDA:
-            ns = s[0]
-            for k in range(ns):
-                c = [cc["id"] for cc in comps].index(s[1 + 2 * k])
-                sel.append((c, s[2 + 2 * k] >> 4, s[2 + 2 * k] & 15))
-            scan_start = end
-        elif 0xC2 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
-            raise ValueError("not a baseline sequential JPEG")
-    assert scan_start is not None and len(sel) == len(comps)
-    nc = len(comps)
-    if nc == 1:
-        comps[0]["h"] = comps[0]["v"] = 1
-    hmax = max(c["h"] for c in comps)
-    vmax = max(c["v"] for c in comps)
-    mcux = -(-W // (8 * hmax))
-    mcuy = -(-H // (8 * vmax))
-    coef = [np.zeros((mcuy * c["v"], mcux * c["h"], 64), np.int64) for c in comps]
-    # entropy-coded data -> restart intervals of unstuffed bytes
-    seg = data[scan_start:]
-    intervals, cur, i = [], bytearray(), 0
-    while i < len(seg):
-        b = seg[i]
-        if b == 0xFF and i + 1 < len(seg):
-            nb = seg[i + 1]
+def _entropy(data: bytes, i: int):
+    """the entropy-coded segment starting at data[i]: (restart intervals of unstuffed bytes, index
+    of the marker that ends it).  Stuffed 0xFF00 -> 0xFF, RSTn splits intervals, fill 0xFFs are
+    skipped; any other marker ends the segment."""
+    intervals, cur = [], bytearray()
+    while i < len(data):
+        b = data[i]
+        if b == 0xFF and i + 1 < len(data):
+            nb = data[i + 1]
             if nb == 0x00:
                 cur.append(0xFF)
                 i += 2
@@ -154,45 +93,231 @@ def parse_and_decode(data: bytes):
         cur.append(b)
         i += 1
     intervals.append(bytes(cur))
-    order = [(ci, dv, dh) for ci, c in enumerate(comps) for dv in range(c["v"])
-             for dh in range(c["h"])]
-    nmcu = mcux * mcuy
-    per = restart if restart else nmcu
-    mcu = 0
-    for iv in intervals:
-        if mcu >= nmcu:
+    return intervals, i
+
+
+class _Bits:
+    """big-endian bit reader over one restart interval; zeros past its end (libjpeg's fill)"""
+
+    def __init__(self, buf: bytes):
+        self.v = int.from_bytes(buf + bytes(8), "big")
+        self.n = 8 * (len(buf) + 8)
+        self.pos = 0
+
+    def peek16(self):
+        return (self.v >> (self.n - self.pos - 16)) & 0xFFFF
+
+    def get(self, s):
+        if s == 0:
+            return 0
+        r = (self.v >> (self.n - self.pos - s)) & ((1 << s) - 1)
+        self.pos += s
+        return r
+
+    def huff(self, lut):
+        ln, sym = lut[self.peek16()]
+        self.pos += ln
+        return sym
+
+
+def _nat(k):
+    """jpeg_natural_order with libjpeg's overrun guard (indices past 63 map to 63)"""
+    return ZIGZAG[min(k, 63)]
+
+
+def _decode_scan(sc, comps, coef, geo, dc, ac):
+    """one scan (jdhuff.c: sequential decode_mcu, or the progressive decode_mcu_DC_first /
+    _AC_first / _DC_refine / _AC_refine) into the coefficient arrays (natural order, int64)"""
+    Ss, Se, Ah, Al = sc["Ss"], sc["Se"], sc["Ah"], sc["Al"]
+    sel = sc["sel"]  # [(component index, td, ta)]
+    prog = sc["progressive"]
+    if len(sel) == 1:  # non-interleaved: the component's own blocks, MCU = one block
+        ci = sel[0][0]
+        bw, bh = geo["wib"][ci], geo["hib"][ci]
+        units = [[(ci, by, bx)] for by in range(bh) for bx in range(bw)]
+    else:
+        units = []
+        for my in range(geo["mcuy"]):
+            for mx in range(geo["mcux"]):
+                units.append([(ci, my * comps[ci]["v"] + dv, mx * comps[ci]["h"] + dh)
+                              for ci, _, _ in sel for dv in range(comps[ci]["v"])
+                              for dh in range(comps[ci]["h"])])
+    tabs = {ci: (dc.get(td), ac.get(ta)) for ci, td, ta in sel}
+    per = sc["restart"] if sc["restart"] else len(units)
+    p1, m1 = 1 << Al, -(1 << Al)
+    u = 0
+    for iv in sc["intervals"]:
+        if u >= len(units):
             break
-        bits = "".join(f"{b:08b}" for b in iv) + "0" * 64
-        pos = 0
-        pred = [0] * nc
-        for _ in range(min(per, nmcu - mcu)):
-            my, mx = divmod(mcu, mcux)
-            for ci, dv, dh in order:
-                c, td, ta = sel[ci]
-                blk = coef[ci][my * comps[ci]["v"] + dv, mx * comps[ci]["h"] + dh]
-                ln, s = dc[td][int(bits[pos:pos + 16], 2)]
-                pos += ln
-                diff = _extend(int(bits[pos:pos + s], 2), s) if s else 0
-                pos += s
-                pred[ci] += diff
-                blk[0] = pred[ci]
-                k = 1
-                tbl = ac[ta]
-                while k < 64:
-                    ln, rs = tbl[int(bits[pos:pos + 16], 2)]
-                    pos += ln
-                    r, s = rs >> 4, rs & 15
-                    if s:
-                        k += r
-                        blk[ZIGZAG[min(k, 63)]] = _extend(int(bits[pos:pos + s], 2), s)
-                        pos += s
+        br = _Bits(iv)
+        pred = {ci: 0 for ci, _, _ in sel}
+        eobrun = 0
+        for _ in range(min(per, len(units) - u)):
+            for ci, by, bx in units[u]:
+                blk = coef[ci][by, bx]
+                dct, act = tabs[ci]
+                if not prog:  # sequential: DC then AC of the block
+                    s = br.huff(dct)
+                    pred[ci] += _extend(br.get(s), s) if s else 0
+                    blk[0] = pred[ci]
+                    k = 1
+                    while k < 64:
+                        rs = br.huff(act)
+                        r, s = rs >> 4, rs & 15
+                        if s:
+                            k += r
+                            blk[_nat(k)] = _extend(br.get(s), s)
+                            k += 1
+                        elif r == 15:
+                            k += 16
+                        else:
+                            break
+                elif Ss == 0 and Ah == 0:  # DC first
+                    s = br.huff(dct)
+                    pred[ci] += _extend(br.get(s), s) if s else 0
+                    blk[0] = pred[ci] << Al
+                elif Ss == 0:  # DC refine
+                    if br.get(1):
+                        blk[0] |= p1
+                elif Ah == 0:  # AC first
+                    if eobrun:
+                        eobrun -= 1
+                        continue
+                    k = Ss
+                    while k <= Se:
+                        rs = br.huff(act)
+                        r, s = rs >> 4, rs & 15
+                        if s:
+                            k += r
+                            blk[_nat(k)] = _extend(br.get(s), s) << Al
+                        elif r != 15:
+                            eobrun = (1 << r) + (br.get(r) if r else 0) - 1
+                            break
+                        else:
+                            k += 15
                         k += 1
-                    elif r == 15:
-                        k += 16
-                    else:
-                        break
-            mcu += 1
-    return dict(width=W, height=H, hmax=hmax, vmax=vmax,
+                else:  # AC refine
+                    k = Ss
+                    if eobrun == 0:
+                        while k <= Se:
+                            rs = br.huff(act)
+                            r, s = rs >> 4, rs & 15
+                            if s:
+                                s = p1 if br.get(1) else m1
+                            elif r != 15:
+                                eobrun = (1 << r) + (br.get(r) if r else 0)
+                                break
+                            while k <= Se:
+                                pos = _nat(k)
+                                if blk[pos]:
+                                    if br.get(1) and (blk[pos] & p1) == 0:
+                                        blk[pos] += p1 if blk[pos] >= 0 else m1
+                                else:
+                                    r -= 1
+                                    if r < 0:
+                                        break
+                                k += 1
+                            if s:
+                                blk[_nat(k)] = s
+                            k += 1
+                    if eobrun > 0:
+                        while k <= Se:
+                            pos = _nat(k)
+                            if blk[pos] and br.get(1) and (blk[pos] & p1) == 0:
+                                blk[pos] += p1 if blk[pos] >= 0 else m1
+                            k += 1
+                        eobrun -= 1
+            u += 1
+
+
+def parse_and_decode(data: bytes):
+    """-> dict(width, height, comps=[(h, v, q[64] natural)], coef=[int64 (bh, bw, 64) natural])
+
+    Baseline / extended sequential (SOF0 / SOF1) and progressive (SOF2) Huffman files, one or
+    several scans (tables and the restart interval may change between scans)."""
+    assert data[:2] == b"\xff\xd8", "no SOI"
+    q, dc, ac, comps, restart = {}, {}, {}, [], 0
+    W = H = 0
+    progressive = None
+    coef = geo = None
+    i = 2
+    while i + 4 <= len(data):
+        assert data[i] == 0xFF
+        m = data[i + 1]
+        if m == 0xFF:
+            i += 1
+            continue
+        i += 2
+        if m == 0xD8 or 0xD0 <= m <= 0xD7 or m == 0x01:
+            continue
+        if m == 0xD9:
+            break
+        ln = (data[i] << 8) | data[i + 1]
+        s = data[i + 2:i + ln]
+        end = i + ln
+        if m in (0xC0, 0xC1, 0xC2):
+            assert s[0] == 8
+            progressive = m == 0xC2
+            H, W, nc = (s[1] << 8) | s[2], (s[3] << 8) | s[4], s[5]
+            comps = [dict(id=s[6 + 3 * c], h=s[7 + 3 * c] >> 4, v=s[7 + 3 * c] & 15,
+                          tq=s[8 + 3 * c]) for c in range(nc)]
+            if nc == 1:
+                comps[0]["h"] = comps[0]["v"] = 1
+            hmax = max(c["h"] for c in comps)
+            vmax = max(c["v"] for c in comps)
+            mcux, mcuy = -(-W // (8 * hmax)), -(-H // (8 * vmax))
+            # blocks of each component that carry data (jdinput.c width_in_blocks): what a
+            # non-interleaved scan codes
+            geo = dict(mcux=mcux, mcuy=mcuy, hmax=hmax, vmax=vmax,
+                       wib=[-(-(-(-W * c["h"] // hmax)) // 8) for c in comps],
+                       hib=[-(-(-(-H * c["v"] // vmax)) // 8) for c in comps])
+            coef = [np.zeros((mcuy * c["v"], mcux * c["h"], 64), np.int64) for c in comps]
+            cbits = [[-1] * 6 for _ in comps]
+        elif m == 0xC4:
+            k = 0
+            while k < len(s):
+                tc, th = s[k] >> 4, s[k] & 15
+                bits = [0] + list(s[k + 1:k + 17])
+                n = sum(bits)
+                tbl = _huff_lut(bits, list(s[k + 17:k + 17 + n]))
+                (ac if tc else dc)[th] = tbl
+                k += 17 + n
+        elif m == 0xDB:
+            k = 0
+            while k < len(s):
+                pq, tq = s[k] >> 4, s[k] & 15
+                if pq:
+                    z = [(s[k + 1 + 2 * i2] << 8) | s[k + 2 + 2 * i2] for i2 in range(64)]
+                else:
+                    z = list(s[k + 1:k + 65])
+                nat = np.zeros(64, np.int64)
+                nat[ZIGZAG] = z
+                q[tq] = nat
+                k += 1 + 64 * (2 if pq else 1)
+        elif m == 0xDD:
+            restart = (s[0] << 8) | s[1]
+        elif m == 0xDA:
+            ns = s[0]
+            sel = []
+            for k in range(ns):
+                c = [cc["id"] for cc in comps].index(s[1 + 2 * k])
+                sel.append((c, s[2 + 2 * k] >> 4, s[2 + 2 * k] & 15))
+            ss = s[1 + 2 * ns:]
+            intervals, end = _entropy(data, end)
+            sc = dict(sel=sel, Ss=ss[0], Se=ss[1], Ah=ss[2] >> 4, Al=ss[2] & 15,
+                      progressive=progressive, restart=restart, intervals=intervals)
+            _decode_scan(sc, comps, coef, geo, dc, ac)
+            for ci, _, _ in sel:  # jdphuff.c start_pass: coef_bits[k] = Al for k in Ss..Se
+                for k in range(sc["Ss"], min(sc["Se"], 5) + 1):
+                    cbits[ci][k] = sc["Al"]
+        elif 0xC3 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
+            raise ValueError("lossless / arithmetic / hierarchical JPEG not supported")
+        i = end
+    assert coef is not None, "no frame"
+    if progressive and any(cb[0] >= 0 and any(b != 0 for b in cb[1:]) for cb in cbits):
+        raise NotImplementedError("progressive file leaves AC 1..5 imprecise: libjpeg would "
+                                  "block-smooth it (jdcoefct.c smoothing_ok)")
+    return dict(width=W, height=H, hmax=geo["hmax"], vmax=geo["vmax"],
                 comps=[(c["h"], c["v"], q[c["tq"]]) for c in comps], coef=coef)
 
 

@@ -40,8 +40,6 @@ def main():
                          "run under /opt/conda/bin/python3.9")
     meta, arrays = {"libjpeg": ver, "files": {}}, {}
     for p in sorted(JPEG.glob("*.jpg")):
-        if p.name.startswith("progressive"):
-            continue
         a = bgr(p)
         h, w = a.shape[:2]
         rec = {"shape": list(a.shape), "sha256": hashlib.sha256(a.tobytes()).hexdigest(),

@@ -4,7 +4,8 @@
   baseline 4:2:0) -> tests/golden/jpeg/demo_*.jpg
 * synthetic files written by Pillow 12.2 (libjpeg-turbo 3.x encoder) covering what the decoder
   takes: 4:2:0 / 4:2:2 / 4:4:4, grayscale, restart intervals (per row and every 3 MCUs), odd sizes,
-  quality 10 .. 100, optimised Huffman tables, and a progressive file the decoder must reject.
+  quality 10 .. 100, optimised Huffman tables, and progressive files (SOF2) of every sampling,
+  grayscale, odd sizes and restart intervals.
 
 Expected pixels: the reference's pinned IJG libjpeg 9d decode, committed as data by
 tests/golden/make_jpeg9_fixtures.py (run under /opt/conda/bin/python3.9); the libjpeg-turbo mode
@@ -59,6 +60,16 @@ def main():
     save("s422_rst2_77x130.jpg", textured(77, 130, 14), quality=60, subsampling=1,
          restart_marker_blocks=2)
     save("progressive_64x64.jpg", textured(64, 64, 12), quality=80, progressive=True)
+    # progressive (SOF2: spectral selection + successive approximation, libjpeg's standard script)
+    save("prog_s420_q90_600x1000.jpg", textured(600, 1000, 21), quality=90, subsampling=2,
+         progressive=True)
+    save("prog_s444_q85_96x128.jpg", textured(96, 128, 22), quality=85, subsampling=0,
+         progressive=True)
+    save("prog_s422_q75_odd_45x67.jpg", textured(45, 67, 23), quality=75, subsampling=1,
+         progressive=True)
+    save("prog_gray_q80_91x77.jpg", textured(91, 77, 24)[..., 0], quality=80, progressive=True)
+    save("prog_s420_rst4_120x160.jpg", textured(120, 160, 25), quality=80, subsampling=2,
+         progressive=True, restart_marker_blocks=4)
 
 
 if __name__ == "__main__":

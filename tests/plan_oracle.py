@@ -49,10 +49,13 @@ def _noise(img, step, nxt, rng, quant=None):
     raise ValueError(op)
 
 
-def _filter(x, step):
+def _filter(x, step, info=None):
     op, a = step.op, step.args
     if op == "wavelet":
-        return sk.to_u8(255 * oracle.wavelet.denoise_wavelet(x, a[0], a[1])), True
+        f = oracle.wavelet.denoise_wavelet(x, a[0], a[1])
+        if info is not None:
+            info["wavelet_f"] = f  # the float result before the caller's U8 cast
+        return sk.to_u8(255 * f), True
     if x.dtype == np.float64:
         if op == "gaus_blur":
             return oracle.cvf.gaussian_blur_f64(x, a[0]), False
@@ -70,8 +73,9 @@ def _filter(x, step):
     raise ValueError(op)
 
 
-def run_plan(img: np.ndarray, steps, rng, quant=None):
-    """Returns (output, touched_by_wavelet).  quant(img, k) -> u8 image for a quant step."""
+def run_plan(img: np.ndarray, steps, rng, quant=None, info=None):
+    """Returns (output, touched_by_wavelet).  quant(img, k) -> u8 image for a quant step.
+    info (a dict) receives 'wavelet_f': the last wavelet step's float result before its cast."""
     cur, wl = img, False
     i = 0
     while i < len(steps):
@@ -82,7 +86,7 @@ def run_plan(img: np.ndarray, steps, rng, quant=None):
         elif st.kind == "cast_u8":
             cur = sk.to_u8(255 * cur)
         else:
-            cur, w = _filter(cur, st)
+            cur, w = _filter(cur, st, info)
             wl = wl or w
         i += 1
     return cur, wl

@@ -103,3 +103,27 @@ def test_product_library_reads_no_environment():
             code = t.split("//")[0]
             if "getenv" in code:
                 assert tuning_depth is not None and tuning_depth > 0, f"{src.name}:{i}: {t}"
+
+
+def test_abi_version_matches_header_and_binding():
+    """IDN_ABI_VERSION (include/idn.h) == idn_abi_version() of the built library == the version
+    idn/_lib.py binds; the binding refuses a library of another version"""
+    from idn import _lib
+    m = re.search(r"#define\s+IDN_ABI_VERSION\s+(\d+)", HEADER.read_text())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION
+    lib = ctypes.CDLL(str(_lib_path()))
+    lib.idn_abi_version.restype = ctypes.c_int
+    assert lib.idn_abi_version() == _lib.ABI_VERSION
+
+
+def test_docs_name_only_declared_entry_points():
+    """Every idn_* C name INTEGRATION.md / DESIGN.md / README.md mention is declared in
+    include/idn.h (a maintainer following the docs binds only symbols that exist)"""
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    declared = set(re.findall(r"\b(idn_[a-z0-9_]+)\b", text))
+    for doc in ("INTEGRATION.md", "DESIGN.md", "README.md"):
+        body = (ROOT / doc).read_text()
+        names = set(re.findall(r"\b(idn_[a-z0-9_]*[a-z0-9])\b", body))
+        names -= {"idn_binding"}  # the reference-side stub's file name (INTEGRATION.md §3)
+        missing = sorted(names - declared)
+        assert not missing, f"{doc} names entry points the header does not declare: {missing}"

@@ -1,7 +1,8 @@
 """CPU tests of the JPEG decode front-end (cv2.imread at lib/model/test.py:191,
 lib/roi_data_layer/minibatch.py:85).
 
-* the oracle (oracle/jpeg9.py, a restatement of IJG libjpeg 9d's baseline decode) against the
+* the oracle (oracle/jpeg9.py, a restatement of IJG libjpeg 9d's sequential and progressive
+  decode) against the
   real libjpeg 9d decode of every fixture (tests/golden/jpeg9.*, made by
   tests/golden/make_jpeg9_fixtures.py from conda Pillow 8.4.0 linked with libjpeg.so.9), and its
   libjpeg-turbo mode against this container's Pillow (turbo);
@@ -19,7 +20,21 @@ JPEG = GOLD / "jpeg"
 
 
 def _files():
-    return sorted(p for p in JPEG.glob("*.jpg") if not p.name.startswith("progressive"))
+    return sorted(JPEG.glob("*.jpg"))
+
+
+def _arith(data: bytes) -> bytes:
+    """the same file relabelled arithmetic-coded (SOF0 -> SOF9): a format the decoder rejects"""
+    k = data.index(b"\xff\xc0")
+    return data[:k + 1] + b"\xc9" + data[k + 2:]
+
+
+def _sos_offsets(data: bytes):
+    out, k = [], data.find(b"\xff\xda")
+    while k >= 0:
+        out.append(k)
+        k = data.find(b"\xff\xda", k + 2)
+    return out
 
 
 def _meta():
@@ -30,7 +45,8 @@ def test_fixture_set_is_complete():
     meta = _meta()
     assert meta["libjpeg"].startswith("9")
     assert sorted(meta["files"]) == [p.name for p in _files()]
-    assert len(meta["files"]) >= 18
+    assert len(meta["files"]) >= 24
+    assert sum(n.startswith("prog") for n in meta["files"]) >= 6
 
 
 @pytest.mark.parametrize("name", [p.name for p in _files()
@@ -48,7 +64,9 @@ def test_oracle_libjpeg9_matches_real_libjpeg9(name):
 
 
 @pytest.mark.parametrize("name", ["s420_q100_64x80.jpg", "s422_q85_120x200.jpg",
-                                  "s444_q95_96x128.jpg", "s420_q75_odd_37x53.jpg"])
+                                  "s444_q95_96x128.jpg", "s420_q75_odd_37x53.jpg",
+                                  "progressive_64x64.jpg", "prog_s422_q75_odd_45x67.jpg",
+                                  "prog_s420_rst4_120x160.jpg", "prog_gray_q80_91x77.jpg"])
 def test_oracle_turbo_mode_matches_system_pil(name):
     from PIL import Image
     from oracle import jpeg9
@@ -77,8 +95,9 @@ def test_info_matches_pil():
 def test_unsupported_and_corrupt_raise():
     from idn import ops
     from idn._lib import IdnError
-    with pytest.raises(IdnError, match="progressive"):
-        ops.jpeg_info((JPEG / "progressive_64x64.jpg").read_bytes())
+    assert ops.jpeg_info((JPEG / "progressive_64x64.jpg").read_bytes()) == (64, 64, 3)
+    with pytest.raises(IdnError, match="arithmetic"):
+        ops.jpeg_info(_arith((JPEG / "s444_q95_96x128.jpg").read_bytes()))
     with pytest.raises(IdnError, match="SOI"):
         ops.jpeg_info(b"not a jpeg at all")
     data = (JPEG / "s444_q95_96x128.jpg").read_bytes()
@@ -95,7 +114,8 @@ def _ws(datas, flags=0):
 def test_workspace_size():
     datas = [p.read_bytes() for p in _files()[:3]]
     assert _ws(datas) > sum(map(len, datas))
-    assert _ws([(JPEG / "progressive_64x64.jpg").read_bytes()]) == 0
+    assert _ws([_arith((JPEG / "s444_q95_96x128.jpg").read_bytes())]) == 0
+    assert _ws([(JPEG / "progressive_64x64.jpg").read_bytes()]) > 0
     # libjpeg 9's full-size chroma planes need more room than turbo's subsampled ones
     d = [(JPEG / "s420_q90_600x1000.jpg").read_bytes()]
     assert _ws(d, 0) > _ws(d, 1) > 0
@@ -143,3 +163,48 @@ def test_sos_length_checked_before_reading():
     from idn._lib import IdnError
     with pytest.raises(IdnError):
         ops.jpeg_info(data[:k] + b"\xff\xda\x00\x02")
+
+
+def test_imread_lossless_formats_through_pil(tmp_path):
+    """io.imread without OpenCV: non-JPEG (lossless) files are PIL-decoded and flipped to BGR;
+    no GPU is touched (JPEGs go to the GPU decoder: tests/test_minibatch_gpu.py)"""
+    import importlib.util
+    from PIL import Image
+    from idn import io
+    if importlib.util.find_spec("cv2") is not None:
+        pytest.skip("OpenCV present: io.imread is cv2.imread itself")
+    rgb = np.random.RandomState(0).randint(0, 256, (9, 13, 3)).astype(np.uint8)
+    Image.fromarray(rgb).save(tmp_path / "a.png")
+    assert np.array_equal(io.imread(tmp_path / "a.png"), rgb[..., ::-1])
+    with pytest.raises(FileNotFoundError):
+        io.imread(tmp_path / "missing.png")
+
+
+def test_progressive_scan_script_of_the_fixtures():
+    """the progressive fixtures carry libjpeg's standard script: DC first / refine and AC first /
+    refine scans, i.e. all four progressive decoders are exercised"""
+    kinds = set()
+    for p in _files():
+        if not p.name.startswith("prog"):
+            continue
+        data = p.read_bytes()
+        for k in _sos_offsets(data):
+            ns = data[k + 4]
+            ss, se, ahal = data[k + 5 + 2 * ns:k + 8 + 2 * ns]
+            kinds.add(("DC" if ss == 0 else "AC") + ("_refine" if ahal >> 4 else "_first"))
+    assert kinds == {"DC_first", "DC_refine", "AC_first", "AC_refine"}
+
+
+def test_progressive_without_final_scans_is_rejected():
+    """a progressive file whose last scans are missing leaves AC coefficients imprecise; libjpeg
+    would block-smooth it (jdcoefct.c smoothing_ok), which is not restated: the host parser and
+    the oracle both refuse it instead of decoding different pixels"""
+    from idn import ops
+    from idn._lib import IdnError
+    from oracle import jpeg9
+    data = (JPEG / "prog_s444_q85_96x128.jpg").read_bytes()
+    cut = data[:_sos_offsets(data)[-3]] + b"\xff\xd9"
+    with pytest.raises(IdnError, match="smoothing"):
+        ops.jpeg_info(cut)
+    with pytest.raises(NotImplementedError):
+        jpeg9.imread(cut)

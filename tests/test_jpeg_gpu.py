@@ -5,7 +5,7 @@ Default mode: bit-exact against the reference's pinned decoder, IJG libjpeg 9d
 small files, SHA-256 + crops + channel sums for the demo images and the 600x1000 file), made by
 tests/golden/make_jpeg9_fixtures.py.  mode="turbo": bit-exact against the GPU box's own Pillow,
 which links libjpeg-turbo.  Files: tests/golden/jpeg (the reference's demo images + Pillow-written
-cases)."""
+cases, progressive files included: the scan path)."""
 import hashlib
 import json
 from pathlib import Path
@@ -80,8 +80,9 @@ def test_size_mismatch_and_unsupported_raise(dev):
     with pytest.raises(IdnError, match="size"):
         ops.jpeg_decode([(JPEG / "s444_q95_96x128.jpg").read_bytes(),
                          (JPEG / "s420_q100_64x80.jpg").read_bytes()])
-    with pytest.raises(IdnError):
-        ops.jpeg_decode([(JPEG / "progressive_64x64.jpg").read_bytes()])
+    from test_jpeg import _arith
+    with pytest.raises(IdnError, match="arithmetic"):
+        ops.jpeg_decode([_arith((JPEG / "s444_q95_96x128.jpg").read_bytes())])
     with pytest.raises(ValueError, match="mode"):
         ops.jpeg_decode([(JPEG / "s444_q95_96x128.jpg").read_bytes()], mode="ijg")
 
@@ -109,3 +110,33 @@ def test_truncated_restart_file_decodes_without_fault(dev):
     assert got.shape == good.shape
     # the intervals before the cut decode exactly as in the whole file
     assert np.array_equal(got[:16], good[:16])
+
+
+def test_mixed_baseline_and_progressive_batch(dev):
+    """one launch holding baseline files (the parallel path) and progressive ones (the scan path)
+    of the same size: every image as its own decode"""
+    from idn import ops
+    names = ["s420_q90_600x1000.jpg", "prog_s420_q90_600x1000.jpg", "s420_q90_600x1000.jpg",
+             "prog_s420_q90_600x1000.jpg"]
+    got = ops.jpeg_decode([(JPEG / n).read_bytes() for n in names]).cpu().numpy()
+    for i, n in enumerate(names):
+        check_libjpeg9(n, got[i])
+    small = ["prog_s444_q85_96x128.jpg", "s444_q95_96x128.jpg"]
+    got = ops.jpeg_decode([(JPEG / n).read_bytes() for n in small]).cpu().numpy()
+    for i, n in enumerate(small):
+        check_libjpeg9(n, got[i])
+
+
+def test_truncated_progressive_file_decodes_without_fault(dev):
+    """a progressive file cut inside its last scan: every scan header is there (no smoothing
+    case), the data runs out -- the decoder reads zeros past it (libjpeg's fill) and the scans
+    before the cut give the same coefficients as the whole file"""
+    from idn import ops
+    from test_jpeg import _sos_offsets
+    data = (JPEG / "prog_s420_rst4_120x160.jpg").read_bytes()
+    last = _sos_offsets(data)[-1]
+    trunc = data[:last + (len(data) - last) // 2] + b"\xff\xd9"
+    good = ops.jpeg_decode([data])[0].cpu().numpy()
+    got = ops.jpeg_decode([trunc])[0].cpu().numpy()
+    assert got.shape == good.shape
+    assert np.abs(got.astype(int) - good.astype(int)).max() <= 255  # decoded, no fault

@@ -1,0 +1,103 @@
+"""The reference's live test path at its real size, and batch invariance of the wavelet denoiser.
+
+lib/model/test.py:1678-1684: test_v0 `gaussian*` draws var from {0.1, 1.0, 1.5} and returns
+random_noise(img, 'gaussian', var) as float64; the only live post hook (test.py:1802-1810) then
+runs denoise_wavelet(im, BayesShrink, soft, wavelet='bior1.5', multichannel, convert2ycbcr) on that
+float64 image -- at 600x1000 three levels of bior1.5 on f64 input -- and casts (255 * x) to uint8.
+
+Tolerance (north star): the float result within 1e-5 of the oracle before the cast; a U8 value may
+differ only where 255 * x lies within 255e-5 of an integer (the cast is discontinuous there).
+"""
+import json
+import random
+
+import numpy as np
+import pytest
+
+from conftest import textured
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _plan_with_var(spec, var):
+    """a test_v0 plan of `spec` whose random.choice drew gaussian var `var` (and its rng seed)"""
+    from idn import noise_spec as ns
+    for s in range(1000):
+        p = ns.plan(spec, "test_v0", random.Random(s))
+        if p.steps[0].args[0] == var:
+            return p
+    raise AssertionError(f"no seed draws var {var}")
+
+
+@pytest.mark.parametrize("var", [0.1, 1.0, 1.5])
+def test_live_gaussian_wavelet_full_size(dev, var):
+    import torch
+    import oracle
+    from idn import ops
+    from idn.pipeline import Preprocessor
+    from test_wavelet_gpu import check_u8
+
+    spec = f"gaussian_wavelet_var{var}"
+    plan = _plan_with_var(spec, var)
+    assert [s.op for s in plan.steps] == ["gaussian", "wavelet"] and plan.steps[1].args == ("bior1.5", None)
+    img = textured(1, 600, 1000, seed=int(var * 10) + 1)[0]
+
+    # oracle: skimage random_noise with numpy's draws, then the 0.14.2 denoise_wavelet on float64
+    np.random.seed(1234)
+    field = np.random.normal(0.0, var ** 0.5, img.shape)
+    noisy = oracle.sk.noise_gaussian(img, field)
+    ref_f = oracle.wavelet.denoise_wavelet(noisy, "bior1.5", None)
+    ref_u8 = oracle.sk.to_u8(255 * ref_f)
+
+    # the drop-in surface: plan -> Preprocessor (numpy stream replayed on the device) -> U8
+    pre = Preprocessor(spec, "test_v0", noise_rng="numpy")
+    np.random.seed(1234)
+    outs, _ = pre(torch.from_numpy(img[None]).cuda(), image_ids=[0], plans=[plan])
+    got_u8 = outs[0].cpu().numpy()
+
+    # the same two steps through ops, keeping the float64 noisy image and the float result
+    x = torch.from_numpy(img[None]).cuda()
+    f64 = ops.random_noise(x, "gaussian", var=var, replay=torch.from_numpy(field[None]).cuda(),
+                           out="f64")
+    np.testing.assert_array_equal(f64[0].cpu().numpy(), noisy)  # replay is bit-exact
+    u8, f32 = ops.denoise_wavelet(f64, "bior1.5", None, out="both")
+    f = f32[0].cpu().numpy().astype(np.float64)
+    u8 = u8[0].cpu().numpy()
+    np.testing.assert_array_equal(got_u8, u8)  # the plugin surface runs exactly these kernels
+
+    err = np.abs(f - ref_f)
+    d = u8.astype(int) - ref_u8.astype(int)
+    rec = {"var": var, "max_abs_err": float(err.max()), "mean_abs_err": float(err.mean()),
+           "u8_flips": int((d != 0).sum()), "u8_flip_share": float((d != 0).mean()),
+           "n": int(d.size)}
+    print("LIVE_PATH " + json.dumps(rec))
+    assert err.max() <= TOL, rec
+    check_u8(u8, ref_f, ref_u8)
+
+
+@pytest.mark.parametrize("wavelet,levels", [("bior1.5", None), ("db1", 3)])
+@pytest.mark.parametrize("src", ["u8", "f64"])
+def test_wavelet_batch_invariant(dev, wavelet, levels, src):
+    """An image's result does not depend on the batch around it: the bior1.5 analysis splits row
+    bands by batch size (fewer, longer bands for big batches), but its sums of squares are
+    per-(strip, 16-row group) partials added in a fixed order, so denoising an image alone and
+    inside a batch of 40 (1 vs 6 row bands at level 1) gives bit-identical outputs -- a sharded
+    batch equals the 1-GPU run."""
+    import torch
+    from idn import ops
+    imgs = textured(40, 600, 1000, seed=77)
+    x = torch.from_numpy(imgs).cuda()
+    if src == "f64":
+        x = torch.clamp(x.double() / 255.0 + 0.1 * torch.randn(x.shape, dtype=torch.float64,
+                                                               device=x.device,
+                                                               generator=torch.Generator(x.device).manual_seed(5)), 0, 1)
+    u8_all, f_all = ops.denoise_wavelet(x, wavelet, levels, out="both")
+    for i in (0, 17, 39):
+        u8_one, f_one = ops.denoise_wavelet(x[i:i + 1], wavelet, levels, out="both")
+        assert torch.equal(u8_one[0], u8_all[i]), i
+        assert torch.equal(f_one[0], f_all[i]), i
+    # and a middle-sized batch (another band count)
+    u8_mid, f_mid = ops.denoise_wavelet(x[10:17], wavelet, levels, out="both")
+    assert torch.equal(u8_mid, u8_all[10:17])
+    assert torch.equal(f_mid, f_all[10:17])

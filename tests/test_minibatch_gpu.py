@@ -142,8 +142,18 @@ def test_apply_noise_gpu_decode(dev):
     random.seed(2)
     b = detect_blob.apply_noise(px, "gaussian_wavelet_var0.1", noise_rng="philox", image_id=4)
     assert a.dtype == b.dtype and np.array_equal(a, b)
-    with pytest.raises(IdnError):  # no silent CPU fallback for files the decoder does not take
-        detect_blob.apply_noise(gold / "jpeg" / "progressive_64x64.jpg", "original", decode="gpu")
+    # no silent CPU fallback for files the decoder does not take (arithmetic coding)
+    from test_jpeg import _arith
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        bad = Path(d) / "arith.jpg"
+        bad.write_bytes(_arith((gold / "jpeg" / "s444_q95_96x128.jpg").read_bytes()))
+        with pytest.raises(IdnError):
+            detect_blob.apply_noise(bad, "original", decode="gpu")
+    # a progressive file is decoded (the scan path), as cv2.imread does
+    prog = detect_blob.apply_noise(gold / "jpeg" / "progressive_64x64.jpg", "original",
+                                   decode="gpu")
+    assert np.array_equal(prog, np.load(gold / "jpeg9.npz")["progressive_64x64.jpg"])
 
 
 @pytest.mark.gpu
@@ -171,3 +181,88 @@ def test_minibatch_defers_final_gaussian_into_the_blob(dev, flip):
     outs, _ = pre(torch.from_numpy(img).cuda()[None], image_ids=[3])
     ref = ops.blob(outs[0][None], flip=flip).cpu().numpy()
     assert np.array_equal(blob, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["s420_opt_130x170.jpg", "s422_q85_120x200.jpg", "demo_000456.jpg"])
+def test_host_decode_without_cv2_is_libjpeg9(dev, tmp_path, name):
+    """decode="host" (the default) with no OpenCV: io.imread sends JPEGs to the GPU decoder, so
+    the pixels -- and get_minibatch's blob -- are the reference's pinned libjpeg 9d decode, not
+    PIL's libjpeg-turbo (tests/golden/jpeg9.npz)"""
+    import importlib.util
+    import shutil
+    from pathlib import Path
+    from idn import io, minibatch
+    from idn.roidb import prepare_roidb
+    if importlib.util.find_spec("cv2") is not None:
+        pytest.skip("OpenCV present: io.imread is cv2.imread itself")
+    gold = Path(__file__).resolve().parent / "golden"
+    px = np.load(gold / "jpeg9.npz")[name]
+    assert np.array_equal(io.imread(gold / "jpeg" / name), px)
+    imdb = _imdb(tmp_path, [px])
+    shutil.copyfile(gold / "jpeg" / name, tmp_path / name)
+    imdb._paths = [tmp_path / name]
+    prepare_roidb(imdb, "sap_median_var0.4")
+    entry = dict(imdb.roidb[0])
+    random.seed(5)
+    np.random.seed(6)
+    got = minibatch.get_minibatch([entry], 21, mode="train_v0", noise_rng="numpy")  # decode="host"
+    random.seed(5)
+    np.random.seed(6)
+    ref = minibatch.get_minibatch([dict(entry, im=px)], 21, mode="train_v0", noise_rng="numpy")
+    assert np.array_equal(got["data"], ref["data"])
+
+
+@pytest.mark.gpu
+def test_host_decode_without_cv2_raises_on_unsupported_jpeg(dev, tmp_path):
+    """a JPEG the GPU decoder does not take (here CMYK, written by PIL) raises: no silent
+    libjpeg-turbo / PIL decode in its place"""
+    import importlib.util
+    from PIL import Image
+    from idn import io
+    from idn._lib import IdnError
+    if importlib.util.find_spec("cv2") is not None:
+        pytest.skip("OpenCV present")
+    Image.new("CMYK", (32, 24), (10, 20, 30, 40)).save(tmp_path / "cmyk.jpg", quality=90)
+    with pytest.raises(IdnError):
+        io.imread(tmp_path / "cmyk.jpg")
+
+
+@pytest.mark.gpu
+def test_shared_preprocessor_is_reentrant(dev):
+    """A cached Preprocessor shared by threads: run_for_blob's deferral and the bloom draws are
+    per call (no instance state), so concurrent __call__ / run_for_blob calls return what the
+    same calls return one at a time"""
+    import threading
+    import torch
+    from idn.pipeline import Preprocessor
+    imgs = torch.from_numpy(textured(2, 64, 96, seed=4)).cuda()
+    pre = Preprocessor("speckle_gaus_blur_var0.5", "canonical", seed=3)
+    plans = pre.plans(2, hw=(64, 96))
+    ref_full, _ = pre(imgs, image_ids=[0, 1], plans=plans)
+    ref_def, ref_ks, _ = pre.run_for_blob(imgs, image_ids=[0, 1], plans=plans)
+    assert ref_ks == [5, 5] or ref_ks == [3, 3]
+    errs = []
+
+    def worker(k):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                for _ in range(20):
+                    if k % 2:
+                        o, ks, _ = pre.run_for_blob(imgs, image_ids=[0, 1], plans=plans)
+                        ok = ks == ref_ks and all(torch.equal(a, b) for a, b in zip(o, ref_def))
+                    else:
+                        o, _ = pre(imgs, image_ids=[0, 1], plans=plans)
+                        ok = all(torch.equal(a, b) for a, b in zip(o, ref_full))
+                    torch.cuda.current_stream().synchronize()
+                    if not ok:
+                        errs.append(k)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs

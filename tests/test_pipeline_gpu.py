@@ -63,7 +63,8 @@ def test_plan_parity(dev, mode, spec):
     np.random.seed(123)
     orng = random.Random(77)
     for i, p in enumerate(plans):
-        ref, wl = run_plan(imgs[i], p.steps, orng, quant=_quant_checker(pre.seed, i))
+        info = {}
+        ref, wl = run_plan(imgs[i], p.steps, orng, quant=_quant_checker(pre.seed, i), info=info)
         got = outs[i].cpu().numpy()
         assert got.dtype == ref.dtype == (np.uint8 if p.out_dtype == "u8" else np.float64), p
         if got.dtype == np.float64:
@@ -73,14 +74,21 @@ def test_plan_parity(dev, mode, spec):
         has_bil = any(s.op == "bilateral" for s in p.steps)
         has_bloom = any(s.op == "bloom" for s in p.steps)
         if wl:
-            # wavelet vs numpy within the north-star 1e-5 (bior1.5 synthesises in fp32, ~3e-7):
-            # a U8 cast flips only where 255*x sits within 255e-5 of an integer, at most ~0.5 %
-            # of the values per wavelet step (<= 1 LSB); train_v0's double filtering (closure
-            # wavelet + hook wavelet) feeds such a flipped pixel into the second wavelet, whose
-            # output moves by a fraction of an LSB around it, so the bound is one LSB per wavelet
-            # step and the flip share 5e-3 per step
             n_wl = sum(s.op == "wavelet" for s in p.steps)
-            assert d.max() <= n_wl and (d > 0).mean() < 5e-3 * n_wl, (p, d.max(), (d > 0).mean())
+            share = float((d > 0).mean())
+            print(f"PLAN_FLIPS {mode} {spec} image {i}: {n_wl} wavelet step(s), "
+                  f"max {int(d.max())}, share {share:.3e}")
+            if n_wl == 1 and p.steps[-1].op == "wavelet":
+                # wavelet vs numpy within the north-star 1e-5 (bior1.5 synthesises in fp32,
+                # ~3e-7): the U8 cast may flip only where 255*x lies within 255e-5 of an integer
+                from test_wavelet_gpu import check_u8
+                check_u8(got, info["wavelet_f"], ref)
+            else:
+                # train_v0's double filtering (closure wavelet + hook wavelet): a value flipped at
+                # the first cast feeds the second wavelet, whose output moves by a fraction of an
+                # LSB around it -- no boundary rule holds after the second step.  Bound: one LSB
+                # per wavelet step, and the share measured on the GPU (profiles/r04/plan_flips.txt)
+                assert d.max() <= n_wl and share < 5e-3 * n_wl, (p, d.max(), share)
         elif has_bil or has_bloom:
             assert d.max() <= 1 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
         else:
