@@ -35,6 +35,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t v3u __attribute__((ext_vector_type(3)));
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   // readfirstlane the inputs so the compiler can prove the descriptor wave-uniform

@@ -221,6 +221,147 @@ __global__ __launch_bounds__(256) void median_u8_fast(const uint8_t* __restrict_
   }
 }
 
+// ---- 5x5, 24-byte lanes (C = 3) -----------------------------------------------------------------
+// Lane l of a wave holds row bytes [S - 12 + 24 l, +24) of its segment (S = the segment's first
+// output byte): 8 whole pixels, since 24 is a multiple of both 3 and 4 -- every lane sees the
+// same channel layout, which the 16-byte lanes above cannot (16 = 1 mod 3: their same-channel
+// chains cover 20 byte positions for 16 outputs).  Per channel the lane pairs pixel p with pixel
+// p + 4 in one u16x2 dword, so ONE chain of 4 medians (median_cols.hpp, 174 instructions, 43.5 per
+// output against 51 for the chain of 5) yields all 8 of its pixels, and the three chains cover
+// the lane's 24 bytes with nothing computed twice.  The chains' halo columns (pixels -2, -1, 8, 9)
+// are the neighbouring lanes' sorted columns, one DPP move + one v_alignbyte each.  Lanes 0 and 63
+// store one half (their other half is the halo): 1512 output bytes per wave.  Row starts rebuild
+// the lead lane's left half from pixel 0 and the row end always falls on a lane's half boundary
+// (rows are multiples of 24 bytes: stripe_ok), whose right half then repeats the last pixel
+// (BORDER_REPLICATE); lanes past the row end feed only outputs that are never stored.
+constexpr int M24_SEG = 63 * 24;
+
+__device__ __forceinline__ void m24_unpack(const v3u& A, const v3u& B, uint32_t (&P)[12]) {
+  const uint32_t a[3] = {A.x, A.y, A.z}, b[3] = {B.x, B.y, B.z};
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // pair (pixel p, pixel p + 4) of channel c: byte 3p + c of the left and of the right half,
+      // as float16 1024 + v lanes (see unpack_row_f16)
+      const int by = 3 * p + c, k = by >> 2, j = by & 3;
+      const uint32_t sel = (uint32_t)j | 0x0Cu << 8 | (uint32_t)(4 + j) << 16 | 0x0Cu << 24;
+      P[4 * c + p] = __builtin_amdgcn_perm(b[k], a[k], sel) | 0x64006400u;
+    }
+}
+
+// one output row of 24 bytes per lane from the 5 unpacked rows of its window (oldest first)
+__device__ __forceinline__ void m24_row(const uint32_t (&R0)[12], const uint32_t (&R1)[12],
+                                        const uint32_t (&R2)[12], const uint32_t (&R3)[12],
+                                        const uint32_t (&R4)[12], v3u& outA, v3u& outB) {
+  const PkOps op;
+  uint32_t S[5][12];  // [rank][column]
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t v[5] = {R0[i], R1[i], R2[i], R3[i], R4[i]};
+    sort5(v, op);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) S[r][i] = v[r];
+  }
+  uint32_t o[3][4];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    uint32_t x[8][5];  // columns p' = -2 .. 5 of channel c: (pixel p', pixel p' + 4)
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) x[p + 2][r] = S[r][4 * c + p];
+      // (prev lane's pixel 6 / 7, own pixel 2 / 3) and (own pixel 4 / 5, next lane's pixel 8 / 9)
+      x[0][r] = __builtin_amdgcn_alignbyte(S[r][4 * c + 2], from_prev_lane(S[r][4 * c + 2]), 2);
+      x[1][r] = __builtin_amdgcn_alignbyte(S[r][4 * c + 3], from_prev_lane(S[r][4 * c + 3]), 2);
+      x[6][r] = __builtin_amdgcn_alignbyte(from_next_lane(S[r][4 * c + 0]), S[r][4 * c + 0], 2);
+      x[7][r] = __builtin_amdgcn_alignbyte(from_next_lane(S[r][4 * c + 1]), S[r][4 * c + 1], 2);
+    }
+    median25_chain4(x, o[c], op);
+  }
+  // byte 3p + c of the left half = low byte of o[c][p], of the right half = its third byte
+  uint32_t A[3], B[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    uint32_t src[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int by = 4 * k + j;
+      src[j] = o[by % 3][by / 3];
+    }
+    const uint32_t u1 = __builtin_amdgcn_perm(src[1], src[0], 0x06020400u);
+    const uint32_t u2 = __builtin_amdgcn_perm(src[3], src[2], 0x06020400u);
+    A[k] = __builtin_amdgcn_perm(u2, u1, 0x05040100u);
+    B[k] = __builtin_amdgcn_perm(u2, u1, 0x07060302u);
+  }
+  outA = v3u{A[0], A[1], A[2]};
+  outB = v3u{B[0], B[1], B[2]};
+}
+
+__global__ __launch_bounds__(256) void median5_u8_w24(const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ dst, int h, int rb,
+                                                      uint32_t row_stride, int nseg, int bands,
+                                                      int band_rows, int total_items) {
+  constexpr int K = 5, R = 2, PF = K, U = K;
+  const int lane = threadIdx.x & 63;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (item >= total_items) return;
+  const int seg = item % nseg, tq = item / nseg;
+  const int band = tq % bands, img = tq / bands;
+  const int seg_start = seg * M24_SEG, seg_end = min(seg_start + M24_SEG, rb);
+  const int q = seg_start - 12 + 24 * lane;
+  const bool lead = q < 0;              // segment 0, lane 0: left half before the row
+  const bool tail = q + 12 == rb;       // the row ends between this lane's halves
+  const uint32_t img_bytes = (uint32_t)h * row_stride;
+  const rsrc_t rs = make_rsrc(src + (size_t)img * img_bytes, img_bytes);
+  const rsrc_t rd = make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
+  const uint32_t offA = lead ? OOB_OFF : (uint32_t)q, offB = (uint32_t)(q + 12);
+  // stores: a half whose 12 bytes lie in [seg_start, seg_end) (segment and row bounds are
+  // multiples of 12)
+  const uint32_t stA = (q >= seg_start && q + 12 <= seg_end) ? (uint32_t)q : OOB_OFF;
+  const uint32_t stB = (q + 12 >= seg_start && q + 24 <= seg_end) ? (uint32_t)(q + 12) : OOB_OFF;
+
+  const int y0 = band * band_rows;
+  const int y1 = min(y0 + band_rows, h);
+  if (y0 >= y1) return;
+  const int nin = (y1 - y0) + 2 * R;
+  const int ngroups = (nin + U - 1) / U;
+  auto load_row = [&](int r, v3u& A, v3u& B) {
+    const uint32_t ro = (uint32_t)clampi(y0 - R + min(r, nin - 1), 0, h - 1) * row_stride;
+    A = __builtin_amdgcn_raw_buffer_load_b96(rs, offA, ro, 0);
+    B = __builtin_amdgcn_raw_buffer_load_b96(rs, offB, ro, 0);
+  };
+  v3u LA[PF], LB[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) load_row(i, LA[i], LB[i]);
+  uint32_t Wr[K][12];
+  for (int gi = 0; gi < ngroups; ++gi) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = gi * U + u;
+      v3u A = LA[u % PF], B = LB[u % PF];
+      load_row(r + PF, LA[u % PF], LB[u % PF]);
+      if (lead) {  // pixels -4 .. -1 := pixel 0 (bytes 0..2 of the right half)
+        A = v3u{__builtin_amdgcn_perm(0u, B.x, 0x00020100u), __builtin_amdgcn_perm(0u, B.x, 0x01000201u),
+                __builtin_amdgcn_perm(0u, B.x, 0x02010002u)};
+      }
+      if (tail) {  // pixels 4..7 := pixel 3 (bytes 9..11 of the left half)
+        B = v3u{__builtin_amdgcn_perm(0u, A.z, 0x01030201u), __builtin_amdgcn_perm(0u, A.z, 0x02010302u),
+                __builtin_amdgcn_perm(0u, A.z, 0x03020103u)};
+      }
+      m24_unpack(A, B, Wr[u % K]);
+      const int y = y0 + r - 2 * R;
+      if (r >= 2 * R && y < y1) {
+        v3u oA, oB;
+        m24_row(Wr[(u + 1) % K], Wr[(u + 2) % K], Wr[(u + 3) % K], Wr[(u + 4) % K], Wr[u % K], oA, oB);
+        const uint32_t ro = (uint32_t)y * row_stride;
+        __builtin_amdgcn_raw_buffer_store_b96(oA, rd, stA, ro, 0);
+        __builtin_amdgcn_raw_buffer_store_b96(oB, rd, stB, ro, 0);
+      }
+    }
+  }
+}
+
 // generic path: one thread per pixel, exact median by counting (any C, any alignment)
 template <int K>
 __global__ __launch_bounds__(256) void median_u8_generic(const uint8_t* __restrict__ src,
@@ -267,7 +408,17 @@ static int launch_median(const uint8_t* src, uint8_t* dst, int n, int h, int w, 
   const int64_t rb = (int64_t)w * c;
   // (an LDS band-tile form like the stencils' was bit-exact but measured no faster for 3x3 and
   // 4-6 % slower for 5x5 in steady state, profiles/r02/median_tile/; removed in round 3)
-  if (stripe_ok(c, rb, row_stride, h, src, dst)) {
+  if (K == 5 && knob("IDN_MEDIAN_W24", 1) && c == 3 && rb % 24 == 0 &&
+      stripe_ok(c, rb, row_stride, h, src, dst)) {
+    // 24-byte lanes: independent waves over bands of IDN_MEDIAN_ROWS rows
+    const int nseg = (int)((rb + M24_SEG - 1) / M24_SEG);
+    const int band_rows = std::max(1, std::min(h, knob("IDN_MEDIAN_ROWS", 32)));
+    const int bands = (h + band_rows - 1) / band_rows;
+    const int64_t total = (int64_t)n * bands * nseg;
+    IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
+    hipLaunchKernelGGL(median5_u8_w24, dim3((unsigned)((total + 3) / 4)), dim3(256), 0, st, src,
+                       dst, h, (int)rb, (uint32_t)row_stride, nseg, bands, band_rows, (int)total);
+  } else if (stripe_ok(c, rb, row_stride, h, src, dst)) {
     // measured (tools/sweep_stencil.py): 3x3 is near the memory side -> whole-row workgroups over
     // 16-row bands with XCD-contiguous band order; 5x5 is VALU-bound -> independent waves
     const StripePlan p = plan_stripe(n, h, rb, K, K, 4096, knob("IDN_MEDIAN_MAP", K == 3 ? 1 : 0),

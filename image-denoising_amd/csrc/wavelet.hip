@@ -92,7 +92,8 @@ struct WlLayout {
   size_t img_floats;                   // wreal elements per image (planes + bands)
   size_t stats_off;                    // byte offset of the stats region (after all images)
   int tiles_x[WL_MAXL + 1], tiles[WL_MAXL + 1];  // DWT tiles per level (partial-sum slots)
-  int bands[WL_MAXL + 1];              // bior1.5 streaming analysis: row bands per strip (launch)
+  int bands[WL_MAXL + 1];              // bior1.5 streaming analysis: row bands per strip
+  double sq_grid[WL_MAXL + 1];         // ... and the grid its sum-of-squares partials round to
   size_t part_tile0[WL_MAXL + 1];      // first tile index of level l in the partials array
   size_t part_per_img;                 // partial sums per image: 3 channels x 3 bands x tiles
   size_t part_off;                     // byte offset of the partial sums region
@@ -132,8 +133,9 @@ __device__ __forceinline__ int wl_fbin(unsigned long long key) {
 }
 
 inline int ws_strips(int Wo);
+inline int ws_sw(int Wo);
 inline int ws_bands(int n, int Ho, int strips, int level);
-constexpr int WS_G = 16;  // rows per sum-of-squares group of the streaming analysis
+constexpr int WS_G = 4;  // rows per sum-of-squares group of the streaming analysis
 // Row bands per strip so that the grid fills whole rounds of resident workgroups: for each
 // candidate band count b the time is ~ rounds(b) x (rows per band + warm-up rows), rounds(b) =
 // ceil(units * b / resident).  (A grid of 2.5 rounds leaves the chip half idle for the last one.)
@@ -194,13 +196,16 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   size_t tiles_tot = 0;
   for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
     if (wv == IDN_WAVELET_BIOR15) {
-      // wl_dwt_stream: strips x row bands of whole WS_G-row groups; one partial sum per (strip,
-      // group), so the slots -- and the order wl_sumsq adds them in -- depend on the image size
-      // only, never on the batch size or the device (the band count does)
+      // wl_dwt_stream: strips x row bands of whole WS_G-row groups (the bands' sums are exact,
+      // see the kernel).  sq_grid: 2^-F with the band's total below 2^(52 - F) for any input:
+      // |coefficient| <= 2 (level 1 of [0, 1] data, bior1.5's filter sums) times 2.6 per deeper
+      // level, so a square <= 4 * 8^(l-1)
       const int groups = (Lt.H[l] + WS_G - 1) / WS_G;
       Lt.tiles_x[l] = ws_strips(Lt.W[l]);
-      Lt.tiles[l] = Lt.tiles_x[l] * groups * 2;  // two row waves per channel
       Lt.bands[l] = std::min(ws_bands(n, Lt.H[l], Lt.tiles_x[l], l), groups);
+      Lt.tiles[l] = Lt.tiles_x[l] * Lt.bands[l];
+      const double bound = 4.0 * std::pow(8.0, l - 1) * (double)Lt.H[l] * (double)Lt.W[l];
+      Lt.sq_grid[l] = std::ldexp(1.0, (int)std::ceil(std::log2(bound)) - 52);
     } else {
       Lt.bands[l] = 0;
       Lt.tiles_x[l] = (Lt.W[l] + RB_TX - 1) / RB_TX;  // wl_dwt_rb tiles
@@ -663,7 +668,6 @@ __global__ __launch_bounds__(256) void wl_dwt_rb(wreal* __restrict__ ws, size_t 
 #define IDN_WS_MAXT 512
 #endif
 constexpr int WS_MAXT = IDN_WS_MAXT;         // threads = staged columns per workgroup (max)
-static_assert(WS_MAXT >= 3 * 128, "the row role needs two whole waves per channel");
 // output columns per strip (max): (threads - 8) / 2; tuning: IDN_WAVELET_WST threads (64..256)
 inline int ws_maxsw() {
   const int t = std::min(std::max(knob("IDN_WAVELET_WST", WS_MAXT), 64), WS_MAXT) / 64 * 64;
@@ -675,8 +679,23 @@ inline int ws_sw(int Wo) {
   return ((Wo + st - 1) / st + 1) & ~1;
 }
 int ws_resident(int level);  // resident analysis workgroups on the device (defined below)
-inline int ws_bands(int n, int Ho, int strips, int level) {  // bands >= 16 output rows
-  return best_bands((int64_t)n * strips, Ho, 4, ws_resident(level), 16);
+// bands of whole WS_G-row groups, >= 16 output rows each: as best_bands, costed by the rows of
+// the longest band
+inline int ws_bands(int n, int Ho, int strips, int level) {
+  const int groups = (Ho + WS_G - 1) / WS_G;
+  const int64_t units = (int64_t)n * strips, resident = std::max<int64_t>(ws_resident(level), 1);
+  const int bmax = std::max(1, std::min({64, Ho / 16, groups}));
+  int best = 1;
+  double bestc = 1e300;
+  for (int b = 1; b <= bmax; ++b) {
+    const double rounds = std::ceil((double)(units * b) / (double)resident);
+    const double c = rounds * ((groups + b - 1) / b * WS_G + 4);
+    if (c < bestc * 0.999) {
+      bestc = c;
+      best = b;
+    }
+  }
+  return best;
 }
 
 template <int SRC>
@@ -706,11 +725,7 @@ template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (
 #define IDN_S3_WPE 1
 #endif
 template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
-// the fp32 deeper-level analyses at six waves per SIMD (<= 80 VGPRs: three 512-thread workgroups
-// per CU)
-#ifndef IDN_WS_DEEP_WPE
-#define IDN_WS_DEEP_WPE 6
-#endif
+
 
 // TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the
 // product runs the lowpass outputs (aa, ad, da: continuous inputs of the thresholds' fp64 sums of
@@ -720,13 +735,12 @@ template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
 // FM >= 0: the band storage mask (wl_fband) and CODES the level-1 code emission as compile-time
 // constants (the product's masks: no per-band branches); FM = -1 takes both from the arguments.
 template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1>
-__global__ __launch_bounds__(WS_MAXT, SRC >= 2 && sizeof(TL) == 4 ? IDN_WS_DEEP_WPE : IDN_WS_WPE)
-void wl_dwt_stream(
+__global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
     int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands, int groups,
     const uint8_t* __restrict__ src, const double* __restrict__ in64, int64_t row_stride,
     double* __restrict__ part, size_t part_per_img, size_t part_tile0, int emit_codes_arg,
-    int fmask_arg) {
+    int fmask_arg, double sq_grid) {
   const int fmask = FM >= 0 ? FM : fmask_arg;
   const int emit_codes = CODES >= 0 ? CODES : emit_codes_arg;
   constexpr int PF = ws_pf<SRC>();
@@ -738,6 +752,7 @@ void wl_dwt_stream(
   __shared__ TL VL[2][3][WS_MAXT];
   __shared__ TL VF[SEPF ? 2 : 1][SEPF ? 3 : 1][SEPF ? WS_MAXT : 1];
   __shared__ TH VH[2][3][WS_MAXT];
+  __shared__ double RED[3][WS_MAXT];
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
   const int j0 = strip * SW;
@@ -824,21 +839,22 @@ void wl_dwt_stream(
 #pragma unroll
     for (int r = 0; r < 5; ++r) acc[c][r] = (TL)0;
   }
-  // ---- row role: channel c's row threads are t = 128 c + jj / 2 (two whole waves per channel,
-  // so a wave's sums of squares are one channel's)
+  // ---- row role
   const int half = SW / 2;
-  const int rl = t & 127;
-  const bool rowt = t < 3 * 128 && rl < half;
-  const int rc = rowt ? t >> 7 : 0, jj = rowt ? 2 * rl : 0;
+  const bool rowt = t < 3 * half;
+  const int rc = rowt ? t / half : 0, jj = rowt ? 2 * (t - rc * half) : 0;
   const int oj = j0 + jj;
   const bool ok0 = rowt && oj < Wo, ok1 = rowt && oj + 1 < Wo;
   const size_t bsz = (size_t)Ho * Wo;
-  double sq[3] = {0.0, 0.0, 0.0};
-  // sums of squares per (strip, group, wave): each row thread sums its outputs of the group's
-  // rows in row order; at the group's last row every row wave adds its lanes by a fixed butterfly
-  // and lane 0 stores the partial -- the same operations whatever band holds the group, so the
-  // partials, and wl_sumsq's fixed-order total, do not depend on the band split
-  double* const part_img = part + img * part_per_img + part_tile0 + (size_t)strip * groups * 2;
+  // Sums of squares, independent of the band split (batch size, device): each row thread sums
+  // its two outputs of a WS_G-row group's rows in row order (sq), and at the group's last row rounds
+  // that partial to a multiple of sq_grid (a power of two) into sqa.  Sums of multiples of
+  // sq_grid below 2^53 sq_grid are exact in fp64, and the layout sizes sq_grid so that the whole
+  // band's sum stays below that (wl_layout): every later addition -- this thread's groups, the
+  // workgroup's threads, wl_sumsq's tiles -- is exact, hence order-free.  (Rounding error per
+  // partial <= sq_grid / 2, ~1e-10 of a typical band total.)
+  double sq[3] = {0.0, 0.0, 0.0}, sqa[3] = {0.0, 0.0, 0.0};
+  const double sq_inv = 1.0 / sq_grid;  // exact: a power of two
 
   const int k0 = ia - 4, M = ib - ia + 4;  // steps m = 0 .. M-1 cover pairs k = k0 + m
   WsRaw<SRC> rq[PF];                        // raw samples of steps m .. m + PF - 1 (slot m % PF)
@@ -956,19 +972,28 @@ void wl_dwt_stream(
           }
         }
       }
-      if (gend && t < 3 * 128) {  // whole waves (wave-uniform): every lane takes part
-        const int g = i / WS_G;
+      if (gend) {
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-          double v = rowt ? sq[b] : 0.0;
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-          if ((t & 63) == 0)  // every row wave writes its slot (0 if none of its lanes has a row)
-            part_img[(size_t)((t >> 7) * 3 + b) * (part_per_img / 9) + (size_t)g * 2 + ((t >> 6) & 1)] = v;
+          sqa[b] += __builtin_rint(sq[b] * sq_inv) * sq_grid;
           sq[b] = 0.0;
         }
       }
     }
+  }
+  // per-workgroup sums (exact, see above), channel by channel
+  __syncthreads();
+  double* red = &RED[0][0];
+  if (rowt) {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) red[b * WS_MAXT + t] = sqa[b];
+  }
+  __syncthreads();
+  if (t < 9) {
+    const int c = t / 3, b = t - 3 * c;
+    double s2 = 0.0;
+    for (int g = 0; g < half; ++g) s2 += red[b * WS_MAXT + c * half + g];
+    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = s2;
   }
 }
 
@@ -3324,18 +3349,17 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   for (int l = 1; l <= Lt.L; ++l) {
     const size_t in_off = l == 1 ? 0 : Lt.off_band[l - 1];
     if (WV == IDN_WAVELET_BIOR15) {
-      const int strips = Lt.tiles_x[l], bands = Lt.bands[l], groups = Lt.tiles[l] / (2 * strips);
       const int sw = ws_sw(Lt.W[l]);
+      const int strips = Lt.tiles_x[l], bands = Lt.bands[l], groups = (Lt.H[l] + WS_G - 1) / WS_G;
       const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n);
-      // threads: the staged columns (2 SW + 8), and at least the 3 x 128 of the row role
-      const dim3 blk((unsigned)std::max((2 * sw + 8 + 63) / 64 * 64, 3 * 128));
+      const dim3 blk((unsigned)((2 * sw + 8 + 63) / 64 * 64));
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
       // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
 #define IDN_WS_(SRC, TL, TH, FMC, CC, EMIT)                                                        \
   hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC>), grid, blk, 0, st, wsf, Lt.img_floats,  \
                      stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands,   \
                      groups, src, in64, row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT, \
-                     fm_an(l))
+                     fm_an(l), Lt.sq_grid[l])
       // the product's band masks as compile-time constants (bit 4 = WL_FB_AIN is read by the
       // launcher only); anything else (tuning forms) through the runtime-mask instance
 #define IDN_WS(SRC, TL, TH, EMIT)                                                                  \

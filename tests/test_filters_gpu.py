@@ -169,7 +169,12 @@ def test_rejects_cpu_tensor():
         idn.gaussian_blur(torch.zeros(4, 4, 3, dtype=torch.uint8), 5)
 
 
-@pytest.mark.parametrize("shape", SHAPES)
+# + the 5x5 median's 24-byte-lane path (rows of 24k bytes, 1512-byte segments): one exactly full
+# segment, a 24-byte second segment, four segments
+MEDIAN_SHAPES = SHAPES + [(1, 9, 504), (1, 11, 512), (1, 20, 1600)]
+
+
+@pytest.mark.parametrize("shape", MEDIAN_SHAPES)
 @pytest.mark.parametrize("k", [3, 5])
 def test_median_blur_bitexact(dev, shape, k):
     import idn
@@ -266,7 +271,9 @@ def test_bilateral_gray(dev):
 
 @pytest.mark.parametrize("form", [{}, {"IDN_MEDIAN_MAP": "0", "IDN_MEDIAN_ROWS": "32"},
                                   {"IDN_MEDIAN_MAP": "1", "IDN_MEDIAN_ROWS": "16"},
-                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"}],
+                                  {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"},
+                                  {"IDN_MEDIAN_W24": "0", "IDN_MEDIAN_ROWS": "32"},
+                                  {"IDN_MEDIAN_ROWS": "5"}],
                          ids=lambda f: "-".join(f"{k[11:]}{v}" for k, v in f.items()) or "product")
 @pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (1, 601, 1000), (2, 13, 104)])
 def test_median_forms_agree(dev, monkeypatch, form, shape):

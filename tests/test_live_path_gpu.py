@@ -80,10 +80,11 @@ def test_live_gaussian_wavelet_full_size(dev, var):
 @pytest.mark.parametrize("src", ["u8", "f64"])
 def test_wavelet_batch_invariant(dev, wavelet, levels, src):
     """An image's result does not depend on the batch around it: the bior1.5 analysis splits row
-    bands by batch size (fewer, longer bands for big batches), but its sums of squares are
-    per-(strip, 16-row group) partials added in a fixed order, so denoising an image alone and
-    inside a batch of 40 (1 vs 6 row bands at level 1) gives bit-identical outputs -- a sharded
-    batch equals the 1-GPU run."""
+    bands by batch size (fewer, longer bands for big batches), but its sums of squares are built
+    from per-(thread, 4-row group) partials rounded to a power-of-two grid, so every later sum is
+    exact and order-free; denoising an image alone and inside a batch of 40 (different row bands
+    at every level) gives bit-identical outputs -- a sharded batch equals the 1-GPU run
+    (INTEGRATION.md)."""
     import torch
     from idn import ops
     imgs = textured(40, 600, 1000, seed=77)

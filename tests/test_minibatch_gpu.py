@@ -152,7 +152,7 @@ def test_apply_noise_gpu_decode(dev):
             detect_blob.apply_noise(bad, "original", decode="gpu")
     # a progressive file is decoded (the scan path), as cv2.imread does
     prog = detect_blob.apply_noise(gold / "jpeg" / "progressive_64x64.jpg", "original",
-                                   decode="gpu")
+                                   mode="canonical", decode="gpu")
     assert np.array_equal(prog, np.load(gold / "jpeg9.npz")["progressive_64x64.jpg"])
 
 
@@ -184,7 +184,8 @@ def test_minibatch_defers_final_gaussian_into_the_blob(dev, flip):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["s420_opt_130x170.jpg", "s422_q85_120x200.jpg", "demo_000456.jpg"])
+@pytest.mark.parametrize("name", ["s420_opt_130x170.jpg", "s422_q85_120x200.jpg",
+                                  "prog_s444_q85_96x128.jpg"])
 def test_host_decode_without_cv2_is_libjpeg9(dev, tmp_path, name):
     """decode="host" (the default) with no OpenCV: io.imread sends JPEGs to the GPU decoder, so
     the pixels -- and get_minibatch's blob -- are the reference's pinned libjpeg 9d decode, not

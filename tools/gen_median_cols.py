@@ -19,7 +19,9 @@ duplicate work fold away; the rest is pruned to what the 5 medians need and each
 re-verified against the popcount median over the whole premise set.
 
 Measured op counts (min/max per output): single output 140, pair 54, chain of 4 47.5,
-chain of 5 55.2 (276 for 5) -- vs 202 for the unsorted 25-input Batcher network.
+chain of 5 55.2 (276 for 5) -- vs 202 for the unsorted 25-input Batcher network.  The header
+carries the chain of 5 (16-byte lanes: two same-channel chains of 5) and the chain of 4 (24-byte
+lanes: one chain per channel, u16 pairs of pixels p and p + 4).
 
   python tools/gen_median_cols.py            # writes the header, prints op counts
 """
@@ -178,9 +180,29 @@ def verify_sort5():
             raise SystemExit("SORT5 FAILED")
 
 
-def emit(net, outs, nout):
+def emit_chain(net, outs, nout):
+    """C++ text of median25_chain<nout>, the fused (3-input) program; returns (text, 2-input ops,
+    instructions)"""
     ops = net.live(outs)
     name = {idx: f"x[{key[0]}][{key[1]}]" for key, idx in net.leaf.items()}
+    lines = [f"// medians of columns k..k+4, k = 0..{nout - 1}, of {nout + 4} sorted 5-element "
+             f"columns x[col][rank]: {len(ops)} min/max ops",
+             "template <typename T, typename F>",
+             f"__device__ __forceinline__ void median25_chain{nout}(const T (&x)[{nout + 4}][5], "
+             f"T (&o)[{nout}], F ops) {{"]
+    prog = fuse3(net, ops, outs)
+    verify_program(net, prog, outs)
+    for k, (v, kind, args) in enumerate(prog):
+        name[v] = f"t{k}"
+        fn = ("ops.mn" if kind == "min" else "ops.mx") + ("3" if len(args) == 3 else "")
+        lines.append(f"  const T t{k} = {fn}({', '.join(name[a] for a in args)});")
+    for k, o in enumerate(outs):
+        lines.append(f"  o[{k}] = {name[o]};")
+    lines += ["}", ""]
+    return lines, len(ops), len(prog)
+
+
+def emit(chains):
     lines = [
         "// GENERATED by tools/gen_median_cols.py -- do not edit.",
         "// 5x5 median over pre-sorted window columns (proven by the 0-1 principle under the",
@@ -196,23 +218,15 @@ def emit(net, outs, nout):
     for i, j in SORT5:
         lines.append(f"  {{ const T a = v[{i}], b = v[{j}]; v[{i}] = ops.mn(a, b); "
                      f"v[{j}] = ops.mx(a, b); }}")
-    lines += ["}", "",
-              f"// medians of columns k..k+4, k = 0..{nout - 1}, of {nout + 4} sorted 5-element "
-              f"columns x[col][rank]: {len(ops)} min/max ops",
-              "template <typename T, typename F>",
-              f"__device__ __forceinline__ void median25_chain{nout}(const T (&x)[{nout + 4}][5], "
-              f"T (&o)[{nout}], F ops) {{"]
-    prog = fuse3(net, ops, outs)
-    verify_program(net, prog, outs)
-    for k, (v, kind, args) in enumerate(prog):
-        name[v] = f"t{k}"
-        fn = ("ops.mn" if kind == "min" else "ops.mx") + ("3" if len(args) == 3 else "")
-        lines.append(f"  const T t{k} = {fn}({', '.join(name[a] for a in args)});")
-    for k, o in enumerate(outs):
-        lines.append(f"  o[{k}] = {name[o]};")
-    lines += ["}", "", "}  // namespace idn", ""]
+    lines += ["}", ""]
+    stats = []
+    for net, outs, nout in chains:
+        text, n, nf = emit_chain(net, outs, nout)
+        lines += text
+        stats.append((nout, n, nf))
+    lines += ["}  // namespace idn", ""]
     OUT.write_text("\n".join(lines))
-    return len(ops), len(prog)
+    return stats
 
 
 def fuse3(net, ops, outs):
@@ -257,12 +271,14 @@ def verify_program(net, prog, outs):
 
 def main():
     verify_sort5()
-    nout = 5
-    net, outs = chain_net(nout)
-    n, nf = emit(net, outs, nout)
-    print(f"sort5: 9 comparators PROVEN; chain of {nout}: {n} 2-input ops ({n / nout:.1f} per "
-          f"output), {nf} after 3-input fusion; 0-1 principle PROVEN over {net.n} premise "
-          f"vectors; wrote {OUT}")
+    chains = []
+    for nout in (5, 4):
+        net, outs = chain_net(nout)
+        chains.append((net, outs, nout))
+    for nout, n, nf in emit(chains):
+        print(f"chain of {nout}: {n} 2-input ops ({n / nout:.1f} per output), {nf} after "
+              f"3-input fusion; 0-1 principle PROVEN")
+    print(f"sort5: 9 comparators PROVEN; wrote {OUT}")
 
 
 if __name__ == "__main__":

@@ -11,7 +11,7 @@ L=image-denoising_amd/idn/libidn_hip.so
 cp $L ab/product.so
 timeout -k 10 200 python -u tools/diag_live.py old wpe1 product > "$OUT/diag.txt" 2>&1 || exit 1
 grep -v "^ " "$OUT/diag.txt" | cut -c1-200
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
     -p no:cacheprovider -s > "$OUT/pytest.txt" 2>&1
 rc=$?
 grep -h "LIVE_PATH\|PLAN_FLIPS" "$OUT/pytest.txt" > "$OUT/flips.txt"
