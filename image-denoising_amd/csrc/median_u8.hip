@@ -250,19 +250,9 @@ __device__ __forceinline__ void m24_unpack(const v3u& A, const v3u& B, uint32_t 
     }
 }
 
-// one output row of 24 bytes per lane from the 5 unpacked rows of its window (oldest first)
-__device__ __forceinline__ void m24_row(const uint32_t (&R0)[12], const uint32_t (&R1)[12],
-                                        const uint32_t (&R2)[12], const uint32_t (&R3)[12],
-                                        const uint32_t (&R4)[12], v3u& outA, v3u& outB) {
+// the lane's 24 output bytes from its sorted window columns S[rank][column]
+__device__ __forceinline__ void m24_select(const uint32_t (&S)[5][12], v3u& outA, v3u& outB) {
   const PkOps op;
-  uint32_t S[5][12];  // [rank][column]
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint32_t v[5] = {R0[i], R1[i], R2[i], R3[i], R4[i]};
-    sort5(v, op);
-#pragma unroll
-    for (int r = 0; r < 5; ++r) S[r][i] = v[r];
-  }
   uint32_t o[3][4];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -296,6 +286,63 @@ __device__ __forceinline__ void m24_row(const uint32_t (&R0)[12], const uint32_t
   }
   outA = v3u{A[0], A[1], A[2]};
   outB = v3u{B[0], B[1], B[2]};
+}
+
+// one output row of 24 bytes per lane from the 5 unpacked rows of its window (oldest first)
+__device__ __forceinline__ void m24_row(const uint32_t (&R0)[12], const uint32_t (&R1)[12],
+                                        const uint32_t (&R2)[12], const uint32_t (&R3)[12],
+                                        const uint32_t (&R4)[12], v3u& outA, v3u& outB) {
+  const PkOps op;
+  uint32_t S[5][12];  // [rank][column]
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t v[5] = {R0[i], R1[i], R2[i], R3[i], R4[i]};
+    sort5(v, op);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) S[r][i] = v[r];
+  }
+  m24_select(S, outA, outB);
+}
+
+// two vertically adjacent output rows: their windows share 4 rows (C1..C4), sorted once per
+// column (5 comparators); each output then inserts its own fifth row (Xa: the row above, Xb: the
+// row below) into the sorted 4: rank i = max(c[i-1], min(x, c[i])), 8 min/max.  26 min/max per
+// column for the two rows instead of 2 x 18.
+__device__ __forceinline__ void m24_pair(const uint32_t (&Xa)[12], const uint32_t (&C1)[12],
+                                         const uint32_t (&C2)[12], const uint32_t (&C3)[12],
+                                         const uint32_t (&C4)[12], const uint32_t (&Xb)[12],
+                                         v3u& oA0, v3u& oB0, v3u& oA1, v3u& oB1) {
+  const PkOps op;
+  uint32_t c[4][12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t a = C1[i], b = C2[i], d = C3[i], e = C4[i], t;
+    t = op.mn(a, b); b = op.mx(a, b); a = t;   // (0, 1)
+    t = op.mn(d, e); e = op.mx(d, e); d = t;   // (2, 3)
+    t = op.mn(a, d); d = op.mx(a, d); a = t;   // (0, 2)
+    t = op.mn(b, e); e = op.mx(b, e); b = t;   // (1, 3)
+    t = op.mn(b, d); d = op.mx(b, d); b = t;   // (1, 2)
+    c[0][i] = a;
+    c[1][i] = b;
+    c[2][i] = d;
+    c[3][i] = e;
+  }
+  uint32_t S[5][12];
+  auto insert = [&](const uint32_t (&X)[12]) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const uint32_t x = X[i];
+      S[0][i] = op.mn(x, c[0][i]);
+      S[1][i] = op.mx(c[0][i], op.mn(x, c[1][i]));
+      S[2][i] = op.mx(c[1][i], op.mn(x, c[2][i]));
+      S[3][i] = op.mx(c[2][i], op.mn(x, c[3][i]));
+      S[4][i] = op.mx(x, c[3][i]);
+    }
+  };
+  insert(Xa);
+  m24_select(S, oA0, oB0);
+  insert(Xb);
+  m24_select(S, oA1, oB1);
 }
 
 __global__ __launch_bounds__(256) void median5_u8_w24(const uint8_t* __restrict__ src,
@@ -362,6 +409,80 @@ __global__ __launch_bounds__(256) void median5_u8_w24(const uint8_t* __restrict_
   }
 }
 
+// the 24-byte-lane 5x5 median two output rows at a time (m24_pair): a six-row ring, rows taken in
+// pairs; three pairs per unrolled group keep every ring slot a compile-time index
+__global__ __launch_bounds__(256) void median5_u8_w24p(const uint8_t* __restrict__ src,
+                                                       uint8_t* __restrict__ dst, int h, int rb,
+                                                       uint32_t row_stride, int nseg, int bands,
+                                                       int band_rows, int total_items) {
+  // prefetch one pair ahead: a pair's ~1800 VALU hide the loads, and 2 waves per SIMD (<= 256
+  // VGPRs) need the registers
+  constexpr int R = 2, PF = 2;
+  const int lane = threadIdx.x & 63;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (item >= total_items) return;
+  const int seg = item % nseg, tq = item / nseg;
+  const int band = tq % bands, img = tq / bands;
+  const int seg_start = seg * M24_SEG, seg_end = min(seg_start + M24_SEG, rb);
+  const int q = seg_start - 12 + 24 * lane;
+  const bool lead = q < 0, tail = q + 12 == rb;
+  const uint32_t img_bytes = (uint32_t)h * row_stride;
+  const rsrc_t rs = make_rsrc(src + (size_t)img * img_bytes, img_bytes);
+  const rsrc_t rd = make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
+  const uint32_t offA = lead ? OOB_OFF : (uint32_t)q, offB = (uint32_t)(q + 12);
+  const uint32_t stA = (q >= seg_start && q + 12 <= seg_end) ? (uint32_t)q : OOB_OFF;
+  const uint32_t stB = (q + 12 >= seg_start && q + 24 <= seg_end) ? (uint32_t)(q + 12) : OOB_OFF;
+
+  const int y0 = band * band_rows;
+  const int y1 = min(y0 + band_rows, h);
+  if (y0 >= y1) return;
+  const int nin = (y1 - y0) + 2 * R;
+  auto load_row = [&](int r, v3u& A, v3u& B) {
+    const uint32_t ro = (uint32_t)clampi(y0 - R + min(r, nin - 1), 0, h - 1) * row_stride;
+    A = __builtin_amdgcn_raw_buffer_load_b96(rs, offA, ro, 0);
+    B = __builtin_amdgcn_raw_buffer_load_b96(rs, offB, ro, 0);
+  };
+  v3u LA[PF], LB[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) load_row(i, LA[i], LB[i]);
+  uint32_t Wr[6][12];
+  auto take = [&](int r, int slot) {  // slot == r % 6; the load queue slot is r % 2
+    v3u A = LA[slot & 1], B = LB[slot & 1];
+    load_row(r + PF, LA[slot & 1], LB[slot & 1]);
+    if (lead)
+      A = v3u{__builtin_amdgcn_perm(0u, B.x, 0x00020100u), __builtin_amdgcn_perm(0u, B.x, 0x01000201u),
+              __builtin_amdgcn_perm(0u, B.x, 0x02010002u)};
+    if (tail)
+      B = v3u{__builtin_amdgcn_perm(0u, A.z, 0x01030201u), __builtin_amdgcn_perm(0u, A.z, 0x02010302u),
+              __builtin_amdgcn_perm(0u, A.z, 0x03020103u)};
+    m24_unpack(A, B, Wr[slot]);
+  };
+#pragma unroll
+  for (int r = 0; r < 4; ++r) take(r, r);
+  const int npairs = (y1 - y0 + 1) / 2;
+  for (int j0 = 0; j0 < npairs; j0 += 3) {
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const int j = j0 + jj;
+      if (j >= npairs) break;  // wave-uniform
+      // pair j: outputs y0 + 2j (input rows 2j .. 2j+4) and y0 + 2j + 1 (2j+1 .. 2j+5)
+      const int ra = 4 + 2 * j;
+      take(ra, (4 + 2 * jj) % 6);
+      take(ra + 1, (5 + 2 * jj) % 6);
+      v3u oA0, oB0, oA1, oB1;
+      m24_pair(Wr[(2 * jj) % 6], Wr[(2 * jj + 1) % 6], Wr[(2 * jj + 2) % 6], Wr[(2 * jj + 3) % 6],
+               Wr[(4 + 2 * jj) % 6], Wr[(5 + 2 * jj) % 6], oA0, oB0, oA1, oB1);
+      const int ya = y0 + 2 * j;
+      const uint32_t ro0 = (uint32_t)ya * row_stride;
+      __builtin_amdgcn_raw_buffer_store_b96(oA0, rd, stA, ro0, 0);
+      __builtin_amdgcn_raw_buffer_store_b96(oB0, rd, stB, ro0, 0);
+      const uint32_t ro1 = ya + 1 < y1 ? ro0 + row_stride : OOB_OFF;
+      __builtin_amdgcn_raw_buffer_store_b96(oA1, rd, stA, ro1, 0);
+      __builtin_amdgcn_raw_buffer_store_b96(oB1, rd, stB, ro1, 0);
+    }
+  }
+}
+
 // generic path: one thread per pixel, exact median by counting (any C, any alignment)
 template <int K>
 __global__ __launch_bounds__(256) void median_u8_generic(const uint8_t* __restrict__ src,
@@ -416,8 +537,12 @@ static int launch_median(const uint8_t* src, uint8_t* dst, int n, int h, int w, 
     const int bands = (h + band_rows - 1) / band_rows;
     const int64_t total = (int64_t)n * bands * nseg;
     IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "idn_median_blur_u8: batch too large");
-    hipLaunchKernelGGL(median5_u8_w24, dim3((unsigned)((total + 3) / 4)), dim3(256), 0, st, src,
-                       dst, h, (int)rb, (uint32_t)row_stride, nseg, bands, band_rows, (int)total);
+    if (knob("IDN_MEDIAN_PAIR", 1))
+      hipLaunchKernelGGL(median5_u8_w24p, dim3((unsigned)((total + 3) / 4)), dim3(256), 0, st, src,
+                         dst, h, (int)rb, (uint32_t)row_stride, nseg, bands, band_rows, (int)total);
+    else
+      hipLaunchKernelGGL(median5_u8_w24, dim3((unsigned)((total + 3) / 4)), dim3(256), 0, st, src,
+                         dst, h, (int)rb, (uint32_t)row_stride, nseg, bands, band_rows, (int)total);
   } else if (stripe_ok(c, rb, row_stride, h, src, dst)) {
     // measured (tools/sweep_stencil.py): 3x3 is near the memory side -> whole-row workgroups over
     // 16-row bands with XCD-contiguous band order; 5x5 is VALU-bound -> independent waves

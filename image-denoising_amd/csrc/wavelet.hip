@@ -134,8 +134,10 @@ __device__ __forceinline__ int wl_fbin(unsigned long long key) {
 
 inline int ws_strips(int Wo);
 inline int ws_sw(int Wo);
-inline int ws_bands(int n, int Ho, int strips, int level);
-constexpr int WS_G = 4;  // rows per sum-of-squares group of the streaming analysis
+inline int ws_bands(int n, int Ho, int Wo, int strips, int level);
+// rows per sum-of-squares group of the streaming analysis: 5, the step loop's unroll, so a group
+// ends at the same static position of every unrolled iteration (no per-row test or branch)
+constexpr int WS_G = 5;
 // Row bands per strip so that the grid fills whole rounds of resident workgroups: for each
 // candidate band count b the time is ~ rounds(b) x (rows per band + warm-up rows), rounds(b) =
 // ceil(units * b / resident).  (A grid of 2.5 rounds leaves the chip half idle for the last one.)
@@ -202,7 +204,7 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
       // level, so a square <= 4 * 8^(l-1)
       const int groups = (Lt.H[l] + WS_G - 1) / WS_G;
       Lt.tiles_x[l] = ws_strips(Lt.W[l]);
-      Lt.bands[l] = std::min(ws_bands(n, Lt.H[l], Lt.tiles_x[l], l), groups);
+      Lt.bands[l] = std::min(ws_bands(n, Lt.H[l], Lt.W[l], Lt.tiles_x[l], l), groups);
       Lt.tiles[l] = Lt.tiles_x[l] * Lt.bands[l];
       const double bound = 4.0 * std::pow(8.0, l - 1) * (double)Lt.H[l] * (double)Lt.W[l];
       Lt.sq_grid[l] = std::ldexp(1.0, (int)std::ceil(std::log2(bound)) - 52);
@@ -678,12 +680,15 @@ inline int ws_sw(int Wo) {
   const int st = ws_strips(Wo);
   return ((Wo + st - 1) / st + 1) & ~1;
 }
-int ws_resident(int level);  // resident analysis workgroups on the device (defined below)
+int ws_resident(int level, int block);  // resident analysis workgroups (defined below)
 // bands of whole WS_G-row groups, >= 16 output rows each: as best_bands, costed by the rows of
 // the longest band
-inline int ws_bands(int n, int Ho, int strips, int level) {
+inline int ws_bands(int n, int Ho, int Wo, int strips, int level) {
   const int groups = (Ho + WS_G - 1) / WS_G;
-  const int64_t units = (int64_t)n * strips, resident = std::max<int64_t>(ws_resident(level), 1);
+  // resident workgroups at the launch's block size (the staged columns of a strip, whole waves:
+  // 320 threads at the deeper 600x1000 levels, where a 512-thread query had halved the count)
+  const int block = (2 * ws_sw(Wo) + 8 + 63) / 64 * 64;
+  const int64_t units = (int64_t)n * strips, resident = std::max<int64_t>(ws_resident(level, block), 1);
   const int bmax = std::max(1, std::min({64, Ho / 16, groups}));
   int best = 1;
   double bestc = 1e300;
@@ -899,7 +904,6 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
       if (m < 4) continue;  // accumulator fill (wave-uniform)
       __syncthreads();
       const int i = k;  // output row
-      const bool gend = (i + 1) % WS_G == 0 || i + 1 == ib;
       if (rowt) {
         const TL* vl = &VL[buf][rc][2 * jj];
         const TH* vhe = &VH[buf][rc][jj];                 // element 2 jj + m, m even: vhe[m / 2]
@@ -972,15 +976,20 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
           }
         }
       }
-      if (gend) {
+      // the group ends at this row: i + 1 = ia - 3 + m is a multiple of WS_G = 5 exactly when
+      // r = m - m0 = 3 (ia and m0 are multiples of 5)
+      if (r == 3) {
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-          sqa[b] += __builtin_rint(sq[b] * sq_inv) * sq_grid;
+          sqa[b] = __fma_rn(__builtin_rint(sq[b] * sq_inv), sq_grid, sqa[b]);
           sq[b] = 0.0;
         }
       }
     }
   }
+#pragma unroll
+  for (int b = 0; b < 3; ++b)  // the image's last group when Ho is not a multiple of 5 (else 0)
+    sqa[b] = __fma_rn(__builtin_rint(sq[b] * sq_inv), sq_grid, sqa[b]);
   // per-workgroup sums (exact, see above), channel by channel
   __syncthreads();
   double* red = &RED[0][0];
@@ -999,11 +1008,11 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
 
 // resident workgroups of the product's streaming analysis of a level (level 1: u8 / fp32-lowpass;
 // deeper: fp32 'aa' input), used by wl_layout's band count for every form of that level
-int ws_resident(int level) {
+int ws_resident(int level, int block) {
   const void* k = level == 1
       ? reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1>)
       : reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0>);
-  return cu_count() * occ_wgs(k, WS_MAXT);
+  return cu_count() * occ_wgs(k, block);
 }
 
 // ---- 3: sum of squares per detail band ----------------------------------------------------------

@@ -273,6 +273,7 @@ def test_bilateral_gray(dev):
                                   {"IDN_MEDIAN_MAP": "1", "IDN_MEDIAN_ROWS": "16"},
                                   {"IDN_MEDIAN_MAP": "2", "IDN_MEDIAN_ROWS": "7"},
                                   {"IDN_MEDIAN_W24": "0", "IDN_MEDIAN_ROWS": "32"},
+                                  {"IDN_MEDIAN_PAIR": "0", "IDN_MEDIAN_ROWS": "9"},
                                   {"IDN_MEDIAN_ROWS": "5"}],
                          ids=lambda f: "-".join(f"{k[11:]}{v}" for k, v in f.items()) or "product")
 @pytest.mark.parametrize("shape", [(2, 100, 1000), (1, 37, 336), (1, 601, 1000), (2, 13, 104)])

@@ -8,14 +8,14 @@ export TMPDIR=/tmp
 L=image-denoising_amd/idn/libidn_hip.so
 cp $L ab/product.so
 timeout -k 10 600 python -u -m pytest tests/test_wavelet_gpu.py tests/test_live_path_gpu.py \
-    tests/test_pipeline_gpu.py -q --timeout 300 --timeout-method thread -p no:cacheprovider -s \
+    tests/test_pipeline_gpu.py tests/test_filters_gpu.py -q --timeout 300 --timeout-method thread -p no:cacheprovider -s \
     > "$OUT/pytest.txt" 2>&1
 rc=$?
 grep -h "LIVE_PATH\|PLAN_FLIPS" "$OUT/pytest.txt" > "$OUT/flips.txt"
 tail -3 "$OUT/pytest.txt"
 [ $rc = 0 ] || exit $rc
-for rep in 1 2 3; do
-  for v in old product; do
+for rep in 1 2; do
+  for v in old product g8 g16; do
     cp ab/$v.so $L || exit 1
     for op in wavelet_bior15 wavelet_bior15_f64; do
       timeout -k 10 120 python bench.py --op $op --no-cpu --no-copy --steps 20 --warmup 3 \
@@ -23,7 +23,13 @@ for rep in 1 2 3; do
     done
   done
 done
-for v in old product; do for op in wavelet_bior15 wavelet_bior15_f64; do
+cp ab/product.so $L
+for rep in 1 2; do for pr in 0 1; do
+  IDN_MEDIAN_PAIR=$pr timeout -k 10 120 python bench.py --op median5 --lib tuning --no-cpu --no-copy \
+      --steps 20 --warmup 3 >> "$OUT/ab_pair_$pr.jsonl" 2>> "$OUT/ab.err" || exit 1
+done; done
+for pr in 0 1; do echo "pair=$pr median5 $(grep -ho '"kernel_ms_avg": [0-9.]*' "$OUT/ab_pair_$pr.jsonl" | tr '\n' ' ')"; done
+for v in old product g8 g16; do for op in wavelet_bior15 wavelet_bior15_f64; do
   echo "$v $op $(grep -ho '"kernel_ms_avg": [0-9.]*' "$OUT/ab_${v}_$op.jsonl" | tr '\n' ' ')"; done; done
 cp ab/product.so $L
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/ks_wl" -o k --output-format csv \
