@@ -205,6 +205,9 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
       const int groups = (Lt.H[l] + WS_G - 1) / WS_G;
       Lt.tiles_x[l] = ws_strips(Lt.W[l]);
       Lt.bands[l] = std::min(ws_bands(n, Lt.H[l], Lt.W[l], Lt.tiles_x[l], l), groups);
+      // tuning: a fixed band count per level (bit field: level l's count in bits 8(l-1)..)
+      if (const int fb = (knob("IDN_WAVELET_BANDS", 0) >> (8 * (l - 1))) & 0xFF)
+        Lt.bands[l] = std::min(fb, groups);
       Lt.tiles[l] = Lt.tiles_x[l] * Lt.bands[l];
       const double bound = 4.0 * std::pow(8.0, l - 1) * (double)Lt.H[l] * (double)Lt.W[l];
       Lt.sq_grid[l] = std::ldexp(1.0, (int)std::ceil(std::log2(bound)) - 52);
@@ -685,9 +688,12 @@ int ws_resident(int level, int block);  // resident analysis workgroups (defined
 // the longest band
 inline int ws_bands(int n, int Ho, int Wo, int strips, int level) {
   const int groups = (Ho + WS_G - 1) / WS_G;
-  // resident workgroups at the launch's block size (the staged columns of a strip, whole waves:
-  // 320 threads at the deeper 600x1000 levels, where a 512-thread query had halved the count)
-  const int block = (2 * ws_sw(Wo) + 8 + 63) / 64 * 64;
+  // resident workgroups as a 512-thread launch would have them.  (The deeper 600x1000 levels
+  // launch 320 threads; counting those -- twice the workgroups per CU -- picked more, shorter bands
+  // and measured 20 % slower at levels 2-3: the analysis is throughput-bound there, and extra bands
+  // only add warm-up rows, profiles/r04/wavelet/.)
+  (void)Wo;
+  const int block = ws_maxsw() * 2 + 8 <= 64 ? 64 : WS_MAXT;  // one-wave strips: their own count
   const int64_t units = (int64_t)n * strips, resident = std::max<int64_t>(ws_resident(level, block), 1);
   const int bmax = std::max(1, std::min({64, Ho / 16, groups}));
   int best = 1;
@@ -739,8 +745,10 @@ template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
 // median's population); deeper levels (no median) run both paths in fp32.
 // FM >= 0: the band storage mask (wl_fband) and CODES the level-1 code emission as compile-time
 // constants (the product's masks: no per-band branches); FM = -1 takes both from the arguments.
-template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1>
-__global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
+// NT: threads per workgroup the LDS arrays are sized for (512; 64 for one-wave strips)
+template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1,
+          int NT = WS_MAXT>
+__global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
     wreal* __restrict__ ws, size_t img_floats, const double* __restrict__ stats, size_t in_off,
     int Hin, int Win, size_t out_off, int Ho, int Wo, int SW, int strips, int bands, int groups,
     const uint8_t* __restrict__ src, const double* __restrict__ in64, int64_t row_stride,
@@ -754,10 +762,10 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
   // (u & 1) * WS_MAXT / 2 + u / 2) so that the row threads' 16-byte reads (lane stride 4 columns)
   // fill whole bank rows -- interleaved fp64 columns put two lanes on every 16-byte slot
   constexpr bool SEPF = !std::is_same<TL, TH>::value;  // a separate TL copy of the highpass
-  __shared__ TL VL[2][3][WS_MAXT];
-  __shared__ TL VF[SEPF ? 2 : 1][SEPF ? 3 : 1][SEPF ? WS_MAXT : 1];
-  __shared__ TH VH[2][3][WS_MAXT];
-  __shared__ double RED[3][WS_MAXT];
+  __shared__ TL VL[2][3][NT];
+  __shared__ TL VF[SEPF ? 2 : 1][SEPF ? 3 : 1][SEPF ? NT : 1];
+  __shared__ TH VH[2][3][NT];
+  __shared__ double RED[3][NT];
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
   const int j0 = strip * SW;
@@ -894,7 +902,7 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
           const TL lo = fma_t<TL>((TL)B1, ek, acc[c][r]);  // output k complete
           if (m >= 4) {
             VL[buf][c][t] = lo;
-            VH[buf][c][(t & 1) * (WS_MAXT / 2) + (t >> 1)] = hd1[c];
+            VH[buf][c][(t & 1) * (NT / 2) + (t >> 1)] = hd1[c];
             if constexpr (SEPF) VF[buf][c][t] = (TL)hd1[c];
           }
           hd1[c] = hd0[c];
@@ -907,7 +915,7 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
       if (rowt) {
         const TL* vl = &VL[buf][rc][2 * jj];
         const TH* vhe = &VH[buf][rc][jj];                 // element 2 jj + m, m even: vhe[m / 2]
-        const TH* vho = &VH[buf][rc][WS_MAXT / 2 + jj];   //                   m odd:  vho[m / 2]
+        const TH* vho = &VH[buf][rc][NT / 2 + jj];   //                   m odd:  vho[m / 2]
         const TL* vf = SEPF ? &VF[buf][rc][2 * jj] : nullptr;
         TL o[2][3];  // [output][aa, ad, da]
         TH odd[2];   // [output] dd
@@ -995,13 +1003,13 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
   double* red = &RED[0][0];
   if (rowt) {
 #pragma unroll
-    for (int b = 0; b < 3; ++b) red[b * WS_MAXT + t] = sqa[b];
+    for (int b = 0; b < 3; ++b) red[b * NT + t] = sqa[b];
   }
   __syncthreads();
   if (t < 9) {
     const int c = t / 3, b = t - 3 * c;
     double s2 = 0.0;
-    for (int g = 0; g < half; ++g) s2 += red[b * WS_MAXT + c * half + g];
+    for (int g = 0; g < half; ++g) s2 += red[b * NT + c * half + g];
     part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + part_tile0 + blockIdx.x] = s2;
   }
 }
@@ -1010,8 +1018,10 @@ __global__ __launch_bounds__(WS_MAXT, IDN_WS_WPE) void wl_dwt_stream(
 // deeper: fp32 'aa' input), used by wl_layout's band count for every form of that level
 int ws_resident(int level, int block) {
   const void* k = level == 1
-      ? reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1>)
-      : reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0>);
+      ? (block == 64 ? reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1, 64>)
+                     : reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1>))
+      : (block == 64 ? reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0, 64>)
+                     : reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0>));
   return cu_count() * occ_wgs(k, block);
 }
 
@@ -3365,6 +3375,12 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
       // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
 #define IDN_WS_(SRC, TL, TH, FMC, CC, EMIT)                                                        \
+  if (blk.x == 64 && (FMC) >= 0)                                                                   \
+    hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC, 64>), grid, blk, 0, st, wsf,           \
+                       Lt.img_floats, stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, \
+                       strips, bands, groups, src, in64, row_stride, part, Lt.part_per_img,        \
+                       Lt.part_tile0[l], EMIT, fm_an(l), Lt.sq_grid[l]);                           \
+  else                                                                                             \
   hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC>), grid, blk, 0, st, wsf, Lt.img_floats,  \
                      stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands,   \
                      groups, src, in64, row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT, \

@@ -87,8 +87,10 @@ def test_plan_parity(dev, mode, spec):
                 # train_v0's double filtering (closure wavelet + hook wavelet): a value flipped at
                 # the first cast feeds the second wavelet, whose output moves by a fraction of an
                 # LSB around it -- no boundary rule holds after the second step.  Bound: one LSB
-                # per wavelet step, and the share measured on the GPU (profiles/r04/plan_flips.txt)
-                assert d.max() <= n_wl and share < 5e-3 * n_wl, (p, d.max(), share)
+                # per wavelet step, and about twice the share measured on the GPU (round 4: at most
+                # 1.72e-3 for brownian_wavelet_var0.9, profiles/r04/plan_flips.txt; single-step
+                # plans flip 0 - 8e-5, all on integer boundaries)
+                assert d.max() <= n_wl and share < 3.5e-3, (p, d.max(), share)
         elif has_bil or has_bloom:
             assert d.max() <= 1 and (d > 0).mean() < 1e-3, (p, d.max(), (d > 0).mean())
         else:
