@@ -305,6 +305,23 @@ __device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn,
 // per-channel min / max of the YCbCr image (fp64 exact); the planes themselves are never
 // stored: the analysis recomputes Y/Cb/Cr while staging.  Compact u8 rows (row_stride == 3w,
 // dword-aligned) take 4 pixels per thread with three dword loads and no index division.
+// u8 pixels are ranked by exact integer keys first: 1000 x the dot product with skimage's decimal
+// coefficients (65481 r + 128553 g + 24966 b for Y, ...), and of two pixels with different keys the
+// one with the smaller key has the smaller fp64 value (the gaps between keys, >= 1/255000, dwarf the
+// chain's rounding; checked over all 2^24 triples for each channel by tools/check_ycbcr_keys.c).
+// Equal keys with different triples are common and their fp64 values can differ in the last bits,
+// so the fp64 chain runs only for a pixel whose key reaches a tracked extreme: its value is taken
+// on a new extreme key, and min / max-ed in on a tie from another triple.  The integer path is ~20
+// 32-bit VALU per pixel against ~30 mostly fp64 ones.
+struct YccKeys {
+  int32_t k[3];
+  __device__ __forceinline__ explicit YccKeys(uint32_t r, uint32_t g, uint32_t b) {
+    k[0] = (int32_t)(65481u * r + 128553u * g + 24966u * b);
+    k[1] = (int32_t)(112000u * b) - (int32_t)(37797u * r + 74203u * g);
+    k[2] = (int32_t)(112000u * r) - (int32_t)(93786u * g + 18214u * b);
+  }
+};
+template <bool KEYS = true>  // false: the fp64 chain for every pixel (A/B: IDN_WAVELET_KEYS=0)
 __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict__ src,
                                                        const double* __restrict__ in64, int h, int w,
                                                        int64_t row_stride, double* __restrict__ stats) {
@@ -326,6 +343,14 @@ __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src + (int64_t)img * h * row_stride);
     const int nq = (int)(np >> 2);  // groups of 4 pixels = 3 dwords
     const int stride = gridDim.x * blockDim.x;
+    // trackers 0..2: min of channel c, 3..5: max (key negated: smaller is better for all six)
+    int32_t bk[6];
+    uint32_t bt[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      bk[i] = INT32_MAX;
+      bt[i] = 0xFFFFFFFFu;
+    }
     for (int q0 = blockIdx.x * blockDim.x + threadIdx.x; q0 < nq; q0 += 4 * stride) {
       uint32_t d[4][3];  // 4 groups in flight per thread
 #pragma unroll
@@ -339,13 +364,40 @@ __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict
         if (q0 + u * stride >= nq) break;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          double v[3];
+          uint32_t x[3];
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const int k = 3 * p + c;
-            v[c] = (double)((d[u][k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
+            x[c] = (d[u][k >> 2] >> (8 * (k & 3))) & 0xFFu;
           }
-          acc(v[0], v[1], v[2]);
+          if constexpr (!KEYS) {
+            acc((double)x[0] * (1.0 / 255.0), (double)x[1] * (1.0 / 255.0), (double)x[2] * (1.0 / 255.0));
+            continue;
+          }
+          const YccKeys K(x[0], x[1], x[2]);
+          bool need = false;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) need |= (i < 3 ? K.k[i] : -K.k[i - 3]) <= bk[i];
+          if (need) {  // rare: a new extreme or a tie (the wave branches around it otherwise)
+            const uint32_t tr = x[0] | x[1] << 8 | x[2] << 16;
+            double yc[3];
+            ycbcr64((double)x[0] * (1.0 / 255.0), (double)x[1] * (1.0 / 255.0),
+                    (double)x[2] * (1.0 / 255.0), yc);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const int c = i % 3;
+              const int32_t kk = i < 3 ? K.k[c] : -K.k[c];
+              if (kk < bk[i]) {
+                bk[i] = kk;
+                bt[i] = tr;
+                if (i < 3) dmn[c] = yc[c];
+                else dmx[c] = yc[c];
+              } else if (kk == bk[i] && tr != bt[i]) {
+                if (i < 3) dmn[c] = fmin(dmn[c], yc[c]);
+                else dmx[c] = fmax(dmx[c], yc[c]);
+              }
+            }
+          }
         }
       }
     }
@@ -711,7 +763,7 @@ inline int ws_bands(int n, int Ho, int Wo, int strips, int level) {
 
 template <int SRC>
 struct WsRaw;  // the raw input of one step (two rows) for one staged column
-template <> struct WsRaw<0> {  // u8 pixels: 3 bytes of each row
+template <> struct WsRaw<0> {  // u8 pixels: the raw dword holding each row's 3 bytes (see load)
   uint32_t p[2];
 };
 template <> struct WsRaw<1> {  // f64 pixels
@@ -778,6 +830,11 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
   const int NXs = 2 * SW + 8;
   const bool colt = t < NXs;
   const int qc = sym_idx(2 * j0 - 8 + t, Win);  // this thread's input column
+  // u8 source: one unaligned dword per row, bytes 3 qc - 1 .. 3 qc + 2 (bytes 0..3 for column 0),
+  // so it never reaches past the image's last byte; the pixel is at bit qsh of it.  The bytes are
+  // extracted where the step is consumed (norm), PF steps later: packing three byte loads at load
+  // time made every load wait for its data at once, and the ring prefetched nothing.
+  const uint32_t qvo = qc > 0 ? 3u * (uint32_t)qc - 1u : 0u, qsh = qc > 0 ? 8u : 0u;
   wreal mn[3] = {0, 0, 0}, inv[3] = {1, 1, 1}, rcp[3] = {1, 1, 1};
   if (SRC < 2) {
     const double* st = stats + (size_t)img * WL_STATS;
@@ -799,12 +856,8 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       if constexpr (SRC == 0) {
-        // three byte loads (one unaligned dword per pixel measured 8 % slower for the kernel)
-        const uint32_t so = (uint32_t)((int64_t)rows[h2] * row_stride), vo = (uint32_t)qc * 3u;
-        const uint32_t b0 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo, so, 0);
-        const uint32_t b1 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo + 1u, so, 0);
-        const uint32_t b2 = __builtin_amdgcn_raw_buffer_load_b8(rs, vo + 2u, so, 0);
-        R.p[h2] = b0 | b1 << 8 | b2 << 16;
+        const uint32_t so = (uint32_t)((int64_t)rows[h2] * row_stride);
+        R.p[h2] = __builtin_amdgcn_raw_buffer_load_b32(rs, qvo, so, 0);
       } else if constexpr (SRC == 1) {
         const uint32_t so = (uint32_t)rows[h2] * (uint32_t)Win * 24u;
 #pragma unroll
@@ -830,7 +883,7 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
       double px[3];
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3) {
-        if constexpr (SRC == 0) px[k3] = (double)((R.p[h2] >> (8 * k3)) & 0xFFu) * (1.0 / 255.0);
+        if constexpr (SRC == 0) px[k3] = (double)((R.p[h2] >> (qsh + 8 * k3)) & 0xFFu) * (1.0 / 255.0);
         else px[k3] = R.p[h2][k3];
       }
       const wreal a = ycbcr_c(px, c) - mn[c];
@@ -871,22 +924,19 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
 
   const int k0 = ia - 4, M = ib - ia + 4;  // steps m = 0 .. M-1 cover pairs k = k0 + m
   WsRaw<SRC> rq[PF];                        // raw samples of steps m .. m + PF - 1 (slot m % PF)
-  if (colt) {
+  // the ring's loads are unconditional (rows past the band mirror into the image, sym_idx, and are
+  // never used): a load under a branch leaves a phi whose copy waits for the data at once
 #pragma unroll
-    for (int f = 0; f < PF; ++f)
-      if (f < M) load(k0 + f, rq[f]);
-  }
+  for (int f = 0; f < PF; ++f) load(k0 + f, rq[f]);
   for (int m0 = 0; m0 < M; m0 += 5) {
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int m = m0 + r;
-      if (m >= M) break;
       const int k = k0 + m;
       const int buf = m & 1;
       if (colt) {
         const int slot = r % PF;  // PF divides 5 (compile-time after unrolling)
-        const WsRaw<SRC> cur = rq[slot];
-        if (m + PF < M) load(k + PF, rq[slot]);  // refill the slot PF steps ahead
+        const WsRaw<SRC>& cur = rq[slot];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const auto x0 = norm(cur, 0, c), x1 = norm(cur, 1, c);
@@ -909,7 +959,16 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
           hd0[c] = hk;
         }
       }
-      if (m < 4) continue;  // accumulator fill (wave-uniform)
+      // refill the slot PF steps ahead, after its last use and outside the column threads' branch
+      // (every thread loads; a load under the branch, or into a slot still being read, is copied
+      // into the ring at the join and that copy waits for the data at once)
+      load(k + PF, rq[r % PF]);
+      // accumulator fill, and the steps that pad the band to whole 5-step iterations: their column
+      // work is wasted, but every iteration then runs all five steps (wave-uniform).  (A break out of
+      // the unrolled steps merges, at the loop header, a path on which the latest ring load is that
+      // step's, and the compiler's wait at every slot's first use drops to that path's: the ring
+      // would prefetch nothing.)
+      if (m < 4 || m >= M) continue;
       __syncthreads();
       const int i = k;  // output row
       if (rowt) {
@@ -1924,19 +1983,19 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
   };
   __syncthreads();  // TH
   const int r0 = ma, R = (mb - ma) + 4;  // coefficient rows r0 .. r0 + R - 1
+  // the prefetch loads are unconditional and issued after the slot's last use (rows clamp into the
+  // band: load), and the steps past R pad the last iteration instead of breaking out of it: a load
+  // under a branch, or a break merging a shorter path into the loop header, makes the compiler wait
+  // for the load at once (as wl_dwt_stream)
   S3Raw<FM> pf[S3_PF];
-  if (stg) {
 #pragma unroll
-    for (int f = 0; f < S3_PF; ++f)
-      if (f < R) load(r0 + f, pf[f]);
-  }
+  for (int f = 0; f < S3_PF; ++f) load(r0 + f, pf[f]);
   for (int s0 = 0; s0 < R; s0 += 10) {
 #pragma unroll
     for (int rs = 0; rs < 10; ++rs) {
       const int sidx = s0 + rs;
-      if (sidx >= R) break;
       const int r = r0 + sidx, buf = sidx & 1, slot = rs % 5;
-      if (stg) {  // stage row r (details soft-thresholded), refill its prefetch slot
+      if (stg) {  // stage row r (details soft-thresholded)
         const S3Raw<FM>& q = pf[rs % S3_PF];
 #pragma unroll
         for (int c = 0; c < 3; ++c)
@@ -1945,8 +2004,9 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
             const float x = ((FM >> b) & 1) ? q.f[c][s3_slot<FM>(b)] : (float)q.d[c][s3_slot<FM>(b)];
             SB[buf][c * 4 + b][t] = b ? soft_t<float>(x, TH[c * 4 + b]) : x;
           }
-        if (sidx + S3_PF < R) load(r + S3_PF, pf[rs % S3_PF]);
       }
+      load(r + S3_PF, pf[rs % S3_PF]);  // refill the slot
+      if (sidx >= R) continue;          // padding (wave-uniform)
       __syncthreads();
       if (sidx >= 5) flush(r - 5, buf ^ 1);  // the previous step's U8 rows
       if (cmp) {
@@ -3282,7 +3342,8 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
     int gx = (int)((np / 4 + 255) / 256);
     if (gx > 24) gx = 24;
-    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+    hipLaunchKernelGGL(knob("IDN_WAVELET_KEYS", 1) ? wl_color_minmax<true> : wl_color_minmax<false>,
+                       dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
   int nwg_a;
@@ -3348,7 +3409,8 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
     int gx = (int)((np / 4 + 255) / 256);
     if (gx > 24) gx = 24;
-    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+    hipLaunchKernelGGL(knob("IDN_WAVELET_KEYS", 1) ? wl_color_minmax<true> : wl_color_minmax<false>,
+                       dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
   double* part = (double*)((char*)ws + Lt.part_off);

@@ -371,3 +371,36 @@ def test_wavelet_color_minmax_exact(dev):
         mx = _key_to_f64(st[i, 203:206].view(np.uint64))
         np.testing.assert_array_equal(mn.view(np.uint64), ycc.min(axis=(0, 1)).view(np.uint64))
         np.testing.assert_array_equal(mx.view(np.uint64), ycc.max(axis=(0, 1)).view(np.uint64))
+
+
+# (channel, extreme, two triples whose integer keys tie at that channel's extreme while their fp64
+# values differ in the last bits: found over all 2^24 triples, tools/check_ycbcr_keys.c)
+_KEY_TIES = [((12, 1, 2), (1, 0, 36)), ((244, 254, 254), (255, 255, 220)),
+             ((252, 255, 1), (251, 254, 0)), ((2, 4, 255), (0, 2, 253)),
+             ((0, 254, 252), (1, 255, 253)), ((254, 0, 3), (255, 1, 4))]
+
+
+@pytest.mark.parametrize("swap", [False, True])
+def test_wavelet_color_minmax_key_ties(dev, swap):
+    """wl_color_minmax ranks u8 pixels by exact integer keys and evaluates the fp64 chain only at
+    the extremes: each channel's min and max here is reached by two triples with the same key and
+    different fp64 values, adjacent in one thread's pixel group (either order) and again in other
+    threads; the stats must still equal numpy's fp64 min / max bit for bit"""
+    import torch
+    import oracle
+    from oracle.cv import matmul3_fma
+    rs = np.random.RandomState(11)
+    img = rs.randint(40, 201, (96, 160, 3)).astype(np.uint8)  # no pixel reaches the tied extremes
+    flat = img.reshape(-1, 3)
+    for j, (a, b) in enumerate(_KEY_TIES):
+        pair = (b, a) if swap else (a, b)
+        base = 4 * (37 * j + 5)  # one 4-pixel group: one thread, consecutive pixels
+        flat[base], flat[base + 1] = pair
+        flat[4 * (911 + 53 * j) + 2] = pair[1]  # and the second triple again in another group
+    _, _, st = _stats_after(torch.from_numpy(img[None].copy()).cuda(), 2)
+    ycc = matmul3_fma(img.astype(np.float64) * (1.0 / 255.0), oracle.wavelet.YCBCR_FROM_RGB,
+                      post=oracle.wavelet.YCBCR_OFFSET)
+    mn = _key_to_f64(st[0, 200:203].view(np.uint64))
+    mx = _key_to_f64(st[0, 203:206].view(np.uint64))
+    np.testing.assert_array_equal(mn.view(np.uint64), ycc.min(axis=(0, 1)).view(np.uint64))
+    np.testing.assert_array_equal(mx.view(np.uint64), ycc.max(axis=(0, 1)).view(np.uint64))
