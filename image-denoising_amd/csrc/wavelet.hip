@@ -305,23 +305,6 @@ __device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn,
 // per-channel min / max of the YCbCr image (fp64 exact); the planes themselves are never
 // stored: the analysis recomputes Y/Cb/Cr while staging.  Compact u8 rows (row_stride == 3w,
 // dword-aligned) take 4 pixels per thread with three dword loads and no index division.
-// u8 pixels are ranked by exact integer keys first: 1000 x the dot product with skimage's decimal
-// coefficients (65481 r + 128553 g + 24966 b for Y, ...), and of two pixels with different keys the
-// one with the smaller key has the smaller fp64 value (the gaps between keys, >= 1/255000, dwarf the
-// chain's rounding; checked over all 2^24 triples for each channel by tools/check_ycbcr_keys.c).
-// Equal keys with different triples are common and their fp64 values can differ in the last bits,
-// so the fp64 chain runs only for a pixel whose key reaches a tracked extreme: its value is taken
-// on a new extreme key, and min / max-ed in on a tie from another triple.  The integer path is ~20
-// 32-bit VALU per pixel against ~30 mostly fp64 ones.
-struct YccKeys {
-  int32_t k[3];
-  __device__ __forceinline__ explicit YccKeys(uint32_t r, uint32_t g, uint32_t b) {
-    k[0] = (int32_t)(65481u * r + 128553u * g + 24966u * b);
-    k[1] = (int32_t)(112000u * b) - (int32_t)(37797u * r + 74203u * g);
-    k[2] = (int32_t)(112000u * r) - (int32_t)(93786u * g + 18214u * b);
-  }
-};
-template <bool KEYS = true>  // false: the fp64 chain for every pixel (A/B: IDN_WAVELET_KEYS=0)
 __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict__ src,
                                                        const double* __restrict__ in64, int h, int w,
                                                        int64_t row_stride, double* __restrict__ stats) {
@@ -343,14 +326,6 @@ __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src + (int64_t)img * h * row_stride);
     const int nq = (int)(np >> 2);  // groups of 4 pixels = 3 dwords
     const int stride = gridDim.x * blockDim.x;
-    // trackers 0..2: min of channel c, 3..5: max (key negated: smaller is better for all six)
-    int32_t bk[6];
-    uint32_t bt[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      bk[i] = INT32_MAX;
-      bt[i] = 0xFFFFFFFFu;
-    }
     for (int q0 = blockIdx.x * blockDim.x + threadIdx.x; q0 < nq; q0 += 4 * stride) {
       uint32_t d[4][3];  // 4 groups in flight per thread
 #pragma unroll
@@ -364,40 +339,13 @@ __global__ __launch_bounds__(256) void wl_color_minmax(const uint8_t* __restrict
         if (q0 + u * stride >= nq) break;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          uint32_t x[3];
+          double v[3];
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const int k = 3 * p + c;
-            x[c] = (d[u][k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            v[c] = (double)((d[u][k >> 2] >> (8 * (k & 3))) & 0xFFu) * (1.0 / 255.0);
           }
-          if constexpr (!KEYS) {
-            acc((double)x[0] * (1.0 / 255.0), (double)x[1] * (1.0 / 255.0), (double)x[2] * (1.0 / 255.0));
-            continue;
-          }
-          const YccKeys K(x[0], x[1], x[2]);
-          bool need = false;
-#pragma unroll
-          for (int i = 0; i < 6; ++i) need |= (i < 3 ? K.k[i] : -K.k[i - 3]) <= bk[i];
-          if (need) {  // rare: a new extreme or a tie (the wave branches around it otherwise)
-            const uint32_t tr = x[0] | x[1] << 8 | x[2] << 16;
-            double yc[3];
-            ycbcr64((double)x[0] * (1.0 / 255.0), (double)x[1] * (1.0 / 255.0),
-                    (double)x[2] * (1.0 / 255.0), yc);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-              const int c = i % 3;
-              const int32_t kk = i < 3 ? K.k[c] : -K.k[c];
-              if (kk < bk[i]) {
-                bk[i] = kk;
-                bt[i] = tr;
-                if (i < 3) dmn[c] = yc[c];
-                else dmx[c] = yc[c];
-              } else if (kk == bk[i] && tr != bt[i]) {
-                if (i < 3) dmn[c] = fmin(dmn[c], yc[c]);
-                else dmx[c] = fmax(dmx[c], yc[c]);
-              }
-            }
-          }
+          acc(v[0], v[1], v[2]);
         }
       }
     }
@@ -775,9 +723,10 @@ template <> struct WsRaw<2> {  // the level above's 'aa', three channels, fp64
 template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (WL_FB_AIN)
   float p[2][3];
 };
-// prefetch depth (steps; divides 5): the u8 and fp32 rings are small, the fp64 ones are not
-// (fp32 'aa' input: depth 1 keeps the deeper levels at 76 VGPRs, six waves per SIMD; depth 5
-// measured 1 % slower on the whole op)
+// prefetch depth (steps; divides 5): the u8 and fp32 rings are small, the fp64 ones are not.
+// (Round 3 measured the fp32 'aa' ring at depth 5 1 % slower than depth 1 -- when no ring load was
+// in flight past its own step, see the ring comments in wl_dwt_stream; with working prefetch
+// depth 5 is the faster.)
 #ifndef IDN_WS_PF0  // A/B builds set these
 #define IDN_WS_PF0 5
 #endif
@@ -787,7 +736,13 @@ template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (
 #ifndef IDN_S3_WPE
 #define IDN_S3_WPE 1
 #endif
-template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : 1; }
+#ifndef IDN_S3_PAD
+#define IDN_S3_PAD 0
+#endif
+#ifndef IDN_WS_PF3  // the fp32 'aa' input of levels >= 2: a 5-step ring measured 2.773 -> 2.752 ms on
+#define IDN_WS_PF3 5  // the op against 1 (levels 2 / 3: 283 -> 264 / 92 -> 88 us, profiles/r04/wavelet/)
+#endif
+template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : SRC == 3 ? IDN_WS_PF3 : 1; }
 
 
 // TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the
@@ -1006,6 +961,7 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
           }
         }
         const size_t e0 = (size_t)i * Wo + oj;
+        uint32_t code[2];
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
           if (!(d ? ok1 : ok0)) continue;
@@ -1013,10 +969,16 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
           sq[0] = __fma_rn(v1, v1, sq[0]);  // (exact squares for the fp32 bands: = mul + add)
           sq[1] = __fma_rn(v2, v2, sq[1]);
           sq[2] = __fma_rn(v3, v3, sq[2]);
-          if (emit_codes) {
-            const unsigned long long key = absbits((double)odd[d]);
-            reinterpret_cast<uint16_t*>(base + (size_t)rc * Hin * Win)[e0 + d] =
-                (uint16_t)(key ? wl_fbin(key) + 1 : 0);
+          const unsigned long long key = absbits((double)odd[d]);
+          code[d] = key ? wl_fbin(key) + 1 : 0;
+        }
+        if (emit_codes) {  // the pair's two codes as one dword where it is aligned
+          uint16_t* cp = reinterpret_cast<uint16_t*>(base + (size_t)rc * Hin * Win) + e0;
+          if (ok1 && (e0 & 1) == 0) {
+            *reinterpret_cast<uint32_t*>(cp) = code[0] | code[1] << 16;
+          } else {
+            if (ok0) cp[0] = (uint16_t)code[0];
+            if (ok1) cp[1] = (uint16_t)code[1];
           }
         }
         wreal* ob = base + out_off + (size_t)rc * 4 * bsz;
@@ -1914,7 +1876,7 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
     size_t in_off, int Nh, int Nw, int Hout, int Wout, int SWo, int strips, int bands,
     uint8_t* __restrict__ out_u8, int64_t row_stride, float* __restrict__ out_f32, int level = 1,
     size_t out_off = 0, size_t out_chan_stride = 0) {
-  static_assert(!FINAL || (FM & 0b1110) == 0b0110, "level 1: ad / da fp32, dd fp64");
+  static_assert(!FINAL || (FM & 0b0110) == 0b0110, "level 1: ad / da fp32");
   __shared__ float SB[2][12][S3_T];                  // staged row: [c * 4 + band][column]
   __shared__ uint32_t OB[FINAL ? 2 : 1][2][FINAL ? S3_MAXSW * 3 / 4 : 1];  // U8 rows (FINAL)
   __shared__ float TH[12];
@@ -1983,19 +1945,21 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
   };
   __syncthreads();  // TH
   const int r0 = ma, R = (mb - ma) + 4;  // coefficient rows r0 .. r0 + R - 1
-  // the prefetch loads are unconditional and issued after the slot's last use (rows clamp into the
-  // band: load), and the steps past R pad the last iteration instead of breaking out of it: a load
-  // under a branch, or a break merging a shorter path into the loop header, makes the compiler wait
-  // for the load at once (as wl_dwt_stream)
+  // IDN_S3_PAD (A/B builds): wl_dwt_stream's ring form -- unconditional refills, the last iteration
+  // padded instead of left by a break
   S3Raw<FM> pf[S3_PF];
+  if (stg || IDN_S3_PAD) {
 #pragma unroll
-  for (int f = 0; f < S3_PF; ++f) load(r0 + f, pf[f]);
+    for (int f = 0; f < S3_PF; ++f)
+      if (IDN_S3_PAD || f < R) load(r0 + f, pf[f]);
+  }
   for (int s0 = 0; s0 < R; s0 += 10) {
 #pragma unroll
     for (int rs = 0; rs < 10; ++rs) {
       const int sidx = s0 + rs;
+      if (!IDN_S3_PAD && sidx >= R) break;
       const int r = r0 + sidx, buf = sidx & 1, slot = rs % 5;
-      if (stg) {  // stage row r (details soft-thresholded)
+      if (stg) {  // stage row r (details soft-thresholded), refill its prefetch slot
         const S3Raw<FM>& q = pf[rs % S3_PF];
 #pragma unroll
         for (int c = 0; c < 3; ++c)
@@ -2004,9 +1968,12 @@ __global__ __launch_bounds__(S3_T, IDN_S3_WPE) void wl_synth_final3(
             const float x = ((FM >> b) & 1) ? q.f[c][s3_slot<FM>(b)] : (float)q.d[c][s3_slot<FM>(b)];
             SB[buf][c * 4 + b][t] = b ? soft_t<float>(x, TH[c * 4 + b]) : x;
           }
+        if (!IDN_S3_PAD && sidx + S3_PF < R) load(r + S3_PF, pf[rs % S3_PF]);
       }
-      load(r + S3_PF, pf[rs % S3_PF]);  // refill the slot
-      if (sidx >= R) continue;          // padding (wave-uniform)
+      if (IDN_S3_PAD) {
+        load(r + S3_PF, pf[rs % S3_PF]);
+        if (sidx >= R) continue;
+      }
       __syncthreads();
       if (sidx >= 5) flush(r - 5, buf ^ 1);  // the previous step's U8 rows
       if (cmp) {
@@ -2596,6 +2563,71 @@ __device__ __forceinline__ unsigned long long wl_dd1_eval(const Dd1Raw& q, int c
   return absbits(dd);
 }
 
+// bior1.5: the level-1 highpass has two taps, so a finest dd is the 2x2 combination of the
+// normalised samples at rows 2i-4, 2i-3 and columns 2j-4, 2j-3 (pywt 'symmetric' indices), in
+// wl_dwt_stream's op order: the column highpass (two products, then their sum) of both columns,
+// then the row highpass.  The sigma median recomputes the few exact values it needs from the input
+// (wl_haar_median<1, true, true>), so the analysis keeps the level-1 dd band in fp32 only -- all
+// that the synthesis reads of it.
+__device__ __forceinline__ double bior_dd2x2(double x00, double x01, double x10, double x11) {
+  const double h0 = (-S2) * x10 + S2 * x00, h1 = (-S2) * x11 + S2 * x01;  // x[row][column]
+  return (-S2) * h1 + S2 * h0;
+}
+struct BiorDdRaw {  // u8: the dword holding each sample's 3 bytes, and the bit offset of the pixel
+  uint32_t v[2][2];
+  uint32_t sh[2];
+};
+__device__ __forceinline__ BiorDdRaw wl_bior_dd1_load(rsrc_t rs, int h, int w, int64_t row_stride,
+                                                      uint32_t pos, int W1) {
+  const int i = (int)(pos / (uint32_t)W1), j = (int)(pos - (uint32_t)i * (uint32_t)W1);
+  const int y[2] = {sym_idx(2 * i - 4, h), sym_idx(2 * i - 3, h)};
+  const int x[2] = {sym_idx(2 * j - 4, w), sym_idx(2 * j - 3, w)};
+  BiorDdRaw q;
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) q.sh[cc] = x[cc] > 0 ? 8u : 0u;
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)  // bytes 3x - 1 .. 3x + 2 (0 .. 3 at x = 0): never past the end
+      q.v[rr][cc] = __builtin_amdgcn_raw_buffer_load_b32(
+          rs, x[cc] > 0 ? 3u * (uint32_t)x[cc] - 1u : 0u, (uint32_t)((int64_t)y[rr] * row_stride), 0);
+  return q;
+}
+__device__ __forceinline__ unsigned long long wl_bior_dd1_eval(const BiorDdRaw& q, int c, wreal mn,
+                                                               wreal inv, wreal rcp) {
+  double r[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      double px[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        px[ch] = (double)((q.v[rr][cc] >> (q.sh[cc] + 8 * ch)) & 0xFFu) * (1.0 / 255.0);
+      const wreal a = ycbcr_c(px, c) - mn;  // wl_dwt_stream's norm (u8: reciprocal + Markstein)
+      const wreal q0 = a * rcp;
+      r[rr][cc] = __fma_rn(__fma_rn(-q0, inv, a), rcp, q0);
+    }
+  return absbits(bior_dd2x2(r[0][0], r[0][1], r[1][0], r[1][1]));
+}
+__device__ unsigned long long wl_bior_dd1_key64(const double* __restrict__ in64, int img, int h,
+                                                int w, uint32_t pos, int W1, int c, wreal mn,
+                                                wreal inv) {
+  const int i = (int)(pos / (uint32_t)W1), j = (int)(pos - (uint32_t)i * (uint32_t)W1);
+  const int y[2] = {sym_idx(2 * i - 4, h), sym_idx(2 * i - 3, h)};
+  const int x[2] = {sym_idx(2 * j - 4, w), sym_idx(2 * j - 3, w)};
+  double r[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      double px[3];
+      load_rgb64(nullptr, in64, img, h, w, 0, y[rr], x[cc], px);
+      r[rr][cc] = (ycbcr_c(px, c) - mn) / inv;  // wl_dwt_stream's norm for f64 input
+    }
+  return absbits(bior_dd2x2(r[0][0], r[0][1], r[1][0], r[1][1]));
+}
+
 // ---- Haar statistics for u8 input (L >= 2): integer moments instead of fp64 planes ---------------
 // BayesShrink needs per (channel, level, band) the sum of squared detail coefficients, and the
 // sigma median the fine-bin codes of the finest dd.  For u8 input every Haar detail is an integer
@@ -3079,8 +3111,9 @@ constexpr int WLM_WG = 512;
 constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slower: fewer workgroups per CU)
 // BAND: the general path (any wavelet; level-1 dd stored in fp64 by wl_dwt_rb, which also left
 // the codes at the start of the channel's input-plane slot): the exact keys of a position are
-// read from the band instead of recomputed from the pixels.  L is unused then.
-template <int L, bool BAND = false>
+// read from the band instead of recomputed from the pixels.  L is unused then.  BIOR (with BAND):
+// the codes as BAND, the keys recomputed from the input (bior_dd2x2; the band is fp32).
+template <int L, bool BAND = false, bool BIOR = false>
 __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restrict__ src,
                                                        const double* __restrict__ in64,
                                                        int64_t row_stride,
@@ -3235,7 +3268,30 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
     double* kb = mcnt <= LDS_KEYS ? reinterpret_cast<double*>(hist + 2048) : keys;
     // the exact keys of the selected bin, recomputed from the input (u8: 8 positions' loads in
     // flight per thread; the recompute is latency-bound otherwise)
-    if (BAND) {
+    if (BAND && BIOR) {
+      if (in64) {
+        for (uint32_t t = threadIdx.x; t < mcnt; t += WLM_WG)
+          kb[t] = __longlong_as_double((long long)wl_bior_dd1_key64(in64, img, Lt.h, Lt.w,
+                                                                     pos_sel[t], W1, c, mn, inv));
+      } else {
+        const rsrc_t rs = make_rsrc(src + (int64_t)img * Lt.h * row_stride,
+                                    (uint32_t)((int64_t)Lt.h * row_stride));
+        for (uint32_t t0 = threadIdx.x; t0 < mcnt; t0 += 8 * WLM_WG) {
+          BiorDdRaw q[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t t = t0 + (uint32_t)u * WLM_WG;
+            q[u] = wl_bior_dd1_load(rs, Lt.h, Lt.w, row_stride, t < mcnt ? pos_sel[t] : 0u, W1);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t t = t0 + (uint32_t)u * WLM_WG;
+            if (t < mcnt)
+              kb[t] = __longlong_as_double((long long)wl_bior_dd1_eval(q[u], c, mn, inv, rcp));
+          }
+        }
+      }
+    } else if (BAND) {
       for (uint32_t t = threadIdx.x; t < mcnt; t += WLM_WG)
         kb[t] = __longlong_as_double((long long)absbits(band_dd[pos_sel[t]]));
     } else if (in64) {
@@ -3304,10 +3360,22 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       } else {  // it is the smallest key of the next nonempty bin
         unsigned long long nmin = ~0ull;
         for (uint32_t t = threadIdx.x; t < ncnt; t += WLM_WG) {
-          const unsigned long long key =
-              BAND ? absbits(band_dd[pos_next[t]])
-                   : wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride, pos_next[t], W1, c,
-                                      mn, inv, rcp);
+          unsigned long long key;
+          if (BAND && BIOR) {
+            if (in64) {
+              key = wl_bior_dd1_key64(in64, img, Lt.h, Lt.w, pos_next[t], W1, c, mn, inv);
+            } else {
+              const rsrc_t rs = make_rsrc(src + (int64_t)img * Lt.h * row_stride,
+                                          (uint32_t)((int64_t)Lt.h * row_stride));
+              key = wl_bior_dd1_eval(wl_bior_dd1_load(rs, Lt.h, Lt.w, row_stride, pos_next[t], W1),
+                                     c, mn, inv, rcp);
+            }
+          } else if (BAND) {
+            key = absbits(band_dd[pos_next[t]]);
+          } else {
+            key = wl_dd1_key<MARK>(src, in64, img, Lt.h, Lt.w, row_stride, pos_next[t], W1, c, mn,
+                                   inv, rcp);
+          }
           nmin = key < nmin ? key : nmin;
         }
         for (int o = 32; o > 0; o >>= 1) {
@@ -3342,8 +3410,7 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
     int gx = (int)((np / 4 + 255) / 256);
     if (gx > 24) gx = 24;
-    hipLaunchKernelGGL(knob("IDN_WAVELET_KEYS", 1) ? wl_color_minmax<true> : wl_color_minmax<false>,
-                       dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
   int nwg_a;
@@ -3409,8 +3476,7 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
     int gx = (int)((np / 4 + 255) / 256);
     if (gx > 24) gx = 24;
-    hipLaunchKernelGGL(knob("IDN_WAVELET_KEYS", 1) ? wl_color_minmax<true> : wl_color_minmax<false>,
-                       dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
                        row_stride, stats);
   }
   double* part = (double*)((char*)ws + Lt.part_off);
@@ -3419,12 +3485,15 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   const size_t bsz1 = (size_t)Lt.H[1] * Lt.W[1];
   const bool codes = knob("IDN_WAVELET_CODEMED", 1) && (bsz1 + 3) / 4 + 2 * bsz1 <= (size_t)Lt.h * Lt.w;
   const bool fdet = knob("IDN_WAVELET_FDET", 1) != 0;
+  // bior1.5 with the code median: the level-1 dd band in fp32 too (the median recomputes its
+  // exact values from the input, bior_dd2x2; the synthesis reads it as fp32 either way)
+  const bool dd32 = WV == IDN_WAVELET_BIOR15 && codes && fdet && knob("IDN_WAVELET_DD32", 1) != 0;
   // band masks (wl_fband): level 1 / deeper levels, analysis stores and synthesis loads
   auto fm_an = [&](int l) {
     if (!fdet) return 0;
-    return (l == 1 ? 0b0110 : 0b1110 | WL_FB_AIN) | (l < Lt.L ? 0b0001 : 0);
+    return (l == 1 ? (dd32 ? 0b1110 : 0b0110) : 0b1110 | WL_FB_AIN) | (l < Lt.L ? 0b0001 : 0);
   };
-  auto fm_syn = [&](int l) { return !fdet ? 0 : (l == 1 ? 0b0110 : 0b1110); };
+  auto fm_syn = [&](int l) { return !fdet ? 0 : (l == 1 && !dd32 ? 0b0110 : 0b1110); };
   const int coop = knob("IDN_WAVELET_COOP", 1) ? 1 : 0;
   const int a32 = knob("IDN_WAVELET_A32", 3);
   for (int l = 1; l <= Lt.L; ++l) {
@@ -3452,7 +3521,9 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
 #define IDN_WS(SRC, TL, TH, EMIT)                                                                  \
   do {                                                                                             \
     const int fmb = fm_an(l) & 0b1111;                                                             \
-    if (SRC == 0 && fmb == 0b0111 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0111, 1, EMIT);           \
+    if (SRC == 0 && fmb == 0b1111 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b1111, 1, EMIT);           \
+    else if (SRC == 0 && fmb == 0b1110 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b1110, 1, EMIT);      \
+    else if (SRC == 0 && fmb == 0b0111 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0111, 1, EMIT);      \
     else if (SRC == 0 && fmb == 0b0110 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0110, 1, EMIT);      \
     else if (SRC == 3 && fmb == 0b1111) IDN_WS_(SRC, TL, TH, 0b1111, 0, EMIT);                     \
     else if (SRC == 3 && fmb == 0b1110) IDN_WS_(SRC, TL, TH, 0b1110, 0, EMIT);                     \
@@ -3491,7 +3562,10 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
                          Lt.part_tile0[1], codes ? 1 : 0, fm_an(1), coop);
   }
   hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
-  if (codes)
+  if (codes && dd32)
+    hipLaunchKernelGGL((wl_haar_median<1, true, true>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64,
+                       row_stride, wsf, Lt.img_floats, stats, Lt);
+  else if (codes)
     hipLaunchKernelGGL((wl_haar_median<1, true>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64,
                        row_stride, wsf, Lt.img_floats, stats, Lt);
   else
@@ -3562,12 +3636,20 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
                              l, Lt.L, Lt.off_band[l], Lt.H[l], Lt.W[l], Lt.off_band[l - 1], Hout,
                              Wout, (size_t)4 * Hout * Wout, fm_syn2(l), sw, strips, bands,
                              (uint8_t*)nullptr, row_stride, (float*)nullptr);
-      } else if (s32 && s3 && (fm_syn2(1) == 0b0111 || fm_syn2(1) == 0b0110)) {
+      } else if (s32 && s3 && (fm_syn2(1) & 0b0110) == 0b0110) {
         const int strips3 = s3_strips(Wout), sw3 = s3_sw(Wout);
         const int bands3 = ss_bands_occ(n, (Hout + 1) / 2, strips3,
                                         reinterpret_cast<const void*>(&wl_synth_final3<0b0111>), S3_T);
         const dim3 grid3((unsigned)(strips3 * bands3), 1, (unsigned)n);
-        if (fm_syn2(1) == 0b0111)
+        if (fm_syn2(1) == 0b1111)
+          hipLaunchKernelGGL((wl_synth_final3<0b1111>), grid3, dim3(S3_T), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h,
+                             Lt.w, sw3, strips3, bands3, out_u8, row_stride, out_f32);
+        else if (fm_syn2(1) == 0b1110)
+          hipLaunchKernelGGL((wl_synth_final3<0b1110>), grid3, dim3(S3_T), 0, st, wsf,
+                             Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h,
+                             Lt.w, sw3, strips3, bands3, out_u8, row_stride, out_f32);
+        else if (fm_syn2(1) == 0b0111)
           hipLaunchKernelGGL((wl_synth_final3<0b0111>), grid3, dim3(S3_T), 0, st, wsf,
                              Lt.img_floats, stats, Lt.L, Lt.off_band[1], Lt.H[1], Lt.W[1], Lt.h,
                              Lt.w, sw3, strips3, bands3, out_u8, row_stride, out_f32);

@@ -185,6 +185,25 @@ def test_dwt_restatement(gold):
         assert oracle.wavelet.dwt_max_level(int(n), len(oracle.wavelet.FILTERS[w][0])) == lvl
 
 
+@pytest.mark.parametrize("shape", [(37, 53), (8, 9), (600, 1000)])
+def test_bior15_finest_dd_is_a_2x2_combination(shape):
+    """bior1.5's analysis highpass has two taps, so each level-1 dd coefficient (pywt dwtn: axis 0,
+    then axis 1) is the 2x2 combination of the samples at rows 2i-4, 2i-3 and columns 2j-4, 2j-3
+    ('symmetric' indices) in the op order (-S * odd) + (S * even): bit for bit.  The HIP sigma median
+    recomputes its candidates this way (csrc/wavelet.hip bior_dd2x2) instead of storing the fp64
+    band."""
+    from oracle.wavelet import _S, _sym_index, dwtn
+    x = np.random.RandomState(sum(shape)).rand(*shape)
+    dd = dwtn(x, "bior1.5")["dd"]
+    i = np.arange(dd.shape[0])[:, None]
+    j = np.arange(dd.shape[1])[None, :]
+    r0, r1 = _sym_index(2 * i - 4, shape[0]), _sym_index(2 * i - 3, shape[0])
+    c0, c1 = _sym_index(2 * j - 4, shape[1]), _sym_index(2 * j - 3, shape[1])
+    h0 = (-_S) * x[r1, c0] + _S * x[r0, c0]  # column highpass of both columns
+    h1 = (-_S) * x[r1, c1] + _S * x[r0, c1]
+    np.testing.assert_array_equal(((-_S) * h1 + _S * h0).view(np.uint64), dd.view(np.uint64))
+
+
 def test_denoise_wavelet_crops(gold):
     g, m = gold
     for case in m["wavelet"]:
