@@ -862,8 +862,14 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
   }
   // ---- row role
   const int half = SW / 2;
-  const bool rowt = t < 3 * half;
-  const int rc = rowt ? t / half : 0, jj = rowt ? 2 * (t - rc * half) : 0;
+  // task u = (channel rc, column pair jj): at level 1 spread over every wave of the workgroup in
+  // contiguous runs, so that no wave sits at the step's barrier without row work (934 vs 962 us);
+  // deeper levels keep u = t (spread measured 273 vs 262 us at level 2: profiles/r04/wavelet/)
+  const int nwv = (int)(blockDim.x >> 6);  // waves of the launch (NT is only the maximum)
+  const int rw = SRC < 2 ? (3 * half + nwv - 1) / nwv : 64;  // tasks per wave
+  const int u = SRC < 2 ? (t >> 6) * rw + (t & 63) : t;
+  const bool rowt = (t & 63) < rw && u < 3 * half;
+  const int rc = rowt ? u / half : 0, jj = rowt ? 2 * (u - rc * half) : 0;
   const int oj = j0 + jj;
   const bool ok0 = rowt && oj < Wo, ok1 = rowt && oj + 1 < Wo;
   const size_t bsz = (size_t)Ho * Wo;
@@ -1024,7 +1030,7 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
   double* red = &RED[0][0];
   if (rowt) {
 #pragma unroll
-    for (int b = 0; b < 3; ++b) red[b * NT + t] = sqa[b];
+    for (int b = 0; b < 3; ++b) red[b * NT + u] = sqa[b];
   }
   __syncthreads();
   if (t < 9) {
@@ -2585,12 +2591,15 @@ __device__ __forceinline__ BiorDdRaw wl_bior_dd1_load(rsrc_t rs, int h, int w, i
   BiorDdRaw q;
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc) q.sh[cc] = x[cc] > 0 ? 8u : 0u;
+  // bytes 3x - 1 .. 3x + 2 (0 .. 3 at x = 0): never past the end.  The whole offset goes in the
+  // per-lane operand (a per-lane row offset in the scalar one becomes a loop over the lanes)
 #pragma unroll
   for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc)  // bytes 3x - 1 .. 3x + 2 (0 .. 3 at x = 0): never past the end
+    for (int cc = 0; cc < 2; ++cc)
       q.v[rr][cc] = __builtin_amdgcn_raw_buffer_load_b32(
-          rs, x[cc] > 0 ? 3u * (uint32_t)x[cc] - 1u : 0u, (uint32_t)((int64_t)y[rr] * row_stride), 0);
+          rs, (uint32_t)((int64_t)y[rr] * row_stride) + (x[cc] > 0 ? 3u * (uint32_t)x[cc] - 1u : 0u),
+          0u, 0);
   return q;
 }
 __device__ __forceinline__ unsigned long long wl_bior_dd1_eval(const BiorDdRaw& q, int c, wreal mn,
@@ -3108,6 +3117,10 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
 // threads per (image, channel): several workgroups per CU overlap phases (512 measured 0.7 %
 // faster on the whole bior1.5 op than 256 and 1024)
 constexpr int WLM_WG = 512;
+#ifndef IDN_WLM_IT  // A/B builds set it
+#define IDN_WLM_IT 8
+#endif
+constexpr int WLM_IT = IDN_WLM_IT;  // code groups (4 codes, 8 bytes) in flight per lane, passes 1-2
 constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slower: fewer workgroups per CU)
 // BAND: the general path (any wavelet; level-1 dd stored in fp64 by wl_dwt_rb, which also left
 // the codes at the start of the channel's input-plane slot): the exact keys of a position are
@@ -3158,15 +3171,15 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
   auto code_at = [](const uint2& g, int q) -> uint32_t {
     return ((q < 2 ? g.x : g.y) >> (16 * (q & 1))) & 0xFFFFu;
   };
-  for (uint32_t g0 = threadIdx.x; g0 < ngrp; g0 += 8 * WLM_WG) {
-    uint2 gv[8];
+  for (uint32_t g0 = threadIdx.x; g0 < ngrp; g0 += WLM_IT * WLM_WG) {
+    uint2 gv[WLM_IT];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < WLM_IT; ++u) {
       const uint32_t g = g0 + (uint32_t)u * WLM_WG;
       gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < WLM_IT; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t cd = code_at(gv[u], q);
@@ -3220,17 +3233,17 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       off_sel = base_sel + (excl & 0xFFFFu);
       off_next = base_next + (excl >> 16);
     };
-    for (uint32_t gb = 0; gb < ngrp; gb += 8 * WLM_WG) {  // uniform trip count: the scan needs
+    for (uint32_t gb = 0; gb < ngrp; gb += WLM_IT * WLM_WG) {  // uniform trip count: the scan needs
       const uint32_t g0 = gb + threadIdx.x;                // every lane of the wave
-      uint2 gv[8];
+      uint2 gv[WLM_IT];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < WLM_IT; ++u) {
         const uint32_t g = g0 + (uint32_t)u * WLM_WG;
         gv[u] = g < ngrp ? cg[g] : uint2{0u, 0u};
       }
       uint32_t cnt2 = 0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < WLM_IT; ++u)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t cd = code_at(gv[u], q);
@@ -3241,7 +3254,7 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       place(cnt2, os, on);
       if (cnt2) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < WLM_IT; ++u)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint32_t cd = code_at(gv[u], q);
@@ -3276,15 +3289,19 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
       } else {
         const rsrc_t rs = make_rsrc(src + (int64_t)img * Lt.h * row_stride,
                                     (uint32_t)((int64_t)Lt.h * row_stride));
-        for (uint32_t t0 = threadIdx.x; t0 < mcnt; t0 += 8 * WLM_WG) {
-          BiorDdRaw q[8];
+        // BQ positions per thread and round: all positions first (clamped, unconditional: a load
+        // under a branch is waited for at once), then all their pixels.  BQ = 6 keeps the kernel
+        // at <= 80 VGPRs: three 512-thread workgroups per CU, the whole grid resident at once
+        constexpr int BQ = 6;
+        for (uint32_t t0 = threadIdx.x; t0 < mcnt; t0 += BQ * WLM_WG) {
+          uint32_t pp[BQ];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const uint32_t t = t0 + (uint32_t)u * WLM_WG;
-            q[u] = wl_bior_dd1_load(rs, Lt.h, Lt.w, row_stride, t < mcnt ? pos_sel[t] : 0u, W1);
-          }
+          for (int u = 0; u < BQ; ++u) pp[u] = pos_sel[min(t0 + (uint32_t)u * WLM_WG, mcnt - 1)];
+          BiorDdRaw q[BQ];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < BQ; ++u) q[u] = wl_bior_dd1_load(rs, Lt.h, Lt.w, row_stride, pp[u], W1);
+#pragma unroll
+          for (int u = 0; u < BQ; ++u) {
             const uint32_t t = t0 + (uint32_t)u * WLM_WG;
             if (t < mcnt)
               kb[t] = __longlong_as_double((long long)wl_bior_dd1_eval(q[u], c, mn, inv, rcp));
