@@ -3120,7 +3120,11 @@ constexpr int WLM_WG = 512;
 #ifndef IDN_WLM_IT  // A/B builds set it
 #define IDN_WLM_IT 8
 #endif
-constexpr int WLM_IT = IDN_WLM_IT;  // code groups (4 codes, 8 bytes) in flight per lane, passes 1-2
+constexpr int WLM_IT = IDN_WLM_IT;
+#ifndef IDN_WLM_HQ  // A/B builds set it
+#define IDN_WLM_HQ 6
+#endif
+constexpr int HQ = IDN_WLM_HQ;  // Haar median: candidate positions per thread and round  // code groups (4 codes, 8 bytes) in flight per lane, passes 1-2
 constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slower: fewer workgroups per CU)
 // BAND: the general path (any wavelet; level-1 dd stored in fp64 by wl_dwt_rb, which also left
 // the codes at the start of the channel's input-plane slot): the exact keys of a position are
@@ -3316,15 +3320,16 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
         kb[t] = __longlong_as_double((long long)wl_dd1_key<MARK>(
             src, in64, img, Lt.h, Lt.w, row_stride, pos_sel[t], W1, c, mn, inv, rcp));
     } else {
-      for (uint32_t t0 = threadIdx.x; t0 < mcnt; t0 += 8 * WLM_WG) {
-        Dd1Raw q[8];
+      for (uint32_t t0 = threadIdx.x; t0 < mcnt; t0 += HQ * WLM_WG) {
+        // as the bior form: all positions first (clamped, unconditional), then their pixels
+        uint32_t pp[HQ];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const uint32_t t = t0 + (uint32_t)u * WLM_WG;
-          q[u] = wl_dd1_load(src, img, Lt.h, row_stride, t < mcnt ? pos_sel[t] : 0u, W1);
-        }
+        for (int u = 0; u < HQ; ++u) pp[u] = pos_sel[min(t0 + (uint32_t)u * WLM_WG, mcnt - 1)];
+        Dd1Raw q[HQ];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < HQ; ++u) q[u] = wl_dd1_load(src, img, Lt.h, row_stride, pp[u], W1);
+#pragma unroll
+        for (int u = 0; u < HQ; ++u) {
           const uint32_t t = t0 + (uint32_t)u * WLM_WG;
           if (t < mcnt)
             kb[t] = __longlong_as_double((long long)wl_dd1_eval<MARK>(q[u], c, mn, inv, rcp));
