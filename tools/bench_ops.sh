@@ -11,5 +11,6 @@ python - "$OUT/bench.jsonl" <<'PY'
 import json, sys
 for l in open(sys.argv[1]):
     d = json.loads(l); r = d["roofline"]
-    print(f"{d['config']['op']:16s} ms/step {d['ms_per_step']:.4f} kern {r['kernel_ms_avg']:.4f} GB/s {r['achieved']:.0f} frac {r['frac']:.3f}")
+    frac = "-" if r["frac"] is None else f"{r['frac']:.3f}"
+    print(f"{d['config']['op']:16s} ms/step {d['ms_per_step']:.4f} kern {r['kernel_ms_avg']:.4f} GB/s {r['achieved']:.0f} frac {frac}")
 PY
