@@ -2940,7 +2940,11 @@ __device__ __forceinline__ void haar_bfly(double A, double AD, double DA, double
   x[3] = m - q1;
 }
 
-template <int L>
+// S32: the level-1 stage (details, soft thresholds, butterflies, clip, de-normalisation,
+// YCbCr -> RGB) in fp32 with v_med3 clamps, as bior1.5's synthesis: it is continuous in its
+// inputs and no exact zero depends on it (the levels above stay fp64; ~1e-7 on the [0, 1]
+// output against the 1e-5 tolerance).  false: all fp64 (A/B: IDN_WAVELET_HS32=0)
+template <int L, bool S32 = true>
 __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __restrict__ src, int h,
                                                             int w, int64_t row_stride,
                                                             const double* __restrict__ stats,
@@ -3049,6 +3053,17 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
                               {0.004566210045662101 * 255, 0.007910716233554741 * 255, 1.1977497040511743e-08 * 255}};
   const bool dw = out_u8 && ((reinterpret_cast<uintptr_t>(out_u8) | (uintptr_t)row_stride) & 3) == 0;
   uint32_t rowp[2][3];
+  float x1f[3], thf[3][3], invf[3], mof[3];  // S32: the level-1 constants in fp32
+  if constexpr (S32) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      x1f[c] = (float)(0.5 * s1c[c]);
+#pragma unroll
+      for (int b = 0; b < 3; ++b) thf[c][b] = (float)st[WlStats::thrh(c, 0, b)];
+      invf[c] = (float)invc[c];
+      mof[c] = (float)(mnc[c] - (c == 0 ? 16.0 : 128.0));
+    }
+  }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int gy = g >> 1, gx = g & 1;
@@ -3066,6 +3081,53 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
       haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
                px(2 * gy + 1, 6 * gx + 3 + ch), aa, D[0][ch], D[1][ch], D[2][ch]);
     }
+    if constexpr (S32) {
+      constexpr float Rf[3][3] = {
+          {(float)(0.004566210045662101 * 255), (float)(1.1808799897950177e-09 * 255), (float)(0.006258928969943937 * 255)},
+          {(float)(0.004566210045662101 * 255), (float)(-0.0015363236860449021 * 255), (float)(-0.003188110949655707 * 255)},
+          {(float)(0.004566210045662101 * 255), (float)(0.007910716233554741 * 255), (float)(1.1977497040511743e-08 * 255)}};
+      float vf[4][3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float d[3];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {  // soft(x, t) = x - clamp(x, -t, t), one v_med3
+          const float xb = (float)(__mul24(ycc_w(c, 0), D[b][0]) + __mul24(ycc_w(c, 1), D[b][1]) +
+                                   __mul24(ycc_w(c, 2), D[b][2])) * x1f[c];
+          d[b] = xb - __builtin_amdgcn_fmed3f(xb, -thf[c][b], thf[c][b]);
+        }
+        const float A = (float)Ah1[g][c];
+        const float p = A + d[0], m = A - d[0], q0 = d[1] + d[2], q1 = d[1] - d[2];
+        vf[0][c] = p + q0;
+        vf[1][c] = m + q1;
+        vf[2][c] = p - q0;
+        vf[3][c] = m - q1;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i >> 1, s = i & 1;
+        float e[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          e[c] = __fmaf_rn(__builtin_amdgcn_fmed3f(vf[i][c], 0.f, 1.f), invf[c], mof[c]);
+        const int y = y0 + 2 * gy + r, xx = x0 + 2 * gx + s;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float o = __fmaf_rn(e[2], Rf[c][2], __fmaf_rn(e[1], Rf[c][1], e[0] * Rf[c][0]));
+          const uint32_t u = (uint32_t)min(max((int)o, 0), 255);  // as the fp64 form
+          if (dw) {
+            const int bi = (2 * gx + s) * 3 + c;
+            rowp[r][bi >> 2] |= u << (8 * (bi & 3));
+          } else if (out_u8) {
+            out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] =
+                (uint8_t)u;
+          }
+          if (out_f32)
+            out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] =
+                __builtin_amdgcn_fmed3f(o, 0.f, 255.f) * (1.f / 255.f);
+        }
+      }
+    } else {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const double x1 = 0.5 * s1c[c];
@@ -3101,6 +3163,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_haar_synth_int(const uint8_t* __res
           out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = (float)(fmin(fmax(o, 0.0), 255.0) * (1.0 / 255.0));
       }
     }
+    }  // S32
     if (dw && gx == 1) {
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
@@ -3465,8 +3528,12 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
   hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   if constexpr (L >= 2) {
     if (src && knob("IDN_WAVELET_INTSYNTH", 1)) {
-      hipLaunchKernelGGL((wl_haar_synth_int<L>), dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
-                         row_stride, stats, out_u8, out_f32);
+      if (knob("IDN_WAVELET_HS32", 1))
+        hipLaunchKernelGGL((wl_haar_synth_int<L, true>), dim3(nwg, n), dim3(WLH_WG), 0, st, src,
+                           Lt.h, Lt.w, row_stride, stats, out_u8, out_f32);
+      else
+        hipLaunchKernelGGL((wl_haar_synth_int<L, false>), dim3(nwg, n), dim3(WLH_WG), 0, st, src,
+                           Lt.h, Lt.w, row_stride, stats, out_u8, out_f32);
       return;
     }
   }

@@ -242,13 +242,14 @@ int idn_copy_u8(const uint8_t* src, uint8_t* dst, int64_t nbytes, int policy, vo
  * c = 3.  levels <= 0 selects skimage's default max(dwt_max_level - 3, 1).  in_f64 (nullable)
  * replaces src when the caller holds a float image in [0,1] (the reference's f64 branches, dense
  * n*h*w*3).  out_f32 (nullable) receives the float result before the U8 cast (dense n*h*w*3).
- * Precision: Haar (fused and general paths) computes in fp64.  bior1.5 keeps pywt's fp64 op order
- * where an exact value matters -- the normalisation (exact quotient), the level-1 column highpass
- * and the finest dd (whose exact zeros and median give sigma, bit-identical to an all-fp64 run),
- * and the sums of squares -- and runs the lowpass outputs (aa / ad / da), the deeper levels and
- * the synthesis in fp32; intermediate bands live in the workspace as fp32 (the finest dd and the
- * coarsest aa as fp64): |out - reference| <= 1e-5 before the cast (tests: <= 2e-6 from the
- * all-fp64 form).
+ * Precision: Haar computes its statistics exactly (integer moments / fp64) and, on the fused
+ * path, its level-1 synthesis stage in fp32.  bior1.5 keeps pywt's fp64 op order where an exact
+ * value matters -- the normalisation (exact quotient), the level-1 column highpass and the finest
+ * dd (whose exact zeros and median give sigma, bit-identical to an all-fp64 run: the median
+ * recomputes its candidates' exact dd from the input), and the sums of squares -- and runs the
+ * lowpass outputs (aa / ad / da), the deeper levels and the synthesis in fp32; intermediate bands
+ * live in the workspace as fp32 (the coarsest aa as fp64): |out - reference| <= 1e-5 before the
+ * cast (tests: <= 2e-6 from the all-fp64 form).
  * Replaces lib/model/test.py:197-201,1807-1810, minibatch.py:1653-1656,
  * minibatch_before_curvelet.py:85-87. */
 int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,
