@@ -3193,12 +3193,53 @@ constexpr int WLM_NH = 8;    // histogram copies (32 KB of LDS; 16 measured slow
 // the codes at the start of the channel's input-plane slot): the exact keys of a position are
 // read from the band instead of recomputed from the pixels.  L is unused then.  BIOR (with BAND):
 // the codes as BAND, the keys recomputed from the input (bior_dd2x2; the band is fp32).
+// The channel's sums of squares of every detail band over the analysis' per-tile partials (one
+// wave per band, lanes over the tiles in a fixed order: deterministic, and exact for bior1.5 whose
+// partials sit on a power-of-two grid) and its BayesShrink thresholds -- wl_sumsq's and
+// wl_thresh's work for one channel, at the end of its median workgroup.  The degenerate-image
+// flag is only ever raised here (wl_init_stats cleared it), so the three channels' workgroups
+// cannot undo one another.
+__device__ void wl_sums_thresh(double* __restrict__ st, const double* __restrict__ part_img, int c,
+                               const WlLayout& Ls, const WlLayout& Lt, double med, wreal mn,
+                               wreal mx) {
+  __shared__ double sums[3 * WL_MAXL];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = wave; k < 3 * Lt.L; k += WLM_WG / 64) {
+    const int l = k / 3, b = k - 3 * l, lev = l + 1;
+    const double* p = part_img + (size_t)(c * 3 + b) * (Ls.part_per_img / 9) + Ls.part_tile0[lev];
+    double s = 0.0;
+    for (int t = lane; t < Ls.tiles[lev]; t += 64) s += p[t];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) sums[k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const double sigma = med / 0.6744897501960817;
+  const bool bad = !(mx > mn) || !(sigma == sigma);  // 0.14.2: NaN everywhere -> U8 0
+  const double var = sigma * sigma;
+  for (int l = 0; l < Lt.L; ++l)
+    for (int b = 0; b < 3; ++b) {
+      const double sq = sums[3 * l + b];
+      st[WlStats::sumsq(c, l, b, Lt.L)] = sq;
+      const double cnt = (double)Lt.H[l + 1] * Lt.W[l + 1];
+      const double t = var / sqrt(fmax(sq / cnt - var, 2.220446049250313e-16));
+      st[WlStats::thr(c, l, b, Lt.L)] = t;
+      if (Lt.L <= 3) st[WlStats::thrh(c, l, b)] = 0.5 * t;
+    }
+  if (bad) st[WlStats::FLAG] = 1.0;
+}
+
+// part (non-null): the channel's sums of squares over the analysis partials (wl_sumsq's work, in
+// the partials layout Ls) and its BayesShrink thresholds (wl_thresh's) follow the median in the
+// same workgroup -- two launches less per op
 template <int L, bool BAND = false, bool BIOR = false>
 __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restrict__ src,
                                                        const double* __restrict__ in64,
                                                        int64_t row_stride,
                                                        wreal* __restrict__ ws, size_t img_floats,
-                                                       double* __restrict__ stats, WlLayout Lt) {
+                                                       double* __restrict__ stats, WlLayout Lt,
+                                                       const double* __restrict__ part = nullptr,
+                                                       WlLayout Ls = WlLayout{}) {
   constexpr bool MARK = L >= 2;
   const int img = blockIdx.x / 3, c = blockIdx.x % 3;
   const int W1 = Lt.W[1];
@@ -3478,6 +3519,7 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
     st[WlStats::median(c, Lt.L)] = med;
     st[WlStats::DIAG + c] = (double)total;  // diagnostics
   }
+  if (part) wl_sums_thresh(st, part + img * Ls.part_per_img, c, Ls, Lt, med, mn, mx);
 }
 
 template <int L>
@@ -3522,10 +3564,17 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     Ls.tiles[l] = nwg_a;
     Ls.part_tile0[l] = (size_t)(l - 1) * nwg_a;
   }
-  hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * L * 3), dim3(256), 0, st, stats, part, Ls);
-  hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
-                     wsf, Lt.img_floats, stats, Lt);
-  hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  // the median workgroups also reduce the sums of squares and set the thresholds (wl_sumsq and
+  // wl_thresh as separate launches: IDN_WAVELET_FUSETHR=0)
+  if (knob("IDN_WAVELET_FUSETHR", 1)) {
+    hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
+                       wsf, Lt.img_floats, stats, Lt, (const double*)part, Ls);
+  } else {
+    hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * L * 3), dim3(256), 0, st, stats, part, Ls);
+    hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
+                       wsf, Lt.img_floats, stats, Lt, (const double*)nullptr, Ls);
+    hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  }
   if constexpr (L >= 2) {
     if (src && knob("IDN_WAVELET_INTSYNTH", 1)) {
       if (knob("IDN_WAVELET_HS32", 1))
@@ -3650,16 +3699,20 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
                          Lt.tiles_x[1], src, in64, row_stride, part, Lt.part_per_img,
                          Lt.part_tile0[1], codes ? 1 : 0, fm_an(1), coop);
   }
-  hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
+  // the code medians also reduce the sums of squares and set the thresholds (see wl_haar_median)
+  const bool fuse = codes && knob("IDN_WAVELET_FUSETHR", 1);
+  const double* part_f = fuse ? (const double*)part : nullptr;
+  if (!fuse)
+    hipLaunchKernelGGL(wl_sumsq, dim3(n * 3 * Lt.L * 3), dim3(256), 0, st, stats, part, Lt);
   if (codes && dd32)
     hipLaunchKernelGGL((wl_haar_median<1, true, true>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64,
-                       row_stride, wsf, Lt.img_floats, stats, Lt);
+                       row_stride, wsf, Lt.img_floats, stats, Lt, part_f, Lt);
   else if (codes)
     hipLaunchKernelGGL((wl_haar_median<1, true>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64,
-                       row_stride, wsf, Lt.img_floats, stats, Lt);
+                       row_stride, wsf, Lt.img_floats, stats, Lt, part_f, Lt);
   else
     hipLaunchKernelGGL(wl_median, dim3(n * 3), dim3(1024), 0, st, wsf, Lt.img_floats, stats, Lt);
-  hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  if (!fuse) hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
   // bior1.5 synthesis form per level (bit 0: level 1, bit 1: deeper levels): streaming
   // (wl_synth_stream) or tiled (wl_synth / wl_synth_final)
   const int sstream = WV == IDN_WAVELET_BIOR15 ? knob("IDN_WAVELET_SSTREAM", 3) : 0;
