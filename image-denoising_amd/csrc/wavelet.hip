@@ -693,7 +693,7 @@ inline int ws_bands(int n, int Ho, int Wo, int strips, int level) {
   // and measured 20 % slower at levels 2-3: the analysis is throughput-bound there, and extra bands
   // only add warm-up rows, profiles/r04/wavelet/.)
   (void)Wo;
-  const int block = ws_maxsw() * 2 + 8 <= 64 ? 64 : WS_MAXT;  // one-wave strips: their own count
+  const int block = WS_MAXT;
   const int64_t units = (int64_t)n * strips, resident = std::max<int64_t>(ws_resident(level, block), 1);
   const int bmax = std::max(1, std::min({64, Ho / 16, groups}));
   int best = 1;
@@ -752,7 +752,9 @@ template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : SRC ==
 // median's population); deeper levels (no median) run both paths in fp32.
 // FM >= 0: the band storage mask (wl_fband) and CODES the level-1 code emission as compile-time
 // constants (the product's masks: no per-band branches); FM = -1 takes both from the arguments.
-// NT: threads per workgroup the LDS arrays are sized for (512; 64 for one-wave strips)
+// NT: threads per workgroup the LDS arrays are sized for (the product launches 512; instances
+// sized for 64- and 256-thread strips measured slower at every band count: level 1 1.39 / 1.04
+// ms vs 0.93, profiles/r04/wavelet/strips_sweep.txt)
 template <int SRC, typename TL = wreal, typename TH = wreal, int FM = -1, int CODES = -1,
           int NT = WS_MAXT>
 __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
@@ -1045,10 +1047,8 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
 // deeper: fp32 'aa' input), used by wl_layout's band count for every form of that level
 int ws_resident(int level, int block) {
   const void* k = level == 1
-      ? (block == 64 ? reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1, 64>)
-                     : reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b0111, 1>))
-      : (block == 64 ? reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0, 64>)
-                     : reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0>));
+      ? reinterpret_cast<const void*>(&wl_dwt_stream<0, float, wreal, 0b1111, 1>)
+      : reinterpret_cast<const void*>(&wl_dwt_stream<3, float, float, 0b1111, 0>);
   return cu_count() * occ_wgs(k, block);
 }
 
@@ -3644,12 +3644,6 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
       // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
 #define IDN_WS_(SRC, TL, TH, FMC, CC, EMIT)                                                        \
-  if (blk.x == 64 && (FMC) >= 0)                                                                   \
-    hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC, 64>), grid, blk, 0, st, wsf,           \
-                       Lt.img_floats, stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, \
-                       strips, bands, groups, src, in64, row_stride, part, Lt.part_per_img,        \
-                       Lt.part_tile0[l], EMIT, fm_an(l), Lt.sq_grid[l]);                           \
-  else                                                                                             \
   hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC>), grid, blk, 0, st, wsf, Lt.img_floats,  \
                      stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands,   \
                      groups, src, in64, row_stride, part, Lt.part_per_img, Lt.part_tile0[l], EMIT, \
