@@ -1,16 +1,17 @@
 #!/bin/bash
-# rocprofv3 kernel stats of bench ops: bash tools/ks_op.sh <out_dir> <op> [op ...] (env passes through)
+# kernel-trace stats of one bench op: bash tools/ks_op.sh <out_dir> <op> [steps]
 set -u
-OUT=gpurun_out/$1; shift
+OUT=gpurun_out/$1; OP=$2; STEPS=${3:-20}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ROOT=$(pwd)
-for op in "$@"; do
-  timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/ks_$op" -o k --output-format csv \
-    -- python3 bench.py --op $op --no-cpu --no-copy --steps 20 --warmup 3 > "$OUT/ks_$op.log" 2>&1 || { tail "$OUT/ks_$op.log"; exit 1; }
-  python3 - "$OUT/ks_$op/k_kernel_stats.csv" <<'PY'
-import csv, sys
-for r in list(csv.DictReader(open(sys.argv[1])))[:8]:
-    print(f"{r['Name'][:70]:70s} {int(r['Calls']):5d} {float(r['AverageNs'])/1e3:9.1f} us {float(r['Percentage']):5.1f}%")
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/ks" -o k --output-format csv \
+  -- python3 bench.py --op "$OP" --no-cpu --no-copy --steps "$STEPS" --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
+python3 - "$OUT" <<'PY'
+import csv, json, sys
+out = sys.argv[1]
+rows = list(csv.DictReader(open(out + "/ks/k_kernel_stats.csv")))
+for r in rows[:25]:
+    print(f"{r['Name'][:70]:70s} calls {r['Calls']:>6s} avg {float(r['AverageNs'])/1e3:9.1f} us total {float(r['TotalDurationNs'])/1e3:10.1f} us")
+d = json.loads(open(out + "/bench.json").read().strip().splitlines()[-1])
+print("ms_per_step", d["ms_per_step"])
 PY
-done
