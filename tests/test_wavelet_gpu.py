@@ -404,3 +404,50 @@ def test_wavelet_color_minmax_key_ties(dev, swap):
     mx = _key_to_f64(st[0, 203:206].view(np.uint64))
     np.testing.assert_array_equal(mn.view(np.uint64), ycc.min(axis=(0, 1)).view(np.uint64))
     np.testing.assert_array_equal(mx.view(np.uint64), ycc.max(axis=(0, 1)).view(np.uint64))
+
+
+@pytest.mark.parametrize("wavelet,levels,shape", [("bior1.5", None, (600, 1000)),
+                                                  ("bior1.5", None, (37, 53)),
+                                                  ("db1", 3, (120, 200)), ("db1", 2, (64, 96))])
+def test_wavelet_fused_thresholds_match_separate(dev, monkeypatch, wavelet, levels, shape):
+    """the median workgroups reduce each channel's sums of squares and set its BayesShrink
+    thresholds (product) instead of the separate wl_sumsq / wl_thresh launches
+    (IDN_WAVELET_FUSETHR=0, tuning build): bior1.5's partials sit on a power-of-two grid, so its
+    sums -- and every output -- are bit-identical; Haar's partials add in another order (sums to
+    1e-12 relative, outputs to rounding)"""
+    import torch
+    from idn import _lib
+    x = torch.from_numpy(_stat_images(*shape)[:3] if shape != (600, 1000)
+                         else np.stack([make_img(600, 1000, 21)])).cuda()
+    u8a, fa, sa = _stats_after_w(x, wavelet, levels)
+    monkeypatch.setenv("IDN_WAVELET_FUSETHR", "0")
+    with _lib.variant("tuning"):
+        u8b, fb, sb = _stats_after_w(x, wavelet, levels)
+    if wavelet == "bior1.5":
+        np.testing.assert_array_equal(sa.view(np.uint64), sb.view(np.uint64))
+        np.testing.assert_array_equal(u8a, u8b)
+        np.testing.assert_array_equal(fa, fb)
+    else:
+        L = levels
+        fl = np.zeros(256, bool)  # the sums, medians, thresholds and half thresholds
+        fl[8:8 + 9 * L + 3 + 9 * L] = True
+        fl[170:197] = True
+        # (NaN where a channel has no nonzero finest detail: the same in both forms)
+        np.testing.assert_allclose(sa[:, fl], sb[:, fl], rtol=1e-12, atol=0, equal_nan=True)
+        np.testing.assert_array_equal(sa[:, ~fl].view(np.uint64), sb[:, ~fl].view(np.uint64))
+        assert np.abs(fa - fb).max() <= 1e-6
+        d = u8a.astype(int) - u8b.astype(int)
+        assert np.abs(d).max() <= 1 and (d != 0).mean() < 1e-4
+
+
+def _stats_after_w(x, wavelet, levels):
+    """denoise_wavelet on device batch x; returns (u8, f32, per-image stats blocks)"""
+    import torch
+    from idn import _lib, ops
+    u8, f = ops.denoise_wavelet(x, wavelet, levels, out="both")
+    n, h, w, _ = x.shape
+    off = _lib.load().idn_wavelet_stats_offset(n, h, w, ops.WAVELETS[wavelet],
+                                               -1 if levels is None else levels)
+    ws = ops._WS_CACHE[(str(x.device), torch.cuda.current_stream(x.device).cuda_stream)]
+    st = ws[off:off + n * 256 * 8].view(torch.float64).view(n, 256).cpu().numpy().copy()
+    return u8.cpu().numpy(), f.cpu().numpy(), st
