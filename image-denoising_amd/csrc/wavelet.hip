@@ -3653,7 +3653,8 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
 #define IDN_WS(SRC, TL, TH, EMIT)                                                                  \
   do {                                                                                             \
     const int fmb = fm_an(l) & 0b1111;                                                             \
-    if (SRC == 0 && fmb == 0b1111 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b1111, 1, EMIT);           \
+    if ((SRC == 0 || SRC == 1) && fmb == 0b1111 && (EMIT) == 1)                                    \
+      IDN_WS_(SRC, TL, TH, 0b1111, 1, EMIT);                                                       \
     else if (SRC == 0 && fmb == 0b1110 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b1110, 1, EMIT);      \
     else if (SRC == 0 && fmb == 0b0111 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0111, 1, EMIT);      \
     else if (SRC == 0 && fmb == 0b0110 && (EMIT) == 1) IDN_WS_(SRC, TL, TH, 0b0110, 1, EMIT);      \
