@@ -51,8 +51,11 @@ def _flags() -> list[str]:
 
 # per-source flags: the two-column bilateral walk (bilateral_u8_pre2_kernel) is one fully unrolled
 # loop nest whose pre-unroll body exceeds LLVM's default pragma-unroll size limit; left rolled, its
-# shared-weight registers would go to scratch
-_EXTRA = {"bilateral_u8.hip": ["-mllvm", "-pragma-unroll-threshold=131072"]}
+# shared-weight registers would go to scratch.  The median networks (long runs of independent
+# packed min/max) schedule better under LLVM's max-ILP strategy: 5x5 median 0.490 -> 0.479 ms
+# (profiles/r04/sched_median_ab.txt; the same strategy made the bilateral and the wavelet slower)
+_EXTRA = {"bilateral_u8.hip": ["-mllvm", "-pragma-unroll-threshold=131072"],
+          "median_u8.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def _compile_one(src: Path, tuning: bool = False) -> Path:
