@@ -53,9 +53,12 @@ def _flags() -> list[str]:
 # loop nest whose pre-unroll body exceeds LLVM's default pragma-unroll size limit; left rolled, its
 # shared-weight registers would go to scratch.  The median networks (long runs of independent
 # packed min/max) schedule better under LLVM's max-ILP strategy: 5x5 median 0.490 -> 0.479 ms
-# (profiles/r04/sched_median_ab.txt; the same strategy made the bilateral and the wavelet slower)
+# (profiles/r04/sched_median_ab.txt; the same strategy made the bilateral and the wavelet slower),
+# and so does the k-means fit: quant k=7 2.91 -> 2.84 ms (profiles/r04/sched_ops_ab.txt; noise /
+# Poisson / JPEG / stencils: no gain or slower)
+_MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 _EXTRA = {"bilateral_u8.hip": ["-mllvm", "-pragma-unroll-threshold=131072"],
-          "median_u8.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+          "median_u8.hip": _MAX_ILP, "quant.hip": _MAX_ILP}
 
 
 def _compile_one(src: Path, tuning: bool = False) -> Path:
