@@ -140,3 +140,25 @@ def test_truncated_progressive_file_decodes_without_fault(dev):
     got = ops.jpeg_decode([trunc])[0].cpu().numpy()
     assert got.shape == good.shape
     assert np.abs(got.astype(int) - good.astype(int)).max() <= 255  # decoded, no fault
+
+
+def test_large_mixed_batch_bitexact_and_errors(dev):
+    """a 96-file batch of baseline and progressive files in mixed order (the gather runs in parts
+    of the batch, each copied as soon as it is complete): every image as its own decode, in
+    order, and an unsupported file late in the batch still fails the whole call"""
+    from idn import ops
+    from idn._lib import IdnError
+    names = ["s420_q90_600x1000.jpg", "prog_s420_q90_600x1000.jpg"]
+    datas = [(JPEG / n).read_bytes() for n in names]
+    order = [(i * 7 + i // 5) % 2 for i in range(96)]
+    got = ops.jpeg_decode([datas[k] for k in order]).cpu().numpy()
+    first = {k: got[order.index(k)] for k in (0, 1)}
+    for k in (0, 1):
+        check_libjpeg9(names[k], first[k])
+    for i, k in enumerate(order):
+        assert np.array_equal(got[i], first[k]), i
+    from test_jpeg import _arith
+    bad = [datas[0]] * 96
+    bad[90] = _arith(datas[0])
+    with pytest.raises(IdnError, match="unsupported|arithmetic"):
+        ops.jpeg_decode(bad)
