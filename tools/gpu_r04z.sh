@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 last check of HEAD: the whole GPU suite, smoke, the default bench line
 set -u
-OUT=gpurun_out/r04z
+OUT=gpurun_out/${1:-r04z}
 mkdir -p "$OUT"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
     -p no:cacheprovider > "$OUT/pytest.txt" 2>&1
