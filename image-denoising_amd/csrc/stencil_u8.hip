@@ -30,7 +30,9 @@
 
 namespace idn {
 
-enum StencilOp { OP_GAUSS3 = 0, OP_GAUSS5 = 1, OP_BOX3 = 2 };
+// OP_IDENT5: tuning-build probe -- the pitched tile's data movement with the taps reduced to a copy
+// of the centre byte
+enum StencilOp { OP_GAUSS3 = 0, OP_GAUSS5 = 1, OP_BOX3 = 2, OP_IDENT5 = 3 };
 
 template <int OP> struct Stencil;
 template <> struct Stencil<OP_GAUSS3> { static constexpr int K = 3; };
@@ -498,6 +500,303 @@ __global__ __launch_bounds__(TILE_WGT) void stencil_u8_lds(const uint8_t* __rest
 }
 
 
+// ---- pitched LDS tile (round 5) ----------------------------------------------------------------
+// The band's NB + 2R input rows are fetched by LDS-DMA into tile rows of PT_PITCH = 3072 bytes, one
+// fetch round (3 waves x 64 lanes x 16 B) per row: tile row j holds image row
+// reflect101(y0 - R + j) -- the reflected rows of the first / last band are fetched like any other,
+// so every band runs the same straight-line body -- and row byte x sits at tile byte 8 + x.  Lane
+// l's 16-byte chunk [seg_start - 8 + 16 l, +16) then starts at tile byte seg_start + 16 l: with
+// 1008-byte segments every chunk is one aligned, conflict-free ds_read_b128 at a compile-time
+// offset (the flat tile's 3000-byte rows put every other row at 8 mod 16: two 8-byte reads, half
+// of its LDS cycles bank conflicts).  The fetch lanes' global offsets are row * rb + 16 t - 8, so
+// it takes rows of 16 k + 8 bytes (the 600x1000x3 batch: 3000 B); others keep the flat tile.
+//
+// Per output row the arithmetic runs on u16 lanes holding ADJACENT bytes (b, b+1) (the flat tile's
+// (b, b+2) pairs need 8 DPP halo moves and 14 funnel shifts per row; adjacent pairs 6 and 11), and
+// the border reflections are rebuilt on the vertical sums of the row's first and last lane only
+// (wave-uniform branches): no per-input-row fix-up, no per-row address arithmetic.
+//
+// NTP: cache policy of the tile fetch -- 0 default, 1 nontemporal for the band's private rows
+// [2R, NB) (no other band's tile reads them) and default for the shared halo rows, 2 nontemporal
+// for every row, 3 nontemporal for rows [0, NB) (the leading halo: the band above read it
+// first), 4 for rows [2R, NB + 2R) (the trailing halo).  NTS: nontemporal stores.
+constexpr int PT_WGT = 192;
+constexpr int PT_PITCH = 16 * PT_WGT;  // 3072
+constexpr int PT_SEG = 1008;           // 63 output chunks per wave
+constexpr int PT_RBMAX = 3 * PT_SEG;   // 3024
+// The product's band height and cache policy (profiles/r05/stencil/): 9-row bands (13 tile rows,
+// 39 KB: four workgroups per CU), nontemporal loads for the band's private rows and nontemporal
+// stores -- 6.1-6.2 TB/s against 5.6 for 6-row bands at the default policy (which was the flat
+// tile's best); nontemporal stores alone, nontemporal halo rows, sc1 stores, 8 / 10 / 12 / 16-row
+// bands and two waves per segment all measured slower
+#ifndef IDN_STENCIL_PT_NB  // band height of the pitched tile (A/B builds set it)
+#define IDN_STENCIL_PT_NB 9
+#endif
+#ifndef IDN_STENCIL_PT_NTP  // the product's tile-fetch policy (see stencil_u8_pt)
+#define IDN_STENCIL_PT_NTP 1
+#endif
+#ifndef IDN_STENCIL_PT_NTS  // the product's store policy
+#define IDN_STENCIL_PT_NTS 1
+#endif
+
+
+// window of vertical sums as adjacent-byte u16 pairs: W[i] = window bytes (2i, 2i+1) (lo, hi lane);
+// window byte 0 = chunk byte -8
+struct PWin {
+  uint32_t W[16];
+  __device__ __forceinline__ uint32_t at(int b) const {  // window bytes (b, b+1) as a u16 pair
+    return (b & 1) ? __builtin_amdgcn_alignbyte(W[(b + 1) >> 1], W[b >> 1], 2) : W[b >> 1];
+  }
+};
+
+// byte s of the window's pair registers as (register, half)
+__device__ __forceinline__ uint32_t pw_pair(const PWin& V, int slo, int shi) {
+  if ((slo & 1) == 0 && shi == slo + 1) return V.W[slo >> 1];
+  return pick16(V.W[slo >> 1], slo & 1, V.W[shi >> 1], shi & 1);
+}
+
+// source window byte of window byte w for BORDER_REFLECT_101 at the row start (row byte 0 = window
+// byte 16, the row's first lane) or at the row end (row byte rb = window byte `base`)
+template <int C>
+__host__ __device__ constexpr int pw_lead_src(int w) {
+  const int rho = w - 16;  // < 0
+  const int pix = (rho - (C - 1)) / C;  // floor(rho / C)
+  const int ch = rho - pix * C;
+  return 16 + (-pix) * C + ch;
+}
+template <int C>
+__host__ __device__ constexpr int pw_tail_src(int base, int w) {
+  const int k = w - base;  // >= 0
+  return base - 2 * C - (k / C) * C + (k % C);
+}
+
+// rebuild the window bytes [16 - HB, 16) (lead) of `V` from row bytes 0.. (only lane 0 of the
+// row's first wave takes them)
+template <int C, int HB>
+__device__ __forceinline__ void pw_lead_fix(PWin& V, bool lane_is_lead) {
+  constexpr int I0 = (16 - HB) >> 1;
+  uint32_t nw[8 - I0];
+#pragma unroll
+  for (int i = I0; i < 8; ++i) {
+    const int lo = 2 * i < 16 - HB ? 2 * i : pw_lead_src<C>(2 * i);
+    nw[i - I0] = pw_pair(V, lo, pw_lead_src<C>(2 * i + 1));
+  }
+#pragma unroll
+  for (int i = I0; i < 8; ++i) V.W[i] = lane_is_lead ? nw[i - I0] : V.W[i];
+}
+// rebuild window bytes [base, base + HB) past the row end (base = 16 or 24) on the lanes `fix`
+template <int C, int HB>
+__device__ __forceinline__ void pw_tail_fix(PWin& V, int base, bool fix) {
+  const int i0 = base >> 1, i1 = (base + HB + 1) >> 1;  // registers [i0, i1)
+  uint32_t nw[(HB + 1) / 2 + 1];
+#pragma unroll
+  for (int i = i0; i < i1; ++i) {
+    const int hi = 2 * i + 1 < base + HB ? pw_tail_src<C>(base, 2 * i + 1) : 2 * i + 1;
+    nw[i - i0] = pw_pair(V, pw_tail_src<C>(base, 2 * i), hi);
+  }
+#pragma unroll
+  for (int i = i0; i < i1; ++i) V.W[i] = fix ? nw[i - i0] : V.W[i];
+}
+
+// horizontal taps of the output pair at window bytes (P, P+1); GAUSS / IDENT: the result in the
+// high byte of each u16 lane (the +128 rounding bias rides in the vertical sums); BOX: the sum
+template <int C, int OP>
+__device__ __forceinline__ uint32_t ptap(const PWin& V, int P) {
+  if constexpr (OP == OP_GAUSS5) {
+    const uint32_t t = (V.at(P - C) + V.at(P + C)) << 2;
+    return V.at(P - 2 * C) + V.at(P + 2 * C) + pk_mad16(V.at(P), 0x00060006u, t);
+  } else if constexpr (OP == OP_GAUSS3) {
+    const uint32_t x = V.at(P - C) + V.at(P + C) + (V.at(P) << 1);
+    return (x << 4) + 0x00800080u;
+  } else if constexpr (OP == OP_BOX3) {
+    return V.at(P - C) + V.at(P) + V.at(P + C);  // <= 2295
+  } else {
+    return V.at(P);  // identity probe (tuning build): centre byte
+  }
+}
+
+// 8 horizontal results (output pairs (2j, 2j+1) of the chunk) -> the 16 output bytes
+template <int OP>
+__device__ __forceinline__ v4u pfinish(const uint32_t (&A)[8]) {
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if constexpr (OP == OP_BOX3) {
+      // round(S/9) == (S*7280 + 33200) >> 16 (byte 2), S <= 2295; bytes 4k..4k+3 from the lanes
+      // (A[2k].lo, A[2k].hi, A[2k+1].lo, A[2k+1].hi)
+      const uint32_t a = A[2 * k], b = A[2 * k + 1];
+      const uint32_t r0 = mad24(a & 0xFFFFu, 7280u, 33200u), r1 = mad24(a >> 16, 7280u, 33200u);
+      const uint32_t r2 = mad24(b & 0xFFFFu, 7280u, 33200u), r3 = mad24(b >> 16, 7280u, 33200u);
+      const uint32_t lo = __builtin_amdgcn_perm(r1, r0, 0x0C0C0602u);  // r0.b2 | r1.b2 << 8
+      const uint32_t hi = __builtin_amdgcn_perm(r3, r2, 0x06020C0Cu);  // r2.b2 << 16 | r3.b2 << 24
+      o[k] = lo | hi;
+    } else {
+      o[k] = __builtin_amdgcn_perm(A[2 * k + 1], A[2 * k], 0x07050301u);
+    }
+  }
+  return v4u{o[0], o[1], o[2], o[3]};
+}
+
+// one input row chunk -> 8 adjacent-byte u16 pairs (chunk bytes 2j, 2j+1)
+__device__ __forceinline__ void unpack_pairs(const v4u& x, uint32_t (&U)[8]) {
+  const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    U[2 * j] = __builtin_amdgcn_perm(0u, d[j], 0x0C010C00u);
+    U[2 * j + 1] = __builtin_amdgcn_perm(0u, d[j], 0x0C030C02u);
+  }
+}
+
+template <int OP> struct PStencil { static constexpr int K = Stencil<OP>::K; };
+template <> struct PStencil<OP_IDENT5> { static constexpr int K = 5; };
+
+// LEAD: the wave owns the row's first segment (lane 0 rebuilds the left reflection); TAIL: the
+// row's last (lane `fix` rebuilds the right one: rows of 16 k + 8 bytes end at a chunk end)
+template <int C, int OP, bool LEAD, bool TAIL>
+__device__ __forceinline__ v4u pring_row(const uint32_t (&Rg)[PStencil<OP>::K][8], int nw,
+                                         bool lane0, bool fix) {
+  constexpr int K = PStencil<OP>::K;
+  constexpr int R = K / 2;
+  constexpr int HB = R * C;  // halo bytes per side
+  uint32_t Vs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t r0 = Rg[(nw + 1) % K][j], r1 = Rg[(nw + 2) % K][j];
+    if constexpr (OP == OP_GAUSS5) {
+      Vs[j] = vtap<OP>(r0, r1, Rg[(nw + 3) % K][j], Rg[(nw + 4) % K][j], Rg[nw][j]);
+    } else if constexpr (OP == OP_IDENT5) {
+      Vs[j] = Rg[(nw + 3) % K][j] << 8;  // identity: the centre row
+    } else {
+      Vs[j] = vtap<OP>(r0, r1, Rg[nw][j], 0u, 0u);
+    }
+  }
+  PWin V;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) V.W[4 + j] = Vs[j];
+  // halos: window bytes [8 - HB, 8) from the previous lane's chunk, [24, 24 + HB) from the next's
+#pragma unroll
+  for (int i = (8 - HB) >> 1; i < 4; ++i) V.W[i] = from_prev_lane(Vs[i + 4]);
+#pragma unroll
+  for (int i = 0; 2 * i < HB; ++i) V.W[12 + i] = from_next_lane(Vs[i]);
+  if constexpr (LEAD) pw_lead_fix<C, HB>(V, lane0);
+  if constexpr (TAIL) pw_tail_fix<C, HB>(V, 24, fix);
+  uint32_t A[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) A[j] = ptap<C, OP>(V, 8 + 2 * j);
+  return pfinish<OP>(A);
+}
+
+// the compute phase of one wave: the segment's chunk of each tile row, NB output rows
+template <int C, int OP, int NB, int SAUX, bool LEAD, bool TAIL>
+__device__ __forceinline__ void pt_body(const uint8_t* tile, rsrc_t rs, rsrc_t rd, int h, int rb,
+                                        int seg_start, int y0, int lane) {
+  constexpr int K = PStencil<OP>::K;
+  constexpr int R = K / 2;
+  const int seg_end = min(seg_start + PT_SEG, rb);
+  const int q = seg_start - 8 + 16 * lane;  // the lane's chunk: row bytes [q, q + 16)
+  const bool lane0 = lane == 0;
+  const bool fix = q + 16 == rb;  // (TAIL) the row ends at this lane's chunk end
+  // stores: lanes 1..62 16 B, lane 0 its chunk's high 8 B, lane 63 its low 8 B (nothing at or
+  // past the row end); the row offset rides in the scalar offset
+  const int o_lo = max(q, seg_start), o_hi = min(q + 16, seg_end);
+  const int kind = (o_hi <= o_lo) ? 0 : (o_lo == q && o_hi == q + 16) ? 1 : (o_lo == q) ? 2 : 3;
+  const uint32_t full = kind == 1 ? (uint32_t)q : OOB_OFF;
+  const bool hi = kind == 3;
+  const uint32_t half = kind == 2 ? (uint32_t)q : (kind == 3 ? (uint32_t)q + 8u : OOB_OFF);
+  constexpr int aux = SAUX;
+
+  // image row 0 (tile row R of the first band): the fetch slot of row bytes [-8, 8) lies partly
+  // before the image and reads as zeros, so lane 0 takes row bytes 0..7 from a load of its own
+  const bool first_band = LEAD && y0 == 0;  // wave-uniform
+  v2u row0 = {0u, 0u};
+  if (first_band) row0 = __builtin_amdgcn_raw_buffer_load_b64(rs, lane == 0 ? 0u : OOB_OFF, 0, 0);
+  const uint8_t* rd_base = tile + seg_start + 16 * lane;
+  uint32_t Rg[K][8];
+  auto take = [&](int j) {
+    v4u Lv = *reinterpret_cast<const v4u*>(rd_base + j * PT_PITCH);
+    if (j == R && first_band) {
+      Lv.z = lane == 0 ? row0.x : Lv.z;
+      Lv.w = lane == 0 ? row0.y : Lv.w;
+    }
+    unpack_pairs(Lv, Rg[j % K]);
+  };
+#pragma unroll
+  for (int j = 0; j < 2 * R; ++j) take(j);
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int j = 2 * R + u;
+    take(j);
+    const v4u o = pring_row<C, OP, LEAD, TAIL>(Rg, j % K, lane0, fix);
+    const int y = y0 + u;
+    if (y < h) {  // wave-uniform
+      const uint32_t row_off = (uint32_t)y * (uint32_t)rb;
+      __builtin_amdgcn_raw_buffer_store_b128(o, rd, full, row_off, aux);
+      __builtin_amdgcn_raw_buffer_store_b64(hi ? v2u{o.z, o.w} : v2u{o.x, o.y}, rd, half, row_off,
+                                            aux);
+    }
+  }
+}
+
+// LAUX / SAUX: the cache-policy bits of the selected tile rows' loads / of the stores (2 = nt;
+// tuning builds try the sc bits too)
+template <int C, int OP, int NB, int NTP, int SAUX, int LAUX = 2>
+__global__ __launch_bounds__(PT_WGT) void stencil_u8_pt(const uint8_t* __restrict__ src,
+                                                        uint8_t* __restrict__ dst, int h, int rb,
+                                                        int nseg, int bands) {
+  constexpr int K = PStencil<OP>::K;
+  constexpr int R = K / 2;
+  constexpr int ROWS = NB + 2 * R;
+  __shared__ __attribute__((aligned(16))) uint8_t tile[ROWS * PT_PITCH];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // XCD-contiguous block order: a band's neighbours (which fetch its halo rows) run on the same
+  // XCD, so the halo re-reads hit that XCD's L2
+  const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+  const int img = blk / bands, band = blk - img * bands;
+  const uint32_t img_bytes = (uint32_t)h * (uint32_t)rb;
+  const rsrc_t rs = make_rsrc(src + (size_t)img * img_bytes, img_bytes);
+  const int y0 = band * NB;
+
+  // fetch: round j -> tile row j = image row reflect101(y0 - R + j) (rows past the band's last
+  // needed row clamp to a valid row); lane slot t holds row bytes [16 t - 8, 16 t + 8): the
+  // row's first slot reads the previous row's last 8 bytes with the row's first 8 (image row 0:
+  // offset -8 wraps, the whole slot is out of range and reads zeros -- pt_body reloads its row
+  // bytes 0..7), slots starting at or past the row end are not fetched
+  {
+    const int x = 16 * (int)threadIdx.x - 8;
+    const uint32_t vx = x < rb ? (uint32_t)x : OOB_OFF;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int yy = reflect101_1(min(y0 - R + j, h - 1 + R), h);
+      auto* lds = (__attribute__((address_space(3))) void*)(tile + j * PT_PITCH + 1024 * wave);
+      const uint32_t vo = vx + (uint32_t)yy * (uint32_t)rb;
+      if (NTP == 2 || (NTP == 1 && j >= 2 * R && j < NB) || (NTP == 3 && j < NB) ||
+          (NTP == 4 && j >= 2 * R))  // folded after unrolling
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds, 16, vo, 0, 0, LAUX);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds, 16, vo, 0, 0, 0);
+    }
+    // every wave waits for its own DMA before the barrier (the workgroup fence does not promise
+    // that wait for LDS-DMA on gfx9)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (wave >= nseg) return;  // rows narrower than 3 segments: the extra waves only fetched
+
+  const int seg_start = wave * PT_SEG;
+  const bool lead = wave == 0, tail = min(seg_start + PT_SEG, rb) == rb;
+  const rsrc_t rd = make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
+  if (lead && tail)
+    pt_body<C, OP, NB, SAUX, true, true>(tile, rs, rd, h, rb, seg_start, y0, lane);
+  else if (lead)
+    pt_body<C, OP, NB, SAUX, true, false>(tile, rs, rd, h, rb, seg_start, y0, lane);
+  else if (tail)
+    pt_body<C, OP, NB, SAUX, false, true>(tile, rs, rd, h, rb, seg_start, y0, lane);
+  else
+    pt_body<C, OP, NB, SAUX, false, false>(tile, rs, rd, h, rb, seg_start, y0, lane);
+}
+
 // ---- generic path ------------------------------------------------------------------------
 template <int OP>
 __global__ __launch_bounds__(256) void stencil_u8_generic(const uint8_t* __restrict__ src,
@@ -613,6 +912,40 @@ static int launch_f64(const double* src, double* dst, int n, int h, int w, int c
   return IDN_OK;
 }
 
+// pitched-tile launch for the cache policy: ntp (which tile rows take the LAUX bits), the store
+// bits (nts: 1 = nt) -- the product library's are compile-time; the tuning build also takes raw
+// bit values IDN_STENCIL_SAUX / IDN_STENCIL_LAUX for a few combinations
+template <int OP, int NB>
+static int launch_pt(dim3 grid, hipStream_t st, const uint8_t* src, uint8_t* dst, int h, int rb,
+                     int nseg, int bands, int ntp, int nts) {
+  const dim3 block(PT_WGT);
+#define IDN_PT(P, S, L) \
+  hipLaunchKernelGGL((stencil_u8_pt<3, OP, NB, P, S, L>), grid, block, 0, st, src, dst, h, rb, \
+                     nseg, bands)
+#ifdef IDN_TUNING_BUILD
+  const int saux = knob("IDN_STENCIL_SAUX", nts ? 2 : 0), laux = knob("IDN_STENCIL_LAUX", 2);
+  if (ntp == 1 && saux == 2 && laux == 2) { IDN_PT(1, 2, 2); return IDN_OK; }
+  if (ntp == 1 && saux == 16 && laux == 2) { IDN_PT(1, 16, 2); return IDN_OK; }
+  if (ntp == 1 && saux == 18 && laux == 2) { IDN_PT(1, 18, 2); return IDN_OK; }
+  if (ntp == 1 && saux == 17 && laux == 2) { IDN_PT(1, 17, 2); return IDN_OK; }
+  if (ntp == 1 && saux == 2 && laux == 16) { IDN_PT(1, 2, 16); return IDN_OK; }
+  if (ntp == 1 && saux == 2 && laux == 18) { IDN_PT(1, 2, 18); return IDN_OK; }
+  if (ntp == 1 && saux == 0) { IDN_PT(1, 0, 2); return IDN_OK; }
+  if (ntp == 4 && saux == 2) { IDN_PT(4, 2, 2); return IDN_OK; }
+  if (ntp == 2 && saux == 2) { IDN_PT(2, 2, 2); return IDN_OK; }
+  if (ntp == 0 && saux == 2) { IDN_PT(0, 2, 2); return IDN_OK; }
+  if (ntp == 0 && saux == 0) { IDN_PT(0, 0, 2); return IDN_OK; }
+  return set_error(IDN_EUNSUPPORTED, "tuning: no pitched-tile instance for NTP %d SAUX %d LAUX %d",
+                   ntp, saux, laux);
+#else
+  (void)ntp;
+  (void)nts;
+  IDN_PT(IDN_STENCIL_PT_NTP, IDN_STENCIL_PT_NTS ? 2 : 0, 2);
+  return IDN_OK;
+#endif
+#undef IDN_PT
+}
+
 // ---- host launchers --------------------------------------------------------------------------
 // compact rows <= 3024 B: the LDS tile with 6-row bands (10 / 8 input rows in LDS, 30 / 24 KB per
 // workgroup, up to 5-6 workgroups per CU; band heights 4-11 measured, tools/sweep_stencil.py);
@@ -623,7 +956,25 @@ static int launch_stencil(const uint8_t* src, uint8_t* dst, int n, int h, int w,
   constexpr int K = Stencil<OP>::K;
   constexpr int R = K / 2;
   const int64_t rb = (int64_t)w * c;
-  if (stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb && rb <= TILE_RBMAX &&
+  const int form = knob("IDN_STENCIL_FORM", 1);
+  if (form == 1 && stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb &&
+      rb <= PT_RBMAX && rb % 16 == 8 && h > 2 * R) {
+    // pitched tile (rows of 16 k + 8 bytes, the 600x1000x3 batch)
+    constexpr int NB = IDN_STENCIL_PT_NB;
+    const int nseg = (int)((rb + PT_SEG - 1) / PT_SEG);
+    const int bands = (h + NB - 1) / NB;
+    const int64_t blocks = (int64_t)n * bands;
+    IDN_CHECK_ARG(blocks < (int64_t)0x7FFFFFFF, "%s: batch too large", name);
+    const dim3 grid((unsigned)blocks);
+    const int ntp = knob("IDN_STENCIL_NTP", IDN_STENCIL_PT_NTP),
+              nts = knob("IDN_STENCIL_NTS", IDN_STENCIL_PT_NTS);
+    int rc;
+    if (OP == OP_GAUSS5 && knob("IDN_STENCIL_IDENT", 0))  // tuning probe: data movement only
+      rc = launch_pt<OP_IDENT5, NB>(grid, st, src, dst, h, (int)rb, nseg, bands, ntp, nts);
+    else
+      rc = launch_pt<OP, NB>(grid, st, src, dst, h, (int)rb, nseg, bands, ntp, nts);
+    if (rc) return rc;
+  } else if (stripe_ok(c, rb, row_stride, h, src, dst) && row_stride == rb && rb <= TILE_RBMAX &&
       h > 2 * R) {
     const int nseg = (int)((rb + 1007) / 1008);
     const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);

@@ -88,6 +88,78 @@ def test_stencil_tile_fetch_forms(dev, monkeypatch, shape, form):
         assert np.array_equal(_run(idn.blur, img, 3), oracle.cv.blur(img, 3))
 
 
+# rows of 16 k + 8 bytes take the pitched tile (round 5): one, two and three segments (a 24-byte
+# last segment at rb 2040), band tails (h % 6), the first / last band's reflected rows
+PITCHED = [(1, 5, 24), (2, 6, 104), (1, 7, 344), (2, 13, 664), (1, 29, 680), (2, 600, 1000),
+           (1, 601, 1000), (1, 3, 1000), (3, 64, 40)]
+
+
+@pytest.mark.parametrize("shape", PITCHED)
+def test_stencil_pitched_tile(dev, shape):
+    """the pitched LDS tile (rows of 16 k + 8 bytes) against the oracle for all three filters"""
+    import idn
+    import oracle
+    img = textured(*shape, seed=sum(shape) + 11)
+    for k in (3, 5):
+        got = _run(idn.gaussian_blur, img, k)
+        ref = oracle.cv.gaussian_blur(img, k)
+        assert np.array_equal(got, ref), (k, np.argwhere(got != ref)[:8])
+    got = _run(idn.blur, img, 3)
+    ref = oracle.cv.blur(img, 3)
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:8]
+
+
+@pytest.mark.parametrize("knobs", [{"IDN_STENCIL_FORM": "0"}, {"IDN_STENCIL_NTP": "1"},
+                                   {"IDN_STENCIL_NTP": "2", "IDN_STENCIL_NTS": "1"},
+                                   {"IDN_STENCIL_NTS": "1"}, {"IDN_STENCIL_NTP": "1", "IDN_STENCIL_SAUX": "16"},
+                                   {"IDN_STENCIL_NTP": "0", "IDN_STENCIL_NTS": "0"}])
+@pytest.mark.parametrize("shape", [(2, 600, 1000), (1, 13, 664), (2, 7, 104)])
+def test_stencil_forms_and_policies_agree(dev, monkeypatch, knobs, shape):
+    """tuning build: the flat tile (IDN_STENCIL_FORM=0) and the pitched tile's cache policies
+    (nontemporal private rows / every row, nontemporal stores) give the product's bytes"""
+    import idn
+    from idn import _lib
+    img = textured(*shape, seed=sum(shape) + 5)
+    want = {k: _run(idn.gaussian_blur, img, k) for k in (3, 5)}
+    want_box = _run(idn.blur, img, 3)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    with _lib.variant("tuning"):
+        for k in (3, 5):
+            assert np.array_equal(_run(idn.gaussian_blur, img, k), want[k]), k
+        assert np.array_equal(_run(idn.blur, img, 3), want_box)
+
+
+def test_gaussian_headline_batch(dev):
+    """the bench's own launch: 256 x 600 x 1000 x 3 in one call (76,800 workgroup items).  Three
+    images (first, middle, last) bit-exact against the oracle, and the whole batch equal to 256
+    one-image launches of the same images"""
+    import torch
+    import idn
+    import oracle
+    n = 256
+    base = torch.from_numpy(textured(1, 600, 1000, seed=21)).cuda()
+    # distinct images: the textured base shifted and noised per image on the device
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    x = torch.empty((n, 600, 1000, 3), dtype=torch.uint8, device="cuda")
+    for i in range(0, n, 32):
+        m = min(32, n - i)
+        noise = torch.randint(0, 256, (m, 600, 1000, 3), generator=g, device="cuda",
+                              dtype=torch.uint8)
+        x[i:i + m] = torch.where(noise < 16, noise, base.expand(m, -1, -1, -1).roll(i, 2))
+    y = idn.gaussian_blur(x, 5)
+    torch.cuda.synchronize()
+    for i in (0, n // 2, n - 1):
+        img = x[i:i + 1].cpu().numpy()
+        assert np.array_equal(y[i:i + 1].cpu().numpy(), oracle.cv.gaussian_blur(img, 5)), i
+    per = torch.empty_like(y)
+    for i in range(n):
+        idn.gaussian_blur(x[i:i + 1], 5, out=per[i:i + 1])
+    torch.cuda.synchronize()
+    assert torch.equal(per, y)
+
+
 def test_generic_path_forced(dev, monkeypatch):
     """the per-pixel kernel (shapes the lane layout does not take), forced on a shape it would
     not get by itself through the tools-only tuning build"""
