@@ -110,9 +110,10 @@ def main():
                 "traffic_over_algorithmic": rec["traffic_over_algorithmic"],
                 "correction": "FETCH_SIZE x2 (gfx950 16B/lane streaming reads; other widths "
                               "uncalibrated), WRITE_SIZE as-is",
-                "source": f"profiles/r04/pmc/{op}.json (rocprofv3 --pmc, separate FETCH / WRITE passes)",
+                "source": f"{dest.resolve().relative_to(ROOT)}/{op}.json (rocprofv3 --pmc, separate "
+                          f"FETCH / WRITE passes)",
             }
-            if "kernel_form" in old:
+            if "kernel_form" in old and old.get("kernel") == traffic[op]["kernel"]:
                 traffic[op]["kernel_form"] = old["kernel_form"]
         print(op, json.dumps({k: {x: v[x] for x in v if x != "counters"} for k, v in rec["kernels"].items()}))
     traffic_path.write_text(json.dumps(traffic, indent=1) + "\n")
