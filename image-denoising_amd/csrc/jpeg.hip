@@ -145,9 +145,11 @@ static int jpg_fail(std::string* err, const char* msg) {
   return IDN_EUNSUPPORTED;
 }
 
-// the end of a scan-path file (EOI or end of data): at least one scan; a progressive file whose
-// last scans leave AC coefficients 1..5 of a component imprecise would be block-smoothed by
-// libjpeg (jdcoefct.c smoothing_ok): not restated, rejected
+// the end of a scan-path file (EOI or end of data): at least one scan.  libjpeg block-smooths a
+// progressive file (jdcoefct.c smoothing_ok, libjpeg 9d) only when EVERY component has DC data
+// (coef_bits[0] >= 0) and nonzero quantisers Q00 Q01 Q10 Q20 Q11 Q02, and some component's AC
+// coefficients 1..5 stay imprecise after the last scan; that smoothing is not restated, so such a
+// file is rejected -- any other progressive file decodes without it, as libjpeg does
 static int jpg_scans_done(const JpegHost& J, std::string* err) {
   if (J.scans.empty()) return jpg_fail(err, "no SOS");
   if (J.progressive) {
@@ -157,12 +159,16 @@ static int jpg_scans_done(const JpegHost& J, std::string* err) {
     for (const ScanHost& S : J.scans)
       for (int k = 0; k < S.ns; ++k)
         for (int z = S.Ss; z <= std::min(S.Se, 5); ++z) bits[S.comp[k]][z] = S.Al;
+    bool useful = false;
     for (int c = 0; c < J.ncomp; ++c) {
-      if (bits[c][0] < 0) continue;
-      for (int z = 1; z <= 5; ++z)
-        if (bits[c][z] != 0)
-          return jpg_fail(err, "progressive file leaves AC 1..5 imprecise (libjpeg block smoothing)");
+      const uint16_t* q = J.q[J.tq[c]];
+      if (bits[c][0] < 0 || q[0] == 0 || q[1] == 0 || q[8] == 0 || q[16] == 0 || q[9] == 0 ||
+          q[2] == 0)
+        return IDN_OK;  // smoothing_ok() is FALSE for the whole image
+      for (int z = 1; z <= 5; ++z) useful |= bits[c][z] != 0;
     }
+    if (useful)
+      return jpg_fail(err, "progressive file leaves AC 1..5 imprecise (libjpeg block smoothing)");
   }
   return IDN_OK;
 }

@@ -311,6 +311,7 @@ enum TileEpi { EPI_U8 = 0, EPI_BLOB = 1 };
 // partial-chunk stores.
 constexpr int BLOB_LUT = 768;          // floats
 constexpr int BLOB_STAGE = 3 * 1024;   // bytes: one 1 KiB row-segment stage per wave
+template <int AUX = 0>
 __device__ __forceinline__ void blob_row_store(const v4u& o, uint32_t* __restrict__ stage,
                                                const float* __restrict__ lut, int lane,
                                                const StripeGeom& g, const uint32_t (&c4)[3],
@@ -337,7 +338,7 @@ __device__ __forceinline__ void blob_row_store(const v4u& o, uint32_t* __restric
     __builtin_amdgcn_raw_buffer_store_b128(
         v4u{__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]),
             __float_as_uint(f[3])},
-        rd, ok ? 4u * (row_byte + (uint32_t)e) : OOB_OFF, 0, 0);
+        rd, ok ? 4u * (row_byte + (uint32_t)e) : OOB_OFF, 0, AUX);
   }
 }
 
@@ -538,6 +539,18 @@ constexpr int PT_RBMAX = 3 * PT_SEG;   // 3024
 #ifndef IDN_STENCIL_PT_NTS  // the product's store policy
 #define IDN_STENCIL_PT_NTS 1
 #endif
+// the fused blob epilogue's (12 B written per 3 B read): 6-row bands at the default policy,
+// 5.61 TB/s against 5.56-5.57 for the flat tile; the nontemporal policies cost 3-8 % here
+// (profiles/r05/stencil/r05g)
+#ifndef IDN_STENCIL_PT_NB_BLOB
+#define IDN_STENCIL_PT_NB_BLOB 6
+#endif
+#ifndef IDN_STENCIL_PT_NTP_BLOB
+#define IDN_STENCIL_PT_NTP_BLOB 0
+#endif
+#ifndef IDN_STENCIL_PT_NTS_BLOB
+#define IDN_STENCIL_PT_NTS_BLOB 0
+#endif
 
 
 // window of vertical sums as adjacent-byte u16 pairs: W[i] = window bytes (2i, 2i+1) (lo, hi lane);
@@ -687,9 +700,9 @@ __device__ __forceinline__ v4u pring_row(const uint32_t (&Rg)[PStencil<OP>::K][8
 }
 
 // the compute phase of one wave: the segment's chunk of each tile row, NB output rows
-template <int C, int OP, int NB, int SAUX, bool LEAD, bool TAIL>
+template <int C, int OP, int NB, int SAUX, bool LEAD, bool TAIL, int EPI = EPI_U8>
 __device__ __forceinline__ void pt_body(const uint8_t* tile, rsrc_t rs, rsrc_t rd, int h, int rb,
-                                        int seg_start, int y0, int lane) {
+                                        int seg_start, int y0, int lane, uint8_t* extra = nullptr) {
   constexpr int K = PStencil<OP>::K;
   constexpr int R = K / 2;
   const int seg_end = min(seg_start + PT_SEG, rb);
@@ -728,7 +741,20 @@ __device__ __forceinline__ void pt_body(const uint8_t* tile, rsrc_t rs, rsrc_t r
     take(j);
     const v4u o = pring_row<C, OP, LEAD, TAIL>(Rg, j % K, lane0, fix);
     const int y = y0 + u;
-    if (y < h) {  // wave-uniform
+    if constexpr (EPI == EPI_BLOB) {
+      // the blob row through the wave's LDS stage (float stores of 1 KiB per wave-instruction)
+      StripeGeom g;
+      g.seg_start = seg_start;
+      g.seg_end = seg_end;
+      const int c0 = (seg_start + 4 * lane) % 3;
+      uint32_t c4[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) c4[t] = 4u * (uint32_t)((c0 + t) % 3);
+      const int wave = seg_start / PT_SEG;
+      blob_row_store<aux>(o, reinterpret_cast<uint32_t*>(extra + BLOB_LUT * 4 + 1024 * wave),
+                          reinterpret_cast<const float*>(extra), lane, g, c4, rd, y < h,
+                          (uint32_t)y * (uint32_t)rb);
+    } else if (y < h) {  // wave-uniform
       const uint32_t row_off = (uint32_t)y * (uint32_t)rb;
       __builtin_amdgcn_raw_buffer_store_b128(o, rd, full, row_off, aux);
       __builtin_amdgcn_raw_buffer_store_b64(hi ? v2u{o.z, o.w} : v2u{o.x, o.y}, rd, half, row_off,
@@ -739,14 +765,19 @@ __device__ __forceinline__ void pt_body(const uint8_t* tile, rsrc_t rs, rsrc_t r
 
 // LAUX / SAUX: the cache-policy bits of the selected tile rows' loads / of the stores (2 = nt;
 // tuning builds try the sc bits too)
-template <int C, int OP, int NB, int NTP, int SAUX, int LAUX = 2>
+// EPI_BLOB: the fused blob epilogue (idn_gaussian_blob_f32): dst is the float32 blob, the
+// 3 x 256 table of blob values is built from (mb, mg, mr) before the tile barrier
+template <int C, int OP, int NB, int NTP, int SAUX, int LAUX = 2, int EPI = EPI_U8>
 __global__ __launch_bounds__(PT_WGT) void stencil_u8_pt(const uint8_t* __restrict__ src,
                                                         uint8_t* __restrict__ dst, int h, int rb,
-                                                        int nseg, int bands) {
+                                                        int nseg, int bands, double mb = 0.0,
+                                                        double mg = 0.0, double mr = 0.0) {
   constexpr int K = PStencil<OP>::K;
   constexpr int R = K / 2;
   constexpr int ROWS = NB + 2 * R;
-  __shared__ __attribute__((aligned(16))) uint8_t tile[ROWS * PT_PITCH];
+  constexpr int EXTRA = EPI == EPI_BLOB ? BLOB_LUT * 4 + BLOB_STAGE : 0;
+  __shared__ __attribute__((aligned(16))) uint8_t tile[ROWS * PT_PITCH + EXTRA];
+  uint8_t* const extra = tile + ROWS * PT_PITCH;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -777,6 +808,13 @@ __global__ __launch_bounds__(PT_WGT) void stencil_u8_pt(const uint8_t* __restric
       else
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds, 16, vo, 0, 0, 0);
     }
+    if constexpr (EPI == EPI_BLOB) {  // the blob table (published by the tile's barrier)
+      float* lut = reinterpret_cast<float*>(extra);
+      for (int i = threadIdx.x; i < BLOB_LUT; i += PT_WGT) {
+        const int v = i / 3, ch = i - 3 * v;
+        lut[i] = (float)__dsub_rn((double)v, ch == 0 ? mb : ch == 1 ? mg : mr);
+      }
+    }
     // every wave waits for its own DMA before the barrier (the workgroup fence does not promise
     // that wait for LDS-DMA on gfx9)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -786,15 +824,18 @@ __global__ __launch_bounds__(PT_WGT) void stencil_u8_pt(const uint8_t* __restric
 
   const int seg_start = wave * PT_SEG;
   const bool lead = wave == 0, tail = min(seg_start + PT_SEG, rb) == rb;
-  const rsrc_t rd = make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
+  const rsrc_t rd = EPI == EPI_BLOB
+                        ? make_rsrc(reinterpret_cast<float*>(dst) + (size_t)img * img_bytes,
+                                    4u * img_bytes)
+                        : make_rsrc(dst + (size_t)img * img_bytes, img_bytes);
   if (lead && tail)
-    pt_body<C, OP, NB, SAUX, true, true>(tile, rs, rd, h, rb, seg_start, y0, lane);
+    pt_body<C, OP, NB, SAUX, true, true, EPI>(tile, rs, rd, h, rb, seg_start, y0, lane, extra);
   else if (lead)
-    pt_body<C, OP, NB, SAUX, true, false>(tile, rs, rd, h, rb, seg_start, y0, lane);
+    pt_body<C, OP, NB, SAUX, true, false, EPI>(tile, rs, rd, h, rb, seg_start, y0, lane, extra);
   else if (tail)
-    pt_body<C, OP, NB, SAUX, false, true>(tile, rs, rd, h, rb, seg_start, y0, lane);
+    pt_body<C, OP, NB, SAUX, false, true, EPI>(tile, rs, rd, h, rb, seg_start, y0, lane, extra);
   else
-    pt_body<C, OP, NB, SAUX, false, false>(tile, rs, rd, h, rb, seg_start, y0, lane);
+    pt_body<C, OP, NB, SAUX, false, false, EPI>(tile, rs, rd, h, rb, seg_start, y0, lane, extra);
 }
 
 // ---- generic path ------------------------------------------------------------------------
@@ -944,6 +985,30 @@ static int launch_pt(dim3 grid, hipStream_t st, const uint8_t* src, uint8_t* dst
   return IDN_OK;
 #endif
 #undef IDN_PT
+}
+
+// the fused blob form of the pitched tile (ntp / nts as launch_pt; the product's are compile-time)
+template <int OP, int NB>
+static int launch_pt_blob(dim3 grid, hipStream_t st, const uint8_t* src, float* blob, int h, int rb,
+                          int nseg, int bands, int ntp, int nts, const double* mean) {
+  const dim3 block(PT_WGT);
+#define IDN_PTB(P, S) \
+  hipLaunchKernelGGL((stencil_u8_pt<3, OP, NB, P, S, 2, EPI_BLOB>), grid, block, 0, st, src, \
+                     reinterpret_cast<uint8_t*>(blob), h, rb, nseg, bands, mean[0], mean[1], mean[2])
+#ifdef IDN_TUNING_BUILD
+  if (ntp == 1 && nts) { IDN_PTB(1, 2); return IDN_OK; }
+  if (ntp == 1) { IDN_PTB(1, 0); return IDN_OK; }
+  if (ntp == 0 && nts) { IDN_PTB(0, 2); return IDN_OK; }
+  if (ntp == 0) { IDN_PTB(0, 0); return IDN_OK; }
+  return set_error(IDN_EUNSUPPORTED, "tuning: no blob pitched-tile instance for NTP %d NTS %d", ntp,
+                   nts);
+#else
+  (void)ntp;
+  (void)nts;
+  IDN_PTB(IDN_STENCIL_PT_NTP_BLOB, IDN_STENCIL_PT_NTS_BLOB ? 2 : 0);
+  return IDN_OK;
+#endif
+#undef IDN_PTB
 }
 
 // ---- host launchers --------------------------------------------------------------------------
@@ -1103,6 +1168,24 @@ extern "C" int idn_gaussian_blob_f32(const uint8_t* src, float* blob, int n, int
   if (!(stripe_ok(c, rb, row_stride, h, src, blob) && row_stride == rb && rb <= TILE_RBMAX &&
         h > ksize && ((uintptr_t)blob & 15) == 0))
     return set_error(IDN_EUNSUPPORTED, "idn_gaussian_blob_f32: layout not fused");
+  hipStream_t st = as_stream(stream);
+  if (knob("IDN_STENCIL_FORM", 1) == 1 && rb <= PT_RBMAX && rb % 16 == 8) {
+    // the pitched tile (rows of 16 k + 8 bytes, the 600x1000x3 batch)
+    constexpr int NB = IDN_STENCIL_PT_NB_BLOB;
+    const int nsegp = (int)((rb + PT_SEG - 1) / PT_SEG);
+    const int bands = (h + NB - 1) / NB;
+    const int64_t blocks = (int64_t)n * bands;
+    IDN_CHECK_ARG(blocks < (int64_t)0x7FFFFFFF, "idn_gaussian_blob_f32: batch too large");
+    const int ntp = knob("IDN_STENCIL_NTP", IDN_STENCIL_PT_NTP_BLOB),
+              nts = knob("IDN_STENCIL_NTS", IDN_STENCIL_PT_NTS_BLOB);
+    const int rc = ksize == 5 ? launch_pt_blob<OP_GAUSS5, NB>(dim3((unsigned)blocks), st, src, blob,
+                                                              h, (int)rb, nsegp, bands, ntp, nts, mean)
+                              : launch_pt_blob<OP_GAUSS3, NB>(dim3((unsigned)blocks), st, src, blob,
+                                                              h, (int)rb, nsegp, bands, ntp, nts, mean);
+    if (rc) return rc;
+    IDN_CHECK_LAUNCH("idn_gaussian_blob_f32");
+    return IDN_OK;
+  }
   const int nseg = (int)((rb + 1007) / 1008);
   const int seg_len = (int)(((rb + nseg - 1) / nseg + 7) / 8 * 8);
   constexpr int NB = 6;
@@ -1110,7 +1193,6 @@ extern "C" int idn_gaussian_blob_f32(const uint8_t* src, float* blob, int n, int
   const int64_t total = (int64_t)n * bands * nseg;
   IDN_CHECK_ARG(total < (int64_t)0x7FFFFFFF, "idn_gaussian_blob_f32: batch too large");
   const dim3 grid((unsigned)((int64_t)n * bands)), block(TILE_WGT);
-  hipStream_t st = as_stream(stream);
   if (ksize == 5 && knob("IDN_STENCIL_GLDS", 1))  // LDS-DMA tile fetch (as the u8 filters)
     hipLaunchKernelGGL((stencil_u8_lds<3, OP_GAUSS5, NB, EPI_BLOB, 0, 1>), grid, block, 0, st, src,
                        nullptr, h, (int)rb, nseg, seg_len, bands, (int)total, blob, mean[0],

@@ -199,9 +199,10 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
   for (int l = 1; l <= Lt.L && l <= WL_MAXL; ++l) {
     if (wv == IDN_WAVELET_BIOR15) {
       // wl_dwt_stream: strips x row bands of whole WS_G-row groups (the bands' sums are exact,
-      // see the kernel).  sq_grid: 2^-F with the band's total below 2^(52 - F) for any input:
-      // |coefficient| <= 2 (level 1 of [0, 1] data, bior1.5's filter sums) times 2.6 per deeper
-      // level, so a square <= 4 * 8^(l-1)
+      // see the kernel).  sq_grid: 2^-F with the band's total below 2^(52 - F) for any input.
+      // With the filters' L1 norms Llo = 4 B1 + 4 B2 + 2 S2 (~1.967) and Lhi = 2 S2 (~1.414),
+      // level-l data of a [0, 1] image lie within Llo^(2(l-1)) (the 'aa' chain) and a detail
+      // coefficient within Llo * Lhi times that, so a square <= (Llo Lhi)^2 Llo^(4(l-1))
       const int groups = (Lt.H[l] + WS_G - 1) / WS_G;
       Lt.tiles_x[l] = ws_strips(Lt.W[l]);
       Lt.bands[l] = std::min(ws_bands(n, Lt.H[l], Lt.W[l], Lt.tiles_x[l], l), groups);
@@ -209,7 +210,9 @@ inline WlLayout wl_layout(int n, int h, int w, int wv, int levels) {
       if (const int fb = (knob("IDN_WAVELET_BANDS", 0) >> (8 * (l - 1))) & 0xFF)
         Lt.bands[l] = std::min(fb, groups);
       Lt.tiles[l] = Lt.tiles_x[l] * Lt.bands[l];
-      const double bound = 4.0 * std::pow(8.0, l - 1) * (double)Lt.H[l] * (double)Lt.W[l];
+      const double llo = 4.0 * B1 + 4.0 * B2 + 2.0 * S2, lhi = 2.0 * S2;
+      const double bound = (llo * lhi) * (llo * lhi) * std::pow(llo, 4.0 * (l - 1)) *
+                           (double)Lt.H[l] * (double)Lt.W[l];
       Lt.sq_grid[l] = std::ldexp(1.0, (int)std::ceil(std::log2(bound)) - 52);
     } else {
       Lt.bands[l] = 0;

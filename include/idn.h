@@ -308,9 +308,13 @@ int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int
 
 /* ---- decode front-end (cv2.imread: lib/model/test.py:191, minibatch.py:85) --------------- */
 
-/* Header of one JPEG file in host memory (SOI .. SOS): height, width, components (1 or 3).
- * IDN_EUNSUPPORTED for anything the decoder does not take (progressive, arithmetic, 12-bit,
- * CMYK / Adobe RGB, multi-scan, chroma sampling other than 4:4:4 / 4:2:2 / 4:2:0). */
+/* Header of one JPEG file in host memory (SOI .. EOI): height, width, components (1 or 3).
+ * Taken: Huffman-coded baseline, extended sequential and progressive files (SOF0 / SOF1 / SOF2),
+ * one or several scans, restart intervals, 4:4:4 / 4:2:2 / 4:2:0 or grayscale.  IDN_EUNSUPPORTED
+ * for anything else (arithmetic-coded, lossless, hierarchical, 12-bit, CMYK / Adobe RGB, other
+ * chroma sampling) and for a progressive file libjpeg would block-smooth (jdcoefct.c
+ * smoothing_ok: every component with DC data and nonzero low quantisers, and AC 1..5 of some
+ * component left imprecise by the last scan) -- that smoothing is not restated. */
 int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
 
 /* idn_jpeg_decode_u8 flags.  Default (0): the decode of the reference's pinned libjpeg 9d
@@ -323,7 +327,9 @@ int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int*
 #define IDN_JPEG_TURBO 1
 /* device workspace for decoding these files with these flags (0 if any is unsupported) */
 size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n, int flags);
-/* cv2.imread(path) (IMREAD_COLOR) of n baseline JPEG files held in host memory, all h x w, into
+/* cv2.imread(path) (IMREAD_COLOR) of n JPEG files held in host memory (any mix of the kinds
+ * idn_jpeg_info takes: baseline / extended sequential files on the parallel path, progressive and
+ * multi-scan files on the scan path), all h x w, into
  * the device u8 BGR NHWC batch dst (row_stride bytes per row), bit-exact with the library the
  * flags name (replaces cv2.imread at lib/model/test.py:191, lib/roi_data_layer/minibatch.py:85).
  * The entropy-coded segments are copied to the workspace in one transfer; synchronous on

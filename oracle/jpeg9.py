@@ -11,10 +11,12 @@ reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
                selection, successive approximation, EOB runs), one or several scans; a
                non-interleaved scan codes only the component's own blocks (width_in_blocks)
   jdcoefct.c   progressive files are decoded into the whole coefficient buffer first; block
-               smoothing (do_block_smoothing, smoothing_ok) then applies only if a component's AC
+               smoothing (do_block_smoothing, smoothing_ok) then applies only if every component
+               has DC data and nonzero quantisers Q00 Q01 Q10 Q20 Q11 Q02, and some component's AC
                coefficients 1..5 are not all known to full precision after the last scan (coef_bits
                != 0).  Encoders' standard scripts (jpeg_simple_progression) refine every one to
-               Al = 0; a file that does not is rejected here (not restated)
+               Al = 0; a file that libjpeg would smooth is rejected here (not restated), any other
+               decodes as libjpeg decodes it
   jdmaster.c   IDCT scaling: with do_fancy_upsampling (the default) a component whose sampling
                factor divides the maximum by 2 gets a scaled IDCT of twice the size in that
                direction (libjpeg >= 7), so 4:2:0 chroma is decoded by jpeg_idct_16x16 and
@@ -314,7 +316,12 @@ def parse_and_decode(data: bytes):
             raise ValueError("lossless / arithmetic / hierarchical JPEG not supported")
         i = end
     assert coef is not None, "no frame"
-    if progressive and any(cb[0] >= 0 and any(b != 0 for b in cb[1:]) for cb in cbits):
+    # jdcoefct.c smoothing_ok (libjpeg 9d): FALSE unless EVERY component has DC data and nonzero
+    # quantisers Q00 Q01 Q10 Q20 Q11 Q02; then TRUE if some component's AC 1..5 stay imprecise
+    smoothing_ok = progressive and all(
+        cb[0] >= 0 and all(q[c["tq"]][i] != 0 for i in (0, 1, 8, 16, 9, 2))
+        for cb, c in zip(cbits, comps)) and any(any(b != 0 for b in cb[1:]) for cb in cbits)
+    if smoothing_ok:
         raise NotImplementedError("progressive file leaves AC 1..5 imprecise: libjpeg would "
                                   "block-smooth it (jdcoefct.c smoothing_ok)")
     return dict(width=W, height=H, hmax=geo["hmax"], vmax=geo["vmax"],

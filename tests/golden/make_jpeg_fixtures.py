@@ -70,7 +70,57 @@ def main():
     save("prog_gray_q80_91x77.jpg", textured(91, 77, 24)[..., 0], quality=80, progressive=True)
     save("prog_s420_rst4_120x160.jpg", textured(120, 160, 25), quality=80, subsampling=2,
          progressive=True, restart_marker_blocks=4)
+    derived()
+
+
+def _scan_segments(data):
+    """(start, end) of every SOS segment: the SOS marker up to the next marker that is not RSTn"""
+    out, k = [], data.find(b"\xff\xda")
+    while k >= 0:
+        e = k + 2 + ((data[k + 2] << 8) | data[k + 3])
+        while e + 1 < len(data) and not (data[e] == 0xFF and data[e + 1] not in (0x00, 0xFF)
+                                         and not 0xD0 <= data[e + 1] <= 0xD7):
+            e += 1
+        out.append((k, e))
+        k = data.find(b"\xff\xda", e)
+    return out
+
+
+def derived():
+    """prog_nodc_cut_s444_96x128.jpg: prog_s444_q85_96x128.jpg without its DC scans (first and
+    refinement) and without its last two scans.  Its AC 1..5 stay imprecise, but no component has
+    DC data, so libjpeg 9d's smoothing_ok() is FALSE (jdcoefct.c) and it decodes WITHOUT block
+    smoothing (progression warnings only): the case the decoder must accept, not reject"""
+    data = (OUT / "prog_s444_q85_96x128.jpg").read_bytes()
+    segs = _scan_segments(data)
+    parts, prev = [], segs[0][0]
+    parts.append(data[:prev])
+    for k, e in segs[:-2]:
+        parts.append(data[prev:k])  # the tables (DHT) defined between scans
+        ns = data[k + 4]
+        if data[k + 5 + 2 * ns] != 0:  # Ss > 0: an AC scan
+            parts.append(data[k:e])
+        prev = e
+    body = b"".join(parts) + b"\xff\xd9"
+    (OUT / "prog_nodc_cut_s444_96x128.jpg").write_bytes(body)
+    # prog_q0_cut_s444_96x128.jpg: the same file cut before its last two scans (luma AC refinement
+    # missing: imprecise), with the chroma table's Q01 set to 0.  The luma component alone would be
+    # smoothed, but a zero among any component's Q00 Q01 Q10 Q20 Q11 Q02 makes smoothing_ok()
+    # FALSE for the whole image: libjpeg decodes it unsmoothed
+    cut = bytearray(data[:segs[-2][0]] + b"\xff\xd9")
+    k = cut.find(b"\xff\xdb")
+    while k >= 0:
+        seg_end = k + 2 + ((cut[k + 2] << 8) | cut[k + 3])
+        t = k + 4
+        while t < seg_end:
+            pq, tq = cut[t] >> 4, cut[t] & 15
+            if tq == 1 and pq == 0:
+                cut[t + 1 + 1] = 0  # zigzag index 1 = natural Q01
+            t += 1 + 64 * (2 if pq else 1)
+        k = cut.find(b"\xff\xdb", seg_end)
+    (OUT / "prog_q0_cut_s444_96x128.jpg").write_bytes(bytes(cut))
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    derived() if sys.argv[1:] == ["--derived"] else main()

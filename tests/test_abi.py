@@ -127,3 +127,24 @@ def test_docs_name_only_declared_entry_points():
         names -= {"idn_binding"}  # the reference-side stub's file name
         missing = sorted(names - declared)
         assert not missing, f"{doc} names entry points the header does not declare: {missing}"
+
+
+def test_header_jpeg_support_matches_decoder():
+    """include/idn.h's list of what the JPEG decoder takes / rejects agrees with csrc/jpeg.hip: a
+    frame type the parser accepts (SOF0 / SOF1 / SOF2 cases of its marker switch) may not appear
+    among the header's unsupported kinds, and one it rejects must"""
+    import re
+    hdr = (ROOT / "include" / "idn.h").read_text()
+    src = (ROOT / "image-denoising_amd" / "csrc" / "jpeg.hip").read_text()
+    info = hdr[hdr.index("/* Header of one JPEG file"):hdr.index("int idn_jpeg_info")]
+    taken, unsupported = info.split("IDN_EUNSUPPORTED", 1)
+    unsupported = unsupported.split("and for a progressive file libjpeg would block-smooth")[0]
+    accepted_sof = set(re.findall(r"case 0x(C[0-9A-F])", src.split("// DHT")[0]))
+    kinds = {"C0": "baseline", "C1": "extended sequential", "C2": "progressive"}
+    for code, word in kinds.items():
+        if code in accepted_sof:
+            assert word in taken and word not in unsupported, word
+    assert "multi-scan" not in unsupported and "several scans" in taken
+    assert "arithmetic" in unsupported and "lossless" in unsupported
+    dec = hdr[hdr.index("/* cv2.imread(path) (IMREAD_COLOR) of n"):hdr.index("int idn_jpeg_decode_u8")]
+    assert "progressive" in dec and "baseline JPEG files" not in dec

@@ -12,7 +12,9 @@ from conftest import textured
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(3, 600, 1000), (2, 37, 40), (1, 9, 336), (2, 130, 1008), (1, 64, 96)]
+SHAPES = [(3, 600, 1000), (2, 37, 40), (1, 9, 336), (2, 130, 1008), (1, 64, 96),
+          # the pitched tile (rows of 16 k + 8 bytes): band tails, 1-3 segments
+          (2, 601, 1000), (1, 19, 344), (2, 7, 680), (1, 6, 24)]
 
 
 def _t(a):
@@ -28,6 +30,21 @@ def test_gaussian_blob_equals_two_steps(dev, shape, k):
     got = idn.ops.gaussian_blob(x, k)
     ref = idn.ops.blob(idn.gaussian_blur(x, k))
     assert got.dtype == ref.dtype and np.array_equal(got.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.mark.parametrize("knobs", [{"IDN_STENCIL_FORM": "0"}, {"IDN_STENCIL_NTP": "1"},
+                                   {"IDN_STENCIL_NTS": "1", "IDN_STENCIL_NTP": "1"}])
+def test_gaussian_blob_forms_agree(dev, monkeypatch, knobs):
+    """tuning build: the flat tile and the pitched tile's cache policies give the product's blob"""
+    import idn
+    from idn import _lib
+    x = _t(textured(2, 600, 1000, seed=4))
+    want = {k: idn.ops.gaussian_blob(x, k).cpu().numpy() for k in (3, 5)}
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    with _lib.variant("tuning"):
+        for k in (3, 5):
+            assert np.array_equal(idn.ops.gaussian_blob(x, k).cpu().numpy(), want[k]), k
 
 
 @pytest.mark.parametrize("chunk_batch", [1, 5, 70])

@@ -208,3 +208,16 @@ def test_progressive_without_final_scans_is_rejected():
         ops.jpeg_info(cut)
     with pytest.raises(NotImplementedError):
         jpeg9.imread(cut)
+
+
+def test_progressive_smoothing_ok_mirrors_libjpeg():
+    """libjpeg 9d smooths a progressive file only if EVERY component has DC data and nonzero
+    Q00 Q01 Q10 Q20 Q11 Q02 (jdcoefct.c smoothing_ok): a file with imprecise AC but no DC scans,
+    or with a zero chroma Q01, decodes unsmoothed -- accepted by the host parser and the oracle,
+    whose pixels test_oracle_libjpeg9_matches_real_libjpeg9 pins to the real library"""
+    from idn import ops
+    from oracle import jpeg9
+    for name in ("prog_nodc_cut_s444_96x128.jpg", "prog_q0_cut_s444_96x128.jpg"):
+        data = (JPEG / name).read_bytes()
+        assert ops.jpeg_info(data) == (96, 128, 3), name
+        assert jpeg9.imread(data).shape == (96, 128, 3)

@@ -128,18 +128,33 @@ def test_mixed_baseline_and_progressive_batch(dev):
 
 
 def test_truncated_progressive_file_decodes_without_fault(dev):
-    """a progressive file cut inside its last scan: every scan header is there (no smoothing
-    case), the data runs out -- the decoder reads zeros past it (libjpeg's fill) and the scans
-    before the cut give the same coefficients as the whole file"""
+    """a progressive file cut inside its last scan (libjpeg's script: the luma AC refinement,
+    restart markers every 4 blocks): every scan header is there (no smoothing case), the data runs
+    out -- the decoder reads zeros past it (libjpeg's fill).  The restart intervals complete before
+    the cut decode exactly as in the whole file, so every pixel row whose luma blocks all lie in
+    those intervals equals the whole file's decode; the rows after the cut differ"""
     from idn import ops
     from test_jpeg import _sos_offsets
     data = (JPEG / "prog_s420_rst4_120x160.jpg").read_bytes()
     last = _sos_offsets(data)[-1]
-    trunc = data[:last + (len(data) - last) // 2] + b"\xff\xd9"
+    ns = data[last + 4]
+    assert ns == 1 and data[last + 5] == 1  # one component, the luma (component id 1)
+    hdr_end = last + 2 + ((data[last + 2] << 8) | data[last + 3])
+    cut = last + (len(data) - last) // 2
+    trunc = data[:cut] + b"\xff\xd9"
+    k = data.find(b"\xff\xdd")  # DRI: restart interval in MCUs (= blocks in this scan)
+    assert k > 0 and k < last
+    dri = (data[k + 4] << 8) | data[k + 5]
+    seg = data[hdr_end:cut]
+    nrst = sum(1 for i in range(len(seg) - 1) if seg[i] == 0xFF and 0xD0 <= seg[i + 1] <= 0xD7)
+    wib = (160 + 7) // 8  # luma blocks per row
+    rows_ok = 8 * ((nrst * dri) // wib)  # pixel rows whose luma blocks all precede the cut
+    assert 8 <= rows_ok < 120
     good = ops.jpeg_decode([data])[0].cpu().numpy()
     got = ops.jpeg_decode([trunc])[0].cpu().numpy()
     assert got.shape == good.shape
-    assert np.abs(got.astype(int) - good.astype(int)).max() <= 255  # decoded, no fault
+    assert np.array_equal(got[:rows_ok], good[:rows_ok])
+    assert not np.array_equal(got[rows_ok + 8:], good[rows_ok + 8:])
 
 
 def test_large_mixed_batch_bitexact_and_errors(dev):

@@ -81,7 +81,7 @@ def test_live_gaussian_wavelet_full_size(dev, var):
 def test_wavelet_batch_invariant(dev, wavelet, levels, src):
     """An image's result does not depend on the batch around it: the bior1.5 analysis splits row
     bands by batch size (fewer, longer bands for big batches), but its sums of squares are built
-    from per-(thread, 4-row group) partials rounded to a power-of-two grid, so every later sum is
+    from per-(thread, 5-row group: WS_G) partials rounded to a power-of-two grid, so every later sum is
     exact and order-free; denoising an image alone and inside a batch of 40 (different row bands
     at every level) gives bit-identical outputs -- a sharded batch equals the 1-GPU run
     (INTEGRATION.md)."""

@@ -348,3 +348,16 @@ def test_fast_cpu_baseline_bitexact_with_scalar_oracle():
         for k in (3, 5):
             assert np.array_equal(oracle.cv.gaussian_blur_fast(img, k),
                                   oracle.cv.gaussian_blur(img, k)), (shape, k)
+
+
+def test_key_ties_fixture_is_reproduced():
+    """tests/golden/make_key_ties.py (the search over all 2^24 RGB triples for exact YCbCr ties
+    whose fp64 values differ, at each channel's extremes) reproduces the triples the GPU test
+    test_wavelet_color_minmax_key_ties places"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "make_key_ties", Path(__file__).parent / "golden" / "make_key_ties.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    from test_wavelet_gpu import _KEY_TIES
+    assert mod.find_ties() == _KEY_TIES

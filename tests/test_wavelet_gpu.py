@@ -330,6 +330,40 @@ def test_wavelet_bior15_fp32_analysis(dev, monkeypatch, shape, a32):
         check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
 
 
+@pytest.mark.parametrize("shape", [(600, 1000), (130, 77), (37, 53)])
+@pytest.mark.parametrize("src", ["u8", "f64"])
+def test_wavelet_dd32_sigma_bitwise(dev, monkeypatch, shape, src):
+    """IDN_WAVELET_DD32 (product 1): the level-1 dd band stored as fp32, the sigma median
+    recomputing its candidates' exact |dd| from the input (bior_dd2x2 / wl_bior_dd1_key64) in
+    wl_dwt_stream's fp64 op order -- against DD32=0 (the fp64 dd band the median reads back):
+    sigma medians and nonzero counts bit-identical for u8 and float64 input, outputs within 2e-6"""
+    import torch
+    from idn import _lib, ops
+    img = make_img(*shape, 41)
+    x = torch.from_numpy(np.ascontiguousarray(img[None])).cuda()
+    if src == "f64":
+        x = x.double() * (1.0 / 255.0)
+    q = min(shape) // 9
+    lv = max((q.bit_length() - 1 if q >= 1 else 0) - 3, 1)
+    res = {}
+    for dd32 in ("0", "1"):
+        with monkeypatch.context() as mp:
+            mp.setenv("IDN_WAVELET_DD32", dd32)
+            with _lib.variant("tuning"):
+                u8, f = ops.denoise_wavelet(x, "bior1.5", None, out="both")
+                off = _lib.load().idn_wavelet_stats_offset(1, shape[0], shape[1],
+                                                           ops.WAVELETS["bior1.5"], -1)
+        ws = ops._WS_CACHE[(str(x.device), torch.cuda.current_stream(x.device).cuda_stream)]
+        st = ws[off:off + 256 * 8].view(torch.float64).cpu().numpy().copy()
+        res[dd32] = (u8[0].cpu().numpy(), f[0].cpu().numpy().astype(np.float64), st)
+    (u8a, fa, sa), (u8b, fb, sb) = res["0"], res["1"]
+    med = slice(8 + 9 * lv, 8 + 9 * lv + 3)
+    np.testing.assert_array_equal(sa[med].view(np.uint64), sb[med].view(np.uint64))
+    np.testing.assert_array_equal(sa[248:251], sb[248:251])
+    assert np.abs(fa - fb).max() <= 2e-6
+    check_u8(u8b, fa, u8a)
+
+
 @pytest.mark.parametrize("shape", [(601, 999), (37, 53), (9, 11)])
 def test_wavelet_coop_normalisation_bitwise(dev, monkeypatch, shape):
     """IDN_WAVELET_COOP (the tiled analysis wl_dwt_rb, which the general Haar path uses: sizes not
@@ -373,8 +407,9 @@ def test_wavelet_color_minmax_exact(dev):
         np.testing.assert_array_equal(mx.view(np.uint64), ycc.max(axis=(0, 1)).view(np.uint64))
 
 
-# (channel, extreme, two triples whose integer keys tie at that channel's extreme while their fp64
-# values differ in the last bits: found over all 2^24 triples, tools/check_ycbcr_keys.c)
+# per channel (Y, Cb, Cr) and extreme (lowest, highest): two triples whose exact YCbCr values tie
+# (equal integer keys 1000 M . rgb) while their fp64 values differ in the last bits -- the search
+# over all 2^24 triples is tests/golden/make_key_ties.py (test_oracle.py checks it reproduces this)
 _KEY_TIES = [((12, 1, 2), (1, 0, 36)), ((244, 254, 254), (255, 255, 220)),
              ((252, 255, 1), (251, 254, 0)), ((2, 4, 255), (0, 2, 253)),
              ((0, 254, 252), (1, 255, 253)), ((254, 0, 3), (255, 1, 4))]
@@ -382,10 +417,12 @@ _KEY_TIES = [((12, 1, 2), (1, 0, 36)), ((244, 254, 254), (255, 255, 220)),
 
 @pytest.mark.parametrize("swap", [False, True])
 def test_wavelet_color_minmax_key_ties(dev, swap):
-    """wl_color_minmax ranks u8 pixels by exact integer keys and evaluates the fp64 chain only at
-    the extremes: each channel's min and max here is reached by two triples with the same key and
-    different fp64 values, adjacent in one thread's pixel group (either order) and again in other
-    threads; the stats must still equal numpy's fp64 min / max bit for bit"""
+    """wl_color_minmax evaluates the fp64 YCbCr chain on every pixel and reduces min / max per
+    channel (an exact-integer-key ranking was measured slower and not shipped).  Each
+    channel's min and max here is reached by two triples whose exact values tie and whose fp64
+    values differ, adjacent in one thread's pixel group (either order) and again in other
+    threads: the stats must equal numpy's fp64 min / max bit for bit, i.e. the kernel's chain must
+    round exactly as numpy's (a chain that rounds differently picks the other triple's value)"""
     import torch
     import oracle
     from oracle.cv import matmul3_fma
