@@ -188,6 +188,31 @@ DTYPE["wavelet_bior15_f64"] = DTYPE["wavelet_bior15"]
 PARITY["wavelet_bior15_f64"] = PARITY["wavelet_bior15"]
 
 
+def _live_f64(fused):
+    """the live test path's noise + denoise on the batch (lib/model/test.py:1678-1684 ->
+    1802-1810): random_noise(gaussian, var 0.1) as float64, then denoise_wavelet(bior1.5) on that
+    float64 image; fused = the noise kernel reduces the wavelet's colour range as it writes the
+    image (random_noise_ycc -> denoise_wavelet(ycc_keys)), else the two plain calls"""
+    def step(idn, x, y):
+        if fused:
+            f, keys = idn.ops.random_noise_ycc(x, "gaussian", var=0.1, seed=3)
+            idn.ops.denoise_wavelet(f, "bior1.5", None, out_u8=y, ycc_keys=keys)
+        else:
+            f = idn.ops.random_noise(x, "gaussian", var=0.1, seed=3, out="f64")
+            idn.ops.denoise_wavelet(f, "bior1.5", None, out_u8=y)
+    return step
+
+
+# 3 B read + 24 B (f64) written by the noise, 24 B read + 3 B written by the wavelet per pixel
+OPS["live_f64"] = ("gaussian_var0.1 (float64) + bior1.5 wavelet, fused colour range (live test "
+                   "path)", _live_f64(True), 54, "pipeline")
+OPS["live_f64_unfused"] = ("gaussian_var0.1 (float64) + bior1.5 wavelet, two plain calls",
+                           _live_f64(False), 54, "pipeline")
+for _k in ("live_f64", "live_f64_unfused"):
+    DTYPE[_k] = "f64 noise + " + DTYPE["wavelet_bior15"]
+    PARITY[_k] = "Philox f64 gaussian law + skimage 0.14 denoise_wavelet within 1e-5"
+
+
 def _jpeg_files(x, quality=90):
     """the batch encoded once (untimed) by Pillow: baseline 4:2:0 JPEG files in host memory"""
     import io
@@ -293,6 +318,9 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
             "bior1.5", None)]),  # test_v0 quirk: the float64 [0, 1] image goes to the blob
     }
     table["cfg2p"] = table["cfg2"]
+    table["live_f64"] = table["live_f64_unfused"] = lambda a: oracle.sk.to_u8(
+        255 * oracle.wavelet.denoise_wavelet(oracle.sk.noise_gaussian(
+            a[0], np.random.normal(0.0, 0.1 ** 0.5, a[0].shape)), "bior1.5", None))
     if op == "jpeg_decode":  # Pillow's libjpeg-turbo decode of the same kind of file
         import io
         from PIL import Image
@@ -321,7 +349,8 @@ def cpu_baseline(op: str, budget_s: float = 12.0):
         if el >= budget_s or n_img >= 1000000:
             break
     if op in ("noise_gaussian", "noise_sap", "noise_poisson", "wavelet_haar3", "cfg5",
-              "wavelet_bior15", "wavelet_bior15_f64", "detect_e2e"):
+              "wavelet_bior15", "wavelet_bior15_f64", "detect_e2e", "live_f64",
+              "live_f64_unfused"):
         threads, src = 1, "numpy, single thread"
     elif op == "jpeg_decode":
         threads, src = 1, "PIL (libjpeg-turbo) decode, single thread"

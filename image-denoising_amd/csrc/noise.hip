@@ -20,6 +20,7 @@
 // Also: periodic noise pattern (add_periodic_noise, test.py:1128-1298) and cv2.add(u8, u8).
 #include "idn_common.hpp"
 #include "noise_apply.hpp"
+#include "ycc.hpp"
 
 #include <math.h>
 
@@ -44,6 +45,7 @@ struct NoiseArgs {
   const uint64_t* ids;  // optional per-image ids (device); else id = offset + image index
   const int64_t* slots;  // optional batch positions (device): image i of the launch reads and
                          // writes image slots[i] of src / out_u8 / out_f64; else slot = i
+  unsigned long long* ycc;  // noise_gauss_ycc_kernel: per image the colour range keys (ycc.hpp)
 };
 __device__ __forceinline__ uint64_t image_id(const NoiseArgs& a, int img) {
   return a.ids ? a.ids[img] : a.offset + (uint64_t)img;
@@ -116,6 +118,108 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
       store_out(a, img, e, boff, out);
     }
   }
+}
+
+// Float64 gaussian / speckle on compact 3-channel images, with the bior1.5 / Haar wavelet's colour
+// range reduced on the fly (the live test path: random_noise's float64 image goes straight to
+// denoise_wavelet, lib/model/test.py:1678-1684 -> 1807-1810).  One thread per pixel pair = the
+// three element pairs 3q .. 3q+2 of noise_gauss_kernel (the same draws, the same op order: the
+// image is bit-identical), plus per image the fp64 min / max of skimage rgb2ycbcr's three dot
+// products of the output (ycc_dots, wl_color_minmax's chain), reduced per workgroup and folded
+// into ycc[6 img ..] as order-preserving keys with the offsets added after the reduction -- what
+// wl_color_minmax would compute from the stored image, without reading its 24 B/pixel back.
+template <int KIND, int SRC>
+__global__ __launch_bounds__(256) void noise_gauss_ycc_kernel(NoiseArgs a) {
+  const int img = blockIdx.y;
+  const int64_t npp = a.elems / 6;
+  const int64_t slot = slot_of(a, img);
+  const uint8_t* s = a.src + slot * a.elems;
+  double* of = a.out_f64 + slot * a.elems;
+  uint8_t* ou = a.out_u8 ? a.out_u8 + slot * a.elems : nullptr;
+  const uint64_t gimg = image_id(a, img);
+  double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npp;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    double nz[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int64_t pr = 3 * q + k;
+      if constexpr (SRC == SRC_REPLAY) {
+        nz[2 * k] = a.replay[(int64_t)img * a.elems + 2 * pr];
+        nz[2 * k + 1] = a.replay[(int64_t)img * a.elems + 2 * pr + 1];
+      } else {
+        const u32x4 r = philox4x32(u32x4{(uint32_t)pr, 2u ^ ((uint32_t)(pr >> 32) << 8),
+                                         (uint32_t)gimg, (uint32_t)(gimg >> 32)},
+                                   a.key);
+        double z0, z1;
+        normal2_f64(r, z0, z1);
+        nz[2 * k] = __dadd_rn(a.p0, __dmul_rn(a.p1, z0));
+        nz[2 * k + 1] = __dadd_rn(a.p0, __dmul_rn(a.p1, z1));
+      }
+    }
+    const uint16_t* s2 = reinterpret_cast<const uint16_t*>(s + 6 * q);  // 2-byte aligned
+    const uint32_t b01 = s2[0], b23 = s2[1], b45 = s2[2];
+    const uint32_t bytes[6] = {b01 & 0xFFu, b01 >> 8, b23 & 0xFFu, b23 >> 8, b45 & 0xFFu, b45 >> 8};
+    double out[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const double xv = img_as_float(bytes[e]);
+      out[e] = KIND == IDN_NOISE_GAUSSIAN ? clip01(__dadd_rn(xv, nz[e]))
+                                          : clip01(__dadd_rn(xv, __dmul_rn(xv, nz[e])));
+    }
+    double2* o2 = reinterpret_cast<double2*>(of + 6 * q);  // 16-byte aligned (48 q bytes)
+    o2[0] = make_double2(out[0], out[1]);
+    o2[1] = make_double2(out[2], out[3]);
+    o2[2] = make_double2(out[4], out[5]);
+    if (ou) {
+      uint16_t* u2 = reinterpret_cast<uint16_t*>(ou + 6 * q);
+      u2[0] = (uint16_t)(u8_of(out[0]) | (u8_of(out[1]) << 8));
+      u2[1] = (uint16_t)(u8_of(out[2]) | (u8_of(out[3]) << 8));
+      u2[2] = (uint16_t)(u8_of(out[4]) | (u8_of(out[5]) << 8));
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      double d[3];
+      ycc_dots(out[3 * p], out[3 * p + 1], out[3 * p + 2], d);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {  // finite values: fmin / fmax are plain selects
+        mn[c] = fmin(mn[c], d[c]);
+        mx[c] = fmax(mx[c], d[c]);
+      }
+    }
+  }
+  __shared__ double red[2][3][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double da = mn[c], db = mx[c];
+    for (int o = 32; o > 0; o >>= 1) {
+      da = fmin(da, __shfl_xor(da, o));
+      db = fmax(db, __shfl_xor(db, o));
+    }
+    if (lane == 0) {
+      red[0][c][wave] = da;
+      red[1][c][wave] = db;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int c = threadIdx.x;
+    double da = red[0][c][0], db = red[1][c][0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+      da = fmin(da, red[0][c][k]);
+      db = fmax(db, red[1][c][k]);
+    }
+    if (da <= db) {  // a workgroup with no pixel leaves the keys alone
+      atomicMin(a.ycc + 6 * img + c, dkey(__dadd_rn(da, ycc_offset(c))));
+      atomicMax(a.ycc + 6 * img + 3 + c, dkey(__dadd_rn(db, ycc_offset(c))));
+    }
+  }
+}
+
+__global__ void ycc_keys_init(unsigned long long* keys, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 6 * n) keys[i] = (i % 6) < 3 ? ~0ull : 0ull;
 }
 
 // ---- u8 stream, flat form (compact rows): 16 consecutive elements per thread ------------------
@@ -843,6 +947,60 @@ extern "C" int idn_noise_slots_u8(const uint8_t* src, uint8_t* out_u8, double* o
                 "(row_stride %lld != w*c)", (long long)row_stride);
   return noise_u8_impl(src, out_u8, out_f64, n, h, w, c, row_stride, kind, p0, p1, seed, 0,
                        image_ids, slots, nullptr, workspace, ws_bytes, stream);
+}
+
+extern "C" int idn_noise_ycc_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n,
+                                int h, int w, int kind, double p0, double p1, uint64_t seed,
+                                uint64_t offset, const uint64_t* image_ids, const double* replay,
+                                uint64_t* ycc_keys, void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(src && out_f64 && ycc_keys, "idn_noise_ycc_u8: null src / out_f64 / ycc_keys");
+  IDN_CHECK_ARG(kind == IDN_NOISE_GAUSSIAN || kind == IDN_NOISE_SPECKLE,
+                "idn_noise_ycc_u8: gaussian or speckle only (got %d)", kind);
+  IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0, "idn_noise_ycc_u8: bad shape");
+  IDN_CHECK_ARG(p1 >= 0.0, "idn_noise_ycc_u8: var must be >= 0");
+  if (n == 0) return IDN_OK;
+  const int64_t elems = (int64_t)h * w * 3;
+  if (elems % 6 != 0 || ((uintptr_t)src & 1) || ((uintptr_t)out_f64 & 15) ||
+      ((uintptr_t)out_u8 & 1) || n > 65535)
+    return set_error(IDN_EUNSUPPORTED, "idn_noise_ycc_u8: needs an even pixel count per image, "
+                     "2-byte aligned u8 and 16-byte aligned float64 buffers");
+  hipStream_t st = as_stream(stream);
+  NoiseArgs a{};
+  a.src = src;
+  a.out_u8 = out_u8;
+  a.out_f64 = out_f64;
+  a.replay = replay;
+  a.n = n;
+  a.h = h;
+  a.w = w;
+  a.c = 3;
+  a.row_stride = (int64_t)w * 3;
+  a.elems = elems;
+  a.key = seed ^ (KIND_TAG * (uint64_t)(kind + 1));
+  a.offset = offset;
+  a.ids = image_ids;
+  a.p0 = p0;
+  a.p1 = pow(p1, 0.5);
+  a.ycc = reinterpret_cast<unsigned long long*>(ycc_keys);
+  hipLaunchKernelGGL(ycc_keys_init, dim3((6 * n + 255) / 256), dim3(256), 0, st, a.ycc, n);
+  // about 2048 workgroups in all: one image alone spreads over the chip, a batch keeps the
+  // per-workgroup atomics few
+  const int64_t npp = elems / 6;
+  const unsigned gx = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((npp + 255) / 256, (2048 + n - 1) / n));
+  const dim3 grid(gx, (unsigned)n);
+  const bool g = kind == IDN_NOISE_GAUSSIAN;
+  if (replay && g)
+    hipLaunchKernelGGL((noise_gauss_ycc_kernel<IDN_NOISE_GAUSSIAN, SRC_REPLAY>), grid, dim3(256), 0, st, a);
+  else if (replay)
+    hipLaunchKernelGGL((noise_gauss_ycc_kernel<IDN_NOISE_SPECKLE, SRC_REPLAY>), grid, dim3(256), 0, st, a);
+  else if (g)
+    hipLaunchKernelGGL((noise_gauss_ycc_kernel<IDN_NOISE_GAUSSIAN, SRC_F64>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((noise_gauss_ycc_kernel<IDN_NOISE_SPECKLE, SRC_F64>), grid, dim3(256), 0, st, a);
+  IDN_CHECK_LAUNCH("idn_noise_ycc_u8");
+  return IDN_OK;
 }
 
 extern "C" int idn_periodic_pattern_u8(uint8_t* pattern, int h, int w, int c, double amplitude,

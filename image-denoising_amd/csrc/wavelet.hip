@@ -38,6 +38,8 @@
 
 #include <algorithm>
 
+#include "ycc.hpp"
+
 namespace idn {
 
 using wreal = double;  // workspace / arithmetic type of the transform
@@ -243,25 +245,24 @@ __device__ __forceinline__ int sym_idx(int i, int n) {  // pywt 'symmetric' (hal
 }
 
 // ---- 1: colour transform + min / max -----------------------------------------------------------
-__global__ void wl_init_stats(double* stats, int n) {
+// ycc_keys (nullable): the colour range already reduced by the float64 noise kernel that wrote the
+// input (idn_noise_ycc_u8), per image min keys of Y Cb Cr then max keys -- copied in, and
+// wl_color_minmax does not run
+__global__ void wl_init_stats(double* stats, int n, const unsigned long long* ycc_keys = nullptr) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * WL_STATS) return;
-  const int k = i % WL_STATS;
+  const int k = i % WL_STATS, img = i / WL_STATS;
   if (k >= WlStats::MN64 && k < WlStats::MN64 + 3) {
-    reinterpret_cast<unsigned long long*>(stats)[i] = ~0ull;  // min key
+    reinterpret_cast<unsigned long long*>(stats)[i] =
+        ycc_keys ? ycc_keys[6 * img + (k - WlStats::MN64)] : ~0ull;  // min key
   } else if (k >= WlStats::MX64 && k < WlStats::MX64 + 3) {
-    reinterpret_cast<unsigned long long*>(stats)[i] = 0ull;   // max key
+    reinterpret_cast<unsigned long long*>(stats)[i] =
+        ycc_keys ? ycc_keys[6 * img + 3 + (k - WlStats::MX64)] : 0ull;  // max key
   } else {
     stats[i] = 0.0;
   }
 }
 
-// skimage rgb2ycbcr: arr @ ycbcr_from_rgb.T + [16, 128, 128].  numpy's matmul (OpenBLAS dgemm) rounds
-// each dot product as an fma chain over k; reproduced exactly, because the set of exactly-zero finest
-// detail coefficients (and so sigma) depends on the last bit of Y (oracle/filters.c, same chain).
-__device__ __forceinline__ double dot3(double x0, double x1, double x2, double m0, double m1, double m2) {
-  return __fma_rn(x2, m2, __fma_rn(x1, m1, __dmul_rn(x0, m0)));
-}
 __device__ __forceinline__ void ycbcr64(double x0, double x1, double x2, double (&o)[3]) {
   o[0] = __dadd_rn(dot3(x0, x1, x2, 65.481, 128.553, 24.966), 16.0);
   o[1] = __dadd_rn(dot3(x0, x1, x2, -37.797, -74.203, 112.0), 128.0);
@@ -284,21 +285,6 @@ __device__ __forceinline__ void load_rgb64(const uint8_t* __restrict__ src,
   }
 }
 
-// fp64 min / max as order-preserving u64 keys (negative values flip all bits, positive ones the
-// sign bit), so unsigned atomics order any doubles -- f64 inputs outside [0, 1] give negative Cb/Cr
-__device__ __forceinline__ unsigned long long dkey(double v) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-__device__ __forceinline__ double dkey_inv(unsigned long long k) {
-  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
-}
-__device__ __forceinline__ void atomicMinD(double* p, double v) {
-  atomicMin(reinterpret_cast<unsigned long long*>(p), dkey(v));
-}
-__device__ __forceinline__ void atomicMaxD(double* p, double v) {
-  atomicMax(reinterpret_cast<unsigned long long*>(p), dkey(v));
-}
 __device__ __forceinline__ void wl_minmax64(const double* st, int c, double& mn, double& mx) {
   const unsigned long long* u64 = reinterpret_cast<const unsigned long long*>(st);
   mn = dkey_inv(u64[WlStats::MN64 + c]);
@@ -3532,15 +3518,17 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
 
 template <int L>
 static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8, float* out_f32,
-                        const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st) {
+                        const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st,
+                  const unsigned long long* ycc_keys = nullptr) {
   wreal* wsf = (wreal*)ws;
   double* stats = (double*)((char*)ws + Lt.stats_off);
   double* part = (double*)((char*)ws + Lt.part_off);
   const int n = Lt.n;
   const int nthr = (Lt.h >> L) * (Lt.w >> L) * HaarSplit<L>::NS;
   const int nwg = (nthr + WLH_WG - 1) / WLH_WG;
-  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n);
-  {
+  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n,
+                     ycc_keys);
+  if (!ycc_keys) {
     const int64_t np = (int64_t)Lt.h * Lt.w;
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
     int gx = (int)((np / 4 + 255) / 256);
@@ -3612,12 +3600,14 @@ static bool wl_haar_ok(int wavelet, const WlLayout& Lt, const uint8_t* src, int6
 
 template <int WV>
 static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float* out_f32,
-                  const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st) {
+                  const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st,
+                  const unsigned long long* ycc_keys = nullptr) {
   wreal* wsf = (wreal*)ws;
   double* stats = (double*)((char*)ws + Lt.stats_off);
   const int n = Lt.n;
-  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n);
-  {
+  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n,
+                     ycc_keys);
+  if (!ycc_keys) {
     const int64_t np = (int64_t)Lt.h * Lt.w;
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
     int gx = (int)((np / 4 + 255) / 256);
@@ -3846,11 +3836,11 @@ extern "C" size_t idn_wavelet_stats_offset(int n, int h, int w, int wavelet, int
   return wl_layout(n, h, w, wavelet, levels).stats_off;
 }
 
-extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,
-                                      float* out_f32, int n, int h, int w, int64_t row_stride,
-                                      int wavelet, int levels, void* workspace, size_t ws_bytes,
-                                      void* stream) {
-  using namespace idn;
+namespace idn {
+static int wavelet_impl(const uint8_t* src, const double* in_f64,
+                        const unsigned long long* ycc_keys, uint8_t* out_u8, float* out_f32, int n,
+                        int h, int w, int64_t row_stride, int wavelet, int levels, void* workspace,
+                        size_t ws_bytes, void* stream) {
   IDN_CHECK_ARG(src || in_f64, "idn_wavelet_denoise_u8: no input");
   IDN_CHECK_ARG(out_u8 || out_f32, "idn_wavelet_denoise_u8: no output");
   IDN_CHECK_ARG(n >= 0 && h > 0 && w > 0, "idn_wavelet_denoise_u8: bad shape");
@@ -3868,15 +3858,36 @@ extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, 
     return set_error(IDN_EWORKSPACE, "idn_wavelet_denoise_u8: needs %zu workspace bytes (got %zu)",
                      Lt.bytes, ws_bytes);
   hipStream_t st = as_stream(stream);
+  const unsigned long long* K = ycc_keys;
   if (wl_haar_ok(wavelet, Lt, src, row_stride)) {
-    if (Lt.L == 1) wl_run_haar<1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
-    else if (Lt.L == 2) wl_run_haar<2>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
-    else wl_run_haar<3>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+    if (Lt.L == 1) wl_run_haar<1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st, K);
+    else if (Lt.L == 2) wl_run_haar<2>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st, K);
+    else wl_run_haar<3>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st, K);
   } else if (wavelet == IDN_WAVELET_DB1) {
-    wl_run<IDN_WAVELET_DB1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+    wl_run<IDN_WAVELET_DB1>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st, K);
   } else {
-    wl_run<IDN_WAVELET_BIOR15>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st);
+    wl_run<IDN_WAVELET_BIOR15>(src, in_f64, out_u8, out_f32, Lt, row_stride, workspace, st, K);
   }
   IDN_CHECK_LAUNCH("idn_wavelet_denoise_u8");
   return IDN_OK;
+}
+}  // namespace idn
+
+extern "C" int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,
+                                      float* out_f32, int n, int h, int w, int64_t row_stride,
+                                      int wavelet, int levels, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  return idn::wavelet_impl(src, in_f64, nullptr, out_u8, out_f32, n, h, w, row_stride, wavelet,
+                           levels, workspace, ws_bytes, stream);
+}
+
+extern "C" int idn_wavelet_denoise_ycc(const double* in_f64, const uint64_t* ycc_keys,
+                                       uint8_t* out_u8, float* out_f32, int n, int h, int w,
+                                       int wavelet, int levels, void* workspace, size_t ws_bytes,
+                                       void* stream) {
+  using namespace idn;
+  IDN_CHECK_ARG(in_f64 && ycc_keys, "idn_wavelet_denoise_ycc: null input or keys");
+  return wavelet_impl(nullptr, in_f64, reinterpret_cast<const unsigned long long*>(ycc_keys),
+                      out_u8, out_f32, n, h, w, (int64_t)w * 3, wavelet, levels, workspace,
+                      ws_bytes, stream);
 }

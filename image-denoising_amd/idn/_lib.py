@@ -15,7 +15,7 @@ import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libidn_hip.so"
-ABI_VERSION = 4  # IDN_ABI_VERSION of include/idn.h that SIGNATURES binds
+ABI_VERSION = 5  # IDN_ABI_VERSION of include/idn.h that SIGNATURES binds
 VARIANTS = {"tuning": Path(__file__).resolve().parent / "libidn_hip_tuning.so"}
 
 _c_u8p = ctypes.c_void_p
@@ -49,6 +49,8 @@ SIGNATURES = {
     "idn_noise_slots_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64,
                                     _c_int, _c_dbl, _c_dbl, _c_u64, _c_vp, _c_vp, _c_vp, _c_size,
                                     _c_vp]),
+    "idn_noise_ycc_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_dbl,
+                                  _c_dbl, _c_u64, _c_u64, _c_vp, _c_f64p, _c_vp, _c_vp]),
     "idn_noise_add_u8": (_c_int, [_c_u8p, _c_u8p, _c_f64p, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_int,
                                   _c_dbl, _c_dbl, _c_u64, _c_u64, _c_f64p, _c_vp, _c_size, _c_vp]),
     "idn_noise_add_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
@@ -70,6 +72,8 @@ SIGNATURES = {
     "idn_copy_u8": (_c_int, [_c_u8p, _c_u8p, _c_i64, _c_int, _c_vp]),
     "idn_wavelet_denoise_u8": (_c_int, [_c_u8p, _c_f64p, _c_u8p, _c_vp, _c_int, _c_int, _c_int, _c_i64,
                                         _c_int, _c_int, _c_vp, _c_size, _c_vp]),
+    "idn_wavelet_denoise_ycc": (_c_int, [_c_f64p, _c_vp, _c_u8p, _c_vp, _c_int, _c_int, _c_int,
+                                         _c_int, _c_int, _c_vp, _c_size, _c_vp]),
     "idn_wavelet_workspace_size": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "idn_wavelet_stats_offset": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "idn_gaussian_blur_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp]),

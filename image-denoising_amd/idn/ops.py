@@ -194,6 +194,48 @@ def random_noise(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0, 
     return _finish(y8, sq), _finish(y64, sq)
 
 
+def ycc_fusable(x: torch.Tensor) -> bool:
+    """random_noise_ycc takes this batch: uint8, 3 channels, an even pixel count per image"""
+    return x.dtype == torch.uint8 and x.shape[-1] == 3 and (x.shape[-3] * x.shape[-2]) % 2 == 0
+
+
+def random_noise_ycc(x: torch.Tensor, mode: str = "gaussian", *, mean: float = 0.0,
+                     var: float = 0.01, seed: int = 0, offset: int = 0,
+                     replay: Optional[torch.Tensor] = None, image_ids=None):
+    """random_noise(x, mode, out='f64') for gaussian / speckle, fused with the wavelet's colour
+    range (idn_noise_ycc_u8; lib/model/test.py:1678-1684 -> 1807-1810: the float64 image goes
+    straight into denoise_wavelet).  Returns (the float64 image -- the same values as
+    random_noise(..., out='f64') -- and an (N, 6) int64 device tensor of per-image YCbCr min / max
+    keys for denoise_wavelet(..., ycc_keys=...))."""
+    kind = NOISE_KINDS.get(mode.lower())
+    if kind not in (0, 1):
+        raise ValueError(f"random_noise_ycc: gaussian or speckle only (got {mode!r})")
+    xb, sq = _u8_batch(x, "random_noise_ycc")
+    n, h, w, c = xb.shape
+    if c != 3:
+        raise ValueError("random_noise_ycc: needs 3 channels")
+    xb = xb.contiguous()
+    y64 = _empty_like_img(xb, torch.float64)
+    keys = torch.empty((n, 6), dtype=torch.int64, device=xb.device)
+    rp = None
+    if replay is not None:
+        if replay.device != xb.device or replay.dtype != torch.float64 or replay.numel() != xb.numel():
+            raise ValueError("random_noise_ycc: replay must be a float64 field of x's shape on its device")
+        rp = replay.contiguous()
+    ids = None
+    if image_ids is not None:
+        if rp is not None:
+            raise ValueError("random_noise_ycc: image_ids applies to the Philox stream, not to replay")
+        ids = _ids_tensor(image_ids, n, xb.device)
+    rc = _lib.load().idn_noise_ycc_u8(xb.data_ptr(), None, y64.data_ptr(), n, h, w, kind,
+                                      float(mean), float(var), int(seed) & (2 ** 64 - 1),
+                                      int(offset), ids.data_ptr() if ids is not None else None,
+                                      rp.data_ptr() if rp is not None else None, keys.data_ptr(),
+                                      _stream())
+    _lib.check(rc, "idn_noise_ycc_u8")
+    return _finish(y64, sq), keys
+
+
 def _slots_tensor(slots, device) -> torch.Tensor:
     """The caller owns slot validity (0 <= slot < batch size, as for device image-id tensors):
     checking a device tensor's values would cost a host sync per launch."""
@@ -554,11 +596,14 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
 
 
 def denoise_wavelet(x: torch.Tensor, wavelet: str = "bior1.5", levels: Optional[int] = None,
-                    out: str = "u8", out_u8: Optional[torch.Tensor] = None):
+                    out: str = "u8", out_u8: Optional[torch.Tensor] = None,
+                    ycc_keys: Optional[torch.Tensor] = None):
     """(255 * skimage.restoration.denoise_wavelet(x, method='BayesShrink', mode='soft',
     wavelet=wavelet, multichannel=True, convert2ycbcr=True, wavelet_levels=levels)).astype(uint8)
     with skimage 0.14.2's clipping.  x: uint8 (N,)H,W,3 or float64 (N,)H,W,3 in [0, 1].
-    out: 'u8' | 'f32' (float result before the cast) | 'both'."""
+    out: 'u8' | 'f32' (float result before the cast) | 'both'.
+    ycc_keys: float64 x only -- the colour range random_noise_ycc reduced while writing x (the
+    same result, one read of x fewer)."""
     wv = WAVELETS.get(wavelet)
     if wv is None:
         raise ValueError(f"denoise_wavelet: unsupported wavelet {wavelet!r} (db1/haar/bior1.5)")
@@ -581,6 +626,23 @@ def denoise_wavelet(x: torch.Tensor, wavelet: str = "bior1.5", levels: Optional[
     lv = -1 if levels is None else int(levels)
     nbytes = lib.idn_wavelet_workspace_size(n, h, w, wv, lv)
     ws = _workspace(nbytes, xb.device)
+    if ycc_keys is not None:
+        if src64 is None:
+            raise ValueError("denoise_wavelet: ycc_keys applies to float64 input")
+        if (ycc_keys.dtype != torch.int64 or ycc_keys.device != xb.device
+                or tuple(ycc_keys.shape) != (n, 6)):
+            raise ValueError("denoise_wavelet: ycc_keys must be the (N, 6) int64 device tensor of "
+                             "random_noise_ycc")
+        rc = lib.idn_wavelet_denoise_ycc(src64.data_ptr(), ycc_keys.contiguous().data_ptr(),
+                                         y8.data_ptr() if y8 is not None else None,
+                                         y32.data_ptr() if y32 is not None else None,
+                                         n, h, w, wv, lv, ws.data_ptr(), nbytes, _stream())
+        _lib.check(rc, "idn_wavelet_denoise_ycc")
+        if out == "u8":
+            return _finish(y8, sq)
+        if out == "f32":
+            return _finish(y32, sq)
+        return _finish(y8, sq), _finish(y32, sq)
     rc = lib.idn_wavelet_denoise_u8(src.data_ptr() if src is not None else None,
                                     src64.data_ptr() if src64 is not None else None,
                                     y8.data_ptr() if y8 is not None else None,

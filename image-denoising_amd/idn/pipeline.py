@@ -142,6 +142,16 @@ class Preprocessor:
         return ops.random_noise(x, mode, seed=self.seed, offset=int(offsets[0]), replay=replay,
                                 out=out, **kw)
 
+    def _noise_ycc(self, x: torch.Tensor, step: ns.Step, ids: List[int]):
+        """_noise's gaussian / speckle float64 branch with the wavelet's colour range (the same
+        draws and the same image: ops.random_noise_ycc)"""
+        kw = {"var": float(step.args[0])}
+        replay = self._numpy_field(x, step.op, kw) if self.noise_rng == "numpy" else None
+        if replay is None and ids != list(range(ids[0], ids[0] + len(ids))):
+            return ops.random_noise_ycc(x, step.op, seed=self.seed, image_ids=ids, **kw)
+        return ops.random_noise_ycc(x, step.op, seed=self.seed, offset=int(ids[0]),
+                                    replay=replay, **kw)
+
     def _numpy_field(self, x: torch.Tensor, mode: str, kw) -> torch.Tensor:
         """The exact draws skimage.random_noise makes from numpy's global RandomState."""
         host = x.cpu().numpy()
@@ -212,6 +222,14 @@ class Preprocessor:
             if (nxt is None and defer and st.kind == "filter"
                     and st.op == "gaus_blur" and cur.dtype == torch.uint8):
                 return list(cur.unbind(0)), int(st.args[0])  # left to the blob builder
+            if (st.kind == "noise" and st.op in ("gaussian", "speckle") and nxt is not None
+                    and nxt.kind == "filter" and nxt.op == "wavelet" and ops.ycc_fusable(cur)):
+                # the float64 image goes straight into the wavelet (test_v0's live path): the
+                # noise kernel reduces the wavelet's colour range while it writes the image
+                cur, keys = self._noise_ycc(cur, st, ids)
+                cur = ops.denoise_wavelet(cur, nxt.args[0], nxt.args[1], ycc_keys=keys)
+                i += 2
+                continue
             if st.kind == "noise":
                 cur = self._noise(cur, st, nxt, ids, bloom)
                 if nxt is not None and nxt.kind == "cast_u8":

@@ -76,8 +76,9 @@ typedef enum idn_wavelet {
  *   3  idn_jpeg_workspace_size / idn_jpeg_decode_u8 gained `flags` before `workspace`
  *      (IDN_JPEG_TURBO); the default decode became IJG libjpeg 9d's; idn_noise_filter_u8
  *      (the fused noise -> 3x3 / 5x5 filter) was removed: compose idn_noise_u8 and the filter
- *   4  idn_abi_version added (no signature changed) */
-#define IDN_ABI_VERSION 4
+ *   4  idn_abi_version added (no signature changed)
+ *   5  idn_noise_ycc_u8 and idn_wavelet_denoise_ycc added (no signature changed) */
+#define IDN_ABI_VERSION 5
 int idn_abi_version(void);
 const char* idn_version(void);
 const char* idn_last_error(void);
@@ -146,6 +147,21 @@ int idn_noise_slots_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int
                        int c, int64_t row_stride, int kind, double p0, double p1, uint64_t seed,
                        const uint64_t* image_ids, const int64_t* slots, void* workspace,
                        size_t ws_bytes, void* stream);
+
+/* The live test path's float64 gaussian / speckle noise (random_noise(..., 'gaussian') returned as
+ * float64 straight into denoise_wavelet: lib/model/test.py:1678-1684 -> 1807-1810), fused with
+ * the wavelet's colour range: as idn_noise_u8 (kind GAUSSIAN or SPECKLE, c = 3, compact rows,
+ * out_f64 required, out_u8 nullable; the float64 Philox stream, or numpy's field in `replay`;
+ * image ids offset + i, or image_ids[i] when image_ids is non-NULL) -- the same bytes -- and per
+ * image i the fp64 min and max of skimage rgb2ycbcr's Y, Cb, Cr over out_f64, as order-preserving
+ * u64 keys in ycc_keys[6 i .. 6 i + 2] (min) and [6 i + 3 .. 6 i + 5] (max), written whole by the
+ * call, for idn_wavelet_denoise_ycc: the wavelet then does not read the float64 image an extra
+ * time for its colour range.  IDN_EUNSUPPORTED for an odd pixel count or misaligned buffers
+ * (u8 2-byte, float64 16-byte aligned). */
+int idn_noise_ycc_u8(const uint8_t* src, uint8_t* out_u8, double* out_f64, int n, int h, int w,
+                     int kind, double p0, double p1, uint64_t seed, uint64_t offset,
+                     const uint64_t* image_ids, const double* replay, uint64_t* ycc_keys,
+                     void* stream);
 
 /* The reference's own additive noises (not skimage), SURVEY §8f:
  *   IDN_NOISE_UNIFORM   p0 = high   out = img_as_float(x) + U(0, high)         (test.py:767-903)
@@ -255,6 +271,11 @@ int idn_copy_u8(const uint8_t* src, uint8_t* dst, int64_t nbytes, int policy, vo
 int idn_wavelet_denoise_u8(const uint8_t* src, const double* in_f64, uint8_t* out_u8,
                            float* out_f32, int n, int h, int w, int64_t row_stride, int wavelet,
                            int levels, void* workspace, size_t ws_bytes, void* stream);
+/* As idn_wavelet_denoise_u8 on float64 input (dense n*h*w*3) whose colour range idn_noise_ycc_u8
+ * already reduced into ycc_keys: the same outputs bit for bit, one pass over the input fewer. */
+int idn_wavelet_denoise_ycc(const double* in_f64, const uint64_t* ycc_keys, uint8_t* out_u8,
+                            float* out_f32, int n, int h, int w, int wavelet, int levels,
+                            void* workspace, size_t ws_bytes, void* stream);
 size_t idn_wavelet_workspace_size(int n, int h, int w, int wavelet, int levels);
 /* diagnostics: byte offset in the workspace of the per-image statistics blocks (256 doubles per
  * image: channel sums of squared details, sigma medians, thresholds) after a call */

@@ -102,3 +102,68 @@ def test_wavelet_batch_invariant(dev, wavelet, levels, src):
     u8_mid, f_mid = ops.denoise_wavelet(x[10:17], wavelet, levels, out="both")
     assert torch.equal(u8_mid, u8_all[10:17])
     assert torch.equal(f_mid, f_all[10:17])
+
+
+def _plain_keys(x64, wavelet, levels):
+    """the colour-range keys the wavelet computes itself (wl_color_minmax) for float64 x64"""
+    import torch
+    from idn import _lib, ops
+    n, h, w, _ = x64.shape
+    ops.denoise_wavelet(x64, wavelet, levels, out="u8")
+    off = _lib.load().idn_wavelet_stats_offset(n, h, w, ops.WAVELETS[wavelet],
+                                               -1 if levels is None else levels)
+    ws = ops._WS_CACHE[(str(x64.device), torch.cuda.current_stream(x64.device).cuda_stream)]
+    st = ws[off:off + n * 256 * 8].view(torch.int64).view(n, 256)
+    return torch.cat([st[:, 200:203], st[:, 203:206]], dim=1).cpu()
+
+
+@pytest.mark.parametrize("mode,var", [("gaussian", 0.1), ("gaussian", 1.5), ("speckle", 1.0)])
+@pytest.mark.parametrize("form", ["offset", "ids", "replay"])
+def test_noise_ycc_matches_unfused(dev, mode, var, form):
+    """idn_noise_ycc_u8 writes the float64 image random_noise(out='f64') writes (the same draws,
+    bit for bit), and its colour-range keys equal the ones the wavelet's own min / max pass
+    reduces from that image; the wavelet fed those keys gives the unfused outputs bit for bit"""
+    import torch
+    from idn import ops
+    imgs = textured(3, 600, 1000, seed=19)
+    x = torch.from_numpy(imgs).cuda()
+    kw = {"var": var, "seed": 7}
+    if form == "offset":
+        kw["offset"] = 4
+    elif form == "ids":
+        kw["image_ids"] = [9, 2, 40]
+    else:
+        rs = np.random.RandomState(3)
+        kw["replay"] = torch.from_numpy(rs.normal(0.0, var ** 0.5, imgs.shape)).cuda()
+    ref = ops.random_noise(x, mode, out="f64", **kw)
+    got, keys = ops.random_noise_ycc(x, mode, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    for wavelet, levels in (("bior1.5", None), ("db1", 3)):
+        want_keys = _plain_keys(ref, wavelet, levels)
+        assert torch.equal(keys.cpu(), want_keys), wavelet
+        u8a, fa = ops.denoise_wavelet(ref, wavelet, levels, out="both")
+        u8b, fb = ops.denoise_wavelet(got, wavelet, levels, out="both", ycc_keys=keys)
+        torch.cuda.synchronize()
+        assert torch.equal(u8a, u8b) and torch.equal(fa, fb), wavelet
+
+
+def test_live_path_uses_the_fused_pair(dev, monkeypatch):
+    """Preprocessor on test_v0 'gaussian_wavelet_var*' takes random_noise_ycc -> denoise_wavelet
+    with the keys; each image's output equals the two-step composition with its drawn level"""
+    import torch
+    from idn import ops
+    from idn.pipeline import Preprocessor
+    x = torch.from_numpy(textured(3, 600, 1000, seed=23)).cuda()
+    calls = []
+    orig = ops.random_noise_ycc
+    monkeypatch.setattr(ops, "random_noise_ycc", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    pre = Preprocessor("gaussian_wavelet_var0.1", "test_v0", seed=3, rng=random.Random(5))
+    outs, plans = pre(x, image_ids=[0, 1, 2])
+    assert calls, "the fused noise kernel did not run"
+    for i, (o, p) in enumerate(zip(outs, plans)):
+        assert p.steps[0].op == "gaussian" and p.steps[1].op == "wavelet"
+        f = ops.random_noise(x[i:i + 1], "gaussian", var=float(p.steps[0].args[0]), seed=3,
+                             offset=i, out="f64")
+        want = ops.denoise_wavelet(f, p.steps[1].args[0], p.steps[1].args[1])
+        assert torch.equal(o, want[0] if want.dim() == 4 else want), i
