@@ -370,11 +370,11 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 }
 
 // ---- device: entropy decoding -----------------------------------------------------------------
-// Stage 1, jpeg_unstuff_kernel (one workgroup per image): the entropy-coded segment without its
+// Stage 1, jpeg_unstuff_count / _write / _final (16 KiB tiles): the entropy-coded segment without its
 // stuffed 0x00 bytes, fill bytes and RST markers, and the bit offset where each restart interval
 // starts.  The decoders then read a plain big-endian bit string.
 //
-// Stage 2, images without restart markers: the scan is cut into JPG_CHUNK-bit chunks, one thread
+// Stage 2, images without restart markers: the scan is cut into chunk_bits-bit chunks, one thread
 // each, decoded in parallel by self-synchronisation (Huffman codes and the block structure
 // resynchronise: from an arbitrary start state a trajectory joins the true one after ~0.8 kbit
 // median, 9 kbit max on the test images).  A decoder state is (bit position, block of the MCU,
@@ -386,8 +386,20 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 //   prefix   per image: each chunk's first block index and DC predictors
 //   write    every chunk again from its exact start state, writing coefficient blocks
 // Images with restart markers: one thread per restart interval (true start state known).
-constexpr int JPG_CHUNK = 4096;  // default bits per chunk (the ABI's flags may set another; measured
-                                 // 256 x 600x1000 q90: 2048 11.9, 4096 10.4, 8192 11.8 ms)
+// Chunk size: the ABI's flags may set one; the default depends on the batch (jpeg_plan)
+// Checkpoints (round 5): every pass records, per chunk and JPG_SUB-bit sub-chunk, the decoder state
+// at the first symbol that starts at or after the sub-chunk's first bit and the counts (blocks, DC
+// sums) from the chunk start to it.  A later pass that decodes the chunk from a new start state
+// stops at the first checkpoint where its state equals the recorded one -- from there the
+// trajectory is the recorded one, so the end state is and the counts shift by the difference at
+// that checkpoint (a chunk's trajectories typically join within ~1 kbit, so the B passes no
+// longer decode whole chunks) -- and the write pass runs one thread per sub-chunk from the final
+// checkpoints: 8x the threads of one per chunk, each an eighth as long (a single image's write
+// pass was 0.76 ms of serial decoding per thread).
+constexpr uint32_t JPG_SUB = 512;
+__host__ __device__ __forceinline__ uint32_t jpg_nsub(uint32_t chunk_bits) {
+  return (chunk_bits + JPG_SUB - 1) / JPG_SUB;
+}
 
 __device__ __forceinline__ uint32_t jpg_be32(const uint8_t* __restrict__ p) {
   const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
@@ -634,99 +646,173 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
   return jpg_state(pos, ph, z);
 }
 
-// stage 1: unstuff (one 1024-thread workgroup per image, 16-byte tiles per thread)
-// (one workgroup per JpegDev, or per JpegScanDev of the scan path: the same fields)
+// stage 1: unstuff, in 16 KiB tiles of the segment (1024 threads x 16 bytes), every tile its own
+// workgroup (one workgroup per image walked its tiles in sequence: 0.28 ms for a single 600x1000
+// file): count the tile's kept bytes and RST markers, then each tile writes from the sum of the
+// tiles before it, then per segment the length, the zero padding and the missing intervals.
+// (DESC: a JpegDev per image, or a JpegScanDev per scan of the scan path: the same fields)
+constexpr uint32_t UNS_TILE = 1024 * 16;
+
+// the thread's 16 bytes [i0, i0 + 16): bit k of keep = byte i0 + k is data, of rstm = a RST marker
+// ends at byte i0 + k
+// (the segment starts 16-byte aligned and its buffer is padded to whole 16-byte groups: one
+// 16-byte load per thread, plus the bytes either side)
+__device__ __forceinline__ void unstuff_masks(const uint8_t* __restrict__ in, uint32_t n,
+                                              uint32_t i0, uint32_t& keep, uint32_t& rstm,
+                                              uint32_t (&w)[4]) {
+  keep = 0;
+  rstm = 0;
+  const uint4 v = *reinterpret_cast<const uint4*>(in + i0);
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+  uint32_t pv = i0 > 0 ? in[i0 - 1] : 0u;
+  const uint32_t after = i0 + 16 < n ? in[i0 + 16] : 0u;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t i = i0 + k;
+    const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+    const uint32_t nx = k < 15 ? (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu : after;
+    bool kp;
+    if (pv == 0xFF && b == 0x00) {
+      kp = false;  // stuffing
+    } else if (pv == 0xFF && b >= 0xD0 && b <= 0xD7) {
+      kp = false;  // RST marker code
+      if (i < n) rstm |= 1u << k;
+    } else if (b == 0xFF) {
+      kp = i + 1 < n && nx == 0x00;  // data 0xFF (stuffed); else fill / marker prefix
+    } else {
+      kp = true;
+    }
+    if (kp && i < n) keep |= 1u << k;
+    pv = b;
+  }
+}
+
 template <typename DESC>
-__global__ __launch_bounds__(1024) void jpeg_unstuff_kernel(const DESC* __restrict__ imgs,
-                                                            const uint8_t* __restrict__ scans,
-                                                            uint8_t* __restrict__ ub,
-                                                            uint32_t* __restrict__ ivstart,
-                                                            uint32_t* __restrict__ ublen) {
-  __shared__ uint32_t wsum[16], carry_s, rst_s;
-  const DESC& D = imgs[blockIdx.x];
-  const uint8_t* in = scans + D.scan_off;
-  uint8_t* out = ub + D.ub_off;
-  const uint32_t n = D.scan_len;
-  if (threadIdx.x == 0) {
-    carry_s = 0;
-    rst_s = 0;
-    ivstart[D.iv_off] = 0;
+__global__ __launch_bounds__(1024) void jpeg_unstuff_count(const DESC* __restrict__ imgs,
+                                                           const uint8_t* __restrict__ scans,
+                                                           uint2* __restrict__ tcnt, int mt,
+                                                           uint32_t* __restrict__ ivstart) {
+  const DESC& D = imgs[blockIdx.y];
+  if (blockIdx.x == 0) {
+    // intervals whose RST marker is missing (truncated / corrupt file) must not start at
+    // garbage: marked here, set to the end of the data by jpeg_unstuff_final
+    if (threadIdx.x == 0) ivstart[D.iv_off] = 0;
+    for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x)
+      ivstart[D.iv_off + k] = ~0u;
   }
-  // intervals whose RST marker is missing (truncated / corrupt file) must not start at garbage:
-  // marked here, set to the end of the data below
-  for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x) ivstart[D.iv_off + k] = ~0u;
-  __syncthreads();
+  const uint32_t base = blockIdx.x * UNS_TILE;
+  if (base >= D.scan_len) return;  // uniform
+  uint32_t keep = 0, rstm = 0, w[4];
+  if (base + threadIdx.x * 16 < D.scan_len)
+    unstuff_masks(scans + D.scan_off, D.scan_len, base + threadIdx.x * 16, keep, rstm, w);
+  uint32_t a = __popc(keep), r = __popc(rstm);
+  for (int o = 32; o > 0; o >>= 1) {
+    a += (uint32_t)__shfl_xor((int)a, o);
+    r += (uint32_t)__shfl_xor((int)r, o);
+  }
+  __shared__ uint32_t wa[16], wr[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (uint32_t base = 0; base < n; base += 1024 * 16) {
-    const uint32_t i0 = base + threadIdx.x * 16;
-    uint32_t keep = 0;  // bit k: byte i0 + k is data
-    uint32_t rstm = 0;  // bit k: a RST marker ends at byte i0 + k
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t i = i0 + k;
-      if (i >= n) break;
-      const uint32_t b = in[i];
-      const uint32_t pv = i > 0 ? in[i - 1] : 0u;
-      bool kp;
-      if (pv == 0xFF && b == 0x00) {
-        kp = false;  // stuffing
-      } else if (pv == 0xFF && b >= 0xD0 && b <= 0xD7) {
-        kp = false;  // RST marker code
-        rstm |= 1u << k;
-      } else if (b == 0xFF) {
-        kp = i + 1 < n && in[i + 1] == 0x00;  // data 0xFF (stuffed); else fill / marker prefix
-      } else {
-        kp = true;
-      }
-      if (kp) keep |= 1u << k;
-    }
-    // block-wide exclusive scan of kept-byte counts
-    const uint32_t cntk = __popc(keep);
-    uint32_t inc = cntk;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
-      if (lane >= o) inc += t;
-    }
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    uint32_t wbase = 0;
-    for (int k = 0; k < wv; ++k) wbase += wsum[k];
-    uint32_t total = 0;
-    for (int k = 0; k < 16; ++k) total += wsum[k];
-    uint32_t o = carry_s + wbase + inc - cntk;
-    // RST markers: the next interval starts at the unstuffed position after this byte
-    uint32_t orank = 0;
-    {
-      const uint32_t nr = __popc(rstm);
-      uint32_t rinc = nr;
-      for (int q = 1; q < 64; q <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)rinc, q);
-        if (lane >= q) rinc += t;
-      }
-      __syncthreads();
-      if (lane == 63) wsum[wv] = rinc;
-      __syncthreads();
-      uint32_t rbase = 0;
-      for (int k = 0; k < wv; ++k) rbase += wsum[k];
-      orank = rst_s + rbase + rinc - nr;
-      uint32_t rt = 0;
-      for (int k = 0; k < 16; ++k) rt += wsum[k];
-      __syncthreads();
-      if (threadIdx.x == 0) rst_s += rt;
-    }
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t i = i0 + k;
-      if (i >= n) break;
-      if (keep >> k & 1u) out[o++] = in[i];
-      if ((rstm >> k & 1u) && orank + 1 < (uint32_t)D.nintervals)
-        ivstart[D.iv_off + 1 + orank++] = o * 8u;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) carry_s += total;
-    __syncthreads();
+  if (lane == 0) {
+    wa[wv] = a;
+    wr[wv] = r;
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t ta = 0, tr = 0;
+    for (int k = 0; k < 16; ++k) {
+      ta += wa[k];
+      tr += wr[k];
+    }
+    tcnt[(size_t)blockIdx.y * mt + blockIdx.x] = make_uint2(ta, tr);
+  }
+}
+
+template <typename DESC>
+__global__ __launch_bounds__(1024) void jpeg_unstuff_write(const DESC* __restrict__ imgs,
+                                                           const uint8_t* __restrict__ scans,
+                                                           const uint2* __restrict__ tcnt, int mt,
+                                                           uint8_t* __restrict__ ub,
+                                                           uint32_t* __restrict__ ivstart) {
+  const DESC& D = imgs[blockIdx.y];
+  const uint32_t base = blockIdx.x * UNS_TILE;
+  if (base >= D.scan_len) return;  // uniform
+  __shared__ uint32_t wsum[16], wrst[16], base_s[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // kept bytes and RST markers of the tiles before this one
+  if (wv == 0) {
+    uint32_t a = 0, r = 0;
+    for (int k = lane; k < (int)blockIdx.x; k += 64) {
+      const uint2 c = tcnt[(size_t)blockIdx.y * mt + k];
+      a += c.x;
+      r += c.y;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      a += (uint32_t)__shfl_xor((int)a, o);
+      r += (uint32_t)__shfl_xor((int)r, o);
+    }
+    if (lane == 0) {
+      base_s[0] = a;
+      base_s[1] = r;
+    }
+  }
+  const uint8_t* in = scans + D.scan_off;
+  const uint32_t i0 = base + threadIdx.x * 16;
+  uint32_t keep = 0, rstm = 0, w[4] = {0u, 0u, 0u, 0u};
+  if (i0 < D.scan_len) unstuff_masks(in, D.scan_len, i0, keep, rstm, w);
+  // block-wide exclusive scans of the kept-byte and RST-marker counts
+  const uint32_t cntk = __popc(keep), nr = __popc(rstm);
+  uint32_t inc = cntk, rinc = nr;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)inc, o), q = (uint32_t)__shfl_up((int)rinc, o);
+    if (lane >= o) {
+      inc += t;
+      rinc += q;
+    }
+  }
+  if (lane == 63) {
+    wsum[wv] = inc;
+    wrst[wv] = rinc;
+  }
+  __syncthreads();
+  uint32_t wbase = 0, rbase = 0;
+  for (int k = 0; k < wv; ++k) {
+    wbase += wsum[k];
+    rbase += wrst[k];
+  }
+  uint32_t o = base_s[0] + wbase + inc - cntk;
+  uint32_t orank = base_s[1] + rbase + rinc - nr;
+  uint8_t* out = ub + D.ub_off;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (keep >> k & 1u) out[o++] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    // RST markers: the next interval starts at the unstuffed position after this byte
+    if ((rstm >> k & 1u) && orank + 1 < (uint32_t)D.nintervals)
+      ivstart[D.iv_off + 1 + orank++] = o * 8u;
+  }
+}
+
+template <typename DESC>
+__global__ __launch_bounds__(256) void jpeg_unstuff_final(const DESC* __restrict__ imgs,
+                                                          const uint2* __restrict__ tcnt, int mt,
+                                                          uint8_t* __restrict__ ub,
+                                                          uint32_t* __restrict__ ivstart,
+                                                          uint32_t* __restrict__ ublen) {
+  const DESC& D = imgs[blockIdx.x];
+  __shared__ uint32_t len_s;
+  if (threadIdx.x < 64) {
+    const int ntiles = (int)((D.scan_len + UNS_TILE - 1) / UNS_TILE);
+    uint32_t a = 0;
+    for (int k = threadIdx.x; k < ntiles; k += 64) a += tcnt[(size_t)blockIdx.x * mt + k].x;
+    for (int o = 32; o > 0; o >>= 1) a += (uint32_t)__shfl_xor((int)a, o);
+    if (threadIdx.x == 0) len_s = a;
+  }
+  __syncthreads();
+  const uint32_t len = len_s;
   // zero padding behind the data (the bit readers prefetch up to 40 bytes ahead)
-  const uint32_t len = carry_s;
-  if (threadIdx.x < 64) out[len + threadIdx.x] = 0;
+  if (threadIdx.x < 64) ub[D.ub_off + len + threadIdx.x] = 0;
   if (threadIdx.x == 0) ublen[blockIdx.x] = len;
   for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x)
     if (ivstart[D.iv_off + k] == ~0u) ivstart[D.iv_off + k] = len * 8u;
@@ -747,7 +833,9 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
                                                        ChunkOut* __restrict__ cnt,
                                                        uint32_t* __restrict__ changed,
                                                        const uint8_t* __restrict__ chg_prev,
-                                                       uint8_t* __restrict__ chg_next, int all) {
+                                                       uint8_t* __restrict__ chg_next, int all,
+                                                       uint64_t* __restrict__ ck_st,
+                                                       ChunkOut* __restrict__ ck_co) {
   __shared__ JpegLds T;
   const JpegDev& D = imgs[blockIdx.y];
   if (D.restart || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
@@ -770,17 +858,49 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
   if (t == 0) st = 0;
   else if (PASS_A) st = jpg_state(b0, 0, 0);
   else st = prev[D.ch_off + t - 1];
+  const uint32_t nsub = jpg_nsub(D.chunk_bits);
+  uint64_t* cks = ck_st + (size_t)(D.ch_off + t) * nsub;
+  ChunkOut* ckc = ck_co + (size_t)(D.ch_off + t) * nsub;
   ChunkOut co{0u, {0, 0, 0}};
   int pred[3] = {0, 0, 0};
-  // a start state past the chunk (the predecessor ran over it) ends where it starts
   const JpgConst K = jpg_const(D);
-  const uint64_t e = ((uint32_t)st >= b1) ? st
-                                         : jpg_run<false>(K, T, ub + D.ub_off, st, b1, &co, 0, pred, nullptr);
+  uint64_t e = st;
+  for (uint32_t j = 0; j < nsub; ++j) {
+    if (!PASS_A && e == cks[j]) {
+      // joined the trajectory recorded by this chunk's last decode: its end state stands, the
+      // counts from here on shift by the difference at this checkpoint
+      const ChunkOut old = ckc[j];
+      const int32_t dn = (int32_t)(co.nblk - old.nblk);
+      const int32_t d0 = co.dcsum[0] - old.dcsum[0], d1 = co.dcsum[1] - old.dcsum[1],
+                    d2 = co.dcsum[2] - old.dcsum[2];
+      for (uint32_t k = j; k < nsub; ++k) {
+        ChunkOut c = ckc[k];
+        c.nblk += (uint32_t)dn;
+        c.dcsum[0] += d0;
+        c.dcsum[1] += d1;
+        c.dcsum[2] += d2;
+        ckc[k] = c;
+      }
+      const ChunkOut tot = cnt[D.ch_off + t];
+      co.nblk = tot.nblk + (uint32_t)dn;
+      co.dcsum[0] = tot.dcsum[0] + d0;
+      co.dcsum[1] = tot.dcsum[1] + d1;
+      co.dcsum[2] = tot.dcsum[2] + d2;
+      e = prev[D.ch_off + t];
+      break;
+    }
+    cks[j] = e;
+    ckc[j] = co;
+    const uint32_t sub_end = min(b0 + (j + 1) * JPG_SUB, b1);
+    // a state past the sub-chunk (the predecessor ran over it) ends where it starts
+    if ((uint32_t)e < sub_end)
+      e = jpg_run<false>(K, T, ub + D.ub_off, e, sub_end, &co, 0, pred, nullptr);
+  }
   next[D.ch_off + t] = e;
+  cnt[D.ch_off + t] = co;
   if (PASS_A) {
     chg_next[D.ch_off + t] = 1;
   } else {
-    cnt[D.ch_off + t] = co;
     const bool ch = e != prev[D.ch_off + t];
     chg_next[D.ch_off + t] = ch ? 1 : 0;
     if (ch) changed[0] = 1u;
@@ -829,45 +949,50 @@ __global__ __launch_bounds__(256) void jpeg_prefix_kernel(const JpegDev* __restr
   }
 }
 
-// stage 2d: write pass.  Chunks of images without restart markers (grid.x over chunks), or
-// restart intervals (one thread each) of images with them.
+// stage 2d: write pass.  Sub-chunks of images without restart markers (grid.x over chunks x
+// sub-chunks, from the final checkpoints), or restart intervals (one thread each) of images with
+// them.
 __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restrict__ imgs,
                                                         const uint8_t* __restrict__ ub,
                                                         const uint32_t* __restrict__ ublen,
                                                         const uint32_t* __restrict__ ivstart,
-                                                        const uint64_t* __restrict__ states,
+                                                        const uint64_t* __restrict__ ck_st,
+                                                        const ChunkOut* __restrict__ ck_co,
                                                         const ChunkOut* __restrict__ start,
                                                         int16_t* __restrict__ coef) {
   __shared__ JpegLds T;
   const JpegDev& D = imgs[blockIdx.y];
-  const uint32_t nitems = D.restart ? (uint32_t)D.nintervals : D.nchunks;
+  const uint32_t nsub = jpg_nsub(D.chunk_bits);
+  const uint32_t nitems = D.restart ? (uint32_t)D.nintervals : D.nchunks * nsub;
   if (blockIdx.x * 64 >= nitems) return;  // uniform per workgroup
   jpg_load_tables(T, D);
   __syncthreads();
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= nitems) return;
+  const uint32_t u = blockIdx.x * 64 + threadIdx.x;
+  if (u >= nitems) return;
   const uint32_t nbits = ublen[blockIdx.y] * 8u;
   int pred[3] = {0, 0, 0};
   uint64_t st;
   uint32_t b1, dc_limit = 0xFFFFFFFFu;
   int32_t blk;
-  if (D.restart) {  // interval t: restart MCUs from its first bit, DC predictors reset
-    const uint32_t b0 = min(ivstart[D.iv_off + t], nbits);
-    b1 = t + 1 < nitems ? min(ivstart[D.iv_off + t + 1], nbits) : nbits;
+  if (D.restart) {  // interval u: restart MCUs from its first bit, DC predictors reset
+    const uint32_t b0 = min(ivstart[D.iv_off + u], nbits);
+    b1 = u + 1 < nitems ? min(ivstart[D.iv_off + u + 1], nbits) : nbits;
     // stop after the interval's MCUs: the bits behind them are the encoder's padding (1s)
-    const uint32_t mcu0 = t * (uint32_t)D.restart;
+    const uint32_t mcu0 = u * (uint32_t)D.restart;
     dc_limit = min((uint32_t)D.restart, (uint32_t)(D.mcux * D.mcuy) - mcu0) * D.bpm;
     st = jpg_state(b0, 0, 0);
     blk = (int32_t)(mcu0 * D.bpm) - 1;
-  } else {  // chunk t from its exact start state, first block index and DC predictors
+  } else {  // sub-chunk j of chunk t from its checkpoint: state, first block, DC predictors
+    const uint32_t t = u / nsub, j = u - t * nsub;
     const uint32_t b0 = min(t * D.chunk_bits, nbits);
-    b1 = min(b0 + D.chunk_bits, nbits);
-    st = t == 0 ? 0ull : states[D.ch_off + t - 1];
-    const ChunkOut s0 = start[D.ch_off + t];
-    pred[0] = s0.dcsum[0];
-    pred[1] = s0.dcsum[1];
-    pred[2] = s0.dcsum[2];
-    blk = (int32_t)s0.nblk - 1;
+    b1 = min(min(b0 + D.chunk_bits, nbits), b0 + (j + 1) * JPG_SUB);
+    const size_t k = (size_t)(D.ch_off + t) * nsub + j;
+    st = ck_st[k];
+    const ChunkOut c = ck_co[k], s0 = start[D.ch_off + t];
+    pred[0] = s0.dcsum[0] + c.dcsum[0];
+    pred[1] = s0.dcsum[1] + c.dcsum[1];
+    pred[2] = s0.dcsum[2] + c.dcsum[2];
+    blk = (int32_t)(s0.nblk + c.nblk) - 1;
   }
   if ((uint32_t)st >= b1) return;
   ChunkOut dummy{0u, {0, 0, 0}};
@@ -1382,18 +1507,20 @@ struct JpegPlan {
   std::vector<JpegScanDev> scans;   // the scan path's scans, image by image
   std::vector<size_t> scan_src;     // their first byte in the file
   uint64_t scan_bytes = 0, nblk = 0, plane_bytes = 0, ub_bytes = 0;
-  uint32_t nintervals = 0, nchunks = 0, max_items = 1;
+  uint32_t nintervals = 0, nchunks = 0, max_items = 1, max_items_w = 1, nsub = 1;
+  int mt_img = 1, mt_scan = 1;  // most unstuffing tiles of an image / of a scan
   bool any_chunked = false;
   bool scales[2][2] = {};  // IDCT output scales present: [sv - 1][sh - 1]
   size_t off_imgs = 0, off_blkend = 0, off_scans = 0, off_scan = 0, off_coef = 0, off_planes = 0;
   size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_ublen_s = 0, off_s0 = 0, off_s1 = 0,
-         off_cnt = 0, off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, total = 0;
+         off_cnt = 0, off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, off_ck_st = 0,
+         off_ck_co = 0, off_tcnt = 0, total = 0;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // flags: IDN_JPEG_TURBO selects libjpeg-turbo's decode (else libjpeg 9d's); bits 8..23 = entropy
-// chunk size in bits (0: the default JPG_CHUNK; else a multiple of 64, >= 512)
+// chunk size in bits (0: the batch-dependent default; else a multiple of 64, >= 512)
 static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int h, int w,
                      int flags, JpegPlan& P, std::string* err, bool tables = true) {
   const bool turbo = (flags & IDN_JPEG_TURBO) != 0;
@@ -1403,7 +1530,7 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     if (err) *err = "bad flags";
     return IDN_EINVAL;
   }
-  const uint32_t chunk_bits = chunk_req ? chunk_req : (uint32_t)JPG_CHUNK;
+  uint64_t chunked_bits = 0;  // entropy bits of the images the chunked decoder takes
   P.dev.assign(n, JpegDev{});
   P.blk_end.assign(n, 0);
   P.scan_begin.assign(n, 0);
@@ -1505,8 +1632,6 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       D.nintervals = 1;
       P.nintervals += 1;
       D.restart = 0;
-      D.ch_off = P.nchunks;
-      D.chunk_bits = chunk_bits;
       D.nchunks = 0;
       D.scan0 = (uint32_t)P.scans.size();
       D.nscan = (uint32_t)J.scans.size();
@@ -1573,14 +1698,30 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     P.ub_bytes += (D.scan_len + 64 + 15) & ~15u;
     D.iv_off = P.nintervals;
     P.nintervals += (uint32_t)D.nintervals;
+    if (!D.restart) chunked_bits += (uint64_t)D.scan_len * 8;
+  }
+  // entropy chunks (the self-synchronising decoder's threads).  Default size: about 100k chunks
+  // in the batch, within [1536, 6144] bits in steps of 512 -- a single 600x1000 q90 file decodes
+  // in 1.41 ms at 1536-bit chunks against 1.62 at 4096, a batch of 256 in 7.07 ms at 6144
+  // against 7.27 (profiles/r05/jpeg/chunk_sweep.txt): short chunks shorten every pass when the
+  // batch cannot fill the chip, long ones need fewer B passes when it can
+  const uint32_t chunk_bits =
+      chunk_req ? chunk_req
+                : (uint32_t)std::min<uint64_t>(
+                      6144, std::max<uint64_t>(1536, (chunked_bits / 100000 + 511) / 512 * 512));
+  for (int i = 0; i < n; ++i) {
+    JpegDev& D = P.dev[i];
     D.ch_off = P.nchunks;
     D.chunk_bits = chunk_bits;
+    if (D.nscan) continue;  // the scan path: no chunks
     D.nchunks = D.restart ? 0u
                           : (uint32_t)(((uint64_t)D.scan_len * 8 + D.chunk_bits - 1) / D.chunk_bits);
     if (D.nchunks == 0 && !D.restart) D.nchunks = 1;
     P.nchunks += D.nchunks;
     P.any_chunked |= D.restart == 0;
     P.max_items = std::max(P.max_items, std::max(D.nchunks, (uint32_t)D.nintervals));
+    P.max_items_w = std::max(P.max_items_w, std::max(D.nchunks * jpg_nsub(chunk_bits),
+                                                     (uint32_t)D.nintervals));
   }
   P.off_imgs = 0;
   P.off_blkend = align256(P.off_imgs + sizeof(JpegDev) * (size_t)n);
@@ -1599,7 +1740,16 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
   P.off_flag = align256(P.off_start + sizeof(ChunkOut) * (size_t)P.nchunks);
   P.off_chg0 = align256(P.off_flag + 256);
   P.off_chg1 = align256(P.off_chg0 + (size_t)P.nchunks);
-  P.total = align256(P.off_chg1 + (size_t)P.nchunks);
+  P.nsub = jpg_nsub(chunk_bits);
+  P.off_ck_st = align256(P.off_chg1 + (size_t)P.nchunks);
+  P.off_ck_co = align256(P.off_ck_st + sizeof(uint64_t) * (size_t)P.nchunks * P.nsub);
+  for (const JpegDev& D : P.dev)
+    P.mt_img = std::max(P.mt_img, (int)((D.scan_len + UNS_TILE - 1) / UNS_TILE));
+  for (const JpegScanDev& S : P.scans)
+    P.mt_scan = std::max(P.mt_scan, (int)((S.scan_len + UNS_TILE - 1) / UNS_TILE));
+  P.off_tcnt = align256(P.off_ck_co + sizeof(ChunkOut) * (size_t)P.nchunks * P.nsub);
+  const size_t ntc = std::max((size_t)n * P.mt_img, P.scans.size() * (size_t)P.mt_scan);
+  P.total = align256(P.off_tcnt + sizeof(uint2) * ntc);
   return IDN_OK;
 }
 
@@ -1716,38 +1866,64 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   ChunkOut* cnt = reinterpret_cast<ChunkOut*>(ws + P.off_cnt);
   ChunkOut* cstart = reinterpret_cast<ChunkOut*>(ws + P.off_start);
   uint32_t* flag = reinterpret_cast<uint32_t*>(ws + P.off_flag);
+  uint64_t* ck_st = reinterpret_cast<uint64_t*>(ws + P.off_ck_st);
+  ChunkOut* ck_co = reinterpret_cast<ChunkOut*>(ws + P.off_ck_co);
   uint8_t* chg[2] = {reinterpret_cast<uint8_t*>(ws + P.off_chg0),
                      reinterpret_cast<uint8_t*>(ws + P.off_chg1)};
-  hipLaunchKernelGGL(jpeg_unstuff_kernel<JpegDev>, dim3(n), dim3(1024), 0, st, dimg,
-                     ws + P.off_scan, ub, ivs, ublen);
+  uint2* tcnt = reinterpret_cast<uint2*>(ws + P.off_tcnt);
+  {
+    const dim3 g((unsigned)P.mt_img, (unsigned)n);
+    hipLaunchKernelGGL(jpeg_unstuff_count<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
+                       tcnt, P.mt_img, ivs);
+    hipLaunchKernelGGL(jpeg_unstuff_write<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
+                       tcnt, P.mt_img, ub, ivs);
+    hipLaunchKernelGGL(jpeg_unstuff_final<JpegDev>, dim3(n), dim3(256), 0, st, dimg, tcnt,
+                       P.mt_img, ub, ivs, ublen);
+  }
   const JpegScanDev* dscan = reinterpret_cast<const JpegScanDev*>(ws + P.off_scans);
-  if (!P.scans.empty())
-    hipLaunchKernelGGL(jpeg_unstuff_kernel<JpegScanDev>, dim3((unsigned)P.scans.size()), dim3(1024),
-                       0, st, dscan, ws + P.off_scan, ub, ivs,
-                       reinterpret_cast<uint32_t*>(ws + P.off_ublen_s));
+  if (!P.scans.empty()) {
+    // (after the images' unstuffing: the tile counts reuse the same array)
+    const unsigned ns = (unsigned)P.scans.size();
+    const dim3 g((unsigned)P.mt_scan, ns);
+    hipLaunchKernelGGL(jpeg_unstuff_count<JpegScanDev>, g, dim3(1024), 0, st, dscan,
+                       ws + P.off_scan, tcnt, P.mt_scan, ivs);
+    hipLaunchKernelGGL(jpeg_unstuff_write<JpegScanDev>, g, dim3(1024), 0, st, dscan,
+                       ws + P.off_scan, tcnt, P.mt_scan, ub, ivs);
+    hipLaunchKernelGGL(jpeg_unstuff_final<JpegScanDev>, dim3(ns), dim3(256), 0, st, dscan, tcnt,
+                       P.mt_scan, ub, ivs, reinterpret_cast<uint32_t*>(ws + P.off_ublen_s));
+  }
   const dim3 gitems((P.max_items + 63) / 64, n);
   int cur = 0;
   if (P.any_chunked) {
-    // pass A, then pass B until no chunk's end state changes (typically twice)
+    // pass A, then pass B until no chunk's end state changes (typically 3 changing passes and
+    // one that confirms).  The B passes are launched JPG_BROUND at a time with one flag each and
+    // one host read per round: a pass after convergence only copies the states through (no
+    // chunk's start changed), so the passes beyond it cost a launch each -- the host round trip
+    // per pass (a D2H read and a stream synchronisation) was ~60 us of a single file's decode
+    constexpr int JPG_BROUND = 4;
     hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
-                       S[0], cnt, flag, chg[1], chg[0], 1);
-    for (uint32_t it = 0;; ++it) {
-      if (hipMemsetAsync(flag, 0, 4, st) != hipSuccess)
+                       S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co);
+    for (uint32_t it = 0;; it += JPG_BROUND) {
+      if (hipMemsetAsync(flag, 0, 4 * JPG_BROUND, st) != hipSuccess)
         return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
-      hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
-                         S[cur], S[cur ^ 1], cnt, flag, chg[cur], chg[cur ^ 1], it == 0 ? 1 : 0);
-      cur ^= 1;
-      uint32_t changed = 0;
-      if (hipMemcpyAsync(&changed, flag, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      for (int k = 0; k < JPG_BROUND; ++k) {
+        hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
+                           S[cur], S[cur ^ 1], cnt, flag + k, chg[cur], chg[cur ^ 1],
+                           it + k == 0 ? 1 : 0, ck_st, ck_co);
+        cur ^= 1;
+      }
+      uint32_t changed[JPG_BROUND] = {};
+      if (hipMemcpyAsync(changed, flag, sizeof(changed), hipMemcpyDeviceToHost, st) != hipSuccess ||
           hipStreamSynchronize(st) != hipSuccess)
         return set_error(IDN_EHIP, "idn_jpeg_decode_u8: sync pass failed");
-      if (!changed) break;
+      if (!changed[JPG_BROUND - 1]) break;  // the round's last pass changed nothing
       if (it > P.max_items + 2)
         return set_error(IDN_EHIP, "idn_jpeg_decode_u8: entropy decoding did not converge");
     }
     hipLaunchKernelGGL(jpeg_prefix_kernel, dim3(n), dim3(256), 0, st, dimg, cnt, cstart, n);
   }
-  hipLaunchKernelGGL(jpeg_write_kernel, gitems, dim3(64), 0, st, dimg, ub, ublen, ivs, S[cur],
+  const dim3 gwrite((P.max_items_w + 63) / 64, n);
+  hipLaunchKernelGGL(jpeg_write_kernel, gwrite, dim3(64), 0, st, dimg, ub, ublen, ivs, ck_st, ck_co,
                      cstart, coef);
   if (!P.scans.empty())
     hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, coef);

@@ -343,7 +343,8 @@ int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int*
  * libjpeg 9's scaled 16x16 / 16x8 IDCT for 4:2:0 / 4:2:2 chroma (no upsampling pass), libjpeg 9's
  * YCbCr tables.  IDN_JPEG_TURBO: libjpeg-turbo's decode (8x8 IDCT, fancy h2v1 / h2v2
  * upsampling), what a turbo-linked OpenCV or PIL produce.  Bits 8..23: entropy chunk size in bits
- * for the self-synchronising decoder (0 = default 4096; else a multiple of 64, >= 512; does not
+ * for the self-synchronising decoder (0 = the default: ~100k chunks per batch, 1536..6144 bits;
+ * else a multiple of 64, >= 512; does not
  * change the output). */
 #define IDN_JPEG_TURBO 1
 /* device workspace for decoding these files with these flags (0 if any is unsupported) */

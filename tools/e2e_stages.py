@@ -64,12 +64,13 @@ def main():
     torch.cuda.synchronize()
     whole = (time.perf_counter() - t0) * 1e3 / args.iters
     # stages
-    orig = (idn_io.imread_gpu, ops.random_noise, ops.denoise_wavelet, ops.blob_from_f64,
-            blobs.im_list_to_blob)
+    orig = (idn_io.imread_gpu, ops.random_noise_ycc, ops.denoise_wavelet, ops.blob,
+            blobs.im_list_to_blob, ops.random_noise)
     idn_io.imread_gpu = timed("decode (file read + jpeg_info + GPU decode)", orig[0])
-    ops.random_noise = timed("noise (gaussian, float64 out)", orig[1])
+    ops.random_noise_ycc = timed("noise (gaussian, float64 out, fused colour range)", orig[1])
+    ops.random_noise = timed("noise (unfused)", orig[5])
     ops.denoise_wavelet = timed("wavelet (bior1.5 on float64)", orig[2])
-    ops.blob_from_f64 = timed("blob (prep_im_for_blob, float64 -> float32)", orig[3])
+    ops.blob = timed("blob (prep_im_for_blob: u8 -> float32 - means)", orig[3])
     ilb = orig[4]
 
     def im_list_to_blob(ims, as_tensor=False):
