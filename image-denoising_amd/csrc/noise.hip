@@ -19,6 +19,7 @@
 //
 // Also: periodic noise pattern (add_periodic_noise, test.py:1128-1298) and cv2.add(u8, u8).
 #include "idn_common.hpp"
+#include "f64_math.hpp"
 #include "noise_apply.hpp"
 #include "ycc.hpp"
 
@@ -61,14 +62,28 @@ __device__ __forceinline__ void store_out(const NoiseArgs& a, int img, int64_t e
 }
 
 // two standard normals in float64 from one Philox4x32-10 block (counter (pair, 2, image id)):
-// 53-bit uniforms u1 in (0, 1], u2 in [0, 1) (|z| <= 8.57), rad = sqrt(-2 ln u1), (cos, sin)
-// (2 pi u2) by sincospi
-__device__ __forceinline__ void normal2_f64(const u32x4& r, double& z0, double& z1) {
+// 53-bit uniforms u1 = (a + 1) 2^-53 in (0, 1], u2 = b 2^-53 in [0, 1) (|z| <= 8.57),
+// rad = sqrt(-2 ln u1), (cos, sin)(2 pi u2).  ln and (sin, cos) from the integers a + 1, b by the
+// table-driven forms of f64_math.hpp (within ~1.4 ulp; the library log / sincospi, ~130 fp64
+// operations per pair, made the float64 stream fp64-issue-bound)
+// The tables live in LDS (F64mLds, staged once per workgroup): per-lane gathers from the
+// __constant__ copies went through the vector L1 at one cache line per lane and cost more than
+// the fp64 work they save.
+struct F64mLds {
+  double ln[f64m::LN_TAB_N];
+  double sc[f64m::SC_TAB_N];
+};
+__device__ __forceinline__ void stage_f64m(F64mLds& t) {
+  for (int i = threadIdx.x; i < f64m::LN_TAB_N; i += blockDim.x) t.ln[i] = f64m::LN_TAB[i];
+  for (int i = threadIdx.x; i < f64m::SC_TAB_N; i += blockDim.x) t.sc[i] = f64m::SC_TAB[i];
+  __syncthreads();
+}
+__device__ __forceinline__ void normal2_f64(const u32x4& r, const F64mLds& t, double& z0,
+                                            double& z1) {
   const uint64_t a = ((uint64_t)r.x << 21) | (r.y >> 11), b = ((uint64_t)r.z << 21) | (r.w >> 11);
-  const double u1 = (double)(a + 1) * 0x1p-53, u2 = (double)b * 0x1p-53;
-  const double rad = sqrt(-2.0 * log(u1));
+  const double rad = sqrt(fmax(-2.0 * f64m::ln_u53(a + 1, t.ln), 0.0));
   double sn, cs;
-  sincospi(2.0 * u2, &sn, &cs);
+  f64m::sincos2pi_u53(b, t.sc, &sn, &cs);
   z0 = rad * cs;
   z1 = rad * sn;
 }
@@ -80,6 +95,8 @@ __device__ __forceinline__ void normal2_f64(const u32x4& r, double& z0, double& 
 enum NoiseSrc { SRC_REPLAY = 0, SRC_F64 = 1 };
 template <int KIND, int SRC>
 __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
+  __shared__ F64mLds tab;
+  if constexpr (SRC == SRC_F64) stage_f64m(tab);
   const int64_t pairs = (a.elems + 1) / 2;
   const int64_t total = pairs * a.n;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -97,7 +114,7 @@ __global__ __launch_bounds__(256) void noise_gauss_kernel(NoiseArgs a) {
                                        (uint32_t)gimg, (uint32_t)(gimg >> 32)},
                                  a.key);
       double z0, z1;
-      normal2_f64(r, z0, z1);
+      normal2_f64(r, tab, z0, z1);
       // np.random.normal(mean, sd): loc + scale * gauss
       nz[0] = __dadd_rn(a.p0, __dmul_rn(a.p1, z0));
       nz[1] = __dadd_rn(a.p0, __dmul_rn(a.p1, z1));
@@ -137,6 +154,8 @@ __global__ __launch_bounds__(256) void noise_gauss_ycc_kernel(NoiseArgs a) {
   double* of = a.out_f64 + slot * a.elems;
   uint8_t* ou = a.out_u8 ? a.out_u8 + slot * a.elems : nullptr;
   const uint64_t gimg = image_id(a, img);
+  __shared__ F64mLds tab;
+  if constexpr (SRC == SRC_F64) stage_f64m(tab);
   double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npp;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -152,7 +171,7 @@ __global__ __launch_bounds__(256) void noise_gauss_ycc_kernel(NoiseArgs a) {
                                          (uint32_t)gimg, (uint32_t)(gimg >> 32)},
                                    a.key);
         double z0, z1;
-        normal2_f64(r, z0, z1);
+        normal2_f64(r, tab, z0, z1);
         nz[2 * k] = __dadd_rn(a.p0, __dmul_rn(a.p1, z0));
         nz[2 * k + 1] = __dadd_rn(a.p0, __dmul_rn(a.p1, z1));
       }
