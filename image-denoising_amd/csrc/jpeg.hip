@@ -26,7 +26,8 @@
 // optional restart intervals: baseline / extended sequential (SOF0 / SOF1) with one interleaved
 // scan (the parallel path above), and progressive (SOF2) or multi-scan sequential files (the scan
 // path: jpeg_prog_kernel, one wave per image, scans in file order, restart intervals across the
-// lanes).  Anything else (arithmetic, lossless, 12-bit, CMYK) is IDN_EUNSUPPORTED.
+// lanes), with libjpeg 9d's block smoothing of progressive files whose last scan leaves AC 1..5
+// imprecise (jpg_smooth).  Anything else (arithmetic, lossless, 12-bit, CMYK) is IDN_EUNSUPPORTED.
 #include "idn_common.hpp"
 
 #include <string.h>
@@ -64,6 +65,8 @@ struct JpegDev {
   int wib[3], hib[3];       // blocks with data per component row / column (jdinput.c
                             // width_in_blocks): what a non-interleaved scan codes
   uint32_t scan0, nscan;    // scan path: the image's scans in the batch scan table (0: none)
+  int smooth;               // libjpeg 9d block smoothing (jdcoefct.c decompress_smooth_data)
+  int8_t cbits[3][6];       // its coef_bits latch per component (zigzag 0..5; -1: never coded)
   uint8_t ph_comp[10], ph_dv[10], ph_dh[10];  // block of the MCU -> component, block row, column
   uint16_t q[4][64];        // quantisation tables, natural order
   uint16_t lut[4][1 << JPG_LUTB];  // [DC0, DC1, AC0, AC1]: len << 8 | symbol, 0 = longer code
@@ -121,6 +124,8 @@ struct JpegHost {
   size_t scan_begin = 0, scan_end = 0;
   bool adobe_rgb = false;
   bool progressive = false;
+  bool smooth = false;      // libjpeg 9d block-smooths the file (jpg_scans_done)
+  int8_t cbits[3][6] = {};  // its coef_bits latch: per component, zigzag 0..5 (-1: never coded)
   std::vector<ScanHost> scans;  // the scan path (progressive or multi-scan); empty: one scan
 };
 
@@ -147,10 +152,11 @@ static int jpg_fail(std::string* err, const char* msg) {
 
 // the end of a scan-path file (EOI or end of data): at least one scan.  libjpeg block-smooths a
 // progressive file (jdcoefct.c smoothing_ok, libjpeg 9d) only when EVERY component has DC data
-// (coef_bits[0] >= 0) and nonzero quantisers Q00 Q01 Q10 Q20 Q11 Q02, and some component's AC
-// coefficients 1..5 stay imprecise after the last scan; that smoothing is not restated, so such a
-// file is rejected -- any other progressive file decodes without it, as libjpeg does
-static int jpg_scans_done(const JpegHost& J, std::string* err) {
+// (coef_bits[0] >= 0: jdphuff.c sets coef_bits[k] = Al for k in Ss..Se at each scan's start) and
+// nonzero quantisers Q00 Q01 Q10 Q20 Q11 Q02, and some component's AC coefficients 1..5 stay
+// imprecise after the last scan (coef_bits != 0): J.smooth and the latched coef_bits, applied by
+// the IDCT pass (jpg_smooth)
+static int jpg_scans_done(JpegHost& J, std::string* err) {
   if (J.scans.empty()) return jpg_fail(err, "no SOS");
   if (J.progressive) {
     int bits[3][6];
@@ -167,8 +173,9 @@ static int jpg_scans_done(const JpegHost& J, std::string* err) {
         return IDN_OK;  // smoothing_ok() is FALSE for the whole image
       for (int z = 1; z <= 5; ++z) useful |= bits[c][z] != 0;
     }
-    if (useful)
-      return jpg_fail(err, "progressive file leaves AC 1..5 imprecise (libjpeg block smoothing)");
+    J.smooth = useful;
+    for (int c = 0; c < J.ncomp; ++c)
+      for (int z = 0; z < 6; ++z) J.cbits[c][z] = (int8_t)bits[c][z];
   }
   return IDN_OK;
 }
@@ -1301,6 +1308,41 @@ __device__ __forceinline__ void jpg_idct16(const int (&x)[8], int (&o)[16]) {
   o[8] = jpg_descale(tmp27 - tmp13, SH);
 }
 
+// libjpeg 9d block smoothing (jdcoefct.c decompress_smooth_data) of block (bx, by) of component
+// c, on its dequantised coefficients x: a coefficient among AC01 AC10 AC20 AC11 AC02 whose
+// coef_bits latch Al != 0 and whose value is still 0 is estimated from the quantised DC values
+// DC1..DC9 of the 3x3 blocks around it (rows above / own / below; edge blocks repeat at the
+// image's data edges, width_in_blocks x height_in_blocks):
+//   num = mult Q00 term,  pred = ((Qk << 7) + |num|) / (Qk << 8), capped at 2^Al - 1 for Al > 0,
+//   signed as num, stored as a 16-bit JCOEF; then dequantised like the coded coefficients.
+// The estimates never feed a neighbour (libjpeg smooths a copy of each block).
+__device__ __forceinline__ void jpg_smooth(const JpegDev& D, int c, const int16_t* cc, int bx,
+                                           int by, const uint16_t* q, int (&x)[64]) {
+  const int bw = D.bw[c], xl = D.wib[c] - 1, yl = D.hib[c] - 1;
+  const int xs[3] = {max(bx - 1, 0), bx, min(bx + 1, xl)};
+  const int ys[3] = {max(by - 1, 0), by, min(by + 1, yl)};
+  long long dc[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dc[3 * r + k] = cc[((size_t)ys[r] * bw + xs[k]) * 64];
+  const long long q00 = q[0];
+  auto est = [&](int z, int pos, long long num) {
+    const int al = D.cbits[c][z];
+    if (al == 0 || x[pos] != 0) return;  // q[pos] != 0 (smoothing_ok): x == 0 iff the coefficient is
+    const long long qk = q[pos];
+    long long pred = ((qk << 7) + (num >= 0 ? num : -num)) / (qk << 8);
+    if (al > 0 && pred >= (1ll << al)) pred = (1ll << al) - 1;
+    if (num < 0) pred = -pred;
+    x[pos] = (int)(int16_t)pred * (int)qk;
+  };
+  est(1, 1, 36 * q00 * (dc[3] - dc[5]));                      // AC01: DC4 - DC6
+  est(2, 8, 36 * q00 * (dc[1] - dc[7]));                      // AC10: DC2 - DC8
+  est(3, 16, 9 * q00 * (dc[1] + dc[7] - 2 * dc[4]));          // AC20
+  est(4, 9, 5 * q00 * (dc[0] - dc[2] - dc[6] + dc[8]));       // AC11
+  est(5, 2, 9 * q00 * (dc[3] + dc[5] - 2 * dc[4]));           // AC02
+}
+
 // one thread per coefficient block of components whose IDCT output is (8 SV) x (8 SH) samples;
 // blocks of all components of all images in one flat index space (blocks of other scales exit)
 template <int SV, int SH>
@@ -1340,6 +1382,8 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDev* __restric
       x[8 * k + 2 * j + 1] = (int)(int16_t)((uint32_t)w4[j] >> 16) * (int)q[8 * k + 2 * j + 1];
     }
   }
+  if (D.smooth && bx < D.wib[c] && by < D.hib[c])
+    jpg_smooth(D, c, coef + D.blk_off[c] * 64, bx, by, q, x);
   constexpr int R = 8 * SV, C = 8 * SH;  // output rows, columns
   int ws[R * 8];
 #pragma unroll
@@ -1621,6 +1665,11 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       D.hib[c] = (chh + 7) / 8;
     }
     for (int t = 0; t < 4; ++t) memcpy(D.q[t], J.q[t], sizeof(D.q[t]));
+    if (J.smooth && turbo)  // libjpeg-turbo >= 2.1: 9 coefficients from a 5x5 DC neighbourhood
+      return jpg_fail(err, "libjpeg-turbo block smoothing (progressive file with imprecise AC) "
+                           "not supported");
+    D.smooth = J.smooth ? 1 : 0;
+    memcpy(D.cbits, J.cbits, sizeof(D.cbits));
     if (!J.scans.empty()) {  // the scan path: one descriptor per scan, its bytes in this image's
                              // stretch of the batch scan buffer; the parallel path sees no data
       D.scan_off = P.scan_bytes;

@@ -331,18 +331,19 @@ int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int
 
 /* Header of one JPEG file in host memory (SOI .. EOI): height, width, components (1 or 3).
  * Taken: Huffman-coded baseline, extended sequential and progressive files (SOF0 / SOF1 / SOF2),
- * one or several scans, restart intervals, 4:4:4 / 4:2:2 / 4:2:0 or grayscale.  IDN_EUNSUPPORTED
- * for anything else (arithmetic-coded, lossless, hierarchical, 12-bit, CMYK / Adobe RGB, other
- * chroma sampling) and for a progressive file libjpeg would block-smooth (jdcoefct.c
- * smoothing_ok: every component with DC data and nonzero low quantisers, and AC 1..5 of some
- * component left imprecise by the last scan) -- that smoothing is not restated. */
+ * one or several scans, restart intervals, 4:4:4 / 4:2:2 / 4:2:0 or grayscale; a progressive
+ * file whose last scan leaves AC 1..5 imprecise is block-smoothed as libjpeg 9d smooths it
+ * (jdcoefct.c smoothing_ok / decompress_smooth_data).  IDN_EUNSUPPORTED for anything else
+ * (arithmetic-coded, lossless, hierarchical, 12-bit, CMYK / Adobe RGB, other chroma sampling). */
 int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
 
 /* idn_jpeg_decode_u8 flags.  Default (0): the decode of the reference's pinned libjpeg 9d
  * (requirements.txt:74, linked by its OpenCV 3.4.2): 8x8 ISLOW IDCT for full-size components,
  * libjpeg 9's scaled 16x16 / 16x8 IDCT for 4:2:0 / 4:2:2 chroma (no upsampling pass), libjpeg 9's
  * YCbCr tables.  IDN_JPEG_TURBO: libjpeg-turbo's decode (8x8 IDCT, fancy h2v1 / h2v2
- * upsampling), what a turbo-linked OpenCV or PIL produce.  Bits 8..23: entropy chunk size in bits
+ * upsampling), what a turbo-linked OpenCV or PIL produce (a file libjpeg-turbo would
+ * block-smooth is IDN_EUNSUPPORTED in this mode: turbo's smoothing is not restated).  Bits 8..23:
+ * entropy chunk size in bits
  * for the self-synchronising decoder (0 = the default: ~100k chunks per batch, 1536..6144 bits;
  * else a multiple of 64, >= 512; does not
  * change the output). */

@@ -15,8 +15,9 @@ reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
                has DC data and nonzero quantisers Q00 Q01 Q10 Q20 Q11 Q02, and some component's AC
                coefficients 1..5 are not all known to full precision after the last scan (coef_bits
                != 0).  Encoders' standard scripts (jpeg_simple_progression) refine every one to
-               Al = 0; a file that libjpeg would smooth is rejected here (not restated), any other
-               decodes as libjpeg decodes it
+               Al = 0; files cut short of their last scans are smoothed: decompress_smooth_data
+               estimates each still-zero AC01 AC10 AC20 AC11 AC02 from the 3x3 neighbourhood of
+               quantised DC values (block_smooth below)
   jdmaster.c   IDCT scaling: with do_fancy_upsampling (the default) a component whose sampling
                factor divides the maximum by 2 gets a scaled IDCT of twice the size in that
                direction (libjpeg >= 7), so 4:2:0 chroma is decoded by jpeg_idct_16x16 and
@@ -29,6 +30,8 @@ OpenCV then swaps RGB -> BGR (grfmt_jpeg.cpp, no JCS_EXT_BGR in IJG libjpeg).
 
 mode="turbo" instead restates libjpeg-turbo (the system Pillow's decoder): 8x8 IDCT for every
 component, "fancy" triangular h2v1 / h2v2 upsampling (jdsample.c) and FIX(0.34414) for Cb->G.
+(libjpeg-turbo >= 2.1 smooths differently -- nine coefficients from a 5x5 DC neighbourhood -- which
+is not restated: mode="turbo" raises NotImplementedError for a file either library would smooth.)
 
 Pinned by tests/golden/jpeg9.npz / jpeg9.json: the real libjpeg 9d decode of every fixture file
 (tests/golden/make_jpeg9_fixtures.py, conda Pillow 8.4.0); tests/test_jpeg.py checks this
@@ -321,11 +324,48 @@ def parse_and_decode(data: bytes):
     smoothing_ok = progressive and all(
         cb[0] >= 0 and all(q[c["tq"]][i] != 0 for i in (0, 1, 8, 16, 9, 2))
         for cb, c in zip(cbits, comps)) and any(any(b != 0 for b in cb[1:]) for cb in cbits)
-    if smoothing_ok:
-        raise NotImplementedError("progressive file leaves AC 1..5 imprecise: libjpeg would "
-                                  "block-smooth it (jdcoefct.c smoothing_ok)")
     return dict(width=W, height=H, hmax=geo["hmax"], vmax=geo["vmax"],
-                comps=[(c["h"], c["v"], q[c["tq"]]) for c in comps], coef=coef)
+                comps=[(c["h"], c["v"], q[c["tq"]]) for c in comps], coef=coef,
+                smooth=cbits if smoothing_ok else None, wib=geo["wib"], hib=geo["hib"])
+
+
+# jdcoefct.c decompress_smooth_data (libjpeg 9d): (coef_bits index = zigzag k, natural position,
+# multiplier, the DC neighbourhood term) per estimated coefficient; DC1..DC9 are the quantised DC
+# values of the 3x3 blocks around the current one (DC5), row by row
+_SMOOTH = ((1, 1, 36, lambda d: d[4] - d[6]),                 # AC01
+           (2, 8, 36, lambda d: d[2] - d[8]),                 # AC10
+           (3, 16, 9, lambda d: d[2] + d[8] - 2 * d[5]),      # AC20
+           (4, 9, 5, lambda d: d[1] - d[3] - d[7] + d[9]),    # AC11
+           (5, 2, 9, lambda d: d[4] + d[6] - 2 * d[5]))       # AC02
+
+
+def block_smooth(cf, q, cbits, wib: int, hib: int):
+    """libjpeg 9d block smoothing of one component's quantised coefficients cf (bh, bw, 64)
+    (jdcoefct.c decompress_smooth_data): over the blocks that carry data (width_in_blocks x
+    height_in_blocks; the neighbourhood repeats the edge blocks), a coefficient whose coef_bits
+    latch Al != 0 and whose value is still 0 becomes
+        pred = ((Q_k << 7) + |num|) // (Q_k << 8),  num = mult * Q00 * term(DC1..DC9),
+    capped at 2^Al - 1 when Al > 0, with the sign of num.  Works on a copy (the estimates never
+    feed a neighbour)."""
+    out = cf.copy()
+    dc = cf[:hib, :wib, 0].astype(np.int64)
+    pad = np.pad(dc, 1, mode="edge")
+    d = [None] + [pad[r:r + hib, c:c + wib] for r in range(3) for c in range(3)]
+    q00 = int(q[0])
+    for k, pos, mult, term in _SMOOTH:
+        al = cbits[k]
+        if al == 0:
+            continue
+        qk = int(q[pos])
+        num = mult * q00 * term(d)
+        pred = ((qk << 7) + np.abs(num)) // (qk << 8)
+        if al > 0:
+            pred = np.minimum(pred, (1 << al) - 1)
+        pred = np.where(num >= 0, pred, -pred)
+        pred = ((pred + 32768) & 0xFFFF) - 32768  # (JCOEF) pred: a 16-bit store
+        cur = out[:hib, :wib, pos]
+        out[:hib, :wib, pos] = np.where(cur == 0, pred, cur)
+    return out
 
 
 # ---- IDCT kernels (jidctint.c) -------------------------------------------------------------------
@@ -469,6 +509,11 @@ def imread(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
     """cv2.imread(..., IMREAD_COLOR) of a baseline JPEG: (H, W, 3) uint8 BGR"""
     d = parse_and_decode(data)
     W, H, hmax, vmax = d["width"], d["height"], d["hmax"], d["vmax"]
+    if d["smooth"] is not None:
+        if mode != "libjpeg9":
+            raise NotImplementedError("libjpeg-turbo's block smoothing is not restated")
+        d["coef"] = [block_smooth(cf, q, cb, wb, hb) for (_, _, q), cf, cb, wb, hb in
+                     zip(d["comps"], d["coef"], d["smooth"], d["wib"], d["hib"])]
     planes = []
     for (h, v, q), cf in zip(d["comps"], d["coef"]):
         sh = 2 if (mode == "libjpeg9" and hmax % (2 * h) == 0 and h * 2 <= hmax) else 1

@@ -119,6 +119,40 @@ def derived():
             t += 1 + 64 * (2 if pq else 1)
         k = cut.find(b"\xff\xdb", seg_end)
     (OUT / "prog_q0_cut_s444_96x128.jpg").write_bytes(bytes(cut))
+    smoothed()
+
+
+def _keep_scans(src, keep, name):
+    """`src` with only the scans whose indices are in `keep` (file order), the tables between
+    scans kept, ended by EOI"""
+    data = (OUT / src).read_bytes()
+    segs = _scan_segments(data)
+    parts, prev = [data[:segs[0][0]]], segs[0][0]
+    for j, (k, e) in enumerate(segs):
+        parts.append(data[prev:k])
+        if j in keep:
+            parts.append(data[k:e])
+        prev = e
+    (OUT / name).write_bytes(b"".join(parts) + b"\xff\xd9")
+
+
+def smoothed():
+    """progressive files libjpeg 9d block-smooths (jdcoefct.c smoothing_ok TRUE: every component
+    has DC data, nonzero low quantisers, and some AC 1..5 left imprecise by the last scan).  The
+    fixtures' script (jpeg_simple_progression, 3 components): 0 DC first Al 1, 1 Y AC1-5 Al 2,
+    2 Cr AC1-63 Al 1, 3 Cb AC1-63 Al 1, 4 Y AC6-63 Al 2, 5 Y AC1-63 refine Al 1, 6 DC refine,
+    7 Cr refine, 8 Cb refine, 9 Y refine (grayscale: 0 DC, 1 AC1-5, 2 AC6-63, 3 AC refine Al 1,
+    4 DC refine, 5 AC refine Al 0)"""
+    # Y and Cb AC at Al 1, Cr exact (the two last scans cut)
+    _keep_scans("prog_s444_q85_96x128.jpg", set(range(8)), "prog_smooth_cut_s444_96x128.jpg")
+    # DC at Al 1, every AC capped (Al > 0: the 2^Al - 1 clamp), restart intervals
+    _keep_scans("prog_s420_rst4_120x160.jpg", {0, 1, 2, 3}, "prog_smooth_al_s420_rst4_120x160.jpg")
+    # odd 4:2:2 (edge blocks, the 16x8 chroma IDCT), refinements missing
+    _keep_scans("prog_s422_q75_odd_45x67.jpg", set(range(6)), "prog_smooth_s422_odd_45x67.jpg")
+    # chroma AC never sent (coef_bits -1: estimates without a cap), luma AC 1-5 at Al 2
+    _keep_scans("prog_s444_q85_96x128.jpg", {0, 1}, "prog_smooth_dconly_s444_96x128.jpg")
+    # grayscale, DC and the AC refinement missing
+    _keep_scans("prog_gray_q80_91x77.jpg", {0, 1, 2, 3}, "prog_smooth_gray_91x77.jpg")
 
 
 if __name__ == "__main__":

@@ -195,19 +195,33 @@ def test_progressive_scan_script_of_the_fixtures():
     assert kinds == {"DC_first", "DC_refine", "AC_first", "AC_refine"}
 
 
-def test_progressive_without_final_scans_is_rejected():
+def test_progressive_without_final_scans_is_smoothed():
     """a progressive file whose last scans are missing leaves AC coefficients imprecise; libjpeg
-    would block-smooth it (jdcoefct.c smoothing_ok), which is not restated: the host parser and
-    the oracle both refuse it instead of decoding different pixels"""
+    9d block-smooths it (jdcoefct.c smoothing_ok / decompress_smooth_data).  The fixtures
+    prog_smooth_*.jpg cover it (Al > 0 caps, never-coded chroma AC, grayscale, odd 4:2:2, restart
+    intervals) and test_oracle_libjpeg9_matches_real_libjpeg9 pins the oracle's smoothing to the
+    real library; here: the host parser takes them, the smoothing changes pixels (so those tests
+    are not vacuous), and libjpeg-turbo mode refuses them (turbo smooths differently)"""
     from idn import ops
-    from idn._lib import IdnError
     from oracle import jpeg9
-    data = (JPEG / "prog_s444_q85_96x128.jpg").read_bytes()
-    cut = data[:_sos_offsets(data)[-3]] + b"\xff\xd9"
-    with pytest.raises(IdnError, match="smoothing"):
-        ops.jpeg_info(cut)
-    with pytest.raises(NotImplementedError):
-        jpeg9.imread(cut)
+    names = [p.name for p in _files() if p.name.startswith("prog_smooth")]
+    assert len(names) >= 5
+    gold = np.load(GOLD / "jpeg9.npz")
+    for name in names:
+        data = (JPEG / name).read_bytes()
+        d = jpeg9.parse_and_decode(data)
+        assert d["smooth"] is not None, name
+        assert ops.jpeg_info(data)[0] == d["height"]
+        unsmoothed = dict(d, smooth=None)
+        orig = jpeg9.parse_and_decode
+        try:
+            jpeg9.parse_and_decode = lambda _b: unsmoothed
+            plain = jpeg9.imread(data)
+        finally:
+            jpeg9.parse_and_decode = orig
+        assert (plain != gold[name]).mean() > 0.05, name
+        with pytest.raises(NotImplementedError):
+            jpeg9.imread(data, mode="turbo")
 
 
 def test_progressive_smoothing_ok_mirrors_libjpeg():

@@ -55,6 +55,11 @@ def test_decode_turbo_mode_bitexact_vs_pil(dev, name):
     if not (features.version("jpg") or "").startswith(("6", "8", "3")):
         pytest.skip("the box's Pillow does not link libjpeg-turbo")
     from idn import ops
+    if name.startswith("prog_smooth"):  # libjpeg-turbo's block smoothing is not restated
+        from idn._lib import IdnError
+        with pytest.raises(IdnError, match="unsupported"):
+            ops.jpeg_decode([(JPEG / name).read_bytes()], mode="turbo")
+        return
     got = ops.jpeg_decode([(JPEG / name).read_bytes()], mode="turbo")[0].cpu().numpy()
     ref = pil_bgr(JPEG / name)
     d = np.abs(got.astype(int) - ref.astype(int))
@@ -110,6 +115,19 @@ def test_truncated_restart_file_decodes_without_fault(dev):
     assert got.shape == good.shape
     # the intervals before the cut decode exactly as in the whole file
     assert np.array_equal(got[:16], good[:16])
+
+
+def test_smoothed_and_plain_files_in_one_batch(dev):
+    """block smoothing is per image (JpegDev.smooth and its coef_bits latch): one launch of
+    96x128 files -- baseline, complete progressive, two smoothed ones (Al 1 luma / Cb; never-coded
+    chroma AC) and the DC-less cut that libjpeg leaves unsmoothed -- each as libjpeg 9d decodes it"""
+    from idn import ops
+    names = ["prog_smooth_cut_s444_96x128.jpg", "s444_q95_96x128.jpg",
+             "prog_smooth_dconly_s444_96x128.jpg", "prog_s444_q85_96x128.jpg",
+             "prog_nodc_cut_s444_96x128.jpg", "prog_smooth_cut_s444_96x128.jpg"]
+    got = ops.jpeg_decode([(JPEG / n).read_bytes() for n in names]).cpu().numpy()
+    for i, n in enumerate(names):
+        check_libjpeg9(n, got[i])
 
 
 def test_mixed_baseline_and_progressive_batch(dev):
