@@ -27,7 +27,9 @@
 // scan (the parallel path above), and progressive (SOF2) or multi-scan sequential files (the scan
 // path: jpeg_prog_kernel, one wave per image, scans in file order, restart intervals across the
 // lanes), with libjpeg 9d's block smoothing of progressive files whose last scan leaves AC 1..5
-// imprecise (jpg_smooth).  Anything else (arithmetic, lossless, 12-bit, CMYK) is IDN_EUNSUPPORTED.
+// imprecise (jpg_smooth).  Three-component files are YCbCr or RGB as each library decides it
+// (jpg_color_space: JFIF / Adobe markers, component IDs).  Anything else (arithmetic, lossless,
+// 12-bit, CMYK / YCCK, big-gamut colour, extension markers) is IDN_EUNSUPPORTED.
 #include "idn_common.hpp"
 
 #include <string.h>
@@ -54,6 +56,7 @@ struct JpegDev {
   int dw[3], dh[3];         // component plane size after the IDCT (libjpeg downsampled_width)
   int up;                   // chroma upsampling: 0 none (full-size planes), 1 h2v1, 2 h2v2 fancy
   int cb_g;                 // jdcolor.c Cb -> G multiplier: libjpeg 9 22553, turbo 22554
+  int rgb;                  // 1: the components are R, G, B (no colour conversion; jpg_color_space)
   uint64_t blk_off[3];      // first block of each component in the batch coefficient buffer
   uint64_t pl_off[3];       // component plane byte offset in the batch plane buffer
   uint64_t ub_off;          // unstuffed entropy bytes (workspace), capacity scan_len + 64
@@ -122,7 +125,8 @@ struct JpegHost {
   uint16_t q[4][64] = {};  // natural order
   HuffSpec dc[4], ac[4];
   size_t scan_begin = 0, scan_end = 0;
-  bool adobe_rgb = false;
+  bool jfif = false, adobe = false;  // APP0 "JFIF" / APP14 "Adobe" seen (jdmarker.c examine_app0/14)
+  int adobe_transform = 0;
   bool progressive = false;
   bool smooth = false;      // libjpeg 9d block-smooths the file (jpg_scans_done)
   int8_t cbits[3][6] = {};  // its coef_bits latch: per component, zigzag 0..5 (-1: never coded)
@@ -262,15 +266,25 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         if (sl < 2) return jpg_fail(err, "bad DRI");
         J.restart = (s[0] << 8) | s[1];
         break;
-      case 0xEE:  // APP14 Adobe: transform 0 = RGB / CMYK stored as-is
-        if (sl >= 12 && memcmp(s, "Adobe", 5) == 0 && s[11] == 0) J.adobe_rgb = true;
+      case 0xE0:  // APP0: JFIF (jdmarker.c examine_app0: identifier + at least 14 bytes)
+        if (sl >= 14 && memcmp(s, "JFIF", 5) == 0) J.jfif = true;
         break;
+      case 0xEE:  // APP14 Adobe (examine_app14: at least 12 bytes): the colour transform flag
+        if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) {
+          J.adobe = true;
+          J.adobe_transform = s[11];
+        }
+        break;
+      case 0xDE: case 0xDF: case 0xF0: case 0xF1: case 0xF2: case 0xF3: case 0xF4: case 0xF5:
+      case 0xF6: case 0xF7: case 0xF8: case 0xF9: case 0xFA: case 0xFB: case 0xFC: case 0xFD:
+        // DHP / EXP / JPGn: fatal in libjpeg-turbo (read_markers' reserved-marker error); in libjpeg
+        // 9 JPG8 is the LSE colour-transform marker (not restated)
+        return jpg_fail(err, "reserved / extension marker (DHP, EXP, JPGn, LSE) not supported");
       case 0xDA: {  // SOS
         if (!sof) return jpg_fail(err, "SOS before SOF");
         if (sl < 1) return jpg_fail(err, "bad SOS");
         const int ns = s[0];
         if (ns < 1 || ns > J.ncomp || sl < 1 + 2 * (size_t)ns + 3) return jpg_fail(err, "bad SOS");
-        if (J.adobe_rgb) return jpg_fail(err, "Adobe RGB / CMYK JPEG not supported");
         if (J.ncomp == 3) {
           const bool s444 = J.ch[0] == 1 && J.cv[0] == 1;
           const bool s422 = J.ch[0] == 2 && J.cv[0] == 1;
@@ -1501,6 +1515,10 @@ __device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __re
     const int Y = (int)(((i < 4 ? ya : yb) >> (8 * (i & 3))) & 0xFFu);
     if constexpr (GRAY) {
       px[3 * i] = px[3 * i + 1] = px[3 * i + 2] = (uint32_t)Y;
+    } else if (D.rgb) {  // jdcolor.c rgb_convert: a copy (components R, G, B -> BGR)
+      px[3 * i + 0] = (uint32_t)crv[i];
+      px[3 * i + 1] = (uint32_t)cbv[i];
+      px[3 * i + 2] = (uint32_t)Y;
     } else {
       const int xb = cbv[i] - 128, xr = crv[i] - 128;
       px[3 * i + 0] = jpg_clamp(Y + ((116130 * xb + 32768) >> 16));                  // FIX(1.772)
@@ -1541,6 +1559,29 @@ __global__ __launch_bounds__(256) void jpeg_color8_kernel(const JpegDev* __restr
   } else {
     for (int k = 0; k < 24 && x0 + k / 3 < w; ++k) p[k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
   }
+}
+
+// the colour space libjpeg assigns a 3-component file (jdapimin.c default_decompress_parms; the
+// caller asks for RGB): 0 YCbCr (converted), 1 RGB (copied), -1 one that is not restated.
+// libjpeg 9 looks at the component IDs first -- (1, 2, 3) YCbCr, (1, 0x22, 0x23) big-gamut YCC,
+// 'R' 'G' 'B' RGB, 'r' 'g' 'b' big-gamut RGB -- then a JFIF marker (YCbCr), then Adobe's transform
+// (0 RGB, else YCbCr), else YCbCr.  libjpeg-turbo (6b's order) looks at JFIF, then Adobe, then the
+// IDs 'R' 'G' 'B', else YCbCr.
+static int jpg_color_space(const JpegHost& J, bool turbo) {
+  if (J.ncomp != 3) return 0;
+  const int a = J.cid[0], b = J.cid[1], c = J.cid[2];
+  const bool rgb_ids = a == 'R' && b == 'G' && c == 'B';
+  const int adobe = J.adobe_transform == 0 ? 1 : 0;
+  if (!turbo) {
+    if (a == 1 && b == 2 && c == 3) return 0;
+    if ((a == 1 && b == 0x22 && c == 0x23) || (a == 'r' && b == 'g' && c == 'b')) return -1;
+    if (rgb_ids) return 1;
+    if (J.jfif) return 0;
+    return J.adobe ? adobe : 0;
+  }
+  if (J.jfif) return 0;
+  if (J.adobe) return adobe;
+  return rgb_ids ? 1 : 0;
 }
 
 // ---- host: batch plan ---------------------------------------------------------------------------
@@ -1669,6 +1710,8 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       return jpg_fail(err, "libjpeg-turbo block smoothing (progressive file with imprecise AC) "
                            "not supported");
     D.smooth = J.smooth ? 1 : 0;
+    D.rgb = jpg_color_space(J, turbo);
+    if (D.rgb < 0) return jpg_fail(err, "big-gamut (BG_YCC / BG_RGB) JPEG not supported");
     memcpy(D.cbits, J.cbits, sizeof(D.cbits));
     if (!J.scans.empty()) {  // the scan path: one descriptor per scan, its bytes in this image's
                              // stretch of the batch scan buffer; the parallel path sees no data

@@ -25,7 +25,8 @@ reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
   jidctint.c   jpeg_idct_islow (8x8), jpeg_idct_16x16, jpeg_idct_16x8 (integer, CONST_BITS 13,
                PASS1_BITS 2, range centre folded into the DC term, 10-bit wrap range limit)
   jdcolor.c    ycc_rgb_convert with libjpeg 9's tables (FIX(1.402), FIX(1.772),
-               FIX(0.714136286), FIX(0.344136286); SCALEBITS 16)
+               FIX(0.714136286), FIX(0.344136286); SCALEBITS 16); RGB files (jdapimin.c
+               default_decompress_parms: component IDs, JFIF / Adobe markers) are copied
 OpenCV then swaps RGB -> BGR (grfmt_jpeg.cpp, no JCS_EXT_BGR in IJG libjpeg).
 
 mode="turbo" instead restates libjpeg-turbo (the system Pillow's decoder): 8x8 IDCT for every
@@ -242,6 +243,7 @@ def parse_and_decode(data: bytes):
     several scans (tables and the restart interval may change between scans)."""
     assert data[:2] == b"\xff\xd8", "no SOI"
     q, dc, ac, comps, restart = {}, {}, {}, [], 0
+    jfif, adobe = False, None
     W = H = 0
     progressive = None
     coef = geo = None
@@ -301,6 +303,12 @@ def parse_and_decode(data: bytes):
                 k += 1 + 64 * (2 if pq else 1)
         elif m == 0xDD:
             restart = (s[0] << 8) | s[1]
+        elif m == 0xE0 and len(s) >= 14 and s[:5] == b"JFIF\0":  # jdmarker.c examine_app0
+            jfif = True
+        elif m == 0xEE and len(s) >= 12 and s[:5] == b"Adobe":   # examine_app14
+            adobe = s[11]
+        elif m in (0xDE, 0xDF) or 0xF0 <= m <= 0xFD:
+            raise ValueError("reserved / extension marker (DHP, EXP, JPGn, LSE) not supported")
         elif m == 0xDA:
             ns = s[0]
             sel = []
@@ -326,7 +334,36 @@ def parse_and_decode(data: bytes):
         for cb, c in zip(cbits, comps)) and any(any(b != 0 for b in cb[1:]) for cb in cbits)
     return dict(width=W, height=H, hmax=geo["hmax"], vmax=geo["vmax"],
                 comps=[(c["h"], c["v"], q[c["tq"]]) for c in comps], coef=coef,
-                smooth=cbits if smoothing_ok else None, wib=geo["wib"], hib=geo["hib"])
+                smooth=cbits if smoothing_ok else None, wib=geo["wib"], hib=geo["hib"],
+                cids=[c["id"] for c in comps], jfif=jfif, adobe=adobe)
+
+
+def color_space(d, mode: str) -> str:
+    """jdapimin.c default_decompress_parms for 3 components: "ycc" (converted) or "rgb" (copied).
+    libjpeg 9 decides by the component IDs first -- (1, 2, 3) YCbCr, (1, 0x22, 0x23) / 'r' 'g' 'b'
+    big gamut (not restated), 'R' 'G' 'B' RGB -- then a JFIF marker (YCbCr), then Adobe's transform
+    (0 RGB, else YCbCr), else YCbCr; libjpeg-turbo (6b's order) by JFIF, then Adobe, then the IDs
+    'R' 'G' 'B', else YCbCr"""
+    if len(d["cids"]) != 3:
+        return "gray"
+    ids = tuple(d["cids"])
+    rgb_ids = ids == (0x52, 0x47, 0x42)
+    adobe = None if d["adobe"] is None else ("rgb" if d["adobe"] == 0 else "ycc")
+    if mode == "libjpeg9":
+        if ids == (1, 2, 3):
+            return "ycc"
+        if ids in ((1, 0x22, 0x23), (0x72, 0x67, 0x62)):
+            raise ValueError("big-gamut (BG_YCC / BG_RGB) JPEG not supported")
+        if rgb_ids:
+            return "rgb"
+        if d["jfif"]:
+            return "ycc"
+        return adobe or "ycc"
+    if d["jfif"]:
+        return "ycc"
+    if adobe:
+        return adobe
+    return "rgb" if rgb_ids else "ycc"
 
 
 # jdcoefct.c decompress_smooth_data (libjpeg 9d): (coef_bits index = zigzag k, natural position,
@@ -536,6 +573,8 @@ def imread(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
     if len(planes) == 1:
         y = planes[0].astype(np.uint8)
         return np.repeat(y[..., None], 3, -1)
+    if color_space(d, mode) == "rgb":  # jdcolor.c rgb_convert: a copy
+        return np.stack(planes[::-1], -1).astype(np.uint8)
     Y, Cb, Cr = planes
     xb, xr = Cb - 128, Cr - 128
     one_half = 1 << 15

@@ -120,6 +120,68 @@ def derived():
         k = cut.find(b"\xff\xdb", seg_end)
     (OUT / "prog_q0_cut_s444_96x128.jpg").write_bytes(bytes(cut))
     smoothed()
+    colorspaces()
+
+
+def _segments(data):
+    """(marker, start, end) of the marker segments before the first SOS (SOI excluded)"""
+    out, i = [], 2
+    while i + 4 <= len(data) and data[i] == 0xFF:
+        m = data[i + 1]
+        e = i + 2 + ((data[i + 2] << 8) | data[i + 3])
+        out.append((m, i, e))
+        if m == 0xDA:
+            break
+        i = e
+    return out
+
+
+def _recolor(src, name, ids=None, jfif=True, adobe=None):
+    """`src` with its component IDs replaced (frame and every scan header), its APP0 JFIF segment
+    dropped (jfif=False) and / or an APP14 Adobe segment with colour transform `adobe` added"""
+    data = bytearray((OUT / src).read_bytes())
+    if ids is not None:
+        k = data.find(b"\xff\xc0")
+        if k < 0:
+            k = data.find(b"\xff\xc2")
+        old = [data[k + 10 + 3 * c] for c in range(data[k + 9])]
+        remap = dict(zip(old, ids))
+        for c in range(len(old)):
+            data[k + 10 + 3 * c] = remap[old[c]]
+        k = data.find(b"\xff\xda")
+        while k >= 0:
+            for j in range(data[k + 4]):
+                data[k + 5 + 2 * j] = remap[data[k + 5 + 2 * j]]
+            k = data.find(b"\xff\xda", k + 2)
+    body = bytes(data)
+    if not jfif:
+        for m, a, e in _segments(body):
+            if m == 0xE0 and body[a + 4:a + 9] == b"JFIF\0":
+                body = body[:a] + body[e:]
+                break
+    if adobe is not None:
+        app14 = b"\xff\xee\x00\x0eAdobe\x00\x64\x00\x00\x00\x00" + bytes([adobe])
+        body = body[:2] + app14 + body[2:]
+    (OUT / name).write_bytes(body)
+
+
+def colorspaces():
+    """3-component files libjpeg 9 and libjpeg-turbo take as RGB or YCbCr by different rules
+    (jdapimin.c default_decompress_parms: 9 reads the component IDs first, turbo the JFIF / Adobe
+    markers first)"""
+    R, G, B = 0x52, 0x47, 0x42
+    # IDs 'R' 'G' 'B' with the JFIF marker: RGB for libjpeg 9, YCbCr for turbo
+    _recolor("s444_q95_96x128.jpg", "cs_rgbids_jfif_s444_96x128.jpg", ids=(R, G, B))
+    # IDs 'R' 'G' 'B', no marker: RGB for both (subsampled RGB, odd size)
+    _recolor("s420_q75_odd_37x53.jpg", "cs_rgbids_s420_odd_37x53.jpg", ids=(R, G, B), jfif=False)
+    # Adobe transform 0, IDs 1 2 3: YCbCr for libjpeg 9 (IDs first), RGB for turbo
+    _recolor("s444_q95_96x128.jpg", "cs_adobe0_s444_96x128.jpg", jfif=False, adobe=0)
+    # Adobe transform 0, IDs 0 1 2: RGB for both (progressive 4:2:2)
+    _recolor("prog_s422_q75_odd_45x67.jpg", "cs_adobe0_ids012_prog_s422_45x67.jpg", ids=(0, 1, 2),
+             jfif=False, adobe=0)
+    # Adobe transform 1 with IDs 'R' 'G' 'B': RGB for libjpeg 9 (IDs), YCbCr for turbo (Adobe)
+    _recolor("s422_q85_120x200.jpg", "cs_adobe1_rgbids_s422_120x200.jpg", ids=(R, G, B), jfif=False,
+             adobe=1)
 
 
 def _keep_scans(src, keep, name):

@@ -66,7 +66,8 @@ def test_oracle_libjpeg9_matches_real_libjpeg9(name):
 @pytest.mark.parametrize("name", ["s420_q100_64x80.jpg", "s422_q85_120x200.jpg",
                                   "s444_q95_96x128.jpg", "s420_q75_odd_37x53.jpg",
                                   "progressive_64x64.jpg", "prog_s422_q75_odd_45x67.jpg",
-                                  "prog_s420_rst4_120x160.jpg", "prog_gray_q80_91x77.jpg"])
+                                  "prog_s420_rst4_120x160.jpg", "prog_gray_q80_91x77.jpg"] +
+                         [p.name for p in _files() if p.name.startswith("cs_")])
 def test_oracle_turbo_mode_matches_system_pil(name):
     from PIL import Image
     from oracle import jpeg9
@@ -235,3 +236,45 @@ def test_progressive_smoothing_ok_mirrors_libjpeg():
         data = (JPEG / name).read_bytes()
         assert ops.jpeg_info(data) == (96, 128, 3), name
         assert jpeg9.imread(data).shape == (96, 128, 3)
+
+
+# (libjpeg 9d, libjpeg-turbo) colour space of each derived colour-space fixture
+# (tests/golden/make_jpeg_fixtures.py colorspaces(); observed with conda Pillow 8.4 / libjpeg 9 and
+# the system Pillow / libjpeg-turbo when the fixtures were made)
+_CS = {"cs_rgbids_jfif_s444_96x128.jpg": ("rgb", "ycc"),
+       "cs_rgbids_s420_odd_37x53.jpg": ("rgb", "rgb"),
+       "cs_adobe0_s444_96x128.jpg": ("ycc", "rgb"),
+       "cs_adobe0_ids012_prog_s422_45x67.jpg": ("rgb", "rgb"),
+       "cs_adobe1_rgbids_s422_120x200.jpg": ("rgb", "ycc")}
+
+
+def test_colour_space_rules_of_both_libraries():
+    """jdapimin.c default_decompress_parms: libjpeg 9 decides RGB / YCbCr by the component IDs
+    first, libjpeg-turbo by the JFIF / Adobe markers first; the five fixtures separate the two
+    orders (their pixels are pinned by test_oracle_libjpeg9_matches_real_libjpeg9 and
+    test_oracle_turbo_mode_matches_system_pil)"""
+    from oracle import jpeg9
+    assert sorted(_CS) == sorted(p.name for p in _files() if p.name.startswith("cs_"))
+    for name, (nine, turbo) in _CS.items():
+        d = jpeg9.parse_and_decode((JPEG / name).read_bytes())
+        assert (jpeg9.color_space(d, "libjpeg9"), jpeg9.color_space(d, "turbo")) == (nine, turbo)
+
+
+def test_extension_markers_and_big_gamut_are_rejected():
+    """JPGn / DHP / EXP markers stop libjpeg-turbo (and JPG8 is libjpeg 9's LSE colour transform),
+    big-gamut component IDs select a colour space that is not restated: IdnError, not a decode"""
+    from idn import ops
+    from idn._lib import IdnError
+    from oracle import jpeg9
+    data = (JPEG / "s444_q95_96x128.jpg").read_bytes()
+    lse = data[:2] + b"\xff\xf8\x00\x04\x0d\x00" + data[2:]
+    with pytest.raises(IdnError, match="extension marker"):
+        ops.jpeg_info(lse)
+    with pytest.raises(ValueError):
+        jpeg9.imread(lse)
+    k = data.find(b"\xff\xc0")
+    bg = bytearray(data)
+    for c, v in enumerate((0x72, 0x67, 0x62)):  # 'r' 'g' 'b' (scan selectors left: IDs only)
+        bg[k + 10 + 3 * c] = v
+    with pytest.raises(ValueError):
+        jpeg9.imread(bytes(bg))
