@@ -481,7 +481,13 @@ __device__ __forceinline__ int jpg_extend(uint32_t v, int s) {  // HUFF_EXTEND
   return (int)v < (1 << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v;
 }
 
+// mca[t][l - 10] (l = 10..16): the largest code of length <= l, left-aligned to 16 bits with
+// ones below (-1 while there is none; a length without codes repeats the one before), so that
+// "code16 <= mca" is monotone in l and a longer-than-LUT code's length is 10 + the number of
+// lengths it exceeds -- seven compares on two 16-byte LDS reads instead of a walk of dependent
+// maxcode reads (one per length) that every wave took whenever one of its 64 lanes missed the LUT
 struct JpegLds {
+  alignas(16) int32_t mca[4][8];
   uint16_t lut[4][1 << JPG_LUTB];
   int32_t maxcode[4][18], valoff[4][18];
   uint8_t huffval[4][256];
@@ -489,10 +495,19 @@ struct JpegLds {
 
 // the scan path's tables (JpegScanDev slots)
 struct JpegLds6 {
+  alignas(16) int32_t mca[6][8];
   uint16_t lut[6][1 << JPG_LUTB];
   int32_t maxcode[6][18], valoff[6][18];
   uint8_t huffval[6][256];
 };
+
+// entry i of mca (see JpegLds) from a table's maxcode[18]
+__device__ __forceinline__ int32_t jpg_mca(const int32_t* __restrict__ maxcode, int i) {
+  int32_t m = -1;
+  for (int l = 10; l <= 10 + i && l <= 16; ++l)
+    if (maxcode[l] >= 0) m = maxcode[l] << (16 - l) | ((1 << (16 - l)) - 1);
+  return i == 7 ? 0x7FFFFFFF : m;
+}
 
 // one Huffman symbol (nb >= 32 on entry); returns the symbol and its code length in *len
 template <typename TT>
@@ -502,18 +517,17 @@ __device__ __forceinline__ int jpg_decode(const BitStream& br, const TT& T, int 
     *len = (int)(e >> 8);
     return e & 0xFF;
   }
-  int l = JPG_LUTB + 1;
-  int32_t code = (int32_t)(br.acc >> (64 - l));
-  while (l <= 16 && code > T.maxcode[t][l]) {
-    ++l;
-    code = (int32_t)(br.acc >> (64 - l));
-  }
+  const int32_t c16 = (int32_t)(br.acc >> 48);
+  const int4 m0 = *reinterpret_cast<const int4*>(&T.mca[t][0]);
+  const int4 m1 = *reinterpret_cast<const int4*>(&T.mca[t][4]);
+  const int l = 10 + (c16 > m0.x) + (c16 > m0.y) + (c16 > m0.z) + (c16 > m0.w) + (c16 > m1.x) +
+                (c16 > m1.y) + (c16 > m1.z);
   if (l > 16) {  // not a code (only on a speculative trajectory or a corrupt file): skip 16 bits
     *len = 16;
     return 0;
   }
   *len = l;
-  return T.huffval[t][(T.valoff[t][l] + code) & 0xFF];
+  return T.huffval[t][(T.valoff[t][l] + (c16 >> (16 - l))) & 0xFF];
 }
 
 __device__ __forceinline__ void jpg_load_tables(JpegLds& T, const JpegDev& D) {
@@ -525,6 +539,7 @@ __device__ __forceinline__ void jpg_load_tables(JpegLds& T, const JpegDev& D) {
     (&T.valoff[0][0])[k] = (&D.valoff[0][0])[k];
   }
   for (int k = threadIdx.x; k < 4 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&D.huffval[0][0])[k];
+  for (int k = threadIdx.x; k < 4 * 8; k += blockDim.x) T.mca[k >> 3][k & 7] = jpg_mca(D.maxcode[k >> 3], k & 7);
 }
 
 // decoder state packed in 64 bits: bit position | block of the MCU << 32 | z << 40
@@ -607,21 +622,26 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
   if (WRITE && z != 0) bp = jpg_block(K, coef, blk, ph, (int)(K.phase_info >> (6 * ph)) & 3);
   int32_t s0 = 0, s1 = 0, s2 = 0, nblk = 0;
   int p0 = pred[0], p1 = pred[1], p2 = pred[2];
+  // one symbol per iteration, DC or AC through the same decode (a DC symbol is a size 0..15, i.e.
+  // an AC-style run/size byte with run 0): the lanes of a wave sit at different points of their
+  // blocks, and separate DC / AC paths made every iteration run both decodes
   while (pos < end_bit) {
     br.refill();
     const uint32_t info = (uint32_t)(K.phase_info >> (6 * ph));
     const int c = info & 3;
+    const bool dc = z == 0;
+    if (dc && ndc == dc_limit) break;
     int len;
-    if (z == 0) {  // DC
-      if (ndc == dc_limit) break;
+    const int rs = jpg_decode(br, T, dc ? (info >> 2) & 3 : (info >> 4) & 3, &len);
+    br.bits(len);
+    const int r = rs >> 4, s = rs & 15;
+    const int val = s ? jpg_extend(br.bits(s), s) : 0;
+    pos += len + s;
+    if (dc) {
       ++ndc;
-      const int s = jpg_decode(br, T, (info >> 2) & 3, &len);
-      br.bits(len);
-      const int diff = s ? jpg_extend(br.bits(s), s) : 0;
-      pos += len + s;
       if (WRITE) {
         ++blk;
-        const int p = (c == 0 ? p0 : c == 1 ? p1 : p2) + diff;
+        const int p = (c == 0 ? p0 : c == 1 ? p1 : p2) + val;
         if (c == 0) p0 = p;
         else if (c == 1) p1 = p;
         else p2 = p;
@@ -629,19 +649,14 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
         if (bp) bp[0] = (int16_t)p;
       } else {  // (selects: a dynamic index would put the sums in scratch)
         ++nblk;
-        if (c == 0) s0 += diff;
-        else if (c == 1) s1 += diff;
-        else s2 += diff;
+        if (c == 0) s0 += val;
+        else if (c == 1) s1 += val;
+        else s2 += val;
       }
       z = 1;
     } else {
-      const int rs = jpg_decode(br, T, (info >> 4) & 3, &len);
-      br.bits(len);
-      const int r = rs >> 4, s = rs & 15;
-      pos += len + s;
       if (s) {
         z += r;
-        const int val = jpg_extend(br.bits(s), s);
         if (WRITE && bp) bp[jpg_natural[min(z, 79u)]] = (int16_t)val;  // libjpeg's overrun guard
         ++z;
       } else if (r == 15) {
@@ -1037,6 +1052,7 @@ __device__ __forceinline__ void jpg_load_scan_tables(JpegLds6& T, const JpegScan
     (&T.valoff[0][0])[k] = (&S.valoff[0][0])[k];
   }
   for (int k = threadIdx.x; k < 6 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&S.huffval[0][0])[k];
+  for (int k = threadIdx.x; k < 6 * 8; k += blockDim.x) T.mca[k >> 3][k & 7] = jpg_mca(S.maxcode[k >> 3], k & 7);
 }
 
 __device__ __forceinline__ uint32_t jpg_get(BitStream& br, int s) {  // s <= 16
