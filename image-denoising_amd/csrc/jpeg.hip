@@ -42,7 +42,10 @@
 
 namespace idn {
 
-constexpr int JPG_LUTB = 9;  // fast Huffman lookup bits
+#ifndef IDN_JPG_LUTB  // A/B builds set it
+#define IDN_JPG_LUTB 9
+#endif
+constexpr int JPG_LUTB = IDN_JPG_LUTB;  // fast Huffman lookup bits
 
 struct JpegDev {
   uint64_t scan_off;   // entropy-coded bytes in the batch buffer
@@ -488,6 +491,7 @@ __device__ __forceinline__ int jpg_extend(uint32_t v, int s) {  // HUFF_EXTEND
 // maxcode reads (one per length) that every wave took whenever one of its 64 lanes missed the LUT
 struct JpegLds {
   alignas(16) int32_t mca[4][8];
+  uint8_t natural[80];  // jpg_natural (the write pass's coefficient positions)
   uint16_t lut[4][1 << JPG_LUTB];
   int32_t maxcode[4][18], valoff[4][18];
   uint8_t huffval[4][256];
@@ -511,13 +515,13 @@ __device__ __forceinline__ int32_t jpg_mca(const int32_t* __restrict__ maxcode, 
 
 // one Huffman symbol (nb >= 32 on entry); returns the symbol and its code length in *len
 template <typename TT>
-__device__ __forceinline__ int jpg_decode(const BitStream& br, const TT& T, int t, int* len) {
-  const uint32_t e = T.lut[t][br.acc >> (64 - JPG_LUTB)];
+__device__ __forceinline__ int jpg_decode(uint64_t acc, const TT& T, int t, int* len) {
+  const uint32_t e = T.lut[t][acc >> (64 - JPG_LUTB)];
   if (e) {
     *len = (int)(e >> 8);
     return e & 0xFF;
   }
-  const int32_t c16 = (int32_t)(br.acc >> 48);
+  const int32_t c16 = (int32_t)(acc >> 48);
   const int4 m0 = *reinterpret_cast<const int4*>(&T.mca[t][0]);
   const int4 m1 = *reinterpret_cast<const int4*>(&T.mca[t][4]);
   const int l = 10 + (c16 > m0.x) + (c16 > m0.y) + (c16 > m0.z) + (c16 > m0.w) + (c16 > m1.x) +
@@ -540,6 +544,7 @@ __device__ __forceinline__ void jpg_load_tables(JpegLds& T, const JpegDev& D) {
   }
   for (int k = threadIdx.x; k < 4 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&D.huffval[0][0])[k];
   for (int k = threadIdx.x; k < 4 * 8; k += blockDim.x) T.mca[k >> 3][k & 7] = jpg_mca(D.maxcode[k >> 3], k & 7);
+  for (int k = threadIdx.x; k < 80; k += blockDim.x) T.natural[k] = jpg_natural[k];
 }
 
 // decoder state packed in 64 bits: bit position | block of the MCU << 32 | z << 40
@@ -606,69 +611,104 @@ __device__ __forceinline__ int16_t* jpg_block(const JpgConst& K, int16_t* coef, 
   return coef + (bo + (uint64_t)by * bw + bx) * 64;
 }
 
+// The chunk decoders' bit source: a per-lane ring of JRG 16-byte groups of the (byte-swapped)
+// stream in LDS, refilled one group ahead from a range-checked buffer load held in registers.
+// The 64 lanes of a wave sit at unrelated bit positions, so any per-lane branch in the symbol loop
+// is taken by some lane on most iterations and the wave executes it every time; here the refill
+// is branch-free (the next word is read from the ring every iteration, one iteration before it
+// is needed) and only a group change (every 4 words of a lane) branches.
+constexpr int JRG = 4;                 // ring groups per lane
+constexpr int JRING_W = JRG * 4 + 4;   // ring words per lane (one pad group: lane stride 80 bytes)
+
 // Decode symbols from state st while the next symbol starts before end_bit (and at most dc_limit
 // DC symbols).  WRITE: coefficient blocks (blk = the block in progress; a DC symbol starts blk + 1)
 // with DC predictors pred[]; else count DC symbols and DC differences.  Returns the end state.
+// One symbol per iteration, DC or AC through the same decode (a DC symbol is a size 0..15, i.e. a
+// run/size byte with run 0) and the block bookkeeping by selects.
 template <bool WRITE>
-__device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T, const uint8_t* __restrict__ ub,
-                            uint64_t st, uint32_t end_bit, ChunkOut* cnt, int32_t blk,
-                            int (&pred)[3], int16_t* __restrict__ coef,
-                            uint32_t dc_limit = 0xFFFFFFFFu) {
+__device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T, rsrc_t rs,
+                                            uint32_t* __restrict__ ring, uint64_t st,
+                                            uint32_t end_bit, ChunkOut* cnt, int32_t blk,
+                                            int (&pred)[3], int16_t* __restrict__ coef,
+                                            uint32_t dc_limit = 0xFFFFFFFFu) {
   uint32_t ndc = 0;
   uint32_t pos = (uint32_t)st, ph = (uint32_t)(st >> 32) & 0xFF, z = (uint32_t)(st >> 40) & 0xFF;
-  BitStream br;
-  br.start(ub, pos);
+  // ring: words wi .. of groups (wi >> 2) .. (wi >> 2) + JRG - 1 at ring[w & (4 JRG - 1)]; pend =
+  // group (wi >> 2) + JRG, raw
+  uint32_t wi = pos >> 5;
+  {
+    const uint32_t g0 = wi >> 2;
+#pragma unroll
+    for (int k = 0; k < JRG; ++k) {
+      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 + k) * 16u, 0, 0);
+      *reinterpret_cast<v4u*>(ring + ((g0 + k) & (JRG - 1)) * 4) =
+          v4u{__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
+              __builtin_bswap32(v.w)};
+    }
+  }
+  v4u pend = __builtin_amdgcn_raw_buffer_load_b128(rs, ((wi >> 2) + JRG) * 16u, 0, 0);
+  uint64_t acc = 0;
+  int nb = 0;
+  uint32_t nxt = ring[wi & (4 * JRG - 1)];
+  // append word wi (nxt) to acc; a new group retires its predecessor's slot to pend
+  auto append = [&](bool need) {
+    acc |= need ? (uint64_t)nxt << (32 - nb) : 0ull;
+    nb += need ? 32 : 0;
+    wi += need ? 1u : 0u;
+    if (need && (wi & 3) == 0) {
+      *reinterpret_cast<v4u*>(ring + (((wi >> 2) + JRG - 1) & (JRG - 1)) * 4) =
+          v4u{__builtin_bswap32(pend.x), __builtin_bswap32(pend.y), __builtin_bswap32(pend.z),
+              __builtin_bswap32(pend.w)};
+      pend = __builtin_amdgcn_raw_buffer_load_b128(rs, ((wi >> 2) + JRG) * 16u, 0, 0);
+    }
+    nxt = ring[wi & (4 * JRG - 1)];
+  };
+  append(true);
+  append(true);
+  acc <<= (pos & 31);
+  nb -= (int)(pos & 31);
   int16_t* bp = nullptr;
   if (WRITE && z != 0) bp = jpg_block(K, coef, blk, ph, (int)(K.phase_info >> (6 * ph)) & 3);
   int32_t s0 = 0, s1 = 0, s2 = 0, nblk = 0;
   int p0 = pred[0], p1 = pred[1], p2 = pred[2];
-  // one symbol per iteration, DC or AC through the same decode (a DC symbol is a size 0..15, i.e.
-  // an AC-style run/size byte with run 0): the lanes of a wave sit at different points of their
-  // blocks, and separate DC / AC paths made every iteration run both decodes
   while (pos < end_bit) {
-    br.refill();
+    append(nb < 32);
     const uint32_t info = (uint32_t)(K.phase_info >> (6 * ph));
     const int c = info & 3;
     const bool dc = z == 0;
     if (dc && ndc == dc_limit) break;
     int len;
-    const int rs = jpg_decode(br, T, dc ? (info >> 2) & 3 : (info >> 4) & 3, &len);
-    br.bits(len);
-    const int r = rs >> 4, s = rs & 15;
-    const int val = s ? jpg_extend(br.bits(s), s) : 0;
+    const int rs8 = jpg_decode(acc, T, dc ? (info >> 2) & 3 : (info >> 4) & 3, &len);
+    const int r = rs8 >> 4, s = rs8 & 15;
+    const int val = s ? jpg_extend((uint32_t)((acc << len) >> 32) >> (32 - s), s) : 0;
+    acc <<= len + s;
+    nb -= len + s;
     pos += len + s;
-    if (dc) {
-      ++ndc;
-      if (WRITE) {
+    ndc += dc ? 1u : 0u;
+    if (WRITE) {
+      if (dc) {
         ++blk;
         const int p = (c == 0 ? p0 : c == 1 ? p1 : p2) + val;
-        if (c == 0) p0 = p;
-        else if (c == 1) p1 = p;
-        else p2 = p;
+        p0 = c == 0 ? p : p0;
+        p1 = c == 1 ? p : p1;
+        p2 = c == 2 ? p : p2;
         bp = jpg_block(K, coef, blk, ph, c);
         if (bp) bp[0] = (int16_t)p;
-      } else {  // (selects: a dynamic index would put the sums in scratch)
-        ++nblk;
-        if (c == 0) s0 += val;
-        else if (c == 1) s1 += val;
-        else s2 += val;
+      } else if (s && bp) {
+        bp[T.natural[min(z + r, 79u)]] = (int16_t)val;  // libjpeg's overrun guard
       }
-      z = 1;
     } else {
-      if (s) {
-        z += r;
-        if (WRITE && bp) bp[jpg_natural[min(z, 79u)]] = (int16_t)val;  // libjpeg's overrun guard
-        ++z;
-      } else if (r == 15) {
-        z += 16;
-      } else {
-        z = 64;  // EOB
-      }
-      if (z >= 64) {
-        z = 0;
-        ph = ph + 1 == (uint32_t)K.bpm ? 0 : ph + 1;
-      }
+      nblk += dc ? 1 : 0;
+      s0 += dc && c == 0 ? val : 0;
+      s1 += dc && c == 1 ? val : 0;
+      s2 += dc && c == 2 ? val : 0;
     }
+    // next coefficient index: DC -> 1; AC: value r + 1 on, ZRL 16 on, EOB the block's end
+    const uint32_t za = s ? z + r + 1 : (r == 15 ? z + 16 : 64u);
+    const uint32_t zn = dc ? 1u : za;
+    const bool wrap = zn >= 64;
+    z = wrap ? 0u : zn;
+    ph = wrap ? (ph + 1 == (uint32_t)K.bpm ? 0u : ph + 1) : ph;
   }
   pred[0] = p0;
   pred[1] = p1;
@@ -873,6 +913,7 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
                                                        uint64_t* __restrict__ ck_st,
                                                        ChunkOut* __restrict__ ck_co) {
   __shared__ JpegLds T;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
   const JpegDev& D = imgs[blockIdx.y];
   if (D.restart || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
@@ -900,6 +941,7 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
   ChunkOut co{0u, {0, 0, 0}};
   int pred[3] = {0, 0, 0};
   const JpgConst K = jpg_const(D);
+  const rsrc_t rs = make_rsrc(ub + D.ub_off, D.scan_len + 64u);  // past the padding: zeros
   uint64_t e = st;
   for (uint32_t j = 0; j < nsub; ++j) {
     if (!PASS_A && e == cks[j]) {
@@ -930,7 +972,7 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
     const uint32_t sub_end = min(b0 + (j + 1) * JPG_SUB, b1);
     // a state past the sub-chunk (the predecessor ran over it) ends where it starts
     if ((uint32_t)e < sub_end)
-      e = jpg_run<false>(K, T, ub + D.ub_off, e, sub_end, &co, 0, pred, nullptr);
+      e = jpg_run<false>(K, T, rs, ring + threadIdx.x * JRING_W, e, sub_end, &co, 0, pred, nullptr);
   }
   next[D.ch_off + t] = e;
   cnt[D.ch_off + t] = co;
@@ -997,6 +1039,7 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
                                                         const ChunkOut* __restrict__ start,
                                                         int16_t* __restrict__ coef) {
   __shared__ JpegLds T;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
   const JpegDev& D = imgs[blockIdx.y];
   const uint32_t nsub = jpg_nsub(D.chunk_bits);
   const uint32_t nitems = D.restart ? (uint32_t)D.nintervals : D.nchunks * nsub;
@@ -1033,7 +1076,8 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
   if ((uint32_t)st >= b1) return;
   ChunkOut dummy{0u, {0, 0, 0}};
   const JpgConst K = jpg_const(D);
-  jpg_run<true>(K, T, ub + D.ub_off, st, b1, &dummy, blk, pred, coef, dc_limit);
+  const rsrc_t rs = make_rsrc(ub + D.ub_off, D.scan_len + 64u);
+  jpg_run<true>(K, T, rs, ring + threadIdx.x * JRING_W, st, b1, &dummy, blk, pred, coef, dc_limit);
 }
 
 // ---- device: the scan path (progressive / multi-scan files) --------------------------------------
@@ -1062,7 +1106,7 @@ __device__ __forceinline__ uint32_t jpg_get(BitStream& br, int s) {  // s <= 16
 __device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLds6& T, int t) {
   br.refill();
   int len;
-  const int sym = jpg_decode(br, T, t, &len);
+  const int sym = jpg_decode(br.acc, T, t, &len);
   br.bits(len);
   return sym;
 }

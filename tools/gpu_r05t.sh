@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: JPEG symbol decode A/B (old / new jpeg.hip) -- JPEG tests on the new build, then the
+# round 5: JPEG decoder A/B (ab/old.so vs ab/new.so) -- JPEG tests on the new build, then the
 # single-file / batch decode times of both builds, interleaved
 set -u
 OUT=${1:-r05t}

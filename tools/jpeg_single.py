@@ -1,0 +1,29 @@
+"""Decode one synthetic 600x1000 q90 4:2:0 file repeatedly (tools only; for kernel traces):
+  python tools/jpeg_single.py [--iters 20] [--chunk 0]"""
+import argparse
+import io
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "image-denoising_amd"))
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+from PIL import Image  # noqa: E402
+
+import bench  # noqa: E402
+from idn import ops  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--chunk", type=int, default=0)
+a = ap.parse_args()
+x = bench.synth_batch(torch, 1, torch.device("cuda", 0), seed=3).cpu().numpy()
+b = io.BytesIO()
+Image.fromarray(x[0][..., ::-1]).save(b, "JPEG", quality=90, subsampling=2)
+f = b.getvalue()
+print("file bytes", len(f))
+for _ in range(a.iters):
+    ops.jpeg_decode([f], chunk_bits=a.chunk)
+    torch.cuda.synchronize()
