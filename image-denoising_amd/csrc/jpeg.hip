@@ -27,8 +27,9 @@
 // scan (the parallel path above), and progressive (SOF2) or multi-scan sequential files (the scan
 // path: jpeg_prog_kernel, one wave per image, scans in file order, restart intervals across the
 // lanes), with libjpeg 9d's block smoothing of progressive files whose last scan leaves AC 1..5
-// imprecise (jpg_smooth).  Three-component files are YCbCr or RGB as each library decides it
-// (jpg_color_space: JFIF / Adobe markers, component IDs).  Anything else (arithmetic, lossless,
+// imprecise (jpg_smooth); arithmetic-coded files (SOF9 / SOF10) through the scan path's QM-coder
+// (jpeg_arith_kernel).  Three-component files are YCbCr or RGB as each library decides it
+// (jpg_color_space: JFIF / Adobe markers, component IDs).  Anything else (lossless, hierarchical,
 // 12-bit, CMYK / YCCK, big-gamut colour, extension markers) is IDN_EUNSUPPORTED.
 #include "idn_common.hpp"
 
@@ -71,6 +72,7 @@ struct JpegDev {
   int wib[3], hib[3];       // blocks with data per component row / column (jdinput.c
                             // width_in_blocks): what a non-interleaved scan codes
   uint32_t scan0, nscan;    // scan path: the image's scans in the batch scan table (0: none)
+  int arith;                // arithmetic-coded (the scan path's jpeg_arith_kernel)
   int smooth;               // libjpeg 9d block smoothing (jdcoefct.c decompress_smooth_data)
   int8_t cbits[3][6];       // its coef_bits latch per component (zigzag 0..5; -1: never coded)
   uint8_t ph_comp[10], ph_dv[10], ph_dh[10];  // block of the MCU -> component, block row, column
@@ -92,6 +94,9 @@ struct JpegScanDev {
   int nintervals;
   int img, ns, comp[3], Ss, Se, Ah, Al, restart, kind;
   uint32_t nunits;          // MCUs (interleaved) or the component's blocks (non-interleaved)
+  int arith;                // arithmetic-coded: the statistics of tables td / ta per scan component,
+  int td[3], ta[3];         // conditioned by aL / aU (DC) and aK (AC); no Huffman tables
+  uint8_t aL[3], aU[3], aK[3];
   uint16_t lut[6][1 << JPG_LUTB];
   int32_t maxcode[6][18], valoff[6][18];
   uint8_t huffval[6][256];
@@ -119,6 +124,8 @@ struct HuffSpec {
 struct ScanHost {
   int ns = 0, comp[3] = {}, Ss = 0, Se = 63, Ah = 0, Al = 0, restart = 0;
   HuffSpec dc[3], ac[3];  // per scan component
+  int td[3] = {}, ta[3] = {};                   // its table numbers
+  uint8_t aL[3] = {}, aU[3] = {}, aK[3] = {};  // arithmetic conditioning of those tables (DAC)
   size_t begin = 0, end = 0;
 };
 struct JpegHost {
@@ -128,6 +135,10 @@ struct JpegHost {
   uint16_t q[4][64] = {};  // natural order
   HuffSpec dc[4], ac[4];
   size_t scan_begin = 0, scan_end = 0;
+  bool arith = false;       // arithmetic-coded frame (SOF9 / SOF10)
+  // arithmetic conditioning per table (DAC; jdmarker.c get_soi's defaults L 0, U 1, K 5)
+  uint8_t dacL[16] = {}, dacU[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1},
+          dacK[16] = {5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5, 5};
   bool jfif = false, adobe = false;  // APP0 "JFIF" / APP14 "Adobe" seen (jdmarker.c examine_app0/14)
   int adobe_transform = 0;
   bool progressive = false;
@@ -208,10 +219,14 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
     switch (m) {
       case 0xC0:
       case 0xC1:
-      case 0xC2: {  // SOF0 / SOF1 / SOF2: baseline / extended sequential / progressive Huffman
+      case 0xC2:
+      case 0xC9:
+      case 0xCA: {  // SOF0 / 1 / 2: baseline / extended sequential / progressive Huffman; SOF9 /
+                    // SOF10: sequential / progressive arithmetic
         if (sof) return jpg_fail(err, "second frame header");
         if (sl < 6 || s[0] != 8) return jpg_fail(err, "only 8-bit JPEG");
-        J.progressive = m == 0xC2;
+        J.progressive = m == 0xC2 || m == 0xCA;
+        J.arith = m == 0xC9 || m == 0xCA;
         J.height = (s[1] << 8) | s[2];
         J.width = (s[3] << 8) | s[4];
         J.ncomp = s[5];
@@ -228,9 +243,23 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         sof = true;
         break;
       }
-      case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB:
-      case 0xCD: case 0xCE: case 0xCF:
-        return jpg_fail(err, "lossless / hierarchical / arithmetic JPEG not supported");
+      case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
+        return jpg_fail(err, "lossless / hierarchical JPEG not supported");
+      case 0xCC: {  // DAC (jdmarker.c get_dac): arithmetic conditioning, 2 bytes per table
+        if (sl % 2) return jpg_fail(err, "bad DAC length");
+        for (size_t k = 0; k + 2 <= sl; k += 2) {
+          const int idx = s[k], val = s[k + 1];
+          if (idx >= 32) return jpg_fail(err, "bad DAC table index");
+          if (idx >= 16) {
+            J.dacK[idx - 16] = (uint8_t)val;
+          } else {
+            J.dacL[idx] = (uint8_t)(val & 15);
+            J.dacU[idx] = (uint8_t)(val >> 4);
+            if (J.dacL[idx] > J.dacU[idx]) return jpg_fail(err, "bad DAC value");
+          }
+        }
+        break;
+      }
       case 0xC4: {  // DHT
         size_t k = 0;
         while (k < sl) {
@@ -310,6 +339,11 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
           J.ta[c] = ta;
           S.dc[k] = J.dc[td];
           S.ac[k] = J.ac[ta];
+          S.td[k] = td;
+          S.ta[k] = ta;
+          S.aL[k] = J.dacL[td];
+          S.aU[k] = J.dacU[td];
+          S.aK[k] = J.dacK[ta];
         }
         const uint8_t* ss = s + 1 + 2 * ns;
         S.Ss = ss[0];
@@ -329,11 +363,12 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
           if (!J.qpresent[J.tq[c]]) return jpg_fail(err, "missing quantisation table");
           const bool need_dc = S.Ss == 0 && S.Ah == 0, need_ac = S.Se > 0 && !(J.progressive && S.Ah);
           const bool need_ac_ref = J.progressive && S.Ss > 0 && S.Ah;
-          if ((need_dc && !S.dc[k].present) || ((need_ac || need_ac_ref) && !S.ac[k].present))
+          if (!J.arith &&
+              ((need_dc && !S.dc[k].present) || ((need_ac || need_ac_ref) && !S.ac[k].present)))
             return jpg_fail(err, "missing Huffman table");
         }
         S.begin = i + len;
-        if (!J.progressive && J.scans.empty() && ns == J.ncomp) {
+        if (!J.progressive && !J.arith && J.scans.empty() && ns == J.ncomp) {
           // one interleaved sequential scan: the parallel path.  Its segment runs up to the EOI
           // (scanning back from the end) or the end of data
           for (int c = 0; c < J.ncomp; ++c)
@@ -1212,7 +1247,7 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
   __shared__ JpegLds6 T;
   const JpegDev& D = imgs[blockIdx.x];
   const uint32_t nscan = D.nscan;
-  if (nscan == 0) return;  // uniform: a parallel-path image
+  if (nscan == 0 || D.arith) return;  // uniform: a parallel-path or arithmetic-coded image
   for (uint32_t si = 0; si < nscan; ++si) {
     const JpegScanDev& S = scans[D.scan0 + si];
     // the previous scan's coefficient stores visible to every lane, its table reads done
@@ -1242,6 +1277,246 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
                 const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
                 int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
                 jpg_scan_block(br, T, S, k, blk, pred[k], eobrun);
+              }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- device: arithmetic-coded scans (jdarith.c, libjpeg 9d) ------------------------------------
+// The QM-coder (ITU-T T.81 Annex D) over each restart interval's unstuffed bytes, with libjpeg's
+// statistics per table (DC: 64 bins, AC: 256) reset at every interval, the DC conditioning of
+// the DAC parameters (L, U) and the AC split K, restated: decode_mcu (sequential) and
+// decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine.  The structure is the scan path's:
+// one wave per image, scans in file order, lanes over restart intervals (one lane without them:
+// an arithmetic-coded file decodes serially -- correct, not fast; such files are rare).
+#include "jpeg_aritab.inc"  // jpg_aritab[114]: T.81 Table D.2 + the fixed 0.5 state 113
+
+constexpr int JAR_DC = 64, JAR_AC = 256, JAR_LANE = 4 * JAR_DC + 4 * JAR_AC;  // stats bytes per lane
+
+struct ArithDec {
+  const uint8_t* p;
+  uint32_t i, end;  // byte cursor and the interval's end (past it libjpeg reads 0)
+  long long c;      // libjpeg's INT32 registers (long)
+  int a, ct;
+  bool bad;         // JWRN_ARITH_BAD_CODE: the rest of the interval decodes nothing
+};
+
+__device__ __forceinline__ int jar_decode(ArithDec& e, uint8_t* st) {
+  while (e.a < 0x8000) {  // renormalisation and data input (D.2.6)
+    if (--e.ct < 0) {
+      const int data = e.i < e.end ? (int)e.p[e.i] : 0;
+      ++e.i;
+      e.c = (e.c << 8) | data;
+      if ((e.ct += 8) < 0 && ++e.ct == 0) e.a = 0x8000;  // 2 initial bytes: a = 0x10000 below
+    }
+    e.a <<= 1;
+  }
+  int sv = *st;
+  const uint32_t qv = jpg_aritab[sv & 0x7F];
+  const int nl = (int)(qv & 0xFF), nm = (int)((qv >> 8) & 0xFF), qe = (int)(qv >> 16);
+  const int temp = e.a - qe;
+  e.a = temp;
+  const long long t2 = (long long)temp << e.ct;
+  if (e.c >= t2) {  // LPS path, with the conditional exchange (D.2.4 / D.2.5)
+    e.c -= t2;
+    if (e.a < qe) {
+      e.a = qe;
+      *st = (uint8_t)((sv & 0x80) ^ nm);
+    } else {
+      e.a = qe;
+      *st = (uint8_t)((sv & 0x80) ^ nl);
+      sv ^= 0x80;
+    }
+  } else if (e.a < 0x8000) {  // MPS path, conditional exchange
+    if (e.a < qe) {
+      *st = (uint8_t)((sv & 0x80) ^ nl);
+      sv ^= 0x80;
+    } else {
+      *st = (uint8_t)((sv & 0x80) ^ nm);
+    }
+  }
+  return sv >> 7;
+}
+
+// a DC difference (Figures F.19, F.21-F.24), updating the component's conditioning ctx
+__device__ int jar_dc_diff(ArithDec& e, uint8_t* dcs, int& ctx, int L, int U) {
+  uint8_t* st = dcs + ctx;
+  if (jar_decode(e, st) == 0) {
+    ctx = 0;
+    return 0;
+  }
+  const int sign = jar_decode(e, st + 1);
+  st += 2 + sign;
+  int m = jar_decode(e, st);
+  if (m) {
+    st = dcs + 20;  // X1
+    while (jar_decode(e, st)) {
+      if ((m <<= 1) == 0x8000) {
+        e.bad = true;
+        return 0;
+      }
+      ++st;
+    }
+  }
+  if (m < ((1 << L) >> 1)) ctx = 0;
+  else if (m > ((1 << U) >> 1)) ctx = 12 + sign * 4;
+  else ctx = 4 + sign * 4;
+  int v = m;
+  st += 14;
+  while (m >>= 1)
+    if (jar_decode(e, st)) v |= m;
+  v += 1;
+  return sign ? -v : v;
+}
+
+// an AC coefficient's value once its position k is known (st: the bins of its run, 3 (k - 1))
+__device__ int jar_ac_value(ArithDec& e, uint8_t* acs, uint8_t* st, int k, int K, uint8_t* fixed) {
+  const int sign = jar_decode(e, fixed);
+  st += 2;
+  int m = jar_decode(e, st);
+  if (m && jar_decode(e, st)) {
+    m <<= 1;
+    st = acs + (k <= K ? 189 : 217);
+    while (jar_decode(e, st)) {
+      if ((m <<= 1) == 0x8000) {
+        e.bad = true;
+        return 0;
+      }
+      ++st;
+    }
+  }
+  int v = m;
+  st += 14;
+  while (m >>= 1)
+    if (jar_decode(e, st)) v |= m;
+  v += 1;
+  return sign ? -v : v;
+}
+
+// one block of scan component k
+__device__ void jar_block(ArithDec& e, const JpegScanDev& S, int k, uint8_t* dcs, uint8_t* acs,
+                          uint8_t* fixed, int16_t* __restrict__ blk, int& last, int& ctx) {
+  const bool prog = S.kind != JPG_SEQ;
+  if (S.kind == JPG_SEQ || S.kind == JPG_DC_FIRST) {
+    last += jar_dc_diff(e, dcs, ctx, S.aL[k], S.aU[k]);
+    if (e.bad) return;
+    blk[0] = jpg_lshift(last, prog ? S.Al : 0);
+    if (prog) return;
+    int z = 0;  // sequential: AC 1..63
+    while (z < 63) {
+      uint8_t* st = acs + 3 * z;
+      if (jar_decode(e, st)) break;  // EOB
+      for (;;) {
+        ++z;
+        if (jar_decode(e, st + 1)) break;
+        st += 3;
+        if (z >= 63) {
+          e.bad = true;
+          return;
+        }
+      }
+      const int v = jar_ac_value(e, acs, st, z, S.aK[k], fixed);
+      if (e.bad) return;
+      blk[jpg_natural[z]] = (int16_t)v;
+    }
+  } else if (S.kind == JPG_DC_REFINE) {
+    if (jar_decode(e, fixed)) blk[0] = (int16_t)(blk[0] | (1 << S.Al));
+  } else if (S.kind == JPG_AC_FIRST) {
+    int z = S.Ss - 1;
+    while (z < S.Se) {
+      uint8_t* st = acs + 3 * z;
+      if (jar_decode(e, st)) break;
+      for (;;) {
+        ++z;
+        if (jar_decode(e, st + 1)) break;
+        st += 3;
+        if (z >= S.Se) {
+          e.bad = true;
+          return;
+        }
+      }
+      const int v = jar_ac_value(e, acs, st, z, S.aK[k], fixed);
+      if (e.bad) return;
+      blk[jpg_natural[z]] = jpg_lshift(v, S.Al);
+    }
+  } else {  // AC refine
+    const int p1 = 1 << S.Al, m1 = -(1 << S.Al);
+    int kex = S.Se;  // the previous stage's end of block
+    while (kex > 0 && blk[jpg_natural[kex]] == 0) --kex;
+    int z = S.Ss - 1;
+    while (z < S.Se) {
+      uint8_t* st = acs + 3 * z;
+      if (z >= kex && jar_decode(e, st)) break;
+      for (;;) {
+        int16_t* c = blk + jpg_natural[++z];
+        if (*c) {  // previously nonzero: a correction bit
+          if (jar_decode(e, st + 2)) *c = (int16_t)(*c < 0 ? *c + m1 : *c + p1);
+          break;
+        }
+        if (jar_decode(e, st + 1)) {  // newly nonzero
+          *c = (int16_t)(jar_decode(e, fixed) ? m1 : p1);
+          break;
+        }
+        st += 3;
+        if (z >= S.Se) {
+          e.bad = true;
+          return;
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restrict__ imgs,
+                                                        const JpegScanDev* __restrict__ scans,
+                                                        const uint8_t* __restrict__ ub,
+                                                        const uint32_t* __restrict__ ivstart,
+                                                        const uint32_t* __restrict__ ublen_s,
+                                                        int16_t* __restrict__ coef) {
+  __shared__ uint8_t stats[64 * JAR_LANE];
+  const JpegDev& D = imgs[blockIdx.x];
+  const uint32_t nscan = D.nscan;
+  if (nscan == 0 || !D.arith) return;  // uniform
+  uint8_t* mine = stats + threadIdx.x * JAR_LANE;
+  for (uint32_t si = 0; si < nscan; ++si) {
+    const JpegScanDev& S = scans[D.scan0 + si];
+    // the previous scan's coefficient stores visible to every lane
+    __threadfence();
+    __syncthreads();
+    for (int t = threadIdx.x; t < S.nintervals; t += 64) {
+      const uint32_t u0 = S.restart ? (uint32_t)t * (uint32_t)S.restart : 0u;
+      const uint32_t u1 = S.restart ? min(u0 + (uint32_t)S.restart, S.nunits) : S.nunits;
+      for (int k = 0; k < JAR_LANE; k += 16) *reinterpret_cast<uint4*>(mine + k) = make_uint4(0, 0, 0, 0);
+      ArithDec e;
+      e.p = ub + S.ub_off;
+      e.i = ivstart[S.iv_off + t] >> 3;
+      e.end = t + 1 < S.nintervals ? ivstart[S.iv_off + t + 1] >> 3 : ublen_s[D.scan0 + si];
+      e.c = 0;
+      e.a = 0;
+      e.ct = -16;
+      e.bad = false;
+      uint8_t fixed = 113;
+      int last[3] = {0, 0, 0}, ctx[3] = {0, 0, 0};
+      for (uint32_t u = u0; u < u1 && !e.bad; ++u) {
+        if (S.ns == 1) {
+          const int c = S.comp[0];
+          const uint32_t by = u / (uint32_t)D.wib[c], bx = u - by * (uint32_t)D.wib[c];
+          int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
+          jar_block(e, S, 0, mine + S.td[0] * JAR_DC, mine + 4 * JAR_DC + S.ta[0] * JAR_AC, &fixed,
+                    blk, last[0], ctx[0]);
+        } else {
+          const uint32_t my = u / (uint32_t)D.mcux, mx = u - my * (uint32_t)D.mcux;
+          for (int k = 0; k < S.ns && !e.bad; ++k) {
+            const int c = S.comp[k];
+            for (int dv = 0; dv < D.cv[c]; ++dv)
+              for (int dh = 0; dh < D.ch[c] && !e.bad; ++dh) {
+                const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
+                int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
+                jar_block(e, S, k, mine + S.td[k] * JAR_DC, mine + 4 * JAR_DC + S.ta[k] * JAR_AC,
+                          &fixed, blk, last[k], ctx[k]);
               }
           }
         }
@@ -1655,6 +1930,7 @@ struct JpegPlan {
   uint32_t nintervals = 0, nchunks = 0, max_items = 1, max_items_w = 1, nsub = 1;
   int mt_img = 1, mt_scan = 1;  // most unstuffing tiles of an image / of a scan
   bool any_chunked = false;
+  bool any_huff_scan = false, any_arith = false;  // scan-path images of each coding
   bool scales[2][2] = {};  // IDCT output scales present: [sv - 1][sh - 1]
   size_t off_imgs = 0, off_blkend = 0, off_scans = 0, off_scan = 0, off_coef = 0, off_planes = 0;
   size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_ublen_s = 0, off_s0 = 0, off_s1 = 0,
@@ -1770,6 +2046,7 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       return jpg_fail(err, "libjpeg-turbo block smoothing (progressive file with imprecise AC) "
                            "not supported");
     D.smooth = J.smooth ? 1 : 0;
+    D.arith = J.arith ? 1 : 0;
     D.rgb = jpg_color_space(J, turbo);
     if (D.rgb < 0) return jpg_fail(err, "big-gamut (BG_YCC / BG_RGB) JPEG not supported");
     memcpy(D.cbits, J.cbits, sizeof(D.cbits));
@@ -1787,6 +2064,7 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       D.nchunks = 0;
       D.scan0 = (uint32_t)P.scans.size();
       D.nscan = (uint32_t)J.scans.size();
+      (J.arith ? P.any_arith : P.any_huff_scan) = true;
       for (const ScanHost& S : J.scans) {
         JpegScanDev SD;
         memset(&SD, 0, sizeof(SD));
@@ -1805,9 +2083,17 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
                               : (uint32_t)mcus;
         SD.nintervals = S.restart ? (int)((SD.nunits + S.restart - 1) / S.restart) : 1;
         if (SD.nintervals < 1) SD.nintervals = 1;
+        SD.arith = J.arith ? 1 : 0;
+        for (int k = 0; k < 3; ++k) {
+          SD.td[k] = S.td[k];
+          SD.ta[k] = S.ta[k];
+          SD.aL[k] = S.aL[k];
+          SD.aU[k] = S.aU[k];
+          SD.aK[k] = S.aK[k];
+        }
         for (int sl = 0; sl < 6; ++sl)
           for (int k = 0; k < 18; ++k) SD.maxcode[sl][k] = -1;
-        for (int k = 0; k < S.ns && tables; ++k) {
+        for (int k = 0; k < S.ns && tables && !J.arith; ++k) {
           const bool dc = SD.kind == JPG_SEQ || SD.kind == JPG_DC_FIRST;
           const bool ac = SD.kind == JPG_SEQ || SD.kind == JPG_AC_FIRST || SD.kind == JPG_AC_REFINE;
           if (dc) {
@@ -2077,8 +2363,13 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   const dim3 gwrite((P.max_items_w + 63) / 64, n);
   hipLaunchKernelGGL(jpeg_write_kernel, gwrite, dim3(64), 0, st, dimg, ub, ublen, ivs, ck_st, ck_co,
                      cstart, coef);
-  if (!P.scans.empty())
-    hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, coef);
+  if (!P.scans.empty()) {
+    if (P.any_huff_scan)
+      hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, coef);
+    if (P.any_arith)
+      hipLaunchKernelGGL(jpeg_arith_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs,
+                         reinterpret_cast<const uint32_t*>(ws + P.off_ublen_s), coef);
+  }
   const uint64_t gb = (P.nblk + 255) / 256;
   IDN_CHECK_ARG(gb < 0x7FFFFFFF, "idn_jpeg_decode_u8: batch too large");
   const uint64_t* bend = reinterpret_cast<const uint64_t*>(ws + P.off_blkend);

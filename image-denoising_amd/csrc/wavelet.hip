@@ -736,7 +736,12 @@ template <> struct WsRaw<3> {  // the level above's 'aa', three channels, fp32 (
 #ifndef IDN_WS_PF3  // the fp32 'aa' input of levels >= 2: a 5-step ring measured 2.773 -> 2.752 ms on
 #define IDN_WS_PF3 5  // the op against 1 (levels 2 / 3: 283 -> 264 / 92 -> 88 us, profiles/r04/wavelet/)
 #endif
-template <int SRC> constexpr int ws_pf() { return SRC == 0 ? IDN_WS_PF0 : SRC == 3 ? IDN_WS_PF3 : 1; }
+#ifndef IDN_WS_PF1  // the live path's fp64 pixels (A/B builds set it)
+#define IDN_WS_PF1 1
+#endif
+template <int SRC> constexpr int ws_pf() {
+  return SRC == 0 ? IDN_WS_PF0 : SRC == 3 ? IDN_WS_PF3 : SRC == 1 ? IDN_WS_PF1 : 1;
+}
 
 
 // TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the

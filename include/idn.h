@@ -331,12 +331,13 @@ int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int
 
 /* Header of one JPEG file in host memory (SOI .. EOI): height, width, components (1 or 3).
  * Taken: Huffman-coded baseline, extended sequential and progressive files (SOF0 / SOF1 / SOF2),
- * one or several scans, restart intervals, 4:4:4 / 4:2:2 / 4:2:0 or grayscale; a progressive
+ * arithmetic-coded sequential and progressive files (SOF9 / SOF10, DAC conditioning), one or
+ * several scans, restart intervals, 4:4:4 / 4:2:2 / 4:2:0 or grayscale; a progressive
  * file whose last scan leaves AC 1..5 imprecise is block-smoothed as libjpeg 9d smooths it
  * (jdcoefct.c smoothing_ok / decompress_smooth_data); three components are YCbCr or RGB as
  * libjpeg decides it (component IDs, JFIF / Adobe markers).  IDN_EUNSUPPORTED for anything else
- * (arithmetic-coded, lossless, hierarchical, 12-bit, CMYK / YCCK, big-gamut colour, DHP / EXP /
- * JPGn / LSE markers, other chroma sampling). */
+ * (lossless, hierarchical, 12-bit, CMYK / YCCK, big-gamut colour, DHP / EXP / JPGn / LSE
+ * markers, other chroma sampling). */
 int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
 
 /* idn_jpeg_decode_u8 flags.  Default (0): the decode of the reference's pinned libjpeg 9d

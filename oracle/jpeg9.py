@@ -10,6 +10,10 @@ reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
                progressive (decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine: spectral
                selection, successive approximation, EOB runs), one or several scans; a
                non-interleaved scan codes only the component's own blocks (width_in_blocks)
+  jdarith.c    arithmetic-coded files (SOF9 / SOF10): the QM-coder with libjpeg's statistics bins
+               (DC 64 / AC 256 per table, reset per restart interval), the DC conditioning of the
+               DAC parameters L / U and the AC split K; decode_mcu and the four progressive
+               decoders (T.81 Table D.2 from oracle/jpeg_aritab.py)
   jdcoefct.c   progressive files are decoded into the whole coefficient buffer first; block
                smoothing (do_block_smoothing, smoothing_ok) then applies only if every component
                has DC data and nonzero quantisers Q00 Q01 Q10 Q20 Q11 Q02, and some component's AC
@@ -236,6 +240,220 @@ def _decode_scan(sc, comps, coef, geo, dc, ac):
             u += 1
 
 
+# ---- arithmetic decoding (jdarith.c, libjpeg 9d) -------------------------------------------------
+from oracle.jpeg_aritab import ARITAB  # noqa: E402  (T.81 Table D.2, generated)
+
+
+class _Arith:
+    """the QM-coder decoder over one restart interval's (unstuffed) bytes; past their end it reads
+    0 (libjpeg supplies zeros once the interval's marker is reached)"""
+
+    def __init__(self, buf: bytes):
+        self.buf, self.i = buf, 0
+        self.c, self.a, self.ct = 0, 0, -16  # force reading 2 initial bytes
+
+    def decode(self, st, k):
+        """arith_decode on statistics bin st[k] (a bytearray slot)"""
+        while self.a < 0x8000:
+            self.ct -= 1
+            if self.ct < 0:
+                data = self.buf[self.i] if self.i < len(self.buf) else 0
+                self.i += 1
+                self.c = (self.c << 8) | data
+                self.ct += 8
+                if self.ct < 0:
+                    self.ct += 1
+                    if self.ct == 0:
+                        self.a = 0x8000  # got 2 initial bytes: a = 0x10000 after the shift
+            self.a <<= 1
+        sv = st[k]
+        qe = ARITAB[sv & 0x7F]
+        nl, nm, qe = qe & 0xFF, (qe >> 8) & 0xFF, qe >> 16
+        temp = self.a - qe
+        self.a = temp
+        temp <<= self.ct
+        if self.c >= temp:
+            self.c -= temp
+            if self.a < qe:  # conditional LPS exchange
+                self.a = qe
+                st[k] = (sv & 0x80) ^ nm
+            else:
+                self.a = qe
+                st[k] = (sv & 0x80) ^ nl
+                sv ^= 0x80
+        elif self.a < 0x8000:  # conditional MPS exchange
+            if self.a < qe:
+                st[k] = (sv & 0x80) ^ nl
+                sv ^= 0x80
+            else:
+                st[k] = (sv & 0x80) ^ nm
+        return sv >> 7
+
+
+class _BadCode(Exception):
+    """jdarith.c's JWRN_ARITH_BAD_CODE: the rest of the interval decodes nothing (ct = -1)"""
+
+
+def _arith_dc_diff(ar, dcs, ci, ctx, L, U):
+    """Figures F.19 / F.21-F.24: a DC difference, updating the conditioning ctx[ci]"""
+    s0 = ctx[ci]
+    if ar.decode(dcs, s0) == 0:
+        ctx[ci] = 0
+        return 0
+    sign = ar.decode(dcs, s0 + 1)
+    st = s0 + 2 + sign
+    m = ar.decode(dcs, st)
+    if m:
+        st = 20  # X1
+        while ar.decode(dcs, st):
+            m <<= 1
+            if m == 0x8000:
+                raise _BadCode
+            st += 1
+    if m < (1 << L) >> 1:
+        ctx[ci] = 0
+    elif m > (1 << U) >> 1:
+        ctx[ci] = 12 + sign * 4
+    else:
+        ctx[ci] = 4 + sign * 4
+    v = m
+    st += 14
+    m >>= 1
+    while m:
+        if ar.decode(dcs, st):
+            v |= m
+        m >>= 1
+    v += 1
+    return -v if sign else v
+
+
+def _arith_ac_value(ar, acs, st, k, K, fixed):
+    """Figures F.21-F.24 for an AC coefficient whose statistics run starts at st (= 3 (k - 1))"""
+    sign = ar.decode(fixed, 0)
+    st += 2
+    m = ar.decode(acs, st)
+    if m:
+        if ar.decode(acs, st):
+            m <<= 1
+            st = 189 if k <= K else 217
+            while ar.decode(acs, st):
+                m <<= 1
+                if m == 0x8000:
+                    raise _BadCode
+                st += 1
+    v = m
+    st += 14
+    m >>= 1
+    while m:
+        if ar.decode(acs, st):
+            v |= m
+        m >>= 1
+    v += 1
+    return -v if sign else v
+
+
+def _decode_scan_arith(sc, comps, coef, geo, dac):
+    """one arithmetic-coded scan (jdarith.c decode_mcu, decode_mcu_DC_first / _AC_first /
+    _DC_refine / _AC_refine): statistics bins per table, reset with the DC predictions and the
+    conditioning at every restart interval"""
+    Ss, Se, Ah, Al = sc["Ss"], sc["Se"], sc["Ah"], sc["Al"]
+    sel = sc["sel"]
+    prog = sc["progressive"]
+    if len(sel) == 1:
+        ci = sel[0][0]
+        units = [[(ci, by, bx)] for by in range(geo["hib"][ci]) for bx in range(geo["wib"][ci])]
+    else:
+        units = []
+        for my in range(geo["mcuy"]):
+            for mx in range(geo["mcux"]):
+                units.append([(ci, my * comps[ci]["v"] + dv, mx * comps[ci]["h"] + dh)
+                              for ci, _, _ in sel for dv in range(comps[ci]["v"])
+                              for dh in range(comps[ci]["h"])])
+    tbl = {ci: (td, ta) for ci, td, ta in sel}
+    per = sc["restart"] if sc["restart"] else len(units)
+    p1, m1 = 1 << Al, -(1 << Al)
+    u = 0
+    for iv in sc["intervals"]:
+        if u >= len(units):
+            break
+        ar = _Arith(iv)
+        dcs = {t: bytearray(64) for t in range(16)}
+        acs = {t: bytearray(256) for t in range(16)}
+        fixed = bytearray([113])
+        last = {ci: 0 for ci, _, _ in sel}
+        ctx = {ci: 0 for ci, _, _ in sel}
+        bad = False
+        for _ in range(min(per, len(units) - u)):
+            if bad:
+                u += 1
+                continue
+            try:
+                for ci, by, bx in units[u]:
+                    blk = coef[ci][by, bx]
+                    td, ta = tbl[ci]
+                    if not prog or (Ss == 0 and Ah == 0):  # DC of a sequential / DC-first scan
+                        last[ci] += _arith_dc_diff(ar, dcs[td], ci, ctx, dac["L"][td], dac["U"][td])
+                        blk[0] = last[ci] << (Al if prog else 0)
+                        if prog:
+                            continue
+                        k = 0  # sequential: the AC coefficients 1..63
+                        while k < 63:
+                            st = 3 * k
+                            if ar.decode(acs[ta], st):
+                                break  # EOB
+                            while True:
+                                k += 1
+                                if ar.decode(acs[ta], st + 1):
+                                    break
+                                st += 3
+                                if k >= 63:
+                                    raise _BadCode
+                            blk[_nat(k)] = _arith_ac_value(ar, acs[ta], st, k, dac["K"][ta], fixed)
+                    elif Ss == 0:  # DC refine: the next bit of the two's-complement value
+                        if ar.decode(fixed, 0):
+                            blk[0] |= p1
+                    elif Ah == 0:  # AC first
+                        k = Ss - 1
+                        while k < Se:
+                            st = 3 * k
+                            if ar.decode(acs[ta], st):
+                                break
+                            while True:
+                                k += 1
+                                if ar.decode(acs[ta], st + 1):
+                                    break
+                                st += 3
+                                if k >= Se:
+                                    raise _BadCode
+                            blk[_nat(k)] = _arith_ac_value(ar, acs[ta], st, k, dac["K"][ta],
+                                                           fixed) << Al
+                    else:  # AC refine
+                        kex = Se
+                        while kex > 0 and not blk[_nat(kex)]:
+                            kex -= 1
+                        k = Ss - 1
+                        while k < Se:
+                            st = 3 * k
+                            if k >= kex and ar.decode(acs[ta], st):
+                                break
+                            while True:
+                                k += 1
+                                pos = _nat(k)
+                                if blk[pos]:
+                                    if ar.decode(acs[ta], st + 2):
+                                        blk[pos] += m1 if blk[pos] < 0 else p1
+                                    break
+                                if ar.decode(acs[ta], st + 1):
+                                    blk[pos] = m1 if ar.decode(fixed, 0) else p1
+                                    break
+                                st += 3
+                                if k >= Se:
+                                    raise _BadCode
+            except _BadCode:
+                bad = True
+            u += 1
+
+
 def parse_and_decode(data: bytes):
     """-> dict(width, height, comps=[(h, v, q[64] natural)], coef=[int64 (bh, bw, 64) natural])
 
@@ -244,6 +462,9 @@ def parse_and_decode(data: bytes):
     assert data[:2] == b"\xff\xd8", "no SOI"
     q, dc, ac, comps, restart = {}, {}, {}, [], 0
     jfif, adobe = False, None
+    arith = False
+    # arithmetic conditioning per table (jdmarker.c get_soi defaults: L 0, U 1, K 5)
+    dac = dict(L=[0] * 16, U=[1] * 16, K=[5] * 16)
     W = H = 0
     progressive = None
     coef = geo = None
@@ -262,9 +483,10 @@ def parse_and_decode(data: bytes):
         ln = (data[i] << 8) | data[i + 1]
         s = data[i + 2:i + ln]
         end = i + ln
-        if m in (0xC0, 0xC1, 0xC2):
+        if m in (0xC0, 0xC1, 0xC2, 0xC9, 0xCA):
             assert s[0] == 8
-            progressive = m == 0xC2
+            progressive = m in (0xC2, 0xCA)
+            arith = m in (0xC9, 0xCA)
             H, W, nc = (s[1] << 8) | s[2], (s[3] << 8) | s[4], s[5]
             comps = [dict(id=s[6 + 3 * c], h=s[7 + 3 * c] >> 4, v=s[7 + 3 * c] & 15,
                           tq=s[8 + 3 * c]) for c in range(nc)]
@@ -319,12 +541,26 @@ def parse_and_decode(data: bytes):
             intervals, end = _entropy(data, end)
             sc = dict(sel=sel, Ss=ss[0], Se=ss[1], Ah=ss[2] >> 4, Al=ss[2] & 15,
                       progressive=progressive, restart=restart, intervals=intervals)
-            _decode_scan(sc, comps, coef, geo, dc, ac)
+            if arith:
+                _decode_scan_arith(sc, comps, coef, geo, dac)
+            else:
+                _decode_scan(sc, comps, coef, geo, dc, ac)
             for ci, _, _ in sel:  # jdphuff.c start_pass: coef_bits[k] = Al for k in Ss..Se
                 for k in range(sc["Ss"], min(sc["Se"], 5) + 1):
                     cbits[ci][k] = sc["Al"]
+        elif m == 0xCC:  # DAC (jdmarker.c get_dac): conditioning of arithmetic tables
+            for k in range(0, len(s) - 1, 2):
+                idx, val = s[k], s[k + 1]
+                if idx >= 32:
+                    raise ValueError("bad DAC table index")
+                if idx >= 16:
+                    dac["K"][idx - 16] = val
+                else:
+                    dac["L"][idx], dac["U"][idx] = val & 15, val >> 4
+                    if dac["L"][idx] > dac["U"][idx]:
+                        raise ValueError("bad DAC value")
         elif 0xC3 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
-            raise ValueError("lossless / arithmetic / hierarchical JPEG not supported")
+            raise ValueError("lossless / hierarchical JPEG not supported")
         i = end
     assert coef is not None, "no frame"
     # jdcoefct.c smoothing_ok (libjpeg 9d): FALSE unless EVERY component has DC data and nonzero

@@ -121,6 +121,7 @@ def derived():
     (OUT / "prog_q0_cut_s444_96x128.jpg").write_bytes(bytes(cut))
     smoothed()
     colorspaces()
+    arithmetic()
 
 
 def _segments(data):
@@ -182,6 +183,30 @@ def colorspaces():
     # Adobe transform 1 with IDs 'R' 'G' 'B': RGB for libjpeg 9 (IDs), YCbCr for turbo (Adobe)
     _recolor("s422_q85_120x200.jpg", "cs_adobe1_rgbids_s422_120x200.jpg", ids=(R, G, B), jfif=False,
              adobe=1)
+
+
+JPEGTRAN = Path("/opt/conda/bin/jpegtran")  # IJG libjpeg 9's jpegtran (the conda build)
+
+
+def arithmetic():
+    """arithmetic-coded files (SOF9 sequential / SOF10 progressive, QM-coder), losslessly
+    transcoded from Huffman fixtures by libjpeg 9's jpegtran -arithmetic: what cv2.imread's
+    libjpeg 9d decodes and libjpeg-turbo builds without arithmetic support refuse"""
+    import subprocess
+
+    def tran(src, name, *args):
+        out = subprocess.run([str(JPEGTRAN), "-arithmetic", *args, str(OUT / src)],
+                             capture_output=True, check=True).stdout
+        (OUT / name).write_bytes(out)
+
+    tran("s444_q95_96x128.jpg", "arith_s444_96x128.jpg")
+    tran("s420_q75_odd_37x53.jpg", "arith_s420_odd_37x53.jpg")
+    tran("s422_q85_120x200.jpg", "arith_rst_s422_120x200.jpg", "-restart", "1")
+    tran("gray_q80_91x77.jpg", "arith_prog_gray_91x77.jpg", "-progressive")
+    tran("s420_q75_odd_37x53.jpg", "arith_prog_s420_odd_37x53.jpg", "-progressive")
+    tran("s444_q95_96x128.jpg", "arith_prog_rst_s444_96x128.jpg", "-progressive", "-restart", "1")
+    # progressive arithmetic cut before its last two scans: block smoothing on arithmetic data
+    _keep_scans("arith_prog_rst_s444_96x128.jpg", set(range(8)), "arith_prog_smooth_s444_96x128.jpg")
 
 
 def _keep_scans(src, keep, name):

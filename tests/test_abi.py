@@ -139,12 +139,13 @@ def test_header_jpeg_support_matches_decoder():
     info = hdr[hdr.index("/* Header of one JPEG file"):hdr.index("int idn_jpeg_info")]
     taken, unsupported = info.split("IDN_EUNSUPPORTED", 1)
     accepted_sof = set(re.findall(r"case 0x(C[0-9A-F])", src.split("// DHT")[0]))
-    kinds = {"C0": "baseline", "C1": "extended sequential", "C2": "progressive"}
+    kinds = {"C0": "baseline", "C1": "extended sequential", "C2": "progressive",
+             "C9": "arithmetic", "CA": "arithmetic"}
     for code, word in kinds.items():
         if code in accepted_sof:
             assert word in taken and word not in unsupported, word
     assert "multi-scan" not in unsupported and "several scans" in taken
-    assert "arithmetic" in unsupported and "lossless" in unsupported
+    assert "lossless" in unsupported and "hierarchical" in unsupported
     # block smoothing (jpg_smooth) is restated: the header lists it among what is taken
     assert "jpg_smooth(D" in src and "block-smoothed" in taken and "smooth" not in unsupported
     dec = hdr[hdr.index("/* cv2.imread(path) (IMREAD_COLOR) of n"):hdr.index("int idn_jpeg_decode_u8")]

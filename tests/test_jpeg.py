@@ -23,10 +23,10 @@ def _files():
     return sorted(JPEG.glob("*.jpg"))
 
 
-def _arith(data: bytes) -> bytes:
-    """the same file relabelled arithmetic-coded (SOF0 -> SOF9): a format the decoder rejects"""
+def _lossless(data: bytes) -> bytes:
+    """the same file relabelled lossless (SOF0 -> SOF3): a format the decoder rejects"""
     k = data.index(b"\xff\xc0")
-    return data[:k + 1] + b"\xc9" + data[k + 2:]
+    return data[:k + 1] + b"\xc3" + data[k + 2:]
 
 
 def _sos_offsets(data: bytes):
@@ -67,7 +67,9 @@ def test_oracle_libjpeg9_matches_real_libjpeg9(name):
                                   "s444_q95_96x128.jpg", "s420_q75_odd_37x53.jpg",
                                   "progressive_64x64.jpg", "prog_s422_q75_odd_45x67.jpg",
                                   "prog_s420_rst4_120x160.jpg", "prog_gray_q80_91x77.jpg"] +
-                         [p.name for p in _files() if p.name.startswith("cs_")])
+                         [p.name for p in _files() if p.name.startswith("cs_")] +
+                         [p.name for p in _files() if p.name.startswith("arith_") and
+                          "smooth" not in p.name])
 def test_oracle_turbo_mode_matches_system_pil(name):
     from PIL import Image
     from oracle import jpeg9
@@ -97,8 +99,8 @@ def test_unsupported_and_corrupt_raise():
     from idn import ops
     from idn._lib import IdnError
     assert ops.jpeg_info((JPEG / "progressive_64x64.jpg").read_bytes()) == (64, 64, 3)
-    with pytest.raises(IdnError, match="arithmetic"):
-        ops.jpeg_info(_arith((JPEG / "s444_q95_96x128.jpg").read_bytes()))
+    with pytest.raises(IdnError, match="lossless"):
+        ops.jpeg_info(_lossless((JPEG / "s444_q95_96x128.jpg").read_bytes()))
     with pytest.raises(IdnError, match="SOI"):
         ops.jpeg_info(b"not a jpeg at all")
     data = (JPEG / "s444_q95_96x128.jpg").read_bytes()
@@ -115,7 +117,7 @@ def _ws(datas, flags=0):
 def test_workspace_size():
     datas = [p.read_bytes() for p in _files()[:3]]
     assert _ws(datas) > sum(map(len, datas))
-    assert _ws([_arith((JPEG / "s444_q95_96x128.jpg").read_bytes())]) == 0
+    assert _ws([_lossless((JPEG / "s444_q95_96x128.jpg").read_bytes())]) == 0
     assert _ws([(JPEG / "progressive_64x64.jpg").read_bytes()]) > 0
     # libjpeg 9's full-size chroma planes need more room than turbo's subsampled ones
     d = [(JPEG / "s420_q90_600x1000.jpg").read_bytes()]
@@ -278,3 +280,21 @@ def test_extension_markers_and_big_gamut_are_rejected():
         bg[k + 10 + 3 * c] = v
     with pytest.raises(ValueError):
         jpeg9.imread(bytes(bg))
+
+
+def test_arithmetic_fixtures_cover_the_coder():
+    """arithmetic-coded fixtures (jpegtran -arithmetic of libjpeg 9, tests/golden/make_jpeg_fixtures.py
+    arithmetic()): SOF9 sequential and SOF10 progressive, restart intervals, 4:4:4 / 4:2:2 /
+    4:2:0 / grayscale, and a cut progressive file that is block-smoothed.  Their pixels are pinned
+    by test_oracle_libjpeg9_matches_real_libjpeg9; the host parser takes them"""
+    from idn import ops
+    from oracle import jpeg9
+    names = [p.name for p in _files() if p.name.startswith("arith_")]
+    sofs, rst, smooth = set(), False, False
+    for name in names:
+        data = (JPEG / name).read_bytes()
+        sofs |= {m for m in (0xC9, 0xCA) if bytes([0xFF, m]) in data[:data.find(b"\xff\xda")]}
+        rst |= b"\xff\xdd" in data
+        smooth |= jpeg9.parse_and_decode(data)["smooth"] is not None
+        assert ops.jpeg_info(data)[2] in (1, 3)
+    assert len(names) >= 7 and sofs == {0xC9, 0xCA} and rst and smooth

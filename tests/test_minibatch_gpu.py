@@ -142,12 +142,12 @@ def test_apply_noise_gpu_decode(dev):
     random.seed(2)
     b = detect_blob.apply_noise(px, "gaussian_wavelet_var0.1", noise_rng="philox", image_id=4)
     assert a.dtype == b.dtype and np.array_equal(a, b)
-    # no silent CPU fallback for files the decoder does not take (arithmetic coding)
-    from test_jpeg import _arith
+    # no silent CPU fallback for files the decoder does not take (lossless coding)
+    from test_jpeg import _lossless
     import tempfile
     with tempfile.TemporaryDirectory() as d:
-        bad = Path(d) / "arith.jpg"
-        bad.write_bytes(_arith((gold / "jpeg" / "s444_q95_96x128.jpg").read_bytes()))
+        bad = Path(d) / "lossless.jpg"
+        bad.write_bytes(_lossless((gold / "jpeg" / "s444_q95_96x128.jpg").read_bytes()))
         with pytest.raises(IdnError):
             detect_blob.apply_noise(bad, "original", decode="gpu")
     # a progressive file is decoded (the scan path), as cv2.imread does
