@@ -22,15 +22,16 @@
 //                        16x16 / 16x8 for libjpeg 9's scaled chroma) into u8 component planes
 //   3 jpeg_color8_kernel 8 output pixels per thread: chroma upsampling (turbo only) + YCbCr -> BGR
 //                        (or gray -> BGR), written into the caller's NHWC batch
-// Supported: 8-bit Huffman JPEG, 1 or 3 components, sampling 4:4:4 / 4:2:2 (h2v1) / 4:2:0 (h2v2),
+// Supported: 8-bit Huffman JPEG, 1, 3 or 4 components, sampling 4:4:4 / 4:2:2 (h2v1) / 4:2:0 (h2v2),
 // optional restart intervals: baseline / extended sequential (SOF0 / SOF1) with one interleaved
 // scan (the parallel path above), and progressive (SOF2) or multi-scan sequential files (the scan
 // path: jpeg_prog_kernel, one wave per image, scans in file order, restart intervals across the
 // lanes), with libjpeg 9d's block smoothing of progressive files whose last scan leaves AC 1..5
 // imprecise (jpg_smooth); arithmetic-coded files (SOF9 / SOF10) through the scan path's QM-coder
 // (jpeg_arith_kernel).  Three-component files are YCbCr or RGB as each library decides it
-// (jpg_color_space: JFIF / Adobe markers, component IDs).  Anything else (lossless, hierarchical,
-// 12-bit, CMYK / YCCK, big-gamut colour, extension markers) is IDN_EUNSUPPORTED.
+// (jpg_color_space: JFIF / Adobe markers, component IDs); four-component CMYK / YCCK files go
+// through the scan path to libjpeg's CMYK and OpenCV's CMYK -> BGR.  Anything else (lossless,
+// hierarchical, 12-bit, big-gamut colour, extension markers) is IDN_EUNSUPPORTED.
 #include "idn_common.hpp"
 
 #include <string.h>
@@ -53,28 +54,28 @@ struct JpegDev {
   uint32_t scan_len;
   int width, height, ncomp, mcux, mcuy, restart;  // restart: MCUs per interval (0: none)
   int hmax, vmax, nintervals;
-  int ch[3], cv[3], tq[3], td[3], ta[3];
-  int bw[3], bh[3];         // blocks per row / column of each component plane (MCU-padded)
-  int sh[3], sv[3];         // IDCT output scale per component: 1 (8 samples) or 2 (16 samples)
-  int pw[3];                // component plane row pitch in bytes (bw * 8 * sh)
-  int dw[3], dh[3];         // component plane size after the IDCT (libjpeg downsampled_width)
+  int ch[4], cv[4], tq[4], td[4], ta[4];
+  int bw[4], bh[4];         // blocks per row / column of each component plane (MCU-padded)
+  int sh[4], sv[4];         // IDCT output scale per component: 1 (8 samples) or 2 (16 samples)
+  int pw[4];                // component plane row pitch in bytes (bw * 8 * sh)
+  int dw[4], dh[4];         // component plane size after the IDCT (libjpeg downsampled_width)
   int up;                   // chroma upsampling: 0 none (full-size planes), 1 h2v1, 2 h2v2 fancy
   int cb_g;                 // jdcolor.c Cb -> G multiplier: libjpeg 9 22553, turbo 22554
-  int rgb;                  // 1: the components are R, G, B (no colour conversion; jpg_color_space)
-  uint64_t blk_off[3];      // first block of each component in the batch coefficient buffer
-  uint64_t pl_off[3];       // component plane byte offset in the batch plane buffer
+  int rgb;                  // jpg_color_space: 0 YCbCr, 1 RGB, 2 CMYK, 3 YCCK
+  uint64_t blk_off[4];      // first block of each component in the batch coefficient buffer
+  uint64_t pl_off[4];       // component plane byte offset in the batch plane buffer
   uint64_t ub_off;          // unstuffed entropy bytes (workspace), capacity scan_len + 64
   uint32_t iv_off;          // first entry of the image's interval-start table (bits)
   uint32_t ch_off, nchunks; // the image's chunks in the batch chunk arrays
   uint32_t chunk_bits;
   int bpm;                  // blocks per MCU (1 for a single-component scan)
   uint32_t total_blocks;    // MCUs x bpm
-  int wib[3], hib[3];       // blocks with data per component row / column (jdinput.c
+  int wib[4], hib[4];       // blocks with data per component row / column (jdinput.c
                             // width_in_blocks): what a non-interleaved scan codes
   uint32_t scan0, nscan;    // scan path: the image's scans in the batch scan table (0: none)
   int arith;                // arithmetic-coded (the scan path's jpeg_arith_kernel)
   int smooth;               // libjpeg 9d block smoothing (jdcoefct.c decompress_smooth_data)
-  int8_t cbits[3][6];       // its coef_bits latch per component (zigzag 0..5; -1: never coded)
+  int8_t cbits[4][6];       // its coef_bits latch per component (zigzag 0..5; -1: never coded)
   uint8_t ph_comp[10], ph_dv[10], ph_dh[10];  // block of the MCU -> component, block row, column
   uint16_t q[4][64];        // quantisation tables, natural order
   uint16_t lut[4][1 << JPG_LUTB];  // [DC0, DC1, AC0, AC1]: len << 8 | symbol, 0 = longer code
@@ -84,7 +85,7 @@ struct JpegDev {
 };
 
 // one scan of the scan path (progressive / multi-scan files).  Table slots: k = the DC table of
-// scan component k, 3 + k = its AC table (only the slots the scan's kind reads are filled).
+// scan component k, 4 + k = its AC table (only the slots the scan's kind reads are filled).
 enum { JPG_SEQ = 0, JPG_DC_FIRST = 1, JPG_DC_REFINE = 2, JPG_AC_FIRST = 3, JPG_AC_REFINE = 4 };
 struct JpegScanDev {
   uint64_t scan_off;        // entropy-coded bytes in the batch buffer (unstuffed like JpegDev's)
@@ -92,14 +93,14 @@ struct JpegScanDev {
   uint64_t ub_off;
   uint32_t iv_off;
   int nintervals;
-  int img, ns, comp[3], Ss, Se, Ah, Al, restart, kind;
+  int img, ns, comp[4], Ss, Se, Ah, Al, restart, kind;
   uint32_t nunits;          // MCUs (interleaved) or the component's blocks (non-interleaved)
   int arith;                // arithmetic-coded: the statistics of tables td / ta per scan component,
-  int td[3], ta[3];         // conditioned by aL / aU (DC) and aK (AC); no Huffman tables
-  uint8_t aL[3], aU[3], aK[3];
-  uint16_t lut[6][1 << JPG_LUTB];
-  int32_t maxcode[6][18], valoff[6][18];
-  uint8_t huffval[6][256];
+  int td[4], ta[4];         // conditioned by aL / aU (DC) and aK (AC); no Huffman tables
+  uint8_t aL[4], aU[4], aK[4];
+  uint16_t lut[8][1 << JPG_LUTB];
+  int32_t maxcode[8][18], valoff[8][18];
+  uint8_t huffval[8][256];
 };
 
 // jpeg_natural_order: zigzag index -> natural (row-major) index
@@ -122,15 +123,15 @@ struct HuffSpec {
 // one scan of a progressive / multi-scan file: its components (frame indices), their tables as
 // defined when the scan starts, spectral band and successive-approximation bits, restart interval
 struct ScanHost {
-  int ns = 0, comp[3] = {}, Ss = 0, Se = 63, Ah = 0, Al = 0, restart = 0;
-  HuffSpec dc[3], ac[3];  // per scan component
-  int td[3] = {}, ta[3] = {};                   // its table numbers
-  uint8_t aL[3] = {}, aU[3] = {}, aK[3] = {};  // arithmetic conditioning of those tables (DAC)
+  int ns = 0, comp[4] = {}, Ss = 0, Se = 63, Ah = 0, Al = 0, restart = 0;
+  HuffSpec dc[4], ac[4];  // per scan component
+  int td[4] = {}, ta[4] = {};                   // its table numbers
+  uint8_t aL[4] = {}, aU[4] = {}, aK[4] = {};  // arithmetic conditioning of those tables (DAC)
   size_t begin = 0, end = 0;
 };
 struct JpegHost {
   int width = 0, height = 0, ncomp = 0, restart = 0;
-  int cid[3] = {}, ch[3] = {}, cv[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
+  int cid[4] = {}, ch[4] = {}, cv[4] = {}, tq[4] = {}, td[4] = {}, ta[4] = {};
   bool qpresent[4] = {};
   uint16_t q[4][64] = {};  // natural order
   HuffSpec dc[4], ac[4];
@@ -143,7 +144,7 @@ struct JpegHost {
   int adobe_transform = 0;
   bool progressive = false;
   bool smooth = false;      // libjpeg 9d block-smooths the file (jpg_scans_done)
-  int8_t cbits[3][6] = {};  // its coef_bits latch: per component, zigzag 0..5 (-1: never coded)
+  int8_t cbits[4][6] = {};  // its coef_bits latch: per component, zigzag 0..5 (-1: never coded)
   std::vector<ScanHost> scans;  // the scan path (progressive or multi-scan); empty: one scan
 };
 
@@ -177,7 +178,7 @@ static int jpg_fail(std::string* err, const char* msg) {
 static int jpg_scans_done(JpegHost& J, std::string* err) {
   if (J.scans.empty()) return jpg_fail(err, "no SOS");
   if (J.progressive) {
-    int bits[3][6];
+    int bits[4][6];
     for (auto& b : bits)
       for (int& v : b) v = -1;
     for (const ScanHost& S : J.scans)
@@ -230,7 +231,8 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         J.height = (s[1] << 8) | s[2];
         J.width = (s[3] << 8) | s[4];
         J.ncomp = s[5];
-        if (J.ncomp != 1 && J.ncomp != 3) return jpg_fail(err, "only 1 or 3 components");
+        if (J.ncomp != 1 && J.ncomp != 3 && J.ncomp != 4)
+          return jpg_fail(err, "only 1, 3 or 4 components");
         if (sl < 6 + 3 * (size_t)J.ncomp || J.width <= 0 || J.height <= 0)
           return jpg_fail(err, "bad SOF");
         for (int c = 0; c < J.ncomp; ++c) {
@@ -317,11 +319,12 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
         if (sl < 1) return jpg_fail(err, "bad SOS");
         const int ns = s[0];
         if (ns < 1 || ns > J.ncomp || sl < 1 + 2 * (size_t)ns + 3) return jpg_fail(err, "bad SOS");
-        if (J.ncomp == 3) {
+        if (J.ncomp >= 3) {  // (a fourth component, K, sampled as the first)
           const bool s444 = J.ch[0] == 1 && J.cv[0] == 1;
           const bool s422 = J.ch[0] == 2 && J.cv[0] == 1;
           const bool s420 = J.ch[0] == 2 && J.cv[0] == 2;
-          if (!(s444 || s422 || s420) || J.ch[1] != 1 || J.cv[1] != 1 || J.ch[2] != 1 || J.cv[2] != 1)
+          if (!(s444 || s422 || s420) || J.ch[1] != 1 || J.cv[1] != 1 || J.ch[2] != 1 ||
+              J.cv[2] != 1 || (J.ncomp == 4 && (J.ch[3] != J.ch[0] || J.cv[3] != J.cv[0])))
             return jpg_fail(err, "chroma sampling other than 4:4:4 / 4:2:2 / 4:2:0");
         }
         ScanHost S;
@@ -368,7 +371,7 @@ static int jpeg_parse(const uint8_t* p, size_t n, JpegHost& J, std::string* err)
             return jpg_fail(err, "missing Huffman table");
         }
         S.begin = i + len;
-        if (!J.progressive && !J.arith && J.scans.empty() && ns == J.ncomp) {
+        if (!J.progressive && !J.arith && J.ncomp <= 3 && J.scans.empty() && ns == J.ncomp) {
           // one interleaved sequential scan: the parallel path.  Its segment runs up to the EOI
           // (scanning back from the end) or the end of data
           for (int c = 0; c < J.ncomp; ++c)
@@ -534,10 +537,10 @@ struct JpegLds {
 
 // the scan path's tables (JpegScanDev slots)
 struct JpegLds6 {
-  alignas(16) int32_t mca[6][8];
-  uint16_t lut[6][1 << JPG_LUTB];
-  int32_t maxcode[6][18], valoff[6][18];
-  uint8_t huffval[6][256];
+  alignas(16) int32_t mca[8][8];
+  uint16_t lut[8][1 << JPG_LUTB];
+  int32_t maxcode[8][18], valoff[8][18];
+  uint8_t huffval[8][256];
 };
 
 // entry i of mca (see JpegLds) from a table's maxcode[18]
@@ -1126,12 +1129,12 @@ __device__ __forceinline__ void jpg_load_scan_tables(JpegLds6& T, const JpegScan
   const uint32_t* s = reinterpret_cast<const uint32_t*>(&S.lut[0][0]);
   uint32_t* d = reinterpret_cast<uint32_t*>(&T.lut[0][0]);
   for (int k = threadIdx.x; k < (int)(sizeof(T.lut) / 4); k += blockDim.x) d[k] = s[k];
-  for (int k = threadIdx.x; k < 6 * 18; k += blockDim.x) {
+  for (int k = threadIdx.x; k < 8 * 18; k += blockDim.x) {
     (&T.maxcode[0][0])[k] = (&S.maxcode[0][0])[k];
     (&T.valoff[0][0])[k] = (&S.valoff[0][0])[k];
   }
-  for (int k = threadIdx.x; k < 6 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&S.huffval[0][0])[k];
-  for (int k = threadIdx.x; k < 6 * 8; k += blockDim.x) T.mca[k >> 3][k & 7] = jpg_mca(S.maxcode[k >> 3], k & 7);
+  for (int k = threadIdx.x; k < 8 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&S.huffval[0][0])[k];
+  for (int k = threadIdx.x; k < 8 * 8; k += blockDim.x) T.mca[k >> 3][k & 7] = jpg_mca(S.maxcode[k >> 3], k & 7);
 }
 
 __device__ __forceinline__ uint32_t jpg_get(BitStream& br, int s) {  // s <= 16
@@ -1147,7 +1150,7 @@ __device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLds6& T, int t)
 }
 __device__ __forceinline__ int16_t jpg_lshift(int v, int al) { return (int16_t)(int)((uint32_t)v << al); }
 
-// one block of scan component k (slot k: DC table, 3 + k: AC table); eobrun / pred per interval
+// one block of scan component k (slot k: DC table, 4 + k: AC table); eobrun / pred per interval
 __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLds6& T, const JpegScanDev& S,
                                                int k, int16_t* __restrict__ blk, int& pred,
                                                uint32_t& eobrun) {
@@ -1157,7 +1160,7 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLds6& T,
       pred += s ? jpg_extend(jpg_get(br, s), s) : 0;
       blk[0] = (int16_t)pred;
       for (int z = 1; z < 64;) {
-        const int rs = jpg_huff(br, T, 3 + k);
+        const int rs = jpg_huff(br, T, 4 + k);
         const int r = rs >> 4, sz = rs & 15;
         if (sz) {
           z += r;
@@ -1186,7 +1189,7 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLds6& T,
         break;
       }
       for (int z = S.Ss; z <= S.Se; ++z) {
-        const int rs = jpg_huff(br, T, 3);
+        const int rs = jpg_huff(br, T, 4);
         const int r = rs >> 4, sz = rs & 15;
         if (sz) {
           z += r;
@@ -1207,7 +1210,7 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLds6& T,
       int z = S.Ss;
       if (eobrun == 0) {
         for (; z <= S.Se; ++z) {
-          const int rs = jpg_huff(br, T, 3);
+          const int rs = jpg_huff(br, T, 4);
           int r = rs >> 4, sz = rs & 15;
           if (sz) {
             sz = jpg_get(br, 1) ? p1 : m1;
@@ -1260,7 +1263,7 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
       const uint32_t u1 = S.restart ? min(u0 + (uint32_t)S.restart, S.nunits) : S.nunits;
       BitStream br;
       br.start(ub + S.ub_off, ivstart[S.iv_off + t]);
-      int pred[3] = {0, 0, 0};
+      int pred[4] = {0, 0, 0, 0};
       uint32_t eobrun = 0;
       for (uint32_t u = u0; u < u1; ++u) {
         if (S.ns == 1) {  // non-interleaved: the component's own blocks, raster order
@@ -1499,7 +1502,7 @@ __global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restric
       e.ct = -16;
       e.bad = false;
       uint8_t fixed = 113;
-      int last[3] = {0, 0, 0}, ctx[3] = {0, 0, 0};
+      int last[4] = {0, 0, 0, 0}, ctx[4] = {0, 0, 0, 0};
       for (uint32_t u = u0; u < u1 && !e.bad; ++u) {
         if (S.ns == 1) {
           const int c = S.comp[0];
@@ -1845,15 +1848,37 @@ __device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __re
   }
   uint32_t px[24];
   const int cbg = D.cb_g;  // jdcolor.c build_ycc_rgb_table (SCALEBITS 16)
+  uint32_t ka = 0, kb = 0;  // a fourth component (K), sampled as the first
+  if (!GRAY && D.ncomp == 4) {
+    const int pw3 = D.pw[3];
+    const uint8_t* kr = planes + D.pl_off[3] + (int64_t)y * pw3;
+    ka = ld_dw(kr, x0, pw3);
+    kb = ld_dw(kr, x0 + 4, pw3);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int Y = (int)(((i < 4 ? ya : yb) >> (8 * (i & 3))) & 0xFFu);
     if constexpr (GRAY) {
       px[3 * i] = px[3 * i + 1] = px[3 * i + 2] = (uint32_t)Y;
-    } else if (D.rgb) {  // jdcolor.c rgb_convert: a copy (components R, G, B -> BGR)
+    } else if (D.rgb == 1) {  // jdcolor.c rgb_convert: a copy (components R, G, B -> BGR)
       px[3 * i + 0] = (uint32_t)crv[i];
       px[3 * i + 1] = (uint32_t)cbv[i];
       px[3 * i + 2] = (uint32_t)Y;
+    } else if (D.rgb >= 2) {
+      // libjpeg's CMYK output: the components as stored (CMYK), or jdcolor.c ycck_cmyk_convert
+      // (YCCK: 255 minus the YCbCr -> RGB conversion, K unchanged); then OpenCV's
+      // icvCvt_CMYK2BGR_8u_C4C3R (grfmt_jpeg.cpp: Adobe-inverted CMYK), c' = k - ((255 - c) k >> 8)
+      int c0 = Y, c1 = cbv[i], c2 = crv[i];
+      if (D.rgb == 3) {
+        const int xb = cbv[i] - 128, xr = crv[i] - 128;
+        c0 = 255 - (int)jpg_clamp(Y + ((91881 * xr + 32768) >> 16));
+        c1 = 255 - (int)jpg_clamp(Y + ((-46802 * xr + (-cbg * xb + 32768)) >> 16));
+        c2 = 255 - (int)jpg_clamp(Y + ((116130 * xb + 32768) >> 16));
+      }
+      const int k = (int)(((i < 4 ? ka : kb) >> (8 * (i & 3))) & 0xFFu);
+      px[3 * i + 0] = (uint32_t)(k - (((255 - c2) * k) >> 8));
+      px[3 * i + 1] = (uint32_t)(k - (((255 - c1) * k) >> 8));
+      px[3 * i + 2] = (uint32_t)(k - (((255 - c0) * k) >> 8));
     } else {
       const int xb = cbv[i] - 128, xr = crv[i] - 128;
       px[3 * i + 0] = jpg_clamp(Y + ((116130 * xb + 32768) >> 16));                  // FIX(1.772)
@@ -1896,13 +1921,16 @@ __global__ __launch_bounds__(256) void jpeg_color8_kernel(const JpegDev* __restr
   }
 }
 
-// the colour space libjpeg assigns a 3-component file (jdapimin.c default_decompress_parms; the
-// caller asks for RGB): 0 YCbCr (converted), 1 RGB (copied), -1 one that is not restated.
+// the colour space libjpeg assigns a file (jdapimin.c default_decompress_parms; the caller asks
+// for RGB, or CMYK for 4 components): 0 YCbCr (converted), 1 RGB (copied), 2 CMYK (copied), 3 YCCK
+// (converted to CMYK), -1 one that is not restated.
 // libjpeg 9 looks at the component IDs first -- (1, 2, 3) YCbCr, (1, 0x22, 0x23) big-gamut YCC,
 // 'R' 'G' 'B' RGB, 'r' 'g' 'b' big-gamut RGB -- then a JFIF marker (YCbCr), then Adobe's transform
 // (0 RGB, else YCbCr), else YCbCr.  libjpeg-turbo (6b's order) looks at JFIF, then Adobe, then the
 // IDs 'R' 'G' 'B', else YCbCr.
 static int jpg_color_space(const JpegHost& J, bool turbo) {
+  if (J.ncomp == 4)  // CMYK stored as is, or YCCK: Adobe's transform 0 / 2 (else YCCK; no marker: CMYK)
+    return J.adobe && J.adobe_transform != 0 ? 3 : 2;
   if (J.ncomp != 3) return 0;
   const int a = J.cid[0], b = J.cid[1], c = J.cid[2];
   const bool rgb_ids = a == 'R' && b == 'G' && c == 'B';
@@ -1981,7 +2009,7 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       D.mcux = (J.width + 7) / 8;
       D.mcuy = (J.height + 7) / 8;
     } else {
-      for (int c = 0; c < 3; ++c) {
+      for (int c = 0; c < J.ncomp; ++c) {
         D.ch[c] = J.ch[c];
         D.cv[c] = J.cv[c];
       }
@@ -2013,10 +2041,11 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     }
     // what the colour pass still has to upsample (the chroma planes' remaining factor)
     D.up = 0;
-    if (J.ncomp == 3) {
+    if (J.ncomp >= 3) {
       const int fh = D.hmax / (D.ch[1] * D.sh[1]), fv = D.vmax / (D.cv[1] * D.sv[1]);
       if (fh != D.hmax / (D.ch[2] * D.sh[2]) || fv != D.vmax / (D.cv[2] * D.sv[2]) ||
-          D.ch[0] * D.sh[0] != D.hmax || D.cv[0] * D.sv[0] != D.vmax)
+          D.ch[0] * D.sh[0] != D.hmax || D.cv[0] * D.sv[0] != D.vmax ||
+          (J.ncomp == 4 && (D.ch[3] * D.sh[3] != D.hmax || D.cv[3] * D.sv[3] != D.vmax)))
         return jpg_fail(err, "unsupported chroma sampling");
       if (fh == 1 && fv == 1) D.up = 0;
       else if (fh == 2 && fv == 1) D.up = 1;
@@ -2084,14 +2113,14 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
         SD.nintervals = S.restart ? (int)((SD.nunits + S.restart - 1) / S.restart) : 1;
         if (SD.nintervals < 1) SD.nintervals = 1;
         SD.arith = J.arith ? 1 : 0;
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 4; ++k) {
           SD.td[k] = S.td[k];
           SD.ta[k] = S.ta[k];
           SD.aL[k] = S.aL[k];
           SD.aU[k] = S.aU[k];
           SD.aK[k] = S.aK[k];
         }
-        for (int sl = 0; sl < 6; ++sl)
+        for (int sl = 0; sl < 8; ++sl)
           for (int k = 0; k < 18; ++k) SD.maxcode[sl][k] = -1;
         for (int k = 0; k < S.ns && tables && !J.arith; ++k) {
           const bool dc = SD.kind == JPG_SEQ || SD.kind == JPG_DC_FIRST;
@@ -2101,8 +2130,8 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
             if (rc != IDN_OK) return rc;
           }
           if (ac) {
-            rc = jpeg_build_huff(S.ac[k], false, SD.lut[3 + k], SD.maxcode[3 + k], SD.valoff[3 + k],
-                                 SD.huffval[3 + k], err);
+            rc = jpeg_build_huff(S.ac[k], false, SD.lut[4 + k], SD.maxcode[4 + k], SD.valoff[4 + k],
+                                 SD.huffval[4 + k], err);
             if (rc != IDN_OK) return rc;
           }
         }

@@ -329,15 +329,16 @@ int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int
 
 /* ---- decode front-end (cv2.imread: lib/model/test.py:191, minibatch.py:85) --------------- */
 
-/* Header of one JPEG file in host memory (SOI .. EOI): height, width, components (1 or 3).
+/* Header of one JPEG file in host memory (SOI .. EOI): height, width, components (1, 3 or 4).
  * Taken: Huffman-coded baseline, extended sequential and progressive files (SOF0 / SOF1 / SOF2),
  * arithmetic-coded sequential and progressive files (SOF9 / SOF10, DAC conditioning), one or
  * several scans, restart intervals, 4:4:4 / 4:2:2 / 4:2:0 or grayscale; a progressive
  * file whose last scan leaves AC 1..5 imprecise is block-smoothed as libjpeg 9d smooths it
  * (jdcoefct.c smoothing_ok / decompress_smooth_data); three components are YCbCr or RGB as
- * libjpeg decides it (component IDs, JFIF / Adobe markers).  IDN_EUNSUPPORTED for anything else
- * (lossless, hierarchical, 12-bit, CMYK / YCCK, big-gamut colour, DHP / EXP / JPGn / LSE
- * markers, other chroma sampling). */
+ * libjpeg decides it (component IDs, JFIF / Adobe markers); four are CMYK or YCCK (Adobe's
+ * transform; K sampled as the first component), decoded to libjpeg's CMYK and converted to BGR
+ * as OpenCV does (icvCvt_CMYK2BGR_8u_C4C3R).  IDN_EUNSUPPORTED for anything else (lossless,
+ * hierarchical, 12-bit, big-gamut colour, DHP / EXP / JPGn / LSE markers, other sampling). */
 int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
 
 /* idn_jpeg_decode_u8 flags.  Default (0): the decode of the reference's pinned libjpeg 9d

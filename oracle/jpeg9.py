@@ -574,12 +574,25 @@ def parse_and_decode(data: bytes):
                 cids=[c["id"] for c in comps], jfif=jfif, adobe=adobe)
 
 
+def cv_cmyk_to_bgr(cmyk):
+    """OpenCV 3.4.2 icvCvt_CMYK2BGR_8u_C4C3R (imgcodecs utils.cpp, what grfmt_jpeg.cpp applies
+    to libjpeg's JCS_CMYK output of a 4-component file): Adobe-inverted CMYK,
+    c' = k - ((255 - c) k >> 8), written as B = y', G = m', R = c'.  (Restated from the
+    published source; cv2 is not importable here, so this step is parity-unpinned.)"""
+    c = cmyk.astype(np.int64)
+    k = c[..., 3]
+    out = [k - (((255 - c[..., j]) * k) >> 8) for j in (2, 1, 0)]
+    return np.stack(out, -1).astype(np.uint8)
+
+
 def color_space(d, mode: str) -> str:
     """jdapimin.c default_decompress_parms for 3 components: "ycc" (converted) or "rgb" (copied).
     libjpeg 9 decides by the component IDs first -- (1, 2, 3) YCbCr, (1, 0x22, 0x23) / 'r' 'g' 'b'
     big gamut (not restated), 'R' 'G' 'B' RGB -- then a JFIF marker (YCbCr), then Adobe's transform
     (0 RGB, else YCbCr), else YCbCr; libjpeg-turbo (6b's order) by JFIF, then Adobe, then the IDs
     'R' 'G' 'B', else YCbCr"""
+    if len(d["cids"]) == 4:  # Adobe transform 0: CMYK as stored, else YCCK; no marker: CMYK
+        return "ycck" if d["adobe"] not in (None, 0) else "cmyk"
     if len(d["cids"]) != 3:
         return "gray"
     ids = tuple(d["cids"])
@@ -809,9 +822,10 @@ def imread(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
     if len(planes) == 1:
         y = planes[0].astype(np.uint8)
         return np.repeat(y[..., None], 3, -1)
-    if color_space(d, mode) == "rgb":  # jdcolor.c rgb_convert: a copy
+    cs = color_space(d, mode)
+    if cs == "rgb":  # jdcolor.c rgb_convert: a copy
         return np.stack(planes[::-1], -1).astype(np.uint8)
-    Y, Cb, Cr = planes
+    Y, Cb, Cr = planes[:3]
     xb, xr = Cb - 128, Cr - 128
     one_half = 1 << 15
     cb_g = FIXS(0.344136286 if mode == "libjpeg9" else 0.34414)
@@ -819,6 +833,11 @@ def imread(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
     r = Y + ((FIXS(1.402) * xr + one_half) >> 16)
     g = Y + ((-cb_g * xb + one_half - cr_g * xr) >> 16)
     b = Y + ((FIXS(1.772) * xb + one_half) >> 16)
+    if cs == "cmyk":
+        return cv_cmyk_to_bgr(np.stack(planes, -1))
+    if cs == "ycck":  # jdcolor.c ycck_cmyk_convert: 255 - the RGB conversion, K unchanged
+        cmy = [255 - np.clip(v, 0, 255) for v in (r, g, b)]
+        return cv_cmyk_to_bgr(np.stack(cmy + [planes[3]], -1))
     return np.clip(np.stack([b, g, r], -1), 0, 255).astype(np.uint8)
 
 

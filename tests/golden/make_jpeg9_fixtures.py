@@ -29,6 +29,14 @@ FULL_LIMIT = 130 * 200  # files up to this many pixels are stored whole
 
 def bgr(path):
     with Image.open(path) as im:
+        if im.mode == "CMYK":
+            # Pillow reads libjpeg's JCS_CMYK output inverted ("CMYK;I"): undo that, then apply
+            # OpenCV's icvCvt_CMYK2BGR_8u_C4C3R (grfmt_jpeg.cpp's 4-component path), which is
+            # restated from the published OpenCV source (cv2 is not importable here)
+            c = 255 - np.asarray(im).astype(np.int64)
+            k = c[..., 3]
+            return np.ascontiguousarray(np.stack(
+                [k - (((255 - c[..., j]) * k) >> 8) for j in (2, 1, 0)], -1).astype(np.uint8))
         a = np.asarray(im.convert("RGB"))
     return np.ascontiguousarray(a[..., ::-1])
 

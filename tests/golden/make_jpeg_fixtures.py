@@ -122,6 +122,7 @@ def derived():
     smoothed()
     colorspaces()
     arithmetic()
+    cmyk()
 
 
 def _segments(data):
@@ -207,6 +208,32 @@ def arithmetic():
     tran("s444_q95_96x128.jpg", "arith_prog_rst_s444_96x128.jpg", "-progressive", "-restart", "1")
     # progressive arithmetic cut before its last two scans: block smoothing on arithmetic data
     _keep_scans("arith_prog_rst_s444_96x128.jpg", set(range(8)), "arith_prog_smooth_s444_96x128.jpg")
+
+
+def cmyk():
+    """4-component files: CMYK (Pillow writes Adobe-inverted CMYK with an APP14 transform 0) and the
+    same data relabelled YCCK (transform 2), baseline and progressive, and CMYK without the Adobe
+    marker (libjpeg: CMYK).  cv2.imread runs libjpeg's JCS_CMYK output through OpenCV's
+    CMYK -> BGR conversion"""
+    import subprocess
+    rs = np.random.RandomState(31)
+    y, x = np.mgrid[0:40, 0:56]
+    c = np.stack([(x * 4 + rs.randint(0, 20, x.shape)) % 256, (y * 6) % 256, ((x + y) * 3) % 256,
+                  64 + (x * y) % 128], -1).astype(np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(c, "CMYK").save(b, "JPEG", quality=92)
+    data = b.getvalue()
+    (OUT / "cmyk_s444_40x56.jpg").write_bytes(data)
+    k = data.find(b"\xff\xee")
+    assert data[k + 4:k + 9] == b"Adobe" and data[k + 15] == 0
+    ycck = bytearray(data)
+    ycck[k + 15] = 2
+    (OUT / "ycck_s444_40x56.jpg").write_bytes(bytes(ycck))
+    noadobe = data[:k] + data[k + 2 + ((data[k + 2] << 8) | data[k + 3]):]
+    (OUT / "cmyk_noadobe_s444_40x56.jpg").write_bytes(noadobe)
+    prog = subprocess.run([str(JPEGTRAN), "-progressive", str(OUT / "ycck_s444_40x56.jpg")],
+                          capture_output=True, check=True).stdout
+    (OUT / "ycck_prog_s444_40x56.jpg").write_bytes(prog)
 
 
 def _keep_scans(src, keep, name):

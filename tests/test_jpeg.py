@@ -69,12 +69,16 @@ def test_oracle_libjpeg9_matches_real_libjpeg9(name):
                                   "prog_s420_rst4_120x160.jpg", "prog_gray_q80_91x77.jpg"] +
                          [p.name for p in _files() if p.name.startswith("cs_")] +
                          [p.name for p in _files() if p.name.startswith("arith_") and
-                          "smooth" not in p.name])
+                          "smooth" not in p.name] +
+                         [p.name for p in _files() if p.name.startswith(("cmyk", "ycck"))])
 def test_oracle_turbo_mode_matches_system_pil(name):
     from PIL import Image
     from oracle import jpeg9
     with Image.open(JPEG / name) as im:
-        ref = np.asarray(im.convert("RGB"))[..., ::-1]
+        if im.mode == "CMYK":  # libjpeg's CMYK output (Pillow reads it inverted) through OpenCV's
+            ref = jpeg9.cv_cmyk_to_bgr(255 - np.asarray(im).astype(np.int64))
+        else:
+            ref = np.asarray(im.convert("RGB"))[..., ::-1]
     assert np.array_equal(jpeg9.imread((JPEG / name).read_bytes(), mode="turbo"), ref)
 
 
@@ -91,7 +95,7 @@ def test_info_matches_pil():
     for p in _files():
         with Image.open(p) as im:
             w, h = im.size
-            c = 1 if im.mode == "L" else 3
+            c = {"L": 1, "CMYK": 4}.get(im.mode, 3)
         assert ops.jpeg_info(p.read_bytes()) == (h, w, c), p.name
 
 
@@ -298,3 +302,20 @@ def test_arithmetic_fixtures_cover_the_coder():
         smooth |= jpeg9.parse_and_decode(data)["smooth"] is not None
         assert ops.jpeg_info(data)[2] in (1, 3)
     assert len(names) >= 7 and sofs == {0xC9, 0xCA} and rst and smooth
+
+
+def test_four_component_files():
+    """CMYK (Adobe transform 0, or no Adobe marker) and YCCK (transform 2) files, baseline and
+    progressive: libjpeg 9d's CMYK output (ycck_cmyk_convert for YCCK) pinned by the real library
+    (tests/golden/jpeg9.*), then OpenCV's CMYK -> BGR (restated, parity-unpinned: cv2 is not
+    importable here)"""
+    from idn import ops
+    from oracle import jpeg9
+    names = [p.name for p in _files() if p.name.startswith(("cmyk", "ycck"))]
+    assert len(names) >= 4
+    spaces = set()
+    for name in names:
+        data = (JPEG / name).read_bytes()
+        assert ops.jpeg_info(data)[2] == 4
+        spaces.add(jpeg9.color_space(jpeg9.parse_and_decode(data), "libjpeg9"))
+    assert spaces == {"cmyk", "ycck"}

@@ -36,8 +36,13 @@ def check_libjpeg9(name, got):
 
 
 def pil_bgr(path):
+    """the box Pillow's decode as cv2.imread would return it: BGR; a 4-component file through
+    OpenCV's CMYK -> BGR conversion of libjpeg's CMYK output (Pillow reads that inverted)"""
     from PIL import Image
+    from oracle import jpeg9
     with Image.open(path) as im:
+        if im.mode == "CMYK":
+            return jpeg9.cv_cmyk_to_bgr(255 - np.asarray(im).astype(np.int64))
         a = np.asarray(im.convert("RGB"))
     return np.ascontiguousarray(a[..., ::-1])
 

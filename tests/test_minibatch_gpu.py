@@ -216,17 +216,19 @@ def test_host_decode_without_cv2_is_libjpeg9(dev, tmp_path, name):
 
 @pytest.mark.gpu
 def test_host_decode_without_cv2_raises_on_unsupported_jpeg(dev, tmp_path):
-    """a JPEG the GPU decoder does not take (here CMYK, written by PIL) raises: no silent
-    libjpeg-turbo / PIL decode in its place"""
+    """a JPEG the GPU decoder does not take (here a lossless-process frame, SOF3) raises: no
+    silent libjpeg-turbo / PIL decode in its place"""
     import importlib.util
-    from PIL import Image
     from idn import io
     from idn._lib import IdnError
+    from test_jpeg import _lossless
     if importlib.util.find_spec("cv2") is not None:
         pytest.skip("OpenCV present")
-    Image.new("CMYK", (32, 24), (10, 20, 30, 40)).save(tmp_path / "cmyk.jpg", quality=90)
+    import pathlib
+    gold = pathlib.Path(__file__).resolve().parent / "golden" / "jpeg"
+    (tmp_path / "lossless.jpg").write_bytes(_lossless((gold / "s444_q95_96x128.jpg").read_bytes()))
     with pytest.raises(IdnError):
-        io.imread(tmp_path / "cmyk.jpg")
+        io.imread(tmp_path / "lossless.jpg")
 
 
 @pytest.mark.gpu
