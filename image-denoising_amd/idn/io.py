@@ -32,8 +32,22 @@ def imread(path) -> np.ndarray:
         head = f.read(3)
     if head[:2] == b"\xff\xd8":  # JPEG: the libjpeg 9d decode, on the GPU
         return imread_gpu([path])[0].cpu().numpy()
+    return _imread_pil(path)
+
+
+def _imread_pil(path) -> np.ndarray:
+    """a lossless format through PIL, as OpenCV's decoders return it with IMREAD_COLOR: 8-bit BGR,
+    alpha dropped, palettes expanded.  Samples deeper than 8 bits keep their high byte, as
+    grfmt_png.cpp's png_set_strip_16 does (PIL's own 16-bit grayscale -> RGB conversion would clip
+    them at 255 instead); PIL already unpacks 16-bit RGB(A) to its high bytes."""
     from PIL import Image
     with Image.open(path) as im:
+        if im.mode in ("I;16", "I;16B", "I;16L", "I"):
+            g = np.asarray(im).astype(np.int64)
+            if im.mode == "I" and g.max(initial=0) > 0xFFFF:
+                raise ValueError(f"{path}: 32-bit samples are not an OpenCV IMREAD_COLOR input")
+            g = (g >> 8).astype(np.uint8)
+            return np.ascontiguousarray(np.repeat(g[..., None], 3, -1))
         rgb = np.asarray(im.convert("RGB"))
     return np.ascontiguousarray(rgb[..., ::-1])
 

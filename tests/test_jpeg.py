@@ -183,6 +183,19 @@ def test_imread_lossless_formats_through_pil(tmp_path):
     rgb = np.random.RandomState(0).randint(0, 256, (9, 13, 3)).astype(np.uint8)
     Image.fromarray(rgb).save(tmp_path / "a.png")
     assert np.array_equal(io.imread(tmp_path / "a.png"), rgb[..., ::-1])
+    # 16-bit grayscale: OpenCV's png_set_strip_16 keeps the high byte (PIL's convert would clip);
+    # palette and gray + alpha: expanded / alpha dropped.  (cv2 is absent here: the OpenCV
+    # behaviour is restated from grfmt_png.cpp, parity-unpinned)
+    g16 = np.random.RandomState(1).randint(0, 65536, (7, 11)).astype(np.uint16)
+    Image.fromarray(g16, "I;16").save(tmp_path / "g16.png")
+    assert np.array_equal(io.imread(tmp_path / "g16.png"),
+                          np.repeat((g16 >> 8).astype(np.uint8)[..., None], 3, -1))
+    pal = Image.fromarray(rgb).quantize(16)
+    pal.save(tmp_path / "p.png")
+    assert np.array_equal(io.imread(tmp_path / "p.png"), np.asarray(pal.convert("RGB"))[..., ::-1])
+    la = np.stack([rgb[..., 0], rgb[..., 1]], -1)
+    Image.fromarray(la, "LA").save(tmp_path / "la.png")
+    assert np.array_equal(io.imread(tmp_path / "la.png"), np.repeat(la[..., :1], 3, -1))
     with pytest.raises(FileNotFoundError):
         io.imread(tmp_path / "missing.png")
 
