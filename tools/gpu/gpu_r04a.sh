@@ -2,7 +2,7 @@
 # round 4, first GPU call: the whole -m gpu suite (live-path + batch-invariance tests, flip shares
 # printed), then an interleaved A/B of the bior1.5 op over three builds (ab/old = round 3's
 # analysis, ab/wpe1 / ab/wpe6 = per-group sums of squares without / with the 6-wave bound for the
-# fp32 deeper levels) with kernel stats per build.  bash tools/gpu_r04a.sh
+# fp32 deeper levels) with kernel stats per build.  bash tools/gpu/gpu_r04a.sh
 set -u
 OUT=gpurun_out/r04a
 mkdir -p "$OUT"

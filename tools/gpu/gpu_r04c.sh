@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: wavelet per-thread group partials + 24-byte-lane 5x5 median.  Tests of both, then
 # interleaved A/Bs: bior1.5 op (ab/old = round 3's analysis vs the product), median5 op and
-# config 3 (tuning build: IDN_MEDIAN_W24=0 vs 1), kernel stats.  bash tools/gpu_r04c.sh
+# config 3 (tuning build: IDN_MEDIAN_W24=0 vs 1), kernel stats.  bash tools/gpu/gpu_r04c.sh
 set -u
 OUT=gpurun_out/r04c
 mkdir -p "$OUT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: exact grid-rounded sums of squares in the bior1.5 analysis -- wavelet tests, then the
-# interleaved A/B against round 3's analysis (ab/old) with kernel stats.  bash tools/gpu_r04d.sh
+# interleaved A/B against round 3's analysis (ab/old) with kernel stats.  bash tools/gpu/gpu_r04d.sh
 set -u
 OUT=gpurun_out/r04d
 mkdir -p "$OUT"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: static 5-row sum-of-squares groups in the bior1.5 analysis -- wavelet tests, A/B with
 # per-kernel stats of both builds, then the round's counter passes (tools/pmc_r04.sh) and the
-# counter list.  bash tools/gpu_r04e.sh
+# counter list.  bash tools/gpu/gpu_r04e.sh
 set -u
 OUT=gpurun_out/r04e
 mkdir -p "$OUT"

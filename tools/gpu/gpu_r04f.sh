@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: bior1.5 analysis strip width x band count sweep (tuning build: IDN_WAVELET_WST threads
 # per strip, IDN_WAVELET_BANDS level-1 bands) -- kernel stats per config; and the product with
-# the reverted band query.  bash tools/gpu_r04f.sh
+# the reverted band query.  bash tools/gpu/gpu_r04f.sh
 set -u
 OUT=gpurun_out/r04f
 mkdir -p "$OUT"

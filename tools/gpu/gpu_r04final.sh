@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 closing record: whole GPU suite + smoke, every bench op, the default headline line with its
-# kernel stats, and counter passes for the ops that changed late.   bash tools/gpu_r04final.sh <tag>
+# kernel stats, and counter passes for the ops that changed late.   bash tools/gpu/gpu_r04final.sh <tag>
 set -u
 TAG=${1:-final2}
 OUT=gpurun_out/r04$TAG

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: bior1.5 analysis ring loads that really prefetch (unaligned dword per row, refilled after
 # the slot's last use, unconditional) -- wavelet tests, A/B against the previous build, kernel
-# stats and counter passes of the product.  bash tools/gpu_r04g.sh
+# stats and counter passes of the product.  bash tools/gpu/gpu_r04g.sh
 set -u
 OUT=gpurun_out/r04g
 mkdir -p "$OUT"

@@ -1,21 +1,21 @@
 #!/bin/bash
-# round 4: A/B of the level-1 analysis row-task spread (IDN_WS_SPREAD=1 build: every wave of the
-# workgroup takes a contiguous run of row tasks) against the product, same run; wavelet tests on
-# the variant.  bash tools/gpu_r04j.sh
+# round 4: same-run A/B of the bior1.5 ring forms -- product (analysis ring that prefetches, codes
+# as dwords), old (previous commit), s3pad (synthesis in the padded ring form), pf3 (deeper-level
+# analysis with a 5-step ring); wavelet tests on the product first.  bash tools/gpu/gpu_r04h.sh
 set -u
-OUT=gpurun_out/r04j
+OUT=gpurun_out/r04h
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 L=image-denoising_amd/idn/libidn_hip.so
 cp $L ab/product.so
-cp ab/spread.so $L
-timeout -k 10 600 python -u -m pytest tests/test_wavelet_gpu.py tests/test_live_path_gpu.py -q \
-    --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest.txt" 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_wavelet_gpu.py tests/test_live_path_gpu.py \
+    tests/test_pipeline_gpu.py -q --timeout 300 --timeout-method thread -p no:cacheprovider -s \
+    > "$OUT/pytest.txt" 2>&1
 rc=$?
-cp ab/product.so $L
+grep -h "LIVE_PATH\|PLAN_FLIPS" "$OUT/pytest.txt" > "$OUT/flips.txt"
 tail -2 "$OUT/pytest.txt"
 [ $rc = 0 ] || exit $rc
-VS="product spread"
+VS="old product s3pad pf3"
 for rep in 1 2; do
   for v in $VS; do
     cp ab/$v.so $L || exit 1
@@ -30,7 +30,7 @@ for v in $VS; do
       -- python3 bench.py --op wavelet_bior15 --no-cpu --no-copy --steps 10 --warmup 2 > /dev/null 2>&1 || exit 1
   python3 -c "
 import csv
-for r in list(csv.DictReader(open('$OUT/ks_$v/k_kernel_stats.csv')))[:5]: print('$v', r['Name'][:58], round(float(r['AverageNs'])/1e3,1))"
+for r in list(csv.DictReader(open('$OUT/ks_$v/k_kernel_stats.csv')))[:8]: print('$v', r['Name'][:58], round(float(r['AverageNs'])/1e3,1))"
 done
 cp ab/product.so $L
 echo ok

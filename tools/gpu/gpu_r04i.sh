@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: bior1.5 level-1 dd band in fp32 (the sigma median recomputes its exact values from the
 # input) -- wavelet tests, A/B against the previous commit's build, and tuning-build kernel stats
-# with IDN_WAVELET_DD32=0 / 1 in the same run.  bash tools/gpu_r04i.sh
+# with IDN_WAVELET_DD32=0 / 1 in the same run.  bash tools/gpu/gpu_r04i.sh
 set -u
 OUT=gpurun_out/r04i
 mkdir -p "$OUT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 checkpoint: the whole GPU test suite, then the bior1.5 counter passes on the product.
-#   bash tools/gpu_r04m.sh
+#   bash tools/gpu/gpu_r04m.sh
 set -u
 OUT=gpurun_out/r04m
 mkdir -p "$OUT"

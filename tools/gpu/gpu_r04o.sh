@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 record: every bench op on the current code (no CPU leg), then the default headline line
-# (CPU baseline + copy ceilings) and its rocprofv3 kernel stats.   bash tools/gpu_r04o.sh
+# (CPU baseline + copy ceilings) and its rocprofv3 kernel stats.   bash tools/gpu/gpu_r04o.sh
 set -u
 OUT=gpurun_out/r04o
 mkdir -p "$OUT"

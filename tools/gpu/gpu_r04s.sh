@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 checkpoint: whole GPU suite, smoke(), default bench line.   bash tools/gpu_r04s.sh
+# round 4 checkpoint: whole GPU suite, smoke(), default bench line.   bash tools/gpu/gpu_r04s.sh
 set -u
 OUT=gpurun_out/r04s
 mkdir -p "$OUT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: bior1.5 analysis with 256-thread strips whose LDS is sized for them (4 workgroups per
-# CU) against the 512-thread product, tuning build, kernel stats per config.  bash tools/gpu_r04u.sh
+# CU) against the 512-thread product, tuning build, kernel stats per config.  bash tools/gpu/gpu_r04u.sh
 set -u
 OUT=gpurun_out/r04u
 mkdir -p "$OUT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: adaptive default JPEG chunk size -- JPEG / drop-in tests, then the per-image end-to-end
-# op and the batch decode op with kernel stats.   bash tools/gpu_r04x.sh
+# op and the batch decode op with kernel stats.   bash tools/gpu/gpu_r04x.sh
 set -u
 OUT=gpurun_out/r04x
 mkdir -p "$OUT"
