@@ -536,7 +536,7 @@ struct JpegLds {
 };
 
 // the scan path's tables (JpegScanDev slots)
-struct JpegLds6 {
+struct JpegLdsScan {
   alignas(16) int32_t mca[8][8];
   uint16_t lut[8][1 << JPG_LUTB];
   int32_t maxcode[8][18], valoff[8][18];
@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
 // left in the coefficient blocks); within a scan the lanes take the restart intervals (without
 // restart markers lane 0 decodes the scan).  Throughput is not the goal of this path: it makes
 // cv2.imread's progressive files decodable bit-exactly (the parallel path is the baseline one).
-__device__ __forceinline__ void jpg_load_scan_tables(JpegLds6& T, const JpegScanDev& S) {
+__device__ __forceinline__ void jpg_load_scan_tables(JpegLdsScan& T, const JpegScanDev& S) {
   const uint32_t* s = reinterpret_cast<const uint32_t*>(&S.lut[0][0]);
   uint32_t* d = reinterpret_cast<uint32_t*>(&T.lut[0][0]);
   for (int k = threadIdx.x; k < (int)(sizeof(T.lut) / 4); k += blockDim.x) d[k] = s[k];
@@ -1141,7 +1141,7 @@ __device__ __forceinline__ uint32_t jpg_get(BitStream& br, int s) {  // s <= 16
   br.refill();
   return br.bits(s);
 }
-__device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLds6& T, int t) {
+__device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLdsScan& T, int t) {
   br.refill();
   int len;
   const int sym = jpg_decode(br.acc, T, t, &len);
@@ -1151,7 +1151,7 @@ __device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLds6& T, int t)
 __device__ __forceinline__ int16_t jpg_lshift(int v, int al) { return (int16_t)(int)((uint32_t)v << al); }
 
 // one block of scan component k (slot k: DC table, 4 + k: AC table); eobrun / pred per interval
-__device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLds6& T, const JpegScanDev& S,
+__device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan& T, const JpegScanDev& S,
                                                int k, int16_t* __restrict__ blk, int& pred,
                                                uint32_t& eobrun) {
   switch (S.kind) {
@@ -1247,7 +1247,7 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
                                                        const uint8_t* __restrict__ ub,
                                                        const uint32_t* __restrict__ ivstart,
                                                        int16_t* __restrict__ coef) {
-  __shared__ JpegLds6 T;
+  __shared__ JpegLdsScan T;
   const JpegDev& D = imgs[blockIdx.x];
   const uint32_t nscan = D.nscan;
   if (nscan == 0 || D.arith) return;  // uniform: a parallel-path or arithmetic-coded image
