@@ -1,5 +1,5 @@
-// Baseline JPEG decode front-end: cv2.imread(path) (IMREAD_COLOR, BGR u8) for the reference's
-// images (lib/model/test.py:191, lib/roi_data_layer/minibatch.py:85), decoded on the GPU.
+// JPEG decode front-end: cv2.imread(path) (IMREAD_COLOR, BGR u8) for the reference's images
+// (lib/model/test.py:191, lib/roi_data_layer/minibatch.py:85), decoded on the GPU.
 //
 // Output = what the reference's pinned decoder produces with its defaults: IJG libjpeg 9d
 // (requirements.txt:74, under OpenCV 3.4.2) -- the ISLOW integer IDCT (jidctint.c) for full-size
@@ -12,26 +12,30 @@
 // All restated from the published algorithms; tests check bit-exactness against the real libjpeg
 // 9d decode (committed fixtures) and the GPU box's turbo-linked PIL.
 //
-// Host: the marker parser (SOI .. SOS, DQT / DHT / SOF0 / DRI / APPn), Huffman lookup tables per
-// image, one packed host->device copy of the images' entropy-coded segments and tables.
-// Device, three launches per batch:
-//   1 jpeg_huff_kernel   one wave per image; lane r decodes restart interval r, r + 64, ... (lane 0
-//                        decodes the whole scan when the image has no restart markers): Huffman +
-//                        byte unstuffing + DC prediction into int16 coefficient blocks (natural order)
-//   2 jpeg_idct_kernel   one thread per coefficient block: dequantise + ISLOW IDCT (8x8, or
-//                        16x16 / 16x8 for libjpeg 9's scaled chroma) into u8 component planes
-//   3 jpeg_color8_kernel 8 output pixels per thread: chroma upsampling (turbo only) + YCbCr -> BGR
-//                        (or gray -> BGR), written into the caller's NHWC batch
-// Supported: 8-bit Huffman JPEG, 1, 3 or 4 components, sampling 4:4:4 / 4:2:2 (h2v1) / 4:2:0 (h2v2),
-// optional restart intervals: baseline / extended sequential (SOF0 / SOF1) with one interleaved
-// scan (the parallel path above), and progressive (SOF2) or multi-scan sequential files (the scan
-// path: jpeg_prog_kernel, one wave per image, scans in file order, restart intervals across the
-// lanes), with libjpeg 9d's block smoothing of progressive files whose last scan leaves AC 1..5
-// imprecise (jpg_smooth); arithmetic-coded files (SOF9 / SOF10) through the scan path's QM-coder
-// (jpeg_arith_kernel).  Three-component files are YCbCr or RGB as each library decides it
-// (jpg_color_space: JFIF / Adobe markers, component IDs); four-component CMYK / YCCK files go
-// through the scan path to libjpeg's CMYK and OpenCV's CMYK -> BGR.  Anything else (lossless,
-// hierarchical, 12-bit, big-gamut colour, extension markers) is IDN_EUNSUPPORTED.
+// Host: the marker parser (SOI .. SOS: DQT / DHT / DAC / SOFn / DRI / APPn), Huffman lookup tables
+// per image and scan, one packed host->device copy of the images' entropy-coded segments.
+// Device:
+//   unstuff        per 16 KiB tile: the segments without stuffing and RST markers, the bit offset
+//                  of every restart interval
+//   the parallel path: single-scan Huffman files of 1 or 3 components (SOF0 / SOF1)
+//     sync A / B   self-synchronising chunk decoders (restart intervals: one thread each) with
+//                  checkpoints; B passes until no chunk's end state changes
+//     prefix       per image: each chunk's first block and DC predictors
+//     write        one thread per 512-bit sub-chunk from the checkpoints: coefficient blocks
+//   the scan path: progressive (SOF2), multi-scan, arithmetic-coded (SOF9 / SOF10) and
+//     4-component files; one wave per image walks the scans in file order, lanes over restart
+//     intervals: jpeg_prog_kernel (Huffman: jdhuff.c's decoders) or jpeg_arith_kernel
+//     (jdarith.c's QM-coder)
+//   idct           one thread per block: libjpeg 9d block smoothing of progressive files whose last
+//                  scan leaves AC 1..5 imprecise (jpg_smooth), dequantise, ISLOW IDCT (8x8, or
+//                  16x16 / 16x8 for libjpeg 9's scaled chroma) into u8 component planes
+//   color          8 output pixels per thread: chroma upsampling (turbo), then YCbCr -> BGR, RGB
+//                  copied, gray replicated, or CMYK / YCCK (libjpeg's CMYK output) through OpenCV's
+//                  CMYK -> BGR (jpg_color_space: component IDs, JFIF / Adobe markers, per library)
+// Supported: 8-bit DCT JPEG (Huffman or arithmetic), 1, 3 or 4 components, sampling 4:4:4 /
+// 4:2:2 (h2v1) / 4:2:0 (h2v2) (a fourth component sampled as the first), optional restart
+// intervals.  Anything else (lossless, hierarchical, 12-bit, big-gamut colour, extension
+// markers) is IDN_EUNSUPPORTED -- as libjpeg 9d (8-bit, DCT) refuses the first three too.
 #include "idn_common.hpp"
 
 #include <string.h>
@@ -949,9 +953,14 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
                                                        const uint8_t* __restrict__ chg_prev,
                                                        uint8_t* __restrict__ chg_next, int all,
                                                        uint64_t* __restrict__ ck_st,
-                                                       ChunkOut* __restrict__ ck_co) {
+                                                       ChunkOut* __restrict__ ck_co,
+                                                       const uint32_t* __restrict__ settled) {
   __shared__ JpegLds T;
   __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
+  // the previous pass of this launch round changed nothing: the decode has converged and both
+  // state buffers hold the same states (that pass copied every one through), so there is nothing
+  // to do -- the host queues a round of passes without reading a flag between them
+  if (!PASS_A && settled && *settled == 0u) return;
   const JpegDev& D = imgs[blockIdx.y];
   if (D.restart || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
@@ -2362,21 +2371,22 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   const dim3 gitems((P.max_items + 63) / 64, n);
   int cur = 0;
   if (P.any_chunked) {
-    // pass A, then pass B until no chunk's end state changes (typically 3 changing passes and
-    // one that confirms).  The B passes are launched JPG_BROUND at a time with one flag each and
-    // one host read per round: a pass after convergence only copies the states through (no
-    // chunk's start changed), so the passes beyond it cost a launch each -- the host round trip
-    // per pass (a D2H read and a stream synchronisation) was ~60 us of a single file's decode
-    constexpr int JPG_BROUND = 4;
+    // pass A, then pass B until no chunk's end state changes (a batch takes ~4-6 passes, a
+    // single large file ~8-9).  The B passes are launched JPG_BROUND at a time with one flag each
+    // and one host read per round: the pass after the first one that changed nothing returns at
+    // once (its predecessor's flag), so a round costs the passes that work plus a launch each for
+    // the rest -- every host round trip (a D2H read and a stream synchronisation, ~30-40 us)
+    // was a gap in a single file's decode
+    constexpr int JPG_BROUND = 12;
     hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
-                       S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co);
+                       S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co, nullptr);
     for (uint32_t it = 0;; it += JPG_BROUND) {
       if (hipMemsetAsync(flag, 0, 4 * JPG_BROUND, st) != hipSuccess)
         return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
       for (int k = 0; k < JPG_BROUND; ++k) {
         hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
                            S[cur], S[cur ^ 1], cnt, flag + k, chg[cur], chg[cur ^ 1],
-                           it + k == 0 ? 1 : 0, ck_st, ck_co);
+                           it + k == 0 ? 1 : 0, ck_st, ck_co, k > 0 ? flag + k - 1 : nullptr);
         cur ^= 1;
       }
       uint32_t changed[JPG_BROUND] = {};
