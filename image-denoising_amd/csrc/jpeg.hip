@@ -15,8 +15,9 @@
 // Host: the marker parser (SOI .. SOS: DQT / DHT / DAC / SOFn / DRI / APPn), Huffman lookup tables
 // per image and scan, one packed host->device copy of the images' entropy-coded segments.
 // Device:
-//   unstuff        per 16 KiB tile: the segments without stuffing and RST markers, the bit offset
-//                  of every restart interval
+//   unstuff        per 16 KiB tile: the segments without stuffing and markers, every marker's code
+//                  and offset; per segment each restart interval's data as libjpeg reads it
+//                  (jdmarker.c resync on damaged files)
 //   the parallel path: single-scan Huffman files of 1 or 3 components (SOF0 / SOF1)
 //     sync A / B   self-synchronising chunk decoders (restart intervals: one thread each) with
 //                  checkpoints; B passes until no chunk's end state changes
@@ -36,6 +37,9 @@
 // 4:2:2 (h2v1) / 4:2:0 (h2v2) (a fourth component sampled as the first), optional restart
 // intervals.  Anything else (lossless, hierarchical, 12-bit, big-gamut colour, extension
 // markers) is IDN_EUNSUPPORTED -- as libjpeg 9d (8-bit, DCT) refuses the first three too.
+// Damaged entropy-coded data decodes as libjpeg decodes it: past an interval's data the bits are
+// 0 and an MCU is decoded only if the data lasted up to its start (jdhuff.c insufficient_data),
+// a bit pattern that is no code takes 17 bits and decodes as 0.
 #include "idn_common.hpp"
 
 #include <string.h>
@@ -69,7 +73,8 @@ struct JpegDev {
   uint64_t blk_off[4];      // first block of each component in the batch coefficient buffer
   uint64_t pl_off[4];       // component plane byte offset in the batch plane buffer
   uint64_t ub_off;          // unstuffed entropy bytes (workspace), capacity scan_len + 64
-  uint32_t iv_off;          // first entry of the image's interval-start table (bits)
+  uint32_t iv_off;          // first entry of the image's interval tables (jpeg_unstuff_final)
+  uint32_t mk_off, mk_cap;  // the markers found in the segment (jpeg_unstuff_write): first, room
   uint32_t ch_off, nchunks; // the image's chunks in the batch chunk arrays
   uint32_t chunk_bits;
   int bpm;                  // blocks per MCU (1 for a single-component scan)
@@ -96,6 +101,7 @@ struct JpegScanDev {
   uint32_t scan_len;
   uint64_t ub_off;
   uint32_t iv_off;
+  uint32_t mk_off, mk_cap;
   int nintervals;
   int img, ns, comp[4], Ss, Se, Ah, Al, restart, kind;
   uint32_t nunits;          // MCUs (interleaved) or the component's blocks (non-interleaved)
@@ -152,8 +158,9 @@ struct JpegHost {
   std::vector<ScanHost> scans;  // the scan path (progressive or multi-scan); empty: one scan
 };
 
-// end of the entropy-coded segment starting at p[i]: the first marker that is not RSTn (stuffed
-// 0xFF00 and fill bytes skipped)
+// end of the entropy-coded segment starting at p[i]: the first marker that is neither RSTn nor
+// below SOF0 (stuffed 0xFF00 and fill bytes skipped).  A stray marker below SOF0 stays inside: it
+// ends the data of its restart interval (jpeg_unstuff_final), as jdmarker.c's resync reads it.
 static size_t jpg_segment_end(const uint8_t* p, size_t n, size_t i) {
   while (i + 1 < n) {
     if (p[i] != 0xFF) {
@@ -161,7 +168,7 @@ static size_t jpg_segment_end(const uint8_t* p, size_t n, size_t i) {
       continue;
     }
     const uint8_t nb = p[i + 1];
-    if (nb == 0x00 || (nb >= 0xD0 && nb <= 0xD7)) i += 2;
+    if (nb < 0xC0 || (nb >= 0xD0 && nb <= 0xD7)) i += 2;  // (0x00: stuffing)
     else if (nb == 0xFF) i += 1;
     else return i;
   }
@@ -472,41 +479,49 @@ __device__ __forceinline__ uint32_t jpg_be32(const uint8_t* __restrict__ p) {
   return __builtin_bswap32(w);
 }
 
-// reads a plain big-endian bit string (16-byte aligned, zero padded >= 48 bytes): the words of
-// the current 16-byte group in registers, the next group's load already in flight (a chain of
-// dependent loads per symbol made the decode latency-bound: 2100 cycles per symbol)
+// reads one restart interval of a plain big-endian bit string through a range-checked buffer
+// resource: the words of the current 16-byte group in registers, the next group's load already in
+// flight (a chain of dependent loads per symbol made the decode latency-bound: 2100 cycles per
+// symbol).  Bits from `end` on read as 0 (jdhuff.c jpeg_fill_bit_buffer past a marker); `pos`
+// counts the bits taken, so pos > end says the data ran out (libjpeg's insufficient_data).
 struct BitStream {
-  const uint4* g;  // 16-byte groups
+  rsrc_t rs;
   uint64_t acc;    // left-aligned
   int nb, idx;
-  uint32_t gi;
+  uint32_t gi, wbit, pos, end;  // wbit: stream position of the next word to append
   uint32_t buf[4];
-  uint4 pre;
-  __device__ __forceinline__ void take(const uint4 v) {
+  v4u pre;
+  __device__ __forceinline__ void take(const v4u v) {
     buf[0] = __builtin_bswap32(v.x);
     buf[1] = __builtin_bswap32(v.y);
     buf[2] = __builtin_bswap32(v.z);
     buf[3] = __builtin_bswap32(v.w);
   }
   __device__ __forceinline__ uint32_t word() {
-    const uint32_t w = idx == 0 ? buf[0] : idx == 1 ? buf[1] : idx == 2 ? buf[2] : buf[3];
+    uint32_t w = idx == 0 ? buf[0] : idx == 1 ? buf[1] : idx == 2 ? buf[2] : buf[3];
     if (++idx == 4) {
       take(pre);
-      pre = g[++gi + 1];
+      pre = __builtin_amdgcn_raw_buffer_load_b128(rs, (++gi + 1) * 16u, 0, 0);
       idx = 0;
     }
+    const int64_t r = (int64_t)end - (int64_t)wbit;
+    w = r >= 32 ? w : r <= 0 ? 0u : w & ~(0xFFFFFFFFu >> (uint32_t)r);
+    wbit += 32;
     return w;
   }
-  __device__ __forceinline__ void start(const uint8_t* base, uint32_t pos) {
-    g = reinterpret_cast<const uint4*>(base);
-    const uint32_t wi = pos >> 5;
+  __device__ __forceinline__ void start(rsrc_t r, uint32_t p, uint32_t e) {
+    rs = r;
+    end = e;
+    pos = p;
+    const uint32_t wi = p >> 5;
     gi = wi >> 2;
     idx = (int)(wi & 3);
-    take(g[gi]);
-    pre = g[gi + 1];
+    wbit = wi * 32u;
+    take(__builtin_amdgcn_raw_buffer_load_b128(rs, gi * 16u, 0, 0));
+    pre = __builtin_amdgcn_raw_buffer_load_b128(rs, (gi + 1) * 16u, 0, 0);
     const uint32_t w0 = word(), w1 = word();
-    acc = ((uint64_t)w0 << 32 | w1) << (pos & 31);
-    nb = 64 - (int)(pos & 31);
+    acc = ((uint64_t)w0 << 32 | w1) << (p & 31);
+    nb = 64 - (int)(p & 31);
   }
   __device__ __forceinline__ void refill() {
     if (nb < 32) {
@@ -518,6 +533,7 @@ struct BitStream {
     const uint32_t r = s ? (uint32_t)(acc >> (64 - s)) : 0u;
     acc <<= s;
     nb -= s;
+    pos += (uint32_t)s;
     return r;
   }
 };
@@ -555,9 +571,11 @@ __device__ __forceinline__ int32_t jpg_mca(const int32_t* __restrict__ maxcode, 
   return i == 7 ? 0x7FFFFFFF : m;
 }
 
-// one Huffman symbol (nb >= 32 on entry); returns the symbol and its code length in *len
+// one Huffman symbol (nb >= 32 on entry); returns the symbol and its code length in *len.  A bit
+// pattern that is no code: symbol 0, badlen bits, *bad set (see jpeg_write_kernel on badlen)
 template <typename TT>
-__device__ __forceinline__ int jpg_decode(uint64_t acc, const TT& T, int t, int* len) {
+__device__ __forceinline__ int jpg_decode(uint64_t acc, const TT& T, int t, int* len,
+                                          int badlen = 17, bool* bad = nullptr) {
   const uint32_t e = T.lut[t][acc >> (64 - JPG_LUTB)];
   if (e) {
     *len = (int)(e >> 8);
@@ -568,8 +586,9 @@ __device__ __forceinline__ int jpg_decode(uint64_t acc, const TT& T, int t, int*
   const int4 m1 = *reinterpret_cast<const int4*>(&T.mca[t][4]);
   const int l = 10 + (c16 > m0.x) + (c16 > m0.y) + (c16 > m0.z) + (c16 > m0.w) + (c16 > m1.x) +
                 (c16 > m1.y) + (c16 > m1.z);
-  if (l > 16) {  // not a code (only on a speculative trajectory or a corrupt file): skip 16 bits
-    *len = 16;
+  if (l > 16) {  // not a code (a speculative trajectory or a corrupt file): jdhuff.c
+    *len = badlen;  // jpeg_huff_decode reads up to length 17, then JWRN_HUFF_BAD_CODE, symbol 0
+    if (bad) *bad = true;
     return 0;
   }
   *len = l;
@@ -667,13 +686,21 @@ constexpr int JRING_W = JRG * 4 + 4;   // ring words per lane (one pad group: la
 // with DC predictors pred[]; else count DC symbols and DC differences.  Returns the end state.
 // One symbol per iteration, DC or AC through the same decode (a DC symbol is a size 0..15, i.e. a
 // run/size byte with run 0) and the block bookkeeping by selects.
-template <bool WRITE>
+// Where the data ends, libjpeg (jdhuff.c: jpeg_fill_bit_buffer's zero bits, insufficient_data)
+// decodes an MCU only if the data lasted up to its start, reading 0 past the end:
+//   tail  (chunked decoder, WRITE) end_bit is the end of the data: complete the MCU in progress,
+//         and one that starts exactly at the end, never past the image's last block
+//   MASK  (a restart interval, whose data the next one's follows) bits from end_bit on read as 0;
+//         stop at dc_limit DC symbols or at an MCU that starts past end_bit
+template <bool WRITE, bool MASK = false>
 __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T, rsrc_t rs,
                                             uint32_t* __restrict__ ring, uint64_t st,
                                             uint32_t end_bit, ChunkOut* cnt, int32_t blk,
                                             int (&pred)[3], int16_t* __restrict__ coef,
-                                            uint32_t dc_limit = 0xFFFFFFFFu) {
+                                            uint32_t dc_limit = 0xFFFFFFFFu, bool tail = false,
+                                            int badlen = 17, uint32_t* badseen = nullptr) {
   uint32_t ndc = 0;
+  bool bad_real = false;  // WRITE: a bad code inside the image's blocks
   uint32_t pos = (uint32_t)st, ph = (uint32_t)(st >> 32) & 0xFF, z = (uint32_t)(st >> 40) & 0xFF;
   // ring: words wi .. of groups (wi >> 2) .. (wi >> 2) + JRG - 1 at ring[w & (4 JRG - 1)]; pend =
   // group (wi >> 2) + JRG, raw
@@ -691,7 +718,14 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
   v4u pend = __builtin_amdgcn_raw_buffer_load_b128(rs, ((wi >> 2) + JRG) * 16u, 0, 0);
   uint64_t acc = 0;
   int nb = 0;
-  uint32_t nxt = ring[wi & (4 * JRG - 1)];
+  // word wix of the stream (MASK: its bits from end_bit on cleared)
+  auto fetch = [&](uint32_t wix) -> uint32_t {
+    const uint32_t v = ring[wix & (4 * JRG - 1)];
+    if (!MASK) return v;
+    const int64_t r = (int64_t)end_bit - 32 * (int64_t)wix;
+    return r >= 32 ? v : r <= 0 ? 0u : v & ~(0xFFFFFFFFu >> (uint32_t)r);
+  };
+  uint32_t nxt = fetch(wi);
   // append word wi (nxt) to acc; a new group retires its predecessor's slot to pend
   auto append = [&](bool need) {
     acc |= need ? (uint64_t)nxt << (32 - nb) : 0ull;
@@ -703,7 +737,7 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
               __builtin_bswap32(pend.w)};
       pend = __builtin_amdgcn_raw_buffer_load_b128(rs, ((wi >> 2) + JRG) * 16u, 0, 0);
     }
-    nxt = ring[wi & (4 * JRG - 1)];
+    nxt = fetch(wi);
   };
   append(true);
   append(true);
@@ -713,14 +747,26 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
   if (WRITE && z != 0) bp = jpg_block(K, coef, blk, ph, (int)(K.phase_info >> (6 * ph)) & 3);
   int32_t s0 = 0, s1 = 0, s2 = 0, nblk = 0;
   int p0 = pred[0], p1 = pred[1], p2 = pred[2];
-  while (pos < end_bit) {
+  for (;;) {
+    const bool dc = z == 0;
+    if (MASK) {
+      if (dc && ph == 0 && (ndc == dc_limit || pos > end_bit)) break;
+    } else {
+      if (pos >= end_bit) {
+        if (!WRITE || !tail) break;
+        const bool go = dc && ph == 0 ? pos == end_bit && (uint32_t)(blk + 1) < K.total_blocks
+                                      : (uint32_t)blk < K.total_blocks;
+        if (!go) break;
+      }
+      if (dc && ndc == dc_limit) break;
+    }
     append(nb < 32);
     const uint32_t info = (uint32_t)(K.phase_info >> (6 * ph));
     const int c = info & 3;
-    const bool dc = z == 0;
-    if (dc && ndc == dc_limit) break;
     int len;
-    const int rs8 = jpg_decode(acc, T, dc ? (info >> 2) & 3 : (info >> 4) & 3, &len);
+    bool bad = false;
+    const int rs8 = jpg_decode(acc, T, dc ? (info >> 2) & 3 : (info >> 4) & 3, &len, badlen, &bad);
+    if (WRITE) bad_real |= bad && (uint32_t)(dc ? blk + 1 : blk) < K.total_blocks;
     const int r = rs8 >> 4, s = rs8 & 15;
     const int val = s ? jpg_extend((uint32_t)((acc << len) >> 32) >> (32 - s), s) : 0;
     acc <<= len + s;
@@ -755,6 +801,7 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
   pred[0] = p0;
   pred[1] = p1;
   pred[2] = p2;
+  if (WRITE && badseen && bad_real) *badseen = 1u;
   if (!WRITE) {
     cnt->nblk += nblk;
     cnt->dcsum[0] += s0;
@@ -766,20 +813,24 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
 
 // stage 1: unstuff, in 16 KiB tiles of the segment (1024 threads x 16 bytes), every tile its own
 // workgroup (one workgroup per image walked its tiles in sequence: 0.28 ms for a single 600x1000
-// file): count the tile's kept bytes and RST markers, then each tile writes from the sum of the
-// tiles before it, then per segment the length, the zero padding and the missing intervals.
+// file): count the tile's kept bytes and markers, then each tile writes from the sum of the tiles
+// before it (the kept bytes, and every marker's code and unstuffed offset), then per segment the
+// length, the zero padding and the restart intervals (jpeg_unstuff_final).
 // (DESC: a JpegDev per image, or a JpegScanDev per scan of the scan path: the same fields)
 constexpr uint32_t UNS_TILE = 1024 * 16;
+constexpr uint32_t JPG_MK_EXTRA = 64;  // marker table room beyond the restart markers
+constexpr uint32_t JPG_IV_INHERIT = 0x80000000u;  // interval end flag: see jpeg_unstuff_final
+constexpr size_t JPG_MAX_SCAN = ((size_t)1 << 28) - 64;  // bytes: bit positions below the flag
 
-// the thread's 16 bytes [i0, i0 + 16): bit k of keep = byte i0 + k is data, of rstm = a RST marker
-// ends at byte i0 + k
+// the thread's 16 bytes [i0, i0 + 16): bit k of keep = byte i0 + k is data, of mkm = byte i0 + k is
+// a marker's code (0xFF followed by neither 0x00 nor 0xFF: RSTn or any other marker)
 // (the segment starts 16-byte aligned and its buffer is padded to whole 16-byte groups: one
 // 16-byte load per thread, plus the bytes either side)
 __device__ __forceinline__ void unstuff_masks(const uint8_t* __restrict__ in, uint32_t n,
-                                              uint32_t i0, uint32_t& keep, uint32_t& rstm,
+                                              uint32_t i0, uint32_t& keep, uint32_t& mkm,
                                               uint32_t (&w)[4]) {
   keep = 0;
-  rstm = 0;
+  mkm = 0;
   const uint4 v = *reinterpret_cast<const uint4*>(in + i0);
   w[0] = v.x;
   w[1] = v.y;
@@ -795,9 +846,9 @@ __device__ __forceinline__ void unstuff_masks(const uint8_t* __restrict__ in, ui
     bool kp;
     if (pv == 0xFF && b == 0x00) {
       kp = false;  // stuffing
-    } else if (pv == 0xFF && b >= 0xD0 && b <= 0xD7) {
-      kp = false;  // RST marker code
-      if (i < n) rstm |= 1u << k;
+    } else if (pv == 0xFF && b != 0xFF) {
+      kp = false;  // a marker code
+      if (i < n) mkm |= 1u << k;
     } else if (b == 0xFF) {
       kp = i + 1 < n && nx == 0x00;  // data 0xFF (stuffed); else fill / marker prefix
     } else {
@@ -811,22 +862,14 @@ __device__ __forceinline__ void unstuff_masks(const uint8_t* __restrict__ in, ui
 template <typename DESC>
 __global__ __launch_bounds__(1024) void jpeg_unstuff_count(const DESC* __restrict__ imgs,
                                                            const uint8_t* __restrict__ scans,
-                                                           uint2* __restrict__ tcnt, int mt,
-                                                           uint32_t* __restrict__ ivstart) {
+                                                           uint2* __restrict__ tcnt, int mt) {
   const DESC& D = imgs[blockIdx.y];
-  if (blockIdx.x == 0) {
-    // intervals whose RST marker is missing (truncated / corrupt file) must not start at
-    // garbage: marked here, set to the end of the data by jpeg_unstuff_final
-    if (threadIdx.x == 0) ivstart[D.iv_off] = 0;
-    for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x)
-      ivstart[D.iv_off + k] = ~0u;
-  }
   const uint32_t base = blockIdx.x * UNS_TILE;
   if (base >= D.scan_len) return;  // uniform
-  uint32_t keep = 0, rstm = 0, w[4];
+  uint32_t keep = 0, mkm = 0, w[4];
   if (base + threadIdx.x * 16 < D.scan_len)
-    unstuff_masks(scans + D.scan_off, D.scan_len, base + threadIdx.x * 16, keep, rstm, w);
-  uint32_t a = __popc(keep), r = __popc(rstm);
+    unstuff_masks(scans + D.scan_off, D.scan_len, base + threadIdx.x * 16, keep, mkm, w);
+  uint32_t a = __popc(keep), r = __popc(mkm);
   for (int o = 32; o > 0; o >>= 1) {
     a += (uint32_t)__shfl_xor((int)a, o);
     r += (uint32_t)__shfl_xor((int)r, o);
@@ -853,13 +896,13 @@ __global__ __launch_bounds__(1024) void jpeg_unstuff_write(const DESC* __restric
                                                            const uint8_t* __restrict__ scans,
                                                            const uint2* __restrict__ tcnt, int mt,
                                                            uint8_t* __restrict__ ub,
-                                                           uint32_t* __restrict__ ivstart) {
+                                                           uint2* __restrict__ mk) {
   const DESC& D = imgs[blockIdx.y];
   const uint32_t base = blockIdx.x * UNS_TILE;
   if (base >= D.scan_len) return;  // uniform
   __shared__ uint32_t wsum[16], wrst[16], base_s[2];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // kept bytes and RST markers of the tiles before this one
+  // kept bytes and markers of the tiles before this one
   if (wv == 0) {
     uint32_t a = 0, r = 0;
     for (int k = lane; k < (int)blockIdx.x; k += 64) {
@@ -878,10 +921,10 @@ __global__ __launch_bounds__(1024) void jpeg_unstuff_write(const DESC* __restric
   }
   const uint8_t* in = scans + D.scan_off;
   const uint32_t i0 = base + threadIdx.x * 16;
-  uint32_t keep = 0, rstm = 0, w[4] = {0u, 0u, 0u, 0u};
-  if (i0 < D.scan_len) unstuff_masks(in, D.scan_len, i0, keep, rstm, w);
-  // block-wide exclusive scans of the kept-byte and RST-marker counts
-  const uint32_t cntk = __popc(keep), nr = __popc(rstm);
+  uint32_t keep = 0, mkm = 0, w[4] = {0u, 0u, 0u, 0u};
+  if (i0 < D.scan_len) unstuff_masks(in, D.scan_len, i0, keep, mkm, w);
+  // block-wide exclusive scans of the kept-byte and marker counts
+  const uint32_t cntk = __popc(keep), nr = __popc(mkm);
   uint32_t inc = cntk, rinc = nr;
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = (uint32_t)__shfl_up((int)inc, o), q = (uint32_t)__shfl_up((int)rinc, o);
@@ -905,35 +948,120 @@ __global__ __launch_bounds__(1024) void jpeg_unstuff_write(const DESC* __restric
   uint8_t* out = ub + D.ub_off;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (keep >> k & 1u) out[o++] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-    // RST markers: the next interval starts at the unstuffed position after this byte
-    if ((rstm >> k & 1u) && orank + 1 < (uint32_t)D.nintervals)
-      ivstart[D.iv_off + 1 + orank++] = o * 8u;
+    const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+    if (keep >> k & 1u) out[o++] = (uint8_t)b;
+    // a marker: its code and the unstuffed offset where the data before it ends (the table's room
+    // holds every restart marker of an intact file plus JPG_MK_EXTRA others)
+    if (mkm >> k & 1u) {
+      if (orank < D.mk_cap) mk[D.mk_off + orank] = make_uint2(o, b);
+      ++orank;
+    }
   }
 }
 
+// Per segment (one workgroup): its length, the zero padding behind it, and where each restart
+// interval's data begins and ends (bits) -- as libjpeg reads them (jdhuff.c process_restart ->
+// jdmarker.c read_restart_marker / jpeg_resync_to_restart).  The markers split the data into
+// segments; interval 0 reads segment 0.  At each restart the marker ending the current segment is
+// the expected RSTn (taken: the interval reads the next segment), or resync decides: action 1
+// (the expected RST or one too far away) take it; action 2 (a marker below SOF0 or one of the two
+// RSTs before the expected one) skip to the marker after the next segment and decide again;
+// action 3 (any other marker, one of the next two RSTs, or none left: the data ended) leave it --
+// the interval reads nothing and inherits the out-of-data state (JPG_IV_INHERIT in its end entry).
+// An intact file takes the parallel fast path: marker r is RST(r mod 8).  Without restart
+// intervals the data simply ends at the first marker: for the chunked decoder ublen says so.
 template <typename DESC>
 __global__ __launch_bounds__(256) void jpeg_unstuff_final(const DESC* __restrict__ imgs,
                                                           const uint2* __restrict__ tcnt, int mt,
                                                           uint8_t* __restrict__ ub,
+                                                          const uint2* __restrict__ mk,
                                                           uint32_t* __restrict__ ivstart,
+                                                          uint32_t* __restrict__ ivend,
                                                           uint32_t* __restrict__ ublen) {
   const DESC& D = imgs[blockIdx.x];
-  __shared__ uint32_t len_s;
+  __shared__ uint32_t len_s, nmk_s, bad_s;
   if (threadIdx.x < 64) {
     const int ntiles = (int)((D.scan_len + UNS_TILE - 1) / UNS_TILE);
-    uint32_t a = 0;
-    for (int k = threadIdx.x; k < ntiles; k += 64) a += tcnt[(size_t)blockIdx.x * mt + k].x;
-    for (int o = 32; o > 0; o >>= 1) a += (uint32_t)__shfl_xor((int)a, o);
-    if (threadIdx.x == 0) len_s = a;
+    uint32_t a = 0, r = 0;
+    for (int k = threadIdx.x; k < ntiles; k += 64) {
+      const uint2 c = tcnt[(size_t)blockIdx.x * mt + k];
+      a += c.x;
+      r += c.y;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      a += (uint32_t)__shfl_xor((int)a, o);
+      r += (uint32_t)__shfl_xor((int)r, o);
+    }
+    if (threadIdx.x == 0) {
+      len_s = a;
+      nmk_s = min(r, D.mk_cap);
+      bad_s = 0;
+    }
   }
   __syncthreads();
-  const uint32_t len = len_s;
-  // zero padding behind the data (the bit readers prefetch up to 40 bytes ahead)
+  const uint32_t len = len_s, M = nmk_s, n = (uint32_t)D.nintervals;
+  const uint2* m = mk + D.mk_off;
+  // segment s: [start, end) bytes and the marker that ends it (after the last one: EOI)
+  auto seg_start = [&](uint32_t s) { return s == 0 ? 0u : m[s - 1].x; };
+  auto seg_end = [&](uint32_t s) { return s < M ? m[s].x : len; };
+  auto seg_mark = [&](uint32_t s) { return s < M ? m[s].y : 0xD9u; };
+  if (n == 1) {  // no restart intervals: the data ends at the first marker
+    const uint32_t e = seg_end(0);
+    if (threadIdx.x < 64) ub[D.ub_off + e + threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+      ublen[blockIdx.x] = e;
+      ivstart[D.iv_off] = 0;
+      ivend[D.iv_off] = e * 8u;
+    }
+    return;
+  }
   if (threadIdx.x < 64) ub[D.ub_off + len + threadIdx.x] = 0;
   if (threadIdx.x == 0) ublen[blockIdx.x] = len;
-  for (int k = 1 + (int)threadIdx.x; k < D.nintervals; k += blockDim.x)
-    if (ivstart[D.iv_off + k] == ~0u) ivstart[D.iv_off + k] = len * 8u;
+  // fast path: every marker is the next RSTn, no more of them than restarts
+  for (uint32_t r = threadIdx.x; r < M; r += blockDim.x)
+    if (m[r].y != 0xD0u + (r & 7u)) bad_s = 1;
+  __syncthreads();
+  if (!bad_s && M < n) {
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+      const bool has = k <= M;  // interval k reads segment k; past the data's end: nothing
+      ivstart[D.iv_off + k] = has ? seg_start(k) * 8u : len * 8u;
+      ivend[D.iv_off + k] = has ? seg_end(k) * 8u : len * 8u | JPG_IV_INHERIT;
+    }
+    return;
+  }
+  if (threadIdx.x != 0) return;
+  // a damaged file: libjpeg's restart processing, serially
+  uint32_t j = 0, want = 0;
+  ivstart[D.iv_off] = 0;
+  ivend[D.iv_off] = seg_end(0) * 8u;
+  for (uint32_t k = 1; k < n; ++k) {
+    uint32_t mc = seg_mark(j);
+    int act;
+    for (;;) {
+      const uint32_t w0 = 0xD0u + want;
+      if (mc == w0) act = 1;
+      else if (mc < 0xC0u) act = 2;
+      else if (mc < 0xD0u || mc > 0xD7u) act = 3;
+      else if (mc == 0xD0u + ((want + 1) & 7u) || mc == 0xD0u + ((want + 2) & 7u)) act = 3;
+      else if (mc == 0xD0u + ((want - 1) & 7u) || mc == 0xD0u + ((want - 2) & 7u)) act = 2;
+      else act = 1;
+      if (act == 2 && j < M) {
+        ++j;
+        mc = seg_mark(j);
+        continue;
+      }
+      break;
+    }
+    want = (want + 1) & 7u;
+    if (act == 1 && j < M) {
+      ++j;
+      ivstart[D.iv_off + k] = seg_start(j) * 8u;
+      ivend[D.iv_off + k] = seg_end(j) * 8u;
+    } else {
+      ivstart[D.iv_off + k] = len * 8u;
+      ivend[D.iv_off + k] = len * 8u | JPG_IV_INHERIT;
+    }
+  }
 }
 
 // stage 2a/2b: sync passes.  grid (max chunks per image, n).  PASS_A: start from the chunk's
@@ -954,7 +1082,8 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
                                                        uint8_t* __restrict__ chg_next, int all,
                                                        uint64_t* __restrict__ ck_st,
                                                        ChunkOut* __restrict__ ck_co,
-                                                       const uint32_t* __restrict__ settled) {
+                                                       const uint32_t* __restrict__ settled,
+                                                       int badlen) {
   __shared__ JpegLds T;
   __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
   // the previous pass of this launch round changed nothing: the decode has converged and both
@@ -988,7 +1117,7 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
   ChunkOut co{0u, {0, 0, 0}};
   int pred[3] = {0, 0, 0};
   const JpgConst K = jpg_const(D);
-  const rsrc_t rs = make_rsrc(ub + D.ub_off, D.scan_len + 64u);  // past the padding: zeros
+  const rsrc_t rs = make_rsrc(ub + D.ub_off, nbits / 8u + 64u);  // past the padding: zeros
   uint64_t e = st;
   for (uint32_t j = 0; j < nsub; ++j) {
     if (!PASS_A && e == cks[j]) {
@@ -1019,7 +1148,8 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
     const uint32_t sub_end = min(b0 + (j + 1) * JPG_SUB, b1);
     // a state past the sub-chunk (the predecessor ran over it) ends where it starts
     if ((uint32_t)e < sub_end)
-      e = jpg_run<false>(K, T, rs, ring + threadIdx.x * JRING_W, e, sub_end, &co, 0, pred, nullptr);
+      e = jpg_run<false>(K, T, rs, ring + threadIdx.x * JRING_W, e, sub_end, &co, 0, pred, nullptr,
+                         0xFFFFFFFFu, false, badlen);
   }
   next[D.ch_off + t] = e;
   cnt[D.ch_off + t] = co;
@@ -1081,10 +1211,12 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
                                                         const uint8_t* __restrict__ ub,
                                                         const uint32_t* __restrict__ ublen,
                                                         const uint32_t* __restrict__ ivstart,
+                                                        const uint32_t* __restrict__ ivend,
                                                         const uint64_t* __restrict__ ck_st,
                                                         const ChunkOut* __restrict__ ck_co,
                                                         const ChunkOut* __restrict__ start,
-                                                        int16_t* __restrict__ coef) {
+                                                        int16_t* __restrict__ coef, int badlen,
+                                                        uint32_t* __restrict__ badseen) {
   __shared__ JpegLds T;
   __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
   const JpegDev& D = imgs[blockIdx.y];
@@ -1097,34 +1229,54 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
   if (u >= nitems) return;
   const uint32_t nbits = ublen[blockIdx.y] * 8u;
   int pred[3] = {0, 0, 0};
-  uint64_t st;
-  uint32_t b1, dc_limit = 0xFFFFFFFFu;
-  int32_t blk;
-  if (D.restart) {  // interval u: restart MCUs from its first bit, DC predictors reset
-    const uint32_t b0 = min(ivstart[D.iv_off + u], nbits);
-    b1 = u + 1 < nitems ? min(ivstart[D.iv_off + u + 1], nbits) : nbits;
-    // stop after the interval's MCUs: the bits behind them are the encoder's padding (1s)
-    const uint32_t mcu0 = u * (uint32_t)D.restart;
-    dc_limit = min((uint32_t)D.restart, (uint32_t)(D.mcux * D.mcuy) - mcu0) * D.bpm;
-    st = jpg_state(b0, 0, 0);
-    blk = (int32_t)(mcu0 * D.bpm) - 1;
-  } else {  // sub-chunk j of chunk t from its checkpoint: state, first block, DC predictors
-    const uint32_t t = u / nsub, j = u - t * nsub;
-    const uint32_t b0 = min(t * D.chunk_bits, nbits);
-    b1 = min(min(b0 + D.chunk_bits, nbits), b0 + (j + 1) * JPG_SUB);
-    const size_t k = (size_t)(D.ch_off + t) * nsub + j;
-    st = ck_st[k];
-    const ChunkOut c = ck_co[k], s0 = start[D.ch_off + t];
-    pred[0] = s0.dcsum[0] + c.dcsum[0];
-    pred[1] = s0.dcsum[1] + c.dcsum[1];
-    pred[2] = s0.dcsum[2] + c.dcsum[2];
-    blk = (int32_t)(s0.nblk + c.nblk) - 1;
-  }
-  if ((uint32_t)st >= b1) return;
   ChunkOut dummy{0u, {0, 0, 0}};
   const JpgConst K = jpg_const(D);
-  const rsrc_t rs = make_rsrc(ub + D.ub_off, D.scan_len + 64u);
-  jpg_run<true>(K, T, rs, ring + threadIdx.x * JRING_W, st, b1, &dummy, blk, pred, coef, dc_limit);
+  uint32_t* myring = ring + threadIdx.x * JRING_W;
+  if (D.restart) {
+    // interval u: restart MCUs from its first bit, DC predictors reset, its data's end masked.  An
+    // interval that reads nothing and inherits the out-of-data state decodes nothing itself: if
+    // its predecessor did not run out, libjpeg decodes its first MCU from zero bits -- here, by
+    // the predecessor's thread
+    const uint32_t ie = ivend[D.iv_off + u];
+    if (ie & JPG_IV_INHERIT) return;
+    const uint32_t b0 = ivstart[D.iv_off + u], b1 = ie;
+    const uint32_t mcus = (uint32_t)(D.mcux * D.mcuy), mcu0 = u * (uint32_t)D.restart;
+    const uint32_t mcu1 = min(mcu0 + (uint32_t)D.restart, mcus);
+    const rsrc_t rs = make_rsrc(ub + D.ub_off, nbits / 8u + 64u);
+    const uint64_t e = jpg_run<true, true>(K, T, rs, myring, jpg_state(b0, 0, 0), b1, &dummy,
+                                           (int32_t)(mcu0 * D.bpm) - 1, pred, coef,
+                                           (mcu1 - mcu0) * (uint32_t)D.bpm);
+    if (u + 1 < nitems && (ivend[D.iv_off + u + 1] & JPG_IV_INHERIT) && (uint32_t)e <= b1) {
+      int pz[3] = {0, 0, 0};
+      jpg_run<true, true>(K, T, rs, myring, jpg_state(b1, 0, 0), b1, &dummy,
+                          (int32_t)(mcu1 * D.bpm) - 1, pz, coef, (uint32_t)D.bpm);
+    }
+    return;
+  }
+  // sub-chunk j of chunk t from its checkpoint: state, first block, DC predictors.  badlen: the
+  // bits a bad code takes.  libjpeg's is 17, but the sync passes converge a pass sooner with 16
+  // (1.21 against 1.31 ms for a 600x1000 file: bad codes are frequent on the speculative
+  // trajectories), so the host decodes with 16 first; the trajectories agree up to the first bad
+  // code on the true one, which the write pass then reports (badseen) and the host decodes again
+  // with 17 -- only files with a bad code in their data pay for the exact rule
+  const uint32_t t = u / nsub, j = u - t * nsub;
+  const uint32_t b0 = min(t * D.chunk_bits, nbits);
+  const uint32_t b1 = min(min(b0 + D.chunk_bits, nbits), b0 + (j + 1) * JPG_SUB);
+  // the sub-chunk holding the data's last bit (or the first one, without data) finishes the
+  // decode where the data ends
+  const uint32_t tl = nbits ? (nbits - 1) / D.chunk_bits : 0u;
+  const bool tail = t == tl && j == (nbits ? (nbits - 1 - tl * D.chunk_bits) / JPG_SUB : 0u);
+  const size_t k = (size_t)(D.ch_off + t) * nsub + j;
+  const uint64_t st = ck_st[k];
+  const ChunkOut c = ck_co[k], s0 = start[D.ch_off + t];
+  pred[0] = s0.dcsum[0] + c.dcsum[0];
+  pred[1] = s0.dcsum[1] + c.dcsum[1];
+  pred[2] = s0.dcsum[2] + c.dcsum[2];
+  const int32_t blk = (int32_t)(s0.nblk + c.nblk) - 1;
+  if ((uint32_t)st >= b1 && !tail) return;
+  const rsrc_t rs = make_rsrc(ub + D.ub_off, nbits / 8u + 64u);
+  jpg_run<true>(K, T, rs, myring, st, b1, &dummy, blk, pred, coef, 0xFFFFFFFFu, tail, badlen,
+                badseen);
 }
 
 // ---- device: the scan path (progressive / multi-scan files) --------------------------------------
@@ -1251,10 +1403,40 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
   }
 }
 
+// the scan path's unit u of scan S: an MCU (interleaved) or one block of the scan's component
+__device__ __forceinline__ void jpg_scan_unit(BitStream& br, const JpegLdsScan& T, const JpegDev& D,
+                                              const JpegScanDev& S, uint32_t u,
+                                              int16_t* __restrict__ coef, int (&pred)[4],
+                                              uint32_t& eobrun) {
+  if (S.ns == 1) {  // non-interleaved: the component's own blocks, raster order
+    const int c = S.comp[0];
+    const uint32_t by = u / (uint32_t)D.wib[c], bx = u - by * (uint32_t)D.wib[c];
+    int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
+    jpg_scan_block(br, T, S, 0, blk, pred[0], eobrun);
+  } else {  // interleaved MCU (sequential, or a progressive DC scan)
+    const uint32_t my = u / (uint32_t)D.mcux, mx = u - my * (uint32_t)D.mcux;
+    for (int k = 0; k < S.ns; ++k) {
+      const int c = S.comp[k];
+      for (int dv = 0; dv < D.cv[c]; ++dv)
+        for (int dh = 0; dh < D.ch[c]; ++dh) {
+          const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
+          int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
+          jpg_scan_block(br, T, S, k, blk, pred[k], eobrun);
+        }
+    }
+  }
+}
+
+// Out of data (jdhuff.c insufficient_data): a unit is decoded only while the interval's data lasted
+// up to its start (a skipped unit keeps what the earlier scans left); an interval that reads
+// nothing and inherits the out-of-data state is the predecessor's lane's: it decodes the first unit
+// from zero bits if the predecessor did not run out (see jpeg_unstuff_final)
 __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict__ imgs,
                                                        const JpegScanDev* __restrict__ scans,
                                                        const uint8_t* __restrict__ ub,
                                                        const uint32_t* __restrict__ ivstart,
+                                                       const uint32_t* __restrict__ ivend,
+                                                       const uint32_t* __restrict__ ublen_s,
                                                        int16_t* __restrict__ coef) {
   __shared__ JpegLdsScan T;
   const JpegDev& D = imgs[blockIdx.x];
@@ -1267,31 +1449,23 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
     __syncthreads();
     jpg_load_scan_tables(T, S);
     __syncthreads();
+    const rsrc_t rs = make_rsrc(ub + S.ub_off, ublen_s[D.scan0 + si] + 64u);
     for (int t = threadIdx.x; t < S.nintervals; t += 64) {
+      const uint32_t ie = ivend[S.iv_off + t];
+      if (ie & JPG_IV_INHERIT) continue;
       const uint32_t u0 = S.restart ? (uint32_t)t * (uint32_t)S.restart : 0u;
       const uint32_t u1 = S.restart ? min(u0 + (uint32_t)S.restart, S.nunits) : S.nunits;
       BitStream br;
-      br.start(ub + S.ub_off, ivstart[S.iv_off + t]);
+      br.start(rs, ivstart[S.iv_off + t], ie);
       int pred[4] = {0, 0, 0, 0};
       uint32_t eobrun = 0;
-      for (uint32_t u = u0; u < u1; ++u) {
-        if (S.ns == 1) {  // non-interleaved: the component's own blocks, raster order
-          const int c = S.comp[0];
-          const uint32_t by = u / (uint32_t)D.wib[c], bx = u - by * (uint32_t)D.wib[c];
-          int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
-          jpg_scan_block(br, T, S, 0, blk, pred[0], eobrun);
-        } else {  // interleaved MCU (sequential, or a progressive DC scan)
-          const uint32_t my = u / (uint32_t)D.mcux, mx = u - my * (uint32_t)D.mcux;
-          for (int k = 0; k < S.ns; ++k) {
-            const int c = S.comp[k];
-            for (int dv = 0; dv < D.cv[c]; ++dv)
-              for (int dh = 0; dh < D.ch[c]; ++dh) {
-                const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
-                int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
-                jpg_scan_block(br, T, S, k, blk, pred[k], eobrun);
-              }
-          }
-        }
+      for (uint32_t u = u0; u < u1 && br.pos <= ie; ++u) jpg_scan_unit(br, T, D, S, u, coef, pred, eobrun);
+      if (t + 1 < S.nintervals && (ivend[S.iv_off + t + 1] & JPG_IV_INHERIT) && br.pos <= ie &&
+          u1 < S.nunits) {
+        int pz[4] = {0, 0, 0, 0};
+        uint32_t ez = 0;
+        br.start(rs, ie, ie);
+        jpg_scan_unit(br, T, D, S, u1, coef, pz, ez);
       }
     }
   }
@@ -1486,7 +1660,7 @@ __global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restric
                                                         const JpegScanDev* __restrict__ scans,
                                                         const uint8_t* __restrict__ ub,
                                                         const uint32_t* __restrict__ ivstart,
-                                                        const uint32_t* __restrict__ ublen_s,
+                                                        const uint32_t* __restrict__ ivend,
                                                         int16_t* __restrict__ coef) {
   __shared__ uint8_t stats[64 * JAR_LANE];
   const JpegDev& D = imgs[blockIdx.x];
@@ -1504,8 +1678,9 @@ __global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restric
       for (int k = 0; k < JAR_LANE; k += 16) *reinterpret_cast<uint4*>(mine + k) = make_uint4(0, 0, 0, 0);
       ArithDec e;
       e.p = ub + S.ub_off;
+      // (jdarith.c has no out-of-data state: past its data an interval decodes zeros)
       e.i = ivstart[S.iv_off + t] >> 3;
-      e.end = t + 1 < S.nintervals ? ivstart[S.iv_off + t + 1] >> 3 : ublen_s[D.scan0 + si];
+      e.end = (ivend[S.iv_off + t] & ~JPG_IV_INHERIT) >> 3;
       e.c = 0;
       e.a = 0;
       e.ct = -16;
@@ -1965,12 +2140,13 @@ struct JpegPlan {
   std::vector<size_t> scan_src;     // their first byte in the file
   uint64_t scan_bytes = 0, nblk = 0, plane_bytes = 0, ub_bytes = 0;
   uint32_t nintervals = 0, nchunks = 0, max_items = 1, max_items_w = 1, nsub = 1;
+  uint64_t nmk = 0;  // marker table entries
   int mt_img = 1, mt_scan = 1;  // most unstuffing tiles of an image / of a scan
   bool any_chunked = false;
   bool any_huff_scan = false, any_arith = false;  // scan-path images of each coding
   bool scales[2][2] = {};  // IDCT output scales present: [sv - 1][sh - 1]
   size_t off_imgs = 0, off_blkend = 0, off_scans = 0, off_scan = 0, off_coef = 0, off_planes = 0;
-  size_t off_ub = 0, off_iv = 0, off_ublen = 0, off_ublen_s = 0, off_s0 = 0, off_s1 = 0,
+  size_t off_ub = 0, off_iv = 0, off_ivend = 0, off_mk = 0, off_ublen = 0, off_ublen_s = 0, off_s0 = 0, off_s1 = 0,
          off_cnt = 0, off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, off_ck_st = 0,
          off_ck_co = 0, off_tcnt = 0, total = 0;
 };
@@ -2098,6 +2274,8 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
       D.iv_off = P.nintervals;
       D.nintervals = 1;
       P.nintervals += 1;
+      D.mk_off = P.nmk;
+      D.mk_cap = 0;
       D.restart = 0;
       D.nchunks = 0;
       D.scan0 = (uint32_t)P.scans.size();
@@ -2145,7 +2323,7 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
           }
         }
         const size_t len = S.end - S.begin;
-        if ((uint64_t)len * 8 >= 0xFFFFFFF0ull) return jpg_fail(err, "scan too large");
+        if (len >= JPG_MAX_SCAN) return jpg_fail(err, "scan too large");
         SD.scan_off = P.scan_bytes;
         SD.scan_len = (uint32_t)len;
         P.scan_bytes += (len + 15) & ~(size_t)15;
@@ -2153,6 +2331,9 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
         P.ub_bytes += (len + 64 + 15) & ~(size_t)15;
         SD.iv_off = P.nintervals;
         P.nintervals += (uint32_t)SD.nintervals;
+        SD.mk_off = P.nmk;
+        SD.mk_cap = (uint32_t)SD.nintervals + JPG_MK_EXTRA;
+        P.nmk += SD.mk_cap;
         P.scans.push_back(SD);
         P.scan_src.push_back(S.begin);
       }
@@ -2168,12 +2349,15 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     D.scan_off = P.scan_bytes;
     D.scan_len = (uint32_t)(J.scan_end - J.scan_begin);
     P.scan_begin[i] = J.scan_begin;
-    if ((uint64_t)D.scan_len * 8 >= 0xFFFFFFF0ull) return jpg_fail(err, "scan too large");
+    if (J.scan_end - J.scan_begin >= JPG_MAX_SCAN) return jpg_fail(err, "scan too large");
     P.scan_bytes += (D.scan_len + 15) & ~15u;
     D.ub_off = P.ub_bytes;
     P.ub_bytes += (D.scan_len + 64 + 15) & ~15u;
     D.iv_off = P.nintervals;
     P.nintervals += (uint32_t)D.nintervals;
+    D.mk_off = P.nmk;
+    D.mk_cap = (uint32_t)D.nintervals + JPG_MK_EXTRA;
+    P.nmk += D.mk_cap;
     if (!D.restart) chunked_bits += (uint64_t)D.scan_len * 8;
   }
   // entropy chunks (the self-synchronising decoder's threads).  Default size: about 100k chunks
@@ -2207,7 +2391,9 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
   P.off_planes = align256(P.off_coef + P.nblk * 128);
   P.off_ub = align256(P.off_planes + P.plane_bytes);
   P.off_iv = align256(P.off_ub + P.ub_bytes);
-  P.off_ublen = align256(P.off_iv + sizeof(uint32_t) * (size_t)P.nintervals);
+  P.off_ivend = align256(P.off_iv + sizeof(uint32_t) * (size_t)P.nintervals);
+  P.off_mk = align256(P.off_ivend + sizeof(uint32_t) * (size_t)P.nintervals);
+  P.off_ublen = align256(P.off_mk + sizeof(uint2) * (size_t)P.nmk);
   P.off_ublen_s = align256(P.off_ublen + sizeof(uint32_t) * (size_t)n);
   P.off_s0 = align256(P.off_ublen_s + sizeof(uint32_t) * (P.scans.size() + 1));
   P.off_s1 = align256(P.off_s0 + sizeof(uint64_t) * (size_t)P.nchunks);
@@ -2330,12 +2516,13 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     }
     for (auto& t : th) t.join();
   }
-  if (!copy_ok || hipMemsetAsync(ws + P.off_coef, 0, P.nblk * 128, st) != hipSuccess)
-    return set_error(IDN_EHIP, "idn_jpeg_decode_u8: staging copy failed");
+  if (!copy_ok) return set_error(IDN_EHIP, "idn_jpeg_decode_u8: staging copy failed");
   const JpegDev* dimg = reinterpret_cast<const JpegDev*>(ws + P.off_imgs);
   int16_t* coef = reinterpret_cast<int16_t*>(ws + P.off_coef);
   uint8_t* ub = ws + P.off_ub;
   uint32_t* ivs = reinterpret_cast<uint32_t*>(ws + P.off_iv);
+  uint32_t* ive = reinterpret_cast<uint32_t*>(ws + P.off_ivend);
+  uint2* mk = reinterpret_cast<uint2*>(ws + P.off_mk);
   uint32_t* ublen = reinterpret_cast<uint32_t*>(ws + P.off_ublen);
   uint64_t* S[2] = {reinterpret_cast<uint64_t*>(ws + P.off_s0),
                     reinterpret_cast<uint64_t*>(ws + P.off_s1)};
@@ -2350,11 +2537,11 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   {
     const dim3 g((unsigned)P.mt_img, (unsigned)n);
     hipLaunchKernelGGL(jpeg_unstuff_count<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
-                       tcnt, P.mt_img, ivs);
+                       tcnt, P.mt_img);
     hipLaunchKernelGGL(jpeg_unstuff_write<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
-                       tcnt, P.mt_img, ub, ivs);
+                       tcnt, P.mt_img, ub, mk);
     hipLaunchKernelGGL(jpeg_unstuff_final<JpegDev>, dim3(n), dim3(256), 0, st, dimg, tcnt,
-                       P.mt_img, ub, ivs, ublen);
+                       P.mt_img, ub, mk, ivs, ive, ublen);
   }
   const JpegScanDev* dscan = reinterpret_cast<const JpegScanDev*>(ws + P.off_scans);
   if (!P.scans.empty()) {
@@ -2362,69 +2549,88 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     const unsigned ns = (unsigned)P.scans.size();
     const dim3 g((unsigned)P.mt_scan, ns);
     hipLaunchKernelGGL(jpeg_unstuff_count<JpegScanDev>, g, dim3(1024), 0, st, dscan,
-                       ws + P.off_scan, tcnt, P.mt_scan, ivs);
+                       ws + P.off_scan, tcnt, P.mt_scan);
     hipLaunchKernelGGL(jpeg_unstuff_write<JpegScanDev>, g, dim3(1024), 0, st, dscan,
-                       ws + P.off_scan, tcnt, P.mt_scan, ub, ivs);
+                       ws + P.off_scan, tcnt, P.mt_scan, ub, mk);
     hipLaunchKernelGGL(jpeg_unstuff_final<JpegScanDev>, dim3(ns), dim3(256), 0, st, dscan, tcnt,
-                       P.mt_scan, ub, ivs, reinterpret_cast<uint32_t*>(ws + P.off_ublen_s));
+                       P.mt_scan, ub, mk, ivs, ive, reinterpret_cast<uint32_t*>(ws + P.off_ublen_s));
   }
   const dim3 gitems((P.max_items + 63) / 64, n);
-  int cur = 0;
-  if (P.any_chunked) {
-    // pass A, then pass B until no chunk's end state changes (a batch takes ~4-6 passes, a
-    // single large file ~8-9).  The B passes are launched JPG_BROUND at a time with one flag each
-    // and one host read per round: the pass after the first one that changed nothing returns at
-    // once (its predecessor's flag), so a round costs the passes that work plus a launch each for
-    // the rest -- every host round trip (a D2H read and a stream synchronisation, ~30-40 us)
-    // was a gap in a single file's decode
-    constexpr int JPG_BROUND = 12;
-    hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
-                       S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co, nullptr);
-    for (uint32_t it = 0;; it += JPG_BROUND) {
-      if (hipMemsetAsync(flag, 0, 4 * JPG_BROUND, st) != hipSuccess)
-        return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
-      for (int k = 0; k < JPG_BROUND; ++k) {
-        hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
-                           S[cur], S[cur ^ 1], cnt, flag + k, chg[cur], chg[cur ^ 1],
-                           it + k == 0 ? 1 : 0, ck_st, ck_co, k > 0 ? flag + k - 1 : nullptr);
-        cur ^= 1;
+  uint32_t* badseen = flag + 32;  // (past the sync passes' flags)
+  // entropy decoding to the output; badlen: see jpeg_write_kernel
+  auto decode = [&](int badlen) -> int {
+    if (hipMemsetAsync(ws + P.off_coef, 0, P.nblk * 128, st) != hipSuccess ||
+        hipMemsetAsync(badseen, 0, 4, st) != hipSuccess)
+      return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
+    int cur = 0;
+    if (P.any_chunked) {
+      // pass A, then pass B until no chunk's end state changes (a batch takes ~4-6 passes, a
+      // single large file ~8-9).  The B passes are launched JPG_BROUND at a time with one flag each
+      // and one host read per round: the pass after the first one that changed nothing returns at
+      // once (its predecessor's flag), so a round costs the passes that work plus a launch each for
+      // the rest -- every host round trip (a D2H read and a stream synchronisation, ~30-40 us)
+      // was a gap in a single file's decode
+      constexpr int JPG_BROUND = 12;
+      hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
+                         S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co, nullptr, badlen);
+      for (uint32_t it = 0;; it += JPG_BROUND) {
+        if (hipMemsetAsync(flag, 0, 4 * JPG_BROUND, st) != hipSuccess)
+          return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
+        for (int k = 0; k < JPG_BROUND; ++k) {
+          hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
+                             S[cur], S[cur ^ 1], cnt, flag + k, chg[cur], chg[cur ^ 1],
+                             it + k == 0 ? 1 : 0, ck_st, ck_co, k > 0 ? flag + k - 1 : nullptr,
+                             badlen);
+          cur ^= 1;
+        }
+        uint32_t changed[JPG_BROUND] = {};
+        if (hipMemcpyAsync(changed, flag, sizeof(changed), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+          return set_error(IDN_EHIP, "idn_jpeg_decode_u8: sync pass failed");
+        if (!changed[JPG_BROUND - 1]) break;  // the round's last pass changed nothing
+        if (it > P.max_items + 2)
+          return set_error(IDN_EHIP, "idn_jpeg_decode_u8: entropy decoding did not converge");
       }
-      uint32_t changed[JPG_BROUND] = {};
-      if (hipMemcpyAsync(changed, flag, sizeof(changed), hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess)
-        return set_error(IDN_EHIP, "idn_jpeg_decode_u8: sync pass failed");
-      if (!changed[JPG_BROUND - 1]) break;  // the round's last pass changed nothing
-      if (it > P.max_items + 2)
-        return set_error(IDN_EHIP, "idn_jpeg_decode_u8: entropy decoding did not converge");
+      hipLaunchKernelGGL(jpeg_prefix_kernel, dim3(n), dim3(256), 0, st, dimg, cnt, cstart, n);
     }
-    hipLaunchKernelGGL(jpeg_prefix_kernel, dim3(n), dim3(256), 0, st, dimg, cnt, cstart, n);
-  }
-  const dim3 gwrite((P.max_items_w + 63) / 64, n);
-  hipLaunchKernelGGL(jpeg_write_kernel, gwrite, dim3(64), 0, st, dimg, ub, ublen, ivs, ck_st, ck_co,
-                     cstart, coef);
-  if (!P.scans.empty()) {
-    if (P.any_huff_scan)
-      hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, coef);
-    if (P.any_arith)
-      hipLaunchKernelGGL(jpeg_arith_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs,
-                         reinterpret_cast<const uint32_t*>(ws + P.off_ublen_s), coef);
-  }
-  const uint64_t gb = (P.nblk + 255) / 256;
-  IDN_CHECK_ARG(gb < 0x7FFFFFFF, "idn_jpeg_decode_u8: batch too large");
-  const uint64_t* bend = reinterpret_cast<const uint64_t*>(ws + P.off_blkend);
-  if (P.scales[0][0])
-    hipLaunchKernelGGL((jpeg_idct_kernel<1, 1>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
-                       n, P.nblk, coef, ws + P.off_planes);
-  if (P.scales[0][1])
-    hipLaunchKernelGGL((jpeg_idct_kernel<1, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
-                       n, P.nblk, coef, ws + P.off_planes);
-  if (P.scales[1][1])
-    hipLaunchKernelGGL((jpeg_idct_kernel<2, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
-                       n, P.nblk, coef, ws + P.off_planes);
-  {
-    const int64_t gx = ((int64_t)h * ((w + 7) / 8) + 255) / 256;
-    hipLaunchKernelGGL(jpeg_color8_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
-                       ws + P.off_planes, dst, h, w, row_stride);
+    const dim3 gwrite((P.max_items_w + 63) / 64, n);
+    hipLaunchKernelGGL(jpeg_write_kernel, gwrite, dim3(64), 0, st, dimg, ub, ublen, ivs, ive, ck_st,
+                       ck_co, cstart, coef, badlen, badseen);
+    if (!P.scans.empty()) {
+      if (P.any_huff_scan)
+        hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, ive,
+                           reinterpret_cast<const uint32_t*>(ws + P.off_ublen_s), coef);
+      if (P.any_arith)
+        hipLaunchKernelGGL(jpeg_arith_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, ive,
+                           coef);
+    }
+    const uint64_t gb = (P.nblk + 255) / 256;
+    IDN_CHECK_ARG(gb < 0x7FFFFFFF, "idn_jpeg_decode_u8: batch too large");
+    const uint64_t* bend = reinterpret_cast<const uint64_t*>(ws + P.off_blkend);
+    if (P.scales[0][0])
+      hipLaunchKernelGGL((jpeg_idct_kernel<1, 1>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
+                         n, P.nblk, coef, ws + P.off_planes);
+    if (P.scales[0][1])
+      hipLaunchKernelGGL((jpeg_idct_kernel<1, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
+                         n, P.nblk, coef, ws + P.off_planes);
+    if (P.scales[1][1])
+      hipLaunchKernelGGL((jpeg_idct_kernel<2, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
+                         n, P.nblk, coef, ws + P.off_planes);
+    {
+      const int64_t gx = ((int64_t)h * ((w + 7) / 8) + 255) / 256;
+      hipLaunchKernelGGL(jpeg_color8_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
+                         ws + P.off_planes, dst, h, w, row_stride);
+    }
+    return IDN_OK;
+  };
+  int drc = decode(P.any_chunked ? 16 : 17);
+  if (drc != IDN_OK) return drc;
+  if (P.any_chunked) {  // a bad code on a true trajectory: decode again with libjpeg's rule
+    uint32_t bad = 0;
+    if (hipMemcpyAsync(&bad, badseen, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return set_error(IDN_EHIP, "idn_jpeg_decode_u8: decode failed");
+    if (bad && (drc = decode(17)) != IDN_OK) return drc;
   }
   // the staging buffer is reused by the next call: finish here
   if (hipStreamSynchronize(st) != hipSuccess)

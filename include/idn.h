@@ -359,6 +359,10 @@ size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, 
  * multi-scan files on the scan path), all h x w, into
  * the device u8 BGR NHWC batch dst (row_stride bytes per row), bit-exact with the library the
  * flags name (replaces cv2.imread at lib/model/test.py:191, lib/roi_data_layer/minibatch.py:85).
+ * Damaged entropy-coded data decodes as libjpeg decodes it (it only warns): a file cut short (an
+ * EOI appended, or none), bit errors, bad Huffman codes, lost / renumbered restart markers and
+ * stray markers -- the data runs out, the rest of its restart interval stays gray, restart
+ * markers resynchronise as jdmarker.c's jpeg_resync_to_restart does.
  * The entropy-coded segments are copied to the workspace in one transfer; synchronous on
  * `stream`. */
 int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* lens, int n, uint8_t* dst,

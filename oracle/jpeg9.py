@@ -9,7 +9,11 @@ reference's pinned stack decodes them: OpenCV 3.4.2 over IJG libjpeg 9d
   jdhuff.c     Huffman decoding: sequential (DC prediction, AC run/size, restart intervals) and
                progressive (decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine: spectral
                selection, successive approximation, EOB runs), one or several scans; a
-               non-interleaved scan codes only the component's own blocks (width_in_blocks)
+               non-interleaved scan codes only the component's own blocks (width_in_blocks);
+               damaged data as libjpeg treats it: zero bits past an interval's data, an MCU
+               decoded only while the data lasted up to its start (insufficient_data), 17 bits
+               and symbol 0 for a bad code, restart markers taken or resynchronised as
+               jdmarker.c's jpeg_resync_to_restart does (_entropy, _intervals, _Bits)
   jdarith.c    arithmetic-coded files (SOF9 / SOF10): the QM-coder with libjpeg's statistics bins
                (DC 64 / AC 256 per table, reset per restart interval), the DC conditioning of the
                DAC parameters L / U and the AC split K; decode_mcu and the four progressive
@@ -39,8 +43,9 @@ component, "fancy" triangular h2v1 / h2v2 upsampling (jdsample.c) and FIX(0.3441
 is not restated: mode="turbo" raises NotImplementedError for a file either library would smooth.)
 
 Pinned by tests/golden/jpeg9.npz / jpeg9.json: the real libjpeg 9d decode of every fixture file
-(tests/golden/make_jpeg9_fixtures.py, conda Pillow 8.4.0); tests/test_jpeg.py checks this
-restatement against it (and mode="turbo" against the system Pillow).
+(tests/golden/make_jpeg9_fixtures.py, conda Pillow 8.4.0), and by jpeg9_damaged.* its decode of
+168 damaged variants (tests/golden/make_jpeg_damaged.py); tests/test_jpeg.py checks this
+restatement against both (and mode="turbo" against the system Pillow).
 """
 from __future__ import annotations
 
@@ -79,54 +84,111 @@ def _extend(v, s):
 
 
 def _entropy(data: bytes, i: int):
-    """the entropy-coded segment starting at data[i]: (restart intervals of unstuffed bytes, index
-    of the marker that ends it).  Stuffed 0xFF00 -> 0xFF, RSTn splits intervals, fill 0xFFs are
-    skipped; any other marker ends the segment."""
-    intervals, cur = [], bytearray()
-    while i < len(data):
+    """the entropy-coded data from data[i] as libjpeg's source manager delivers it: a list of
+    segments (unstuffed bytes, code of the marker that ends them), up to the first marker that is
+    neither RSTn nor below SOF0 (a valid non-restart marker, jdmarker.c resync_to_restart's
+    action 3), and the index of that marker.  Stuffed 0xFF00 -> 0xFF, fill 0xFFs are skipped; the
+    end of the data is jdatasrc.c's inserted EOI (JWRN_JPEG_EOF)."""
+    segs, cur = [], bytearray()
+    while True:
+        if i >= len(data):
+            segs.append((bytes(cur), 0xD9))
+            return segs, len(data)
         b = data[i]
-        if b == 0xFF and i + 1 < len(data):
-            nb = data[i + 1]
-            if nb == 0x00:
-                cur.append(0xFF)
-                i += 2
+        if b != 0xFF:
+            cur.append(b)
+            i += 1
+            continue
+        j = i + 1
+        while j < len(data) and data[j] == 0xFF:
+            j += 1
+        if j >= len(data):
+            segs.append((bytes(cur), 0xD9))
+            return segs, len(data)
+        if data[j] == 0x00:
+            cur.append(0xFF)
+            i = j + 1
+            continue
+        segs.append((bytes(cur), data[j]))
+        cur = bytearray()
+        if not (0xD0 <= data[j] <= 0xD7 or data[j] < 0xC0):
+            return segs, j - 1
+        i = j + 1
+
+
+def _intervals(segs, restart: int, n: int):
+    """the data each of the scan's n restart intervals decodes, as libjpeg reads them: interval 0
+    the first segment; at every restart, jdhuff.c process_restart -> jdmarker.c
+    read_restart_marker: the marker that ends the current segment is the expected RSTn (taken,
+    the next segment follows), or jpeg_resync_to_restart decides -- action 1 (the expected one, or
+    one too far away) take it; action 2 (a marker below SOF0 or one of the two RSTs before the
+    expected one) skip to the marker after the next segment and decide again; action 3 (a valid
+    non-restart marker or one of the next two RSTs) leave it: the interval reads nothing.  Yields
+    (bytes, reset) -- reset: the out-of-data flag is cleared (the marker was taken)."""
+    j, stuck, want = 0, False, 0
+    yield segs[0][0], True
+    for _ in range(1, n if restart else 1):
+        m = segs[min(j, len(segs) - 1)][1]
+        while True:
+            if m == 0xD0 + want:
+                act = 1
+            elif m < 0xC0:
+                act = 2
+            elif not 0xD0 <= m <= 0xD7:
+                act = 3
+            elif m in (0xD0 + ((want + 1) & 7), 0xD0 + ((want + 2) & 7)):
+                act = 3
+            elif m in (0xD0 + ((want - 1) & 7), 0xD0 + ((want - 2) & 7)):
+                act = 2
+            else:
+                act = 1
+            if act == 2 and j + 1 < len(segs):
+                j += 1
+                m = segs[j][1]
                 continue
-            if 0xD0 <= nb <= 0xD7:
-                intervals.append(bytes(cur))
-                cur = bytearray()
-                i += 2
-                continue
-            if nb == 0xFF:
-                i += 1
-                continue
-            break  # EOI or another marker
-        cur.append(b)
-        i += 1
-    intervals.append(bytes(cur))
-    return intervals, i
+            break
+        want = (want + 1) & 7
+        if act == 1 and j + 1 < len(segs):
+            j += 1
+            yield segs[j][0], True
+        else:  # the marker stays unread: this interval's segment is empty
+            yield b"", False
 
 
 class _Bits:
-    """big-endian bit reader over one restart interval; zeros past its end (libjpeg's fill)"""
+    """big-endian bit reader over one restart interval's bytes; zeros past their end (jdhuff.c
+    jpeg_fill_bit_buffer), and `out` set once a read needed a bit past the end (the entropy
+    decoder's insufficient_data)"""
 
-    def __init__(self, buf: bytes):
-        self.v = int.from_bytes(buf + bytes(8), "big")
-        self.n = 8 * (len(buf) + 8)
+    def __init__(self, buf: bytes, out: bool = False):
+        self.avail = 8 * len(buf)
+        self.v = int.from_bytes(buf, "big")
+        self.n = self.avail
         self.pos = 0
+        self.out = out
 
-    def peek16(self):
-        return (self.v >> (self.n - self.pos - 16)) & 0xFFFF
+    def _ensure(self, k):
+        while self.pos + k > self.n:
+            self.v <<= 64
+            self.n += 64
 
-    def get(self, s):
-        if s == 0:
-            return 0
-        r = (self.v >> (self.n - self.pos - s)) & ((1 << s) - 1)
-        self.pos += s
+    def _take(self, k):
+        self._ensure(k)
+        r = (self.v >> (self.n - self.pos - k)) & ((1 << k) - 1)
+        self.pos += k
+        if self.pos > self.avail:
+            self.out = True
         return r
 
+    def get(self, s):
+        return self._take(s) if s else 0
+
     def huff(self, lut):
-        ln, sym = lut[self.peek16()]
-        self.pos += ln
+        """one symbol; a bit pattern that is no code (jpeg_huff_decode's l > 16) takes 17 bits and
+        decodes as 0 (JWRN_HUFF_BAD_CODE)"""
+        self._ensure(16)
+        ln, sym = lut[(self.v >> (self.n - self.pos - 16)) & 0xFFFF]
+        self._take(ln if ln else 17)
         return sym
 
 
@@ -156,13 +218,18 @@ def _decode_scan(sc, comps, coef, geo, dc, ac):
     per = sc["restart"] if sc["restart"] else len(units)
     p1, m1 = 1 << Al, -(1 << Al)
     u = 0
-    for iv in sc["intervals"]:
+    out = False
+    nint = -(-len(units) // per)
+    for iv, reset in _intervals(sc["segments"], sc["restart"], nint):
         if u >= len(units):
             break
-        br = _Bits(iv)
+        br = _Bits(iv, out and not reset)
         pred = {ci: 0 for ci, _, _ in sel}
         eobrun = 0
         for _ in range(min(per, len(units) - u)):
+            if br.out:  # out of data: the MCU is left as it is (zeros / the earlier scans)
+                u += 1
+                continue
             for ci, by, bx in units[u]:
                 blk = coef[ci][by, bx]
                 dct, act = tabs[ci]
@@ -238,6 +305,7 @@ def _decode_scan(sc, comps, coef, geo, dc, ac):
                             k += 1
                         eobrun -= 1
             u += 1
+        out = br.out
 
 
 # ---- arithmetic decoding (jdarith.c, libjpeg 9d) -------------------------------------------------
@@ -373,7 +441,7 @@ def _decode_scan_arith(sc, comps, coef, geo, dac):
     per = sc["restart"] if sc["restart"] else len(units)
     p1, m1 = 1 << Al, -(1 << Al)
     u = 0
-    for iv in sc["intervals"]:
+    for iv, _ in _intervals(sc["segments"], sc["restart"], -(-len(units) // per)):
         if u >= len(units):
             break
         ar = _Arith(iv)
@@ -538,9 +606,9 @@ def parse_and_decode(data: bytes):
                 c = [cc["id"] for cc in comps].index(s[1 + 2 * k])
                 sel.append((c, s[2 + 2 * k] >> 4, s[2 + 2 * k] & 15))
             ss = s[1 + 2 * ns:]
-            intervals, end = _entropy(data, end)
+            segments, end = _entropy(data, end)
             sc = dict(sel=sel, Ss=ss[0], Se=ss[1], Ah=ss[2] >> 4, Al=ss[2] & 15,
-                      progressive=progressive, restart=restart, intervals=intervals)
+                      progressive=progressive, restart=restart, segments=segments)
             if arith:
                 _decode_scan_arith(sc, comps, coef, geo, dac)
             else:

@@ -332,3 +332,94 @@ def test_four_component_files():
         assert ops.jpeg_info(data)[2] == 4
         spaces.add(jpeg9.color_space(jpeg9.parse_and_decode(data), "libjpeg9"))
     assert spaces == {"cmyk", "ycck"}
+
+
+# ---- damaged files (tests/golden/jpeg_damage.py): what libjpeg does where the data is bad ----------
+def _damaged():
+    import sys
+    if str(GOLD) not in sys.path:
+        sys.path.insert(0, str(GOLD))
+    import jpeg_damage
+    return jpeg_damage
+
+
+def _damaged_meta():
+    return json.loads((GOLD / "jpeg9_damaged.json").read_text())
+
+
+def _damaged_cases(big: bool):
+    """the 600x1000 file's cases take the pure-Python oracle a minute each: only the cut early"""
+    out = []
+    for c in _damaged().cases():
+        if "600x1000" in c[0] and not (big or (c[1] == "cut" and c[2] <= 0.3)):
+            continue
+        out.append(c)
+    return out
+
+
+def test_damaged_fixture_set_is_complete():
+    jd = _damaged()
+    meta = _damaged_meta()
+    assert meta["libjpeg"].startswith("9")
+    assert sorted(meta["cases"]) == sorted(jd.key(c) for c in jd.cases())
+    ops = {c[1] for c in jd.cases()}
+    assert ops == {"cut", "cutrst", "flip", "ones", "junk", "rstnum"}
+    for c in jd.cases():  # every recipe changes the file (a cut at 0.97 may keep all the data)
+        data = (JPEG / c[0]).read_bytes()
+        assert jd.damage(data, c[1], c[2]) != data or c[1] == "cut", c
+
+
+@pytest.mark.parametrize("case", _damaged_cases(False), ids=lambda c: _damaged().key(c))
+def test_oracle_matches_libjpeg9_on_damaged_files(case):
+    """jdhuff.c / jdarith.c / jdmarker.c on bad data, restated (oracle/jpeg9.py _entropy,
+    _intervals, _Bits): an MCU is decoded only while its interval's data lasted up to its start,
+    past the data the bits are 0, a bit pattern that is no code takes 17 bits and decodes as 0,
+    and at every restart the marker is taken or resynchronised by jpeg_resync_to_restart's three
+    actions -- pinned against the real libjpeg 9d's pixels"""
+    from oracle import jpeg9
+    jd = _damaged()
+    rec = _damaged_meta()["cases"][jd.key(case)]
+    got = jpeg9.imread(jd.damage((JPEG / case[0]).read_bytes(), case[1], case[2]))
+    assert list(got.shape) == rec["shape"]
+    if hashlib.sha256(got.tobytes()).hexdigest() != rec["sha256"]:
+        rows = np.load(GOLD / "jpeg9_damaged.npz")[jd.key(case)]
+        bad = np.nonzero((got.astype(np.int64).sum(axis=1) != rows).any(axis=1))[0]
+        raise AssertionError(f"{jd.key(case)}: rows differ from {bad[:1]} ({len(bad)} rows)")
+
+
+_TURBO_DAMAGED = ("s4", "gray", "arith_s", "arith_rst")
+
+
+def test_oracle_turbo_mode_matches_system_pil_on_damaged_files(tmp_path):
+    """libjpeg-turbo's entropy decoders treat bad data as libjpeg 9d's do: the system Pillow's
+    decode of the damaged baseline and arithmetic files.  Its SIMD IDCT saturates differently on
+    the out-of-range coefficients damaged data can give, so Pillow runs here with libjpeg-turbo's C
+    code (JSIMD_FORCENONE, read once per process: a child process)"""
+    import os
+    import subprocess
+    import sys
+    jd = _damaged()
+    cases = [c for c in _damaged_cases(False) if "600x1000" not in c[0] and
+             c[0].startswith(_TURBO_DAMAGED)]
+    assert len(cases) >= 90
+    out = tmp_path / "pil.npz"
+    script = (
+        "import io, sys, numpy as np\n"
+        "from pathlib import Path\n"
+        "from PIL import Image\n"
+        f"sys.path.insert(0, {str(GOLD)!r})\n"
+        "import jpeg_damage as jd\n"
+        "res = {}\n"
+        "for c in jd.cases():\n"
+        "    if '600x1000' in c[0] or not c[0].startswith(%r): continue\n"
+        f"    d = jd.damage(Path({str(JPEG)!r}, c[0]).read_bytes(), c[1], c[2])\n"
+        "    with Image.open(io.BytesIO(d)) as im:\n"
+        "        res[jd.key(c)] = np.asarray(im.convert('RGB'))[..., ::-1]\n"
+        f"np.savez({str(out)!r}, **res)\n") % (_TURBO_DAMAGED,)
+    subprocess.run([sys.executable, "-c", script], check=True,
+                   env=dict(os.environ, JSIMD_FORCENONE="1"))
+    from oracle import jpeg9
+    ref = np.load(out)
+    for c in cases:
+        data = jd.damage((JPEG / c[0]).read_bytes(), c[1], c[2])
+        assert np.array_equal(jpeg9.imread(data, mode="turbo"), ref[jd.key(c)]), jd.key(c)

@@ -200,3 +200,66 @@ def test_large_mixed_batch_bitexact_and_errors(dev):
     bad[90] = _lossless(datas[0])
     with pytest.raises(IdnError, match="unsupported|lossless"):
         ops.jpeg_decode(bad)
+
+
+# ---- damaged files: libjpeg's treatment of bad data (tests/golden/jpeg_damage.py) ---------------
+def _damaged():
+    import sys
+    if str(GOLD) not in sys.path:
+        sys.path.insert(0, str(GOLD))
+    import jpeg_damage
+    return jpeg_damage
+
+
+DAMAGED = json.loads((GOLD / "jpeg9_damaged.json").read_text())["cases"]
+
+
+def check_damaged(key, got):
+    rec = DAMAGED[key]
+    assert list(got.shape) == rec["shape"], key
+    if hashlib.sha256(np.ascontiguousarray(got).tobytes()).hexdigest() != rec["sha256"]:
+        rows = np.load(GOLD / "jpeg9_damaged.npz")[key]
+        bad = np.nonzero((got.astype(np.int64).sum(axis=1) != rows).any(axis=1))[0]
+        raise AssertionError(f"{key}: rows differ from {bad[:1]} ({len(bad)} rows)")
+
+
+@pytest.mark.parametrize("case", _damaged().cases(), ids=lambda c: _damaged().key(c))
+def test_damaged_file_matches_libjpeg9(dev, case):
+    """cut files, bit errors, bad Huffman codes, lost / renumbered restart markers and stray markers
+    decode as the real libjpeg 9d decodes them (cv2.imread returns the image, with warnings):
+    every decoder -- the chunked one, restart intervals, the scan path, arithmetic"""
+    from idn import ops
+    jd = _damaged()
+    data = jd.damage((JPEG / case[0]).read_bytes(), case[1], case[2])
+    check_damaged(jd.key(case), ops.jpeg_decode([data])[0].cpu().numpy())
+
+
+def test_damaged_files_small_chunks_and_one_batch(dev):
+    """the chunked decoder's end-of-data rule with 512-bit chunks (many chunks past the end of a cut
+    file), and every damaged variant of a file in one batch with the intact file"""
+    from idn import ops
+    jd = _damaged()
+    for name in ["s444_q95_96x128.jpg", "gray_q80_91x77.jpg", "s420_opt_130x170.jpg"]:
+        cs = [c for c in jd.cases() if c[0] == name]
+        src = (JPEG / name).read_bytes()
+        datas = [jd.damage(src, c[1], c[2]) for c in cs]
+        for c, d in zip(cs, datas):
+            check_damaged(jd.key(c), ops.jpeg_decode([d], chunk_bits=512)[0].cpu().numpy())
+        got = ops.jpeg_decode([src] + datas).cpu().numpy()
+        check_libjpeg9(name, got[0])
+        for k, c in enumerate(cs):
+            check_damaged(jd.key(c), got[k + 1])
+
+
+def test_damaged_files_turbo_mode_match_the_oracle(dev):
+    """mode="turbo" on damaged baseline / arithmetic files against the oracle's turbo mode (pinned
+    by tests/test_jpeg.py against libjpeg-turbo's C code)"""
+    from idn import ops
+    from oracle import jpeg9
+    jd = _damaged()
+    for c in jd.cases():
+        if "600x1000" in c[0] or not c[0].startswith(("s4", "gray", "arith_s", "arith_rst")):
+            continue
+        data = jd.damage((JPEG / c[0]).read_bytes(), c[1], c[2])
+        got = ops.jpeg_decode([data], mode="turbo")[0].cpu().numpy()
+        assert np.array_equal(got, jpeg9.imread(data, mode="turbo")), jd.key(c)

@@ -1,5 +1,6 @@
-"""Decode one synthetic 600x1000 q90 4:2:0 file repeatedly (tools only; for kernel traces):
-  python tools/jpeg_single.py [--iters 20] [--chunk 0]"""
+"""Decode one synthetic 600x1000 q90 4:2:0 file (or a batch of copies) repeatedly (tools only;
+for kernel traces):
+  python tools/jpeg_single.py [--iters 20] [--chunk 0] [--batch 1]"""
 import argparse
 import io
 import sys
@@ -18,12 +19,15 @@ from idn import ops  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--chunk", type=int, default=0)
+ap.add_argument("--batch", type=int, default=1)
 a = ap.parse_args()
-x = bench.synth_batch(torch, 1, torch.device("cuda", 0), seed=3).cpu().numpy()
-b = io.BytesIO()
-Image.fromarray(x[0][..., ::-1]).save(b, "JPEG", quality=90, subsampling=2)
-f = b.getvalue()
-print("file bytes", len(f))
+x = bench.synth_batch(torch, a.batch, torch.device("cuda", 0), seed=3).cpu().numpy()
+files = []
+for im in x:
+    b = io.BytesIO()
+    Image.fromarray(im[..., ::-1]).save(b, "JPEG", quality=90, subsampling=2)
+    files.append(b.getvalue())
+print("file bytes", len(files[0]))
 for _ in range(a.iters):
-    ops.jpeg_decode([f], chunk_bits=a.chunk)
+    ops.jpeg_decode(files, chunk_bits=a.chunk)
     torch.cuda.synchronize()
