@@ -480,45 +480,46 @@ __device__ __forceinline__ uint32_t jpg_be32(const uint8_t* __restrict__ p) {
 }
 
 // reads one restart interval of a plain big-endian bit string through a range-checked buffer
-// resource: the words of the current 16-byte group in registers, the next group's load already in
-// flight (a chain of dependent loads per symbol made the decode latency-bound: 2100 cycles per
-// symbol).  Bits from `end` on read as 0 (jdhuff.c jpeg_fill_bit_buffer past a marker); `pos`
-// counts the bits taken, so pos > end says the data ran out (libjpeg's insufficient_data).
+// resource, through a per-lane ring of JRG_S byte-swapped 16-byte groups in LDS refilled one group
+// ahead from a load held in a register (as the chunk decoders' jpg_run): a register queue of
+// groups in flight made every group change wait for the youngest load (moving a register whose
+// load is pending waits for it).  Bits from `end` on read as 0 (jdhuff.c jpeg_fill_bit_buffer past
+// a marker); `pos` counts the bits taken, so pos > end says the data ran out (insufficient_data).
+constexpr int JRG_S = 4;
+constexpr int JRING_S = JRG_S * 4 + 4;  // ring words per lane (a pad group)
 struct BitStream {
   rsrc_t rs;
+  uint32_t* ring;
   uint64_t acc;    // left-aligned
-  int nb, idx;
-  uint32_t gi, wbit, pos, end;  // wbit: stream position of the next word to append
-  uint32_t buf[4];
-  v4u pre;
-  __device__ __forceinline__ void take(const v4u v) {
-    buf[0] = __builtin_bswap32(v.x);
-    buf[1] = __builtin_bswap32(v.y);
-    buf[2] = __builtin_bswap32(v.z);
-    buf[3] = __builtin_bswap32(v.w);
+  int nb;
+  uint32_t wi, pos, end;  // wi: the next word to append
+  v4u pend;               // group (wi >> 2) + JRG_S, raw
+  __device__ __forceinline__ void put(uint32_t g, const v4u v) {
+    *reinterpret_cast<v4u*>(ring + (g & (JRG_S - 1)) * 4) =
+        v4u{__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
+            __builtin_bswap32(v.w)};
   }
   __device__ __forceinline__ uint32_t word() {
-    uint32_t w = idx == 0 ? buf[0] : idx == 1 ? buf[1] : idx == 2 ? buf[2] : buf[3];
-    if (++idx == 4) {
-      take(pre);
-      pre = __builtin_amdgcn_raw_buffer_load_b128(rs, (++gi + 1) * 16u, 0, 0);
-      idx = 0;
+    uint32_t w = ring[wi & (4 * JRG_S - 1)];
+    const uint32_t wbit = wi * 32u;  // (bit positions are below 2^31: 32-bit arithmetic)
+    w = wbit + 32u <= end ? w : wbit >= end ? 0u : w & ~(0xFFFFFFFFu >> (end - wbit));
+    if ((++wi & 3) == 0) {  // group (wi >> 2) - 1 retired: its slot takes the pending group
+      put((wi >> 2) + JRG_S - 1, pend);
+      pend = __builtin_amdgcn_raw_buffer_load_b128(rs, ((wi >> 2) + JRG_S) * 16u, 0, 0);
     }
-    const int64_t r = (int64_t)end - (int64_t)wbit;
-    w = r >= 32 ? w : r <= 0 ? 0u : w & ~(0xFFFFFFFFu >> (uint32_t)r);
-    wbit += 32;
     return w;
   }
-  __device__ __forceinline__ void start(rsrc_t r, uint32_t p, uint32_t e) {
+  __device__ __forceinline__ void start(rsrc_t r, uint32_t* rg, uint32_t p, uint32_t e) {
     rs = r;
+    ring = rg;
     end = e;
     pos = p;
-    const uint32_t wi = p >> 5;
-    gi = wi >> 2;
-    idx = (int)(wi & 3);
-    wbit = wi * 32u;
-    take(__builtin_amdgcn_raw_buffer_load_b128(rs, gi * 16u, 0, 0));
-    pre = __builtin_amdgcn_raw_buffer_load_b128(rs, (gi + 1) * 16u, 0, 0);
+    wi = p >> 5;
+    const uint32_t g0 = wi >> 2;
+#pragma unroll
+    for (int k = 0; k < JRG_S; ++k)
+      put(g0 + k, __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 + k) * 16u, 0, 0));
+    pend = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 + JRG_S) * 16u, 0, 0);
     const uint32_t w0 = word(), w1 = word();
     acc = ((uint64_t)w0 << 32 | w1) << (p & 31);
     nb = 64 - (int)(p & 31);
@@ -558,6 +559,7 @@ struct JpegLds {
 // the scan path's tables (JpegScanDev slots)
 struct JpegLdsScan {
   alignas(16) int32_t mca[8][8];
+  uint8_t natural[80];  // jpg_natural: a __constant__ read at a computed index is a vector load
   uint16_t lut[8][1 << JPG_LUTB];
   int32_t maxcode[8][18], valoff[8][18];
   uint8_t huffval[8][256];
@@ -1296,6 +1298,7 @@ __device__ __forceinline__ void jpg_load_scan_tables(JpegLdsScan& T, const JpegS
   }
   for (int k = threadIdx.x; k < 8 * 256; k += blockDim.x) (&T.huffval[0][0])[k] = (&S.huffval[0][0])[k];
   for (int k = threadIdx.x; k < 8 * 8; k += blockDim.x) T.mca[k >> 3][k & 7] = jpg_mca(S.maxcode[k >> 3], k & 7);
+  for (int k = threadIdx.x; k < 80; k += blockDim.x) T.natural[k] = jpg_natural[k];
 }
 
 __device__ __forceinline__ uint32_t jpg_get(BitStream& br, int s) {  // s <= 16
@@ -1312,7 +1315,8 @@ __device__ __forceinline__ int jpg_huff(BitStream& br, const JpegLdsScan& T, int
 __device__ __forceinline__ int16_t jpg_lshift(int v, int al) { return (int16_t)(int)((uint32_t)v << al); }
 
 // one block of scan component k (slot k: DC table, 4 + k: AC table); eobrun / pred per interval
-__device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan& T, const JpegScanDev& S,
+template <typename SK>
+__device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan& T, const SK& S,
                                                int k, int16_t* __restrict__ blk, int& pred,
                                                uint32_t& eobrun) {
   switch (S.kind) {
@@ -1325,7 +1329,7 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
         const int r = rs >> 4, sz = rs & 15;
         if (sz) {
           z += r;
-          blk[jpg_natural[min(z, 79)]] = (int16_t)jpg_extend(jpg_get(br, sz), sz);
+          blk[T.natural[min(z, 79)]] = (int16_t)jpg_extend(jpg_get(br, sz), sz);
           ++z;
         } else if (r == 15) {
           z += 16;
@@ -1341,8 +1345,9 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
       blk[0] = jpg_lshift(pred, S.Al);
       break;
     }
-    case JPG_DC_REFINE:
-      if (jpg_get(br, 1)) blk[0] = (int16_t)(blk[0] | (1 << S.Al));
+    case JPG_DC_REFINE:  // OR the bit into the low half of the block's first dword: no load to
+                         // wait for (blk is 128-byte aligned, Al <= 13)
+      if (jpg_get(br, 1)) atomicOr(reinterpret_cast<unsigned int*>(blk), 1u << S.Al);
       break;
     case JPG_AC_FIRST: {
       if (eobrun) {
@@ -1354,7 +1359,7 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
         const int r = rs >> 4, sz = rs & 15;
         if (sz) {
           z += r;
-          blk[jpg_natural[min(z, 79)]] = jpg_lshift(jpg_extend(jpg_get(br, sz), sz), S.Al);
+          blk[T.natural[min(z, 79)]] = jpg_lshift(jpg_extend(jpg_get(br, sz), sz), S.Al);
         } else if (r != 15) {
           eobrun = 1u << r;
           if (r) eobrun += jpg_get(br, r);
@@ -1381,7 +1386,7 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
             break;
           }
           do {  // refine the nonzero coefficients up to the target zero (r zeros skipped)
-            int16_t* c = blk + jpg_natural[min(z, 79)];
+            int16_t* c = blk + T.natural[min(z, 79)];
             if (*c != 0) {
               if (jpg_get(br, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
             } else if (--r < 0) {
@@ -1389,12 +1394,12 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
             }
             ++z;
           } while (z <= S.Se);
-          if (sz) blk[jpg_natural[min(z, 79)]] = (int16_t)sz;
+          if (sz) blk[T.natural[min(z, 79)]] = (int16_t)sz;
         }
       }
       if (eobrun > 0) {  // the band of this block is in an EOB run: refine its nonzeros
         for (; z <= S.Se; ++z) {
-          int16_t* c = blk + jpg_natural[min(z, 79)];
+          int16_t* c = blk + T.natural[min(z, 79)];
           if (*c != 0 && jpg_get(br, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
         }
         --eobrun;
@@ -1403,34 +1408,122 @@ __device__ __forceinline__ void jpg_scan_block(BitStream& br, const JpegLdsScan&
   }
 }
 
+// a scan's constants, read once per scan: inside the unit loop a read of JpegDev / JpegScanDev
+// (component fields at a computed index) was a vector load waited for at every unit
+struct ScanK {
+  int kind, Ss, Se, Al, ns;
+  uint32_t mcux;
+  uint32_t wib[4], bw[4], cv[4], ch[4];  // per scan component k
+  uint64_t boff[4];                      // its first block
+};
+__device__ __forceinline__ ScanK jpg_scan_k(const JpegDev& D, const JpegScanDev& S) {
+  ScanK K;
+  K.kind = S.kind;
+  K.Ss = S.Ss;
+  K.Se = S.Se;
+  K.Al = S.Al;
+  K.ns = S.ns;
+  K.mcux = (uint32_t)D.mcux;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = k < S.ns ? S.comp[k] : 0;
+    K.wib[k] = (uint32_t)D.wib[c];
+    K.bw[k] = (uint32_t)D.bw[c];
+    K.cv[k] = (uint32_t)D.cv[c];
+    K.ch[k] = (uint32_t)D.ch[c];
+    K.boff[k] = D.blk_off[c];
+  }
+  return K;
+}
+template <typename A>
+__device__ __forceinline__ A jpg_pick(const A (&a)[4], int k) {  // (no dynamic register index)
+  return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
+}
+
 // the scan path's unit u of scan S: an MCU (interleaved) or one block of the scan's component
-__device__ __forceinline__ void jpg_scan_unit(BitStream& br, const JpegLdsScan& T, const JpegDev& D,
-                                              const JpegScanDev& S, uint32_t u,
-                                              int16_t* __restrict__ coef, int (&pred)[4],
-                                              uint32_t& eobrun) {
+__device__ __forceinline__ void jpg_scan_unit(BitStream& br, const JpegLdsScan& T, const ScanK& S,
+                                              uint32_t u, int16_t* __restrict__ coef,
+                                              int (&pred)[4], uint32_t& eobrun) {
   if (S.ns == 1) {  // non-interleaved: the component's own blocks, raster order
-    const int c = S.comp[0];
-    const uint32_t by = u / (uint32_t)D.wib[c], bx = u - by * (uint32_t)D.wib[c];
-    int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
+    const uint32_t by = u / S.wib[0], bx = u - by * S.wib[0];
+    int16_t* blk = coef + (S.boff[0] + (uint64_t)by * S.bw[0] + bx) * 64;
     jpg_scan_block(br, T, S, 0, blk, pred[0], eobrun);
   } else {  // interleaved MCU (sequential, or a progressive DC scan)
-    const uint32_t my = u / (uint32_t)D.mcux, mx = u - my * (uint32_t)D.mcux;
+    const uint32_t my = u / S.mcux, mx = u - my * S.mcux;
     for (int k = 0; k < S.ns; ++k) {
-      const int c = S.comp[k];
-      for (int dv = 0; dv < D.cv[c]; ++dv)
-        for (int dh = 0; dh < D.ch[c]; ++dh) {
-          const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
-          int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
-          jpg_scan_block(br, T, S, k, blk, pred[k], eobrun);
+      const uint32_t cv = jpg_pick(S.cv, k), ch = jpg_pick(S.ch, k), bw = jpg_pick(S.bw, k);
+      const uint64_t bo = jpg_pick(S.boff, k);
+      for (uint32_t dv = 0; dv < cv; ++dv)
+        for (uint32_t dh = 0; dh < ch; ++dh) {
+          const uint64_t by = (uint64_t)my * cv + dv, bx = (uint64_t)mx * ch + dh;
+          jpg_scan_block(br, T, S, k, coef + (bo + by * bw + bx) * 64, pred[k], eobrun);
         }
     }
   }
 }
 
+// One block of an AC refinement scan (jdhuff.c decode_mcu_AC_refine) from its nonzero history h
+// (zigzag positions in the band Ss..Se, before this scan) alone: what the decoder reads never
+// depends on the coefficient values, only on which are nonzero, and a new coefficient is never
+// passed again in its block.  Every history position of the band gets one correction bit, in
+// zigzag order (corr: the K = popcount(h) bits, the first read highest); newp / newn: the
+// positions that become +-2^Al (newn: negative).  libjpeg's overrun guard writes a value past
+// position 63 at 63.  The caller applies it.
+struct RefineOut {
+  uint64_t corr, newp, newn;
+};
+__device__ __forceinline__ void jpg_refine_block(BitStream& br, const JpegLdsScan& T, int Ss, int Se,
+                                                 uint64_t h, uint32_t& eobrun, RefineOut& out) {
+  uint64_t corr = 0, newp = 0, newn = 0;
+  auto take = [&](uint64_t nz) {  // the correction bits of the history positions in nz
+    for (int k = __popcll(nz); k > 0;) {
+      const int s = min(k, 24);
+      corr = corr << s | jpg_get(br, s);
+      k -= s;
+    }
+  };
+  int z = Ss;
+  if (eobrun == 0) {
+    while (z <= Se) {
+      const int rs = jpg_huff(br, T, 4);
+      const int r = rs >> 4, sz = rs & 15;
+      bool neg = false;
+      if (sz) {
+        neg = jpg_get(br, 1) == 0;
+      } else if (r != 15) {
+        eobrun = 1u << r;
+        if (r) eobrun += jpg_get(br, r);
+        break;
+      }
+      // the (r + 1)-th position without history from z on (Se + 1 if the band runs out first)
+      uint64_t zs = ~h & (~0ull << z) & (Se == 63 ? ~0ull : (1ull << (Se + 1)) - 1);
+      for (int i = 0; i < r && zs; ++i) zs &= zs - 1;
+      const int t = zs ? __builtin_ctzll(zs) : Se + 1;
+      take(h & (~0ull << z) & (t >= 64 ? ~0ull : (1ull << t) - 1));
+      if (sz) {
+        const int zt = min(t, 63);
+        newp |= 1ull << zt;
+        newn |= (uint64_t)neg << zt;
+      }
+      z = t + 1;
+    }
+  }
+  if (eobrun > 0) {
+    if (z <= Se) take(h & (~0ull << z));
+    --eobrun;
+  }
+  out = RefineOut{corr, newp, newn};
+}
+
 // Out of data (jdhuff.c insufficient_data): a unit is decoded only while the interval's data lasted
 // up to its start (a skipped unit keeps what the earlier scans left); an interval that reads
 // nothing and inherits the out-of-data state is the predecessor's lane's: it decodes the first unit
-// from zero bits if the predecessor did not run out (see jpeg_unstuff_final)
+// from zero bits if the predecessor did not run out (see jpeg_unstuff_final).
+// A non-interleaved scan without restart intervals (every AC scan) decodes on one lane into blocks
+// the wave stages JPG_PT at a time in LDS (loaded, decoded into, written back): an AC refinement
+// read every block's earlier coefficients as it went, a dependent HBM round trip each, and on gfx9
+// the bit reader's waits for its loads (vmcnt) also waited for every coefficient store before.
+constexpr uint32_t JPG_PT = 256;
 __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict__ imgs,
                                                        const JpegScanDev* __restrict__ scans,
                                                        const uint8_t* __restrict__ ub,
@@ -1439,6 +1532,11 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
                                                        const uint32_t* __restrict__ ublen_s,
                                                        int16_t* __restrict__ coef) {
   __shared__ JpegLdsScan T;
+  __shared__ uint4 tile[JPG_PT * 8];  // JPG_PT blocks of 64 coefficients
+  __shared__ uint64_t ref_hist[JPG_PT];
+  __shared__ RefineOut ref_out[JPG_PT];
+  __shared__ __attribute__((aligned(16))) uint32_t bring[64 * JRING_S];
+  uint32_t* myring = bring + threadIdx.x * JRING_S;
   const JpegDev& D = imgs[blockIdx.x];
   const uint32_t nscan = D.nscan;
   if (nscan == 0 || D.arith) return;  // uniform: a parallel-path or arithmetic-coded image
@@ -1450,22 +1548,85 @@ __global__ __launch_bounds__(64) void jpeg_prog_kernel(const JpegDev* __restrict
     jpg_load_scan_tables(T, S);
     __syncthreads();
     const rsrc_t rs = make_rsrc(ub + S.ub_off, ublen_s[D.scan0 + si] + 64u);
+    const ScanK K = jpg_scan_k(D, S);
+    if (S.ns == 1 && S.nintervals == 1) {  // (interval 0 never inherits)
+      const uint32_t ie = ivend[S.iv_off];
+      const int c = S.comp[0];
+      const uint32_t wib = (uint32_t)D.wib[c], bw = (uint32_t)D.bw[c];
+      int16_t* cb = coef + D.blk_off[c] * 64;
+      const uint64_t band = (S.Se == 63 ? ~0ull : (1ull << (S.Se + 1)) - 1) & (~0ull << S.Ss);
+      const int p1 = 1 << S.Al, m1 = -(1 << S.Al);
+      const bool refine = S.kind == JPG_AC_REFINE;
+      BitStream br;
+      if (threadIdx.x == 0) br.start(rs, myring, ivstart[S.iv_off], ie);
+      uint32_t eobrun = 0;
+      int pred = 0;
+      for (uint32_t t0 = 0; t0 < S.nunits; t0 += JPG_PT) {
+        const uint32_t nt = min(JPG_PT, S.nunits - t0);
+        // 16-byte piece k of the tile: part k % 8 of its block k / 8
+        for (uint32_t k = threadIdx.x; k < nt * 8; k += 64) {
+          const uint32_t u = t0 + k / 8, by = u / wib, bx = u - by * wib;
+          tile[k] = reinterpret_cast<const uint4*>(cb + ((uint64_t)by * bw + bx) * 64)[k % 8];
+        }
+        __syncthreads();
+        if (!refine) {  // the other kinds read nothing back: the blocks in LDS, one lane
+          if (threadIdx.x == 0)
+            for (uint32_t u = 0; u < nt && br.pos <= ie; ++u)
+              jpg_scan_block(br, T, K, 0, reinterpret_cast<int16_t*>(tile + 8 * u), pred, eobrun);
+        }
+        const int16_t* tb = reinterpret_cast<const int16_t*>(tile);
+        for (uint32_t u = threadIdx.x; u < nt && refine; u += 64) {  // nonzero history, zigzag
+          uint64_t h = 0;
+          for (int zz = 0; zz < 64; ++zz) h |= (uint64_t)(tb[u * 64 + T.natural[zz]] != 0) << zz;
+          ref_hist[u] = h & band;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && refine) {
+          uint32_t u = 0;
+          for (; u < nt && br.pos <= ie; ++u)
+            jpg_refine_block(br, T, S.Ss, S.Se, ref_hist[u], eobrun, ref_out[u]);
+          for (; u < nt; ++u) ref_out[u] = RefineOut{0ull, 0ull, 0ull};  // out of data: unchanged
+        }
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < nt && refine; u += 64) {  // corrections, then new ones
+          int16_t* blk = reinterpret_cast<int16_t*>(tile + 8 * u);
+          const RefineOut o = ref_out[u];
+          uint64_t h = ref_hist[u];
+          for (int j = __popcll(h) - 1; h; h &= h - 1, --j) {
+            if (!((o.corr >> j) & 1u)) continue;
+            int16_t* cp = blk + T.natural[__builtin_ctzll(h)];
+            if ((*cp & p1) == 0) *cp = (int16_t)(*cp >= 0 ? *cp + p1 : *cp + m1);
+          }
+          for (uint64_t nw = o.newp; nw; nw &= nw - 1) {
+            const int zz = __builtin_ctzll(nw);
+            blk[T.natural[zz]] = (int16_t)((o.newn >> zz) & 1u ? m1 : p1);
+          }
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nt * 8; k += 64) {
+          const uint32_t u = t0 + k / 8, by = u / wib, bx = u - by * wib;
+          reinterpret_cast<uint4*>(cb + ((uint64_t)by * bw + bx) * 64)[k % 8] = tile[k];
+        }
+        __syncthreads();
+      }
+      continue;
+    }
     for (int t = threadIdx.x; t < S.nintervals; t += 64) {
       const uint32_t ie = ivend[S.iv_off + t];
       if (ie & JPG_IV_INHERIT) continue;
       const uint32_t u0 = S.restart ? (uint32_t)t * (uint32_t)S.restart : 0u;
       const uint32_t u1 = S.restart ? min(u0 + (uint32_t)S.restart, S.nunits) : S.nunits;
       BitStream br;
-      br.start(rs, ivstart[S.iv_off + t], ie);
+      br.start(rs, myring, ivstart[S.iv_off + t], ie);
       int pred[4] = {0, 0, 0, 0};
       uint32_t eobrun = 0;
-      for (uint32_t u = u0; u < u1 && br.pos <= ie; ++u) jpg_scan_unit(br, T, D, S, u, coef, pred, eobrun);
+      for (uint32_t u = u0; u < u1 && br.pos <= ie; ++u) jpg_scan_unit(br, T, K, u, coef, pred, eobrun);
       if (t + 1 < S.nintervals && (ivend[S.iv_off + t + 1] & JPG_IV_INHERIT) && br.pos <= ie &&
           u1 < S.nunits) {
         int pz[4] = {0, 0, 0, 0};
         uint32_t ez = 0;
-        br.start(rs, ie, ie);
-        jpg_scan_unit(br, T, D, S, u1, coef, pz, ez);
+        br.start(rs, myring, ie, ie);
+        jpg_scan_unit(br, T, K, u1, coef, pz, ez);
       }
     }
   }
@@ -1584,7 +1745,8 @@ __device__ int jar_ac_value(ArithDec& e, uint8_t* acs, uint8_t* st, int k, int K
 
 // one block of scan component k
 __device__ void jar_block(ArithDec& e, const JpegScanDev& S, int k, uint8_t* dcs, uint8_t* acs,
-                          uint8_t* fixed, int16_t* __restrict__ blk, int& last, int& ctx) {
+                          uint8_t* fixed, int16_t* __restrict__ blk, int& last, int& ctx,
+                          const uint8_t* nat) {
   const bool prog = S.kind != JPG_SEQ;
   if (S.kind == JPG_SEQ || S.kind == JPG_DC_FIRST) {
     last += jar_dc_diff(e, dcs, ctx, S.aL[k], S.aU[k]);
@@ -1606,7 +1768,7 @@ __device__ void jar_block(ArithDec& e, const JpegScanDev& S, int k, uint8_t* dcs
       }
       const int v = jar_ac_value(e, acs, st, z, S.aK[k], fixed);
       if (e.bad) return;
-      blk[jpg_natural[z]] = (int16_t)v;
+      blk[nat[z]] = (int16_t)v;
     }
   } else if (S.kind == JPG_DC_REFINE) {
     if (jar_decode(e, fixed)) blk[0] = (int16_t)(blk[0] | (1 << S.Al));
@@ -1626,18 +1788,18 @@ __device__ void jar_block(ArithDec& e, const JpegScanDev& S, int k, uint8_t* dcs
       }
       const int v = jar_ac_value(e, acs, st, z, S.aK[k], fixed);
       if (e.bad) return;
-      blk[jpg_natural[z]] = jpg_lshift(v, S.Al);
+      blk[nat[z]] = jpg_lshift(v, S.Al);
     }
   } else {  // AC refine
     const int p1 = 1 << S.Al, m1 = -(1 << S.Al);
     int kex = S.Se;  // the previous stage's end of block
-    while (kex > 0 && blk[jpg_natural[kex]] == 0) --kex;
+    while (kex > 0 && blk[nat[kex]] == 0) --kex;
     int z = S.Ss - 1;
     while (z < S.Se) {
       uint8_t* st = acs + 3 * z;
       if (z >= kex && jar_decode(e, st)) break;
       for (;;) {
-        int16_t* c = blk + jpg_natural[++z];
+        int16_t* c = blk + nat[++z];
         if (*c) {  // previously nonzero: a correction bit
           if (jar_decode(e, st + 2)) *c = (int16_t)(*c < 0 ? *c + m1 : *c + p1);
           break;
@@ -1663,6 +1825,8 @@ __global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restric
                                                         const uint32_t* __restrict__ ivend,
                                                         int16_t* __restrict__ coef) {
   __shared__ uint8_t stats[64 * JAR_LANE];
+  __shared__ uint8_t nat[80];  // jpg_natural in LDS
+  for (int k = threadIdx.x; k < 80; k += 64) nat[k] = jpg_natural[k];
   const JpegDev& D = imgs[blockIdx.x];
   const uint32_t nscan = D.nscan;
   if (nscan == 0 || !D.arith) return;  // uniform
@@ -1693,7 +1857,7 @@ __global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restric
           const uint32_t by = u / (uint32_t)D.wib[c], bx = u - by * (uint32_t)D.wib[c];
           int16_t* blk = coef + (D.blk_off[c] + (uint64_t)by * D.bw[c] + bx) * 64;
           jar_block(e, S, 0, mine + S.td[0] * JAR_DC, mine + 4 * JAR_DC + S.ta[0] * JAR_AC, &fixed,
-                    blk, last[0], ctx[0]);
+                    blk, last[0], ctx[0], nat);
         } else {
           const uint32_t my = u / (uint32_t)D.mcux, mx = u - my * (uint32_t)D.mcux;
           for (int k = 0; k < S.ns && !e.bad; ++k) {
@@ -1703,7 +1867,7 @@ __global__ __launch_bounds__(64) void jpeg_arith_kernel(const JpegDev* __restric
                 const uint64_t by = (uint64_t)my * D.cv[c] + dv, bx = (uint64_t)mx * D.ch[c] + dh;
                 int16_t* blk = coef + (D.blk_off[c] + by * D.bw[c] + bx) * 64;
                 jar_block(e, S, k, mine + S.td[k] * JAR_DC, mine + 4 * JAR_DC + S.ta[k] * JAR_AC,
-                          &fixed, blk, last[k], ctx[k]);
+                          &fixed, blk, last[k], ctx[k], nat);
               }
           }
         }

@@ -1,6 +1,6 @@
 """Decode one synthetic 600x1000 q90 4:2:0 file (or a batch of copies) repeatedly (tools only;
 for kernel traces):
-  python tools/jpeg_single.py [--iters 20] [--chunk 0] [--batch 1]"""
+  python tools/jpeg_single.py [--iters 20] [--chunk 0] [--batch 1] [--progressive]"""
 import argparse
 import io
 import sys
@@ -20,12 +20,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--chunk", type=int, default=0)
 ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--progressive", action="store_true")
 a = ap.parse_args()
 x = bench.synth_batch(torch, a.batch, torch.device("cuda", 0), seed=3).cpu().numpy()
 files = []
 for im in x:
     b = io.BytesIO()
-    Image.fromarray(im[..., ::-1]).save(b, "JPEG", quality=90, subsampling=2)
+    Image.fromarray(im[..., ::-1]).save(b, "JPEG", quality=90, subsampling=2,
+                                        progressive=a.progressive)
     files.append(b.getvalue())
 print("file bytes", len(files[0]))
 for _ in range(a.iters):
