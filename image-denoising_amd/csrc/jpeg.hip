@@ -19,7 +19,7 @@
 //                  and offset; per segment each restart interval's data as libjpeg reads it
 //                  (jdmarker.c resync on damaged files)
 //   the parallel path: single-scan Huffman files of 1 or 3 components (SOF0 / SOF1)
-//     sync A / B   self-synchronising chunk decoders (restart intervals: one thread each) with
+//     sync A / B   self-synchronising chunk decoders (each restart interval its own chunks) with
 //                  checkpoints; B passes until no chunk's end state changes
 //     prefix       per image: each chunk's first block and DC predictors
 //     write        one thread per 512-bit sub-chunk from the checkpoints: coefficient blocks
@@ -458,7 +458,8 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 //            final pass also counts the chunk's DC symbols and per-component DC differences
 //   prefix   per image: each chunk's first block index and DC predictors
 //   write    every chunk again from its exact start state, writing coefficient blocks
-// Images with restart markers: one thread per restart interval (true start state known).
+// Images with restart markers: each interval is cut into its own chunks (jpeg_chunk_map_kernel);
+// an interval's first chunk starts from its known state, the prefix restarts at each interval.
 // Chunk size: the ABI's flags may set one; the default depends on the batch (jpeg_plan)
 // Checkpoints (round 5): every pass records, per chunk and JPG_SUB-bit sub-chunk, the decoder state
 // at the first symbol that starts at or after the sub-chunk's first bit and the counts (blocks, DC
@@ -1066,6 +1067,88 @@ __global__ __launch_bounds__(256) void jpeg_unstuff_final(const DESC* __restrict
   }
 }
 
+// Restart intervals go through the same chunked decoder: each interval is cut into its own chunks
+// (its first chunk starts at the interval's known state, DC predictors 0; the others synchronise
+// as a scan's do), so a file with a few long intervals is not decoded one thread per interval.
+// jpeg_chunk_map_kernel (per image with restart intervals, after unstuffing): interval k gets
+// max(1, ceil(bits / chunk_bits)) chunks from slot iv_ck[k] on (none if it reads nothing and
+// inherits: its first MCU is its predecessor's, see jpeg_write_kernel); ck_iv[slot] names the
+// interval (~0: an unused slot).  The host sized the slots for the worst case.
+__global__ __launch_bounds__(256) void jpeg_chunk_map_kernel(const JpegDev* __restrict__ imgs,
+                                                             const uint32_t* __restrict__ ivstart,
+                                                             const uint32_t* __restrict__ ivend,
+                                                             uint32_t* __restrict__ iv_ck,
+                                                             uint32_t* __restrict__ ck_iv) {
+  const JpegDev& D = imgs[blockIdx.x];
+  if (!D.restart || D.nscan) return;  // uniform
+  __shared__ uint32_t wsum[4], carry_s;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const uint32_t n = (uint32_t)D.nintervals, cb = D.chunk_bits;
+  for (uint32_t k0 = 0; k0 < n; k0 += 256) {
+    const uint32_t k = k0 + threadIdx.x;
+    uint32_t c = 0;
+    if (k < n) {
+      const uint32_t ie = ivend[D.iv_off + k];
+      if (!(ie & JPG_IV_INHERIT)) c = max(1u, (ie - ivstart[D.iv_off + k] + cb - 1) / cb);
+    }
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t off = carry_s + inc - c;
+    for (int w = 0; w < wv; ++w) off += wsum[w];
+    if (k < n) {
+      iv_ck[D.iv_off + k] = off;
+      for (uint32_t q = 0; q < c && off + q < D.nchunks; ++q) ck_iv[D.ch_off + off + q] = k;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  for (uint32_t t = carry_s + threadIdx.x; t < D.nchunks; t += 256) ck_iv[D.ch_off + t] = ~0u;
+}
+
+// chunk t of image D: its bit range [b0, b1), whether it starts a restart interval (or the image's
+// data: a known state) and the interval k; live = false for an unused slot
+struct ChunkPos {
+  bool live, first;
+  uint32_t k, b0, b1, end;  // end: where the interval's (or the image's) data ends
+};
+__device__ __forceinline__ ChunkPos jpg_chunk_pos(const JpegDev& D, uint32_t t, uint32_t nbits,
+                                                  const uint32_t* __restrict__ ck_iv,
+                                                  const uint32_t* __restrict__ iv_ck,
+                                                  const uint32_t* __restrict__ ivstart,
+                                                  const uint32_t* __restrict__ ivend) {
+  ChunkPos c;
+  if (!D.restart) {
+    c.live = t < D.nchunks;
+    c.first = t == 0;
+    c.k = 0;
+    c.end = nbits;
+    c.b0 = min(t * D.chunk_bits, nbits);
+    c.b1 = min(c.b0 + D.chunk_bits, nbits);
+    return c;
+  }
+  c.k = t < D.nchunks ? ck_iv[D.ch_off + t] : ~0u;
+  c.live = c.k != ~0u;
+  if (!c.live) {
+    c.first = false;
+    c.b0 = c.b1 = c.end = 0;
+    return c;
+  }
+  const uint32_t j = t - iv_ck[D.iv_off + c.k];
+  c.first = j == 0;
+  c.end = ivend[D.iv_off + c.k] & ~JPG_IV_INHERIT;
+  c.b0 = min(ivstart[D.iv_off + c.k] + j * D.chunk_bits, c.end);
+  c.b1 = min(c.b0 + D.chunk_bits, c.end);
+  return c;
+}
+
 // stage 2a/2b: sync passes.  grid (max chunks per image, n).  PASS_A: start from the chunk's
 // own first bit; else from the predecessor's end state in `prev` (chunk 0: the true start).
 // chg_prev / chg_next: per chunk, did its end state change in the previous / this pass.  After
@@ -1085,7 +1168,11 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
                                                        uint64_t* __restrict__ ck_st,
                                                        ChunkOut* __restrict__ ck_co,
                                                        const uint32_t* __restrict__ settled,
-                                                       int badlen) {
+                                                       int badlen,
+                                                       const uint32_t* __restrict__ ck_iv,
+                                                       const uint32_t* __restrict__ iv_ck,
+                                                       const uint32_t* __restrict__ ivstart,
+                                                       const uint32_t* __restrict__ ivend) {
   __shared__ JpegLds T;
   __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
   // the previous pass of this launch round changed nothing: the decode has converged and both
@@ -1093,12 +1180,14 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
   // to do -- the host queues a round of passes without reading a flag between them
   if (!PASS_A && settled && *settled == 0u) return;
   const JpegDev& D = imgs[blockIdx.y];
-  if (D.restart || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
+  if (D.nscan || blockIdx.x * 64 >= D.nchunks) return;  // uniform per workgroup
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  bool redo = true;
+  const uint32_t nbits = ublen[blockIdx.y] * 8u;
+  const ChunkPos cp = jpg_chunk_pos(D, t, nbits, ck_iv, iv_ck, ivstart, ivend);
+  bool redo = cp.live;
   if (!PASS_A && !all) {
-    redo = t < D.nchunks && t > 0 && chg_prev[D.ch_off + t - 1];
-    if (t < D.nchunks && !redo) {
+    redo = cp.live && !cp.first && chg_prev[D.ch_off + t - 1];
+    if (cp.live && !redo) {
       next[D.ch_off + t] = prev[D.ch_off + t];
       chg_next[D.ch_off + t] = 0;
     }
@@ -1106,13 +1195,9 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
   }
   jpg_load_tables(T, D);
   __syncthreads();
-  if (t >= D.nchunks || !redo) return;
-  const uint32_t nbits = ublen[blockIdx.y] * 8u;
-  const uint32_t b0 = min(t * D.chunk_bits, nbits), b1 = min(b0 + D.chunk_bits, nbits);
-  uint64_t st;
-  if (t == 0) st = 0;
-  else if (PASS_A) st = jpg_state(b0, 0, 0);
-  else st = prev[D.ch_off + t - 1];
+  if (!redo) return;
+  const uint32_t b0 = cp.b0, b1 = cp.b1;
+  const uint64_t st = PASS_A || cp.first ? jpg_state(b0, 0, 0) : prev[D.ch_off + t - 1];
   const uint32_t nsub = jpg_nsub(D.chunk_bits);
   uint64_t* cks = ck_st + (size_t)(D.ch_off + t) * nsub;
   ChunkOut* ckc = ck_co + (size_t)(D.ch_off + t) * nsub;
@@ -1166,49 +1251,78 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
 
 // stage 2c: per image, the first block index and DC predictors of every chunk
 // one 256-thread workgroup per image: exclusive scan of the chunk counts (block counts and DC
-// sums add), 256 chunks per round (a serial walk per image was a ~300-step latency chain)
+// sums add), 256 chunks per round (a serial walk per image was a ~300-step latency chain),
+// segmented at the chunks that start a restart interval (DC sums from 0, blocks from the
+// interval's first block)
 __global__ __launch_bounds__(256) void jpeg_prefix_kernel(const JpegDev* __restrict__ imgs,
                                                           const ChunkOut* __restrict__ cnt,
-                                                          ChunkOut* __restrict__ start, int n) {
+                                                          ChunkOut* __restrict__ start, int n,
+                                                          const uint32_t* __restrict__ ck_iv,
+                                                          const uint32_t* __restrict__ iv_ck) {
   const JpegDev& D = imgs[blockIdx.x];
-  if (D.restart) return;
+  if (D.nscan) return;
   __shared__ int32_t sv[4][256];
+  __shared__ uint8_t sf[256];
   __shared__ int32_t carry[4];
   if (threadIdx.x < 4) carry[threadIdx.x] = 0;
   for (uint32_t t0 = 0; t0 < D.nchunks; t0 += 256) {
     const uint32_t t = t0 + threadIdx.x;
     ChunkOut c{0u, {0, 0, 0}};
-    if (t < D.nchunks) c = cnt[D.ch_off + t];
-    int32_t v[4] = {(int32_t)c.nblk, c.dcsum[0], c.dcsum[1], c.dcsum[2]};
+    bool first = t == 0;
+    uint32_t k = 0;
+    if (t < D.nchunks) {
+      c = cnt[D.ch_off + t];
+      if (D.restart) {
+        k = ck_iv[D.ch_off + t];
+        first = k != ~0u && iv_ck[D.iv_off + k] == t;
+        if (k == ~0u) c = ChunkOut{0u, {0, 0, 0}};
+      }
+    }
+    const int32_t v[4] = {(int32_t)c.nblk, c.dcsum[0], c.dcsum[1], c.dcsum[2]};
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) sv[k][threadIdx.x] = v[k];
+    for (int q = 0; q < 4; ++q) sv[q][threadIdx.x] = v[q];
+    sf[threadIdx.x] = first ? 1 : 0;
     __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+    for (int o = 1; o < 256; o <<= 1) {  // segmented Hillis-Steele inclusive scan
       int32_t u[4] = {0, 0, 0, 0};
-      if (threadIdx.x >= (unsigned)o)
+      uint8_t fu = 0;
+      if (threadIdx.x >= (unsigned)o) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = sv[k][threadIdx.x - o];
+        for (int q = 0; q < 4; ++q) u[q] = sv[q][threadIdx.x - o];
+        fu = sf[threadIdx.x - o];
+      }
+      const uint8_t fo = sf[threadIdx.x];
       __syncthreads();
+      if (!fo)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) sv[k][threadIdx.x] += u[k];
+        for (int q = 0; q < 4; ++q) sv[q][threadIdx.x] += u[q];
+      sf[threadIdx.x] = fo | fu;
       __syncthreads();
     }
     if (t < D.nchunks) {
-      ChunkOut e;  // exclusive = carry + inclusive - own
-      e.nblk = (uint32_t)(carry[0] + sv[0][threadIdx.x] - v[0]);
+      // exclusive = inclusive - own, plus the carry unless a segment started in this round
+      const bool seg = sf[threadIdx.x] != 0;
+      ChunkOut e;
+      e.nblk = (uint32_t)((seg ? 0 : carry[0]) + sv[0][threadIdx.x] - v[0]);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) e.dcsum[k] = carry[k + 1] + sv[k + 1][threadIdx.x] - v[k + 1];
+      for (int q = 0; q < 3; ++q) e.dcsum[q] = (seg ? 0 : carry[q + 1]) + sv[q + 1][threadIdx.x] - v[q + 1];
+      if (D.restart && k != ~0u) {
+        // blocks from the interval's first one; the chunks before the interval's own start in
+        // this round add nothing (the scan restarted at the interval's first chunk)
+        e.nblk += k * (uint32_t)D.restart * (uint32_t)D.bpm;
+      }
       start[D.ch_off + t] = e;
     }
     __syncthreads();
-    if (threadIdx.x < 4) carry[threadIdx.x] += sv[threadIdx.x][255];
+    if (threadIdx.x < 4)
+      carry[threadIdx.x] = (sf[255] ? 0 : carry[threadIdx.x]) + sv[threadIdx.x][255];
+    __syncthreads();
   }
 }
 
-// stage 2d: write pass.  Sub-chunks of images without restart markers (grid.x over chunks x
-// sub-chunks, from the final checkpoints), or restart intervals (one thread each) of images with
-// them.
+// stage 2d: write pass.  Sub-chunks (grid.x over chunks x sub-chunks, from the final
+// checkpoints) of images without restart markers and of each restart interval.
 __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restrict__ imgs,
                                                         const uint8_t* __restrict__ ub,
                                                         const uint32_t* __restrict__ ublen,
@@ -1218,43 +1332,20 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
                                                         const ChunkOut* __restrict__ ck_co,
                                                         const ChunkOut* __restrict__ start,
                                                         int16_t* __restrict__ coef, int badlen,
-                                                        uint32_t* __restrict__ badseen) {
+                                                        uint32_t* __restrict__ badseen,
+                                                        const uint32_t* __restrict__ ck_iv,
+                                                        const uint32_t* __restrict__ iv_ck) {
   __shared__ JpegLds T;
   __shared__ __attribute__((aligned(16))) uint32_t ring[64 * JRING_W];
   const JpegDev& D = imgs[blockIdx.y];
   const uint32_t nsub = jpg_nsub(D.chunk_bits);
-  const uint32_t nitems = D.restart ? (uint32_t)D.nintervals : D.nchunks * nsub;
+  const uint32_t nitems = D.nscan ? 0u : D.nchunks * nsub;
   if (blockIdx.x * 64 >= nitems) return;  // uniform per workgroup
   jpg_load_tables(T, D);
   __syncthreads();
   const uint32_t u = blockIdx.x * 64 + threadIdx.x;
   if (u >= nitems) return;
   const uint32_t nbits = ublen[blockIdx.y] * 8u;
-  int pred[3] = {0, 0, 0};
-  ChunkOut dummy{0u, {0, 0, 0}};
-  const JpgConst K = jpg_const(D);
-  uint32_t* myring = ring + threadIdx.x * JRING_W;
-  if (D.restart) {
-    // interval u: restart MCUs from its first bit, DC predictors reset, its data's end masked.  An
-    // interval that reads nothing and inherits the out-of-data state decodes nothing itself: if
-    // its predecessor did not run out, libjpeg decodes its first MCU from zero bits -- here, by
-    // the predecessor's thread
-    const uint32_t ie = ivend[D.iv_off + u];
-    if (ie & JPG_IV_INHERIT) return;
-    const uint32_t b0 = ivstart[D.iv_off + u], b1 = ie;
-    const uint32_t mcus = (uint32_t)(D.mcux * D.mcuy), mcu0 = u * (uint32_t)D.restart;
-    const uint32_t mcu1 = min(mcu0 + (uint32_t)D.restart, mcus);
-    const rsrc_t rs = make_rsrc(ub + D.ub_off, nbits / 8u + 64u);
-    const uint64_t e = jpg_run<true, true>(K, T, rs, myring, jpg_state(b0, 0, 0), b1, &dummy,
-                                           (int32_t)(mcu0 * D.bpm) - 1, pred, coef,
-                                           (mcu1 - mcu0) * (uint32_t)D.bpm);
-    if (u + 1 < nitems && (ivend[D.iv_off + u + 1] & JPG_IV_INHERIT) && (uint32_t)e <= b1) {
-      int pz[3] = {0, 0, 0};
-      jpg_run<true, true>(K, T, rs, myring, jpg_state(b1, 0, 0), b1, &dummy,
-                          (int32_t)(mcu1 * D.bpm) - 1, pz, coef, (uint32_t)D.bpm);
-    }
-    return;
-  }
   // sub-chunk j of chunk t from its checkpoint: state, first block, DC predictors.  badlen: the
   // bits a bad code takes.  libjpeg's is 17, but the sync passes converge a pass sooner with 16
   // (1.21 against 1.31 ms for a 600x1000 file: bad codes are frequent on the speculative
@@ -1262,23 +1353,50 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
   // code on the true one, which the write pass then reports (badseen) and the host decodes again
   // with 17 -- only files with a bad code in their data pay for the exact rule
   const uint32_t t = u / nsub, j = u - t * nsub;
-  const uint32_t b0 = min(t * D.chunk_bits, nbits);
-  const uint32_t b1 = min(min(b0 + D.chunk_bits, nbits), b0 + (j + 1) * JPG_SUB);
-  // the sub-chunk holding the data's last bit (or the first one, without data) finishes the
-  // decode where the data ends
-  const uint32_t tl = nbits ? (nbits - 1) / D.chunk_bits : 0u;
-  const bool tail = t == tl && j == (nbits ? (nbits - 1 - tl * D.chunk_bits) / JPG_SUB : 0u);
+  const ChunkPos cp = jpg_chunk_pos(D, t, nbits, ck_iv, iv_ck, ivstart, ivend);
+  if (!cp.live) return;
+  const uint32_t b1 = min(cp.b1, cp.b0 + (j + 1) * JPG_SUB);
+  // the sub-chunk holding the last bit of the data (of the image, or of the restart interval), or
+  // the first one without data, finishes the decode where the data ends
+  const bool tail = cp.b0 < cp.end ? cp.b1 == cp.end && (cp.end - 1 - cp.b0) / JPG_SUB == j
+                                    : cp.first && j == 0;
   const size_t k = (size_t)(D.ch_off + t) * nsub + j;
   const uint64_t st = ck_st[k];
   const ChunkOut c = ck_co[k], s0 = start[D.ch_off + t];
-  pred[0] = s0.dcsum[0] + c.dcsum[0];
-  pred[1] = s0.dcsum[1] + c.dcsum[1];
-  pred[2] = s0.dcsum[2] + c.dcsum[2];
+  int pred[3] = {s0.dcsum[0] + c.dcsum[0], s0.dcsum[1] + c.dcsum[1], s0.dcsum[2] + c.dcsum[2]};
   const int32_t blk = (int32_t)(s0.nblk + c.nblk) - 1;
   if ((uint32_t)st >= b1 && !tail) return;
+  ChunkOut dummy{0u, {0, 0, 0}};
+  JpgConst K = jpg_const(D);
+  uint32_t* myring = ring + threadIdx.x * JRING_W;
   const rsrc_t rs = make_rsrc(ub + D.ub_off, nbits / 8u + 64u);
-  jpg_run<true>(K, T, rs, myring, st, b1, &dummy, blk, pred, coef, 0xFFFFFFFFu, tail, badlen,
-                badseen);
+  if (!D.restart) {
+    jpg_run<true>(K, T, rs, myring, st, b1, &dummy, blk, pred, coef, 0xFFFFFFFFu, tail, badlen,
+                  badseen);
+    return;
+  }
+  // a restart interval: its blocks only (the bits after its last MCU are padding)
+  const uint32_t mcus = (uint32_t)(D.mcux * D.mcuy), R = (uint32_t)D.restart;
+  const uint32_t bhi = min((cp.k + 1) * R, mcus) * (uint32_t)D.bpm;
+  K.total_blocks = bhi;
+  if (!tail) {
+    jpg_run<true>(K, T, rs, myring, st, b1, &dummy, blk, pred, coef, 0xFFFFFFFFu, false, badlen,
+                  badseen);
+    return;
+  }
+  // the interval's end: its MCUs to the last one, the bits past its data 0, an MCU decoded only if
+  // the data lasted up to its start; then, if the next interval reads nothing and inherits the
+  // out-of-data state and this one did not run out, libjpeg decodes the next one's first MCU from
+  // zero bits
+  const uint64_t e = jpg_run<true, true>(K, T, rs, myring, st, cp.end, &dummy, blk, pred, coef,
+                                         bhi - (uint32_t)(blk + 1), false, badlen, badseen);
+  if (cp.k + 1 < (uint32_t)D.nintervals && (ivend[D.iv_off + cp.k + 1] & JPG_IV_INHERIT) &&
+      (uint32_t)e <= cp.end && bhi < mcus * (uint32_t)D.bpm) {
+    int pz[3] = {0, 0, 0};
+    K.total_blocks = min(bhi + R * (uint32_t)D.bpm, mcus * (uint32_t)D.bpm);
+    jpg_run<true, true>(K, T, rs, myring, jpg_state(cp.end, 0, 0), cp.end, &dummy,
+                        (int32_t)bhi - 1, pz, coef, (uint32_t)D.bpm, false, badlen, badseen);
+  }
 }
 
 // ---- device: the scan path (progressive / multi-scan files) --------------------------------------
@@ -2306,13 +2424,13 @@ struct JpegPlan {
   uint32_t nintervals = 0, nchunks = 0, max_items = 1, max_items_w = 1, nsub = 1;
   uint64_t nmk = 0;  // marker table entries
   int mt_img = 1, mt_scan = 1;  // most unstuffing tiles of an image / of a scan
-  bool any_chunked = false;
+  bool any_chunked = false, any_restart = false;
   bool any_huff_scan = false, any_arith = false;  // scan-path images of each coding
   bool scales[2][2] = {};  // IDCT output scales present: [sv - 1][sh - 1]
   size_t off_imgs = 0, off_blkend = 0, off_scans = 0, off_scan = 0, off_coef = 0, off_planes = 0;
   size_t off_ub = 0, off_iv = 0, off_ivend = 0, off_mk = 0, off_ublen = 0, off_ublen_s = 0, off_s0 = 0, off_s1 = 0,
          off_cnt = 0, off_start = 0, off_flag = 0, off_chg0 = 0, off_chg1 = 0, off_ck_st = 0,
-         off_ck_co = 0, off_tcnt = 0, total = 0;
+         off_ck_co = 0, off_tcnt = 0, off_ck_iv = 0, off_iv_ck = 0, total = 0;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2538,14 +2656,15 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     D.ch_off = P.nchunks;
     D.chunk_bits = chunk_bits;
     if (D.nscan) continue;  // the scan path: no chunks
-    D.nchunks = D.restart ? 0u
-                          : (uint32_t)(((uint64_t)D.scan_len * 8 + D.chunk_bits - 1) / D.chunk_bits);
-    if (D.nchunks == 0 && !D.restart) D.nchunks = 1;
+    // (restart intervals: each its own chunks, jpeg_chunk_map_kernel; room for the worst case)
+    D.nchunks = (uint32_t)(((uint64_t)D.scan_len * 8 + D.chunk_bits - 1) / D.chunk_bits) +
+                (D.restart ? (uint32_t)D.nintervals : 0u);
+    if (D.nchunks == 0) D.nchunks = 1;
     P.nchunks += D.nchunks;
-    P.any_chunked |= D.restart == 0;
-    P.max_items = std::max(P.max_items, std::max(D.nchunks, (uint32_t)D.nintervals));
-    P.max_items_w = std::max(P.max_items_w, std::max(D.nchunks * jpg_nsub(chunk_bits),
-                                                     (uint32_t)D.nintervals));
+    P.any_chunked = true;
+    P.any_restart |= D.restart != 0;
+    P.max_items = std::max(P.max_items, D.nchunks);
+    P.max_items_w = std::max(P.max_items_w, D.nchunks * jpg_nsub(chunk_bits));
   }
   P.off_imgs = 0;
   P.off_blkend = align256(P.off_imgs + sizeof(JpegDev) * (size_t)n);
@@ -2573,7 +2692,9 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     P.mt_img = std::max(P.mt_img, (int)((D.scan_len + UNS_TILE - 1) / UNS_TILE));
   for (const JpegScanDev& S : P.scans)
     P.mt_scan = std::max(P.mt_scan, (int)((S.scan_len + UNS_TILE - 1) / UNS_TILE));
-  P.off_tcnt = align256(P.off_ck_co + sizeof(ChunkOut) * (size_t)P.nchunks * P.nsub);
+  P.off_ck_iv = align256(P.off_ck_co + sizeof(ChunkOut) * (size_t)P.nchunks * P.nsub);
+  P.off_iv_ck = align256(P.off_ck_iv + sizeof(uint32_t) * (size_t)P.nchunks);
+  P.off_tcnt = align256(P.off_iv_ck + sizeof(uint32_t) * (size_t)P.nintervals);
   const size_t ntc = std::max((size_t)n * P.mt_img, P.scans.size() * (size_t)P.mt_scan);
   P.total = align256(P.off_tcnt + sizeof(uint2) * ntc);
   return IDN_OK;
@@ -2698,6 +2819,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   uint8_t* chg[2] = {reinterpret_cast<uint8_t*>(ws + P.off_chg0),
                      reinterpret_cast<uint8_t*>(ws + P.off_chg1)};
   uint2* tcnt = reinterpret_cast<uint2*>(ws + P.off_tcnt);
+  uint32_t* ck_iv = reinterpret_cast<uint32_t*>(ws + P.off_ck_iv);
+  uint32_t* iv_ck = reinterpret_cast<uint32_t*>(ws + P.off_iv_ck);
   {
     const dim3 g((unsigned)P.mt_img, (unsigned)n);
     hipLaunchKernelGGL(jpeg_unstuff_count<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
@@ -2707,6 +2830,9 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     hipLaunchKernelGGL(jpeg_unstuff_final<JpegDev>, dim3(n), dim3(256), 0, st, dimg, tcnt,
                        P.mt_img, ub, mk, ivs, ive, ublen);
   }
+  if (P.any_restart)
+    hipLaunchKernelGGL(jpeg_chunk_map_kernel, dim3(n), dim3(256), 0, st, dimg, ivs, ive, iv_ck,
+                       ck_iv);
   const JpegScanDev* dscan = reinterpret_cast<const JpegScanDev*>(ws + P.off_scans);
   if (!P.scans.empty()) {
     // (after the images' unstuffing: the tile counts reuse the same array)
@@ -2736,7 +2862,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
       // was a gap in a single file's decode
       constexpr int JPG_BROUND = 12;
       hipLaunchKernelGGL(jpeg_sync_kernel<true>, gitems, dim3(64), 0, st, dimg, ub, ublen, S[1],
-                         S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co, nullptr, badlen);
+                         S[0], cnt, flag, chg[1], chg[0], 1, ck_st, ck_co, nullptr, badlen, ck_iv,
+                         iv_ck, ivs, ive);
       for (uint32_t it = 0;; it += JPG_BROUND) {
         if (hipMemsetAsync(flag, 0, 4 * JPG_BROUND, st) != hipSuccess)
           return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
@@ -2744,7 +2871,7 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
           hipLaunchKernelGGL(jpeg_sync_kernel<false>, gitems, dim3(64), 0, st, dimg, ub, ublen,
                              S[cur], S[cur ^ 1], cnt, flag + k, chg[cur], chg[cur ^ 1],
                              it + k == 0 ? 1 : 0, ck_st, ck_co, k > 0 ? flag + k - 1 : nullptr,
-                             badlen);
+                             badlen, ck_iv, iv_ck, ivs, ive);
           cur ^= 1;
         }
         uint32_t changed[JPG_BROUND] = {};
@@ -2755,11 +2882,12 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
         if (it > P.max_items + 2)
           return set_error(IDN_EHIP, "idn_jpeg_decode_u8: entropy decoding did not converge");
       }
-      hipLaunchKernelGGL(jpeg_prefix_kernel, dim3(n), dim3(256), 0, st, dimg, cnt, cstart, n);
+      hipLaunchKernelGGL(jpeg_prefix_kernel, dim3(n), dim3(256), 0, st, dimg, cnt, cstart, n, ck_iv,
+                         iv_ck);
     }
     const dim3 gwrite((P.max_items_w + 63) / 64, n);
     hipLaunchKernelGGL(jpeg_write_kernel, gwrite, dim3(64), 0, st, dimg, ub, ublen, ivs, ive, ck_st,
-                       ck_co, cstart, coef, badlen, badseen);
+                       ck_co, cstart, coef, badlen, badseen, ck_iv, iv_ck);
     if (!P.scans.empty()) {
       if (P.any_huff_scan)
         hipLaunchKernelGGL(jpeg_prog_kernel, dim3(n), dim3(64), 0, st, dimg, dscan, ub, ivs, ive,

@@ -263,3 +263,29 @@ def test_damaged_files_turbo_mode_match_the_oracle(dev):
         data = jd.damage((JPEG / c[0]).read_bytes(), c[1], c[2])
         got = ops.jpeg_decode([data], mode="turbo")[0].cpu().numpy()
         assert np.array_equal(got, jpeg9.imread(data, mode="turbo")), jd.key(c)
+
+
+@pytest.mark.parametrize("chunk", [0, 512, 4096])
+def test_restart_intervals_decode_as_the_same_image_without_them(dev, chunk):
+    """restart intervals go through the chunked decoder, each interval cut into its own chunks:
+    a 600x1000 image written with a restart marker every MCU row (38 long intervals), every 3
+    MCUs (short ones) and without any has the same coefficients, so the same pixels, in a mixed
+    batch and at any chunk size"""
+    import io
+    from PIL import Image
+    from idn import ops
+    rng = np.random.default_rng(5)
+    y, x = np.mgrid[0:600, 0:1000]
+    img = np.stack([(x * 0.3 + 50 * np.sin(y / 13.0)) % 256, (y * 0.5) % 256, (x + y) % 256], -1)
+    img = np.clip(img + rng.normal(0, 10, img.shape), 0, 255).astype(np.uint8)
+    files = []
+    for kw in ({}, {"restart_marker_rows": 1}, {"restart_marker_blocks": 3}):
+        b = io.BytesIO()
+        Image.fromarray(img).save(b, "JPEG", quality=90, subsampling=2, **kw)
+        files.append(b.getvalue())
+    assert files[1].count(b"\xff\xdd") == 1 and files[2].count(b"\xff\xdd") == 1
+    got = ops.jpeg_decode(files + files[::-1], chunk_bits=chunk).cpu().numpy()
+    for k in range(1, 6):
+        assert np.array_equal(got[k], got[0]), k
+    check = ops.jpeg_decode([files[1]], mode="turbo", chunk_bits=chunk)[0].cpu().numpy()
+    assert np.array_equal(check, ops.jpeg_decode([files[0]], mode="turbo")[0].cpu().numpy())
