@@ -470,7 +470,10 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 // longer decode whole chunks) -- and the write pass runs one thread per sub-chunk from the final
 // checkpoints: 8x the threads of one per chunk, each an eighth as long (a single image's write
 // pass was 0.76 ms of serial decoding per thread).
-constexpr uint32_t JPG_SUB = 512;
+#ifndef IDN_JPG_SUB  // A/B builds set it
+#define IDN_JPG_SUB 512
+#endif
+constexpr uint32_t JPG_SUB = IDN_JPG_SUB;
 __host__ __device__ __forceinline__ uint32_t jpg_nsub(uint32_t chunk_bits) {
   return (chunk_bits + JPG_SUB - 1) / JPG_SUB;
 }
