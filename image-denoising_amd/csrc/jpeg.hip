@@ -22,7 +22,7 @@
 //     sync A / B   self-synchronising chunk decoders (each restart interval its own chunks) with
 //                  checkpoints; B passes until no chunk's end state changes
 //     prefix       per image: each chunk's first block and DC predictors
-//     write        one thread per 512-bit sub-chunk from the checkpoints: coefficient blocks
+//     write        one thread per 256-bit sub-chunk from the checkpoints: coefficient blocks
 //   the scan path: progressive (SOF2), multi-scan, arithmetic-coded (SOF9 / SOF10) and
 //     4-component files; one wave per image walks the scans in file order, lanes over restart
 //     intervals: jpeg_prog_kernel (Huffman: jdhuff.c's decoders) or jpeg_arith_kernel
@@ -468,10 +468,11 @@ static int jpeg_build_huff(const HuffSpec& H, bool dc, uint16_t* lut, int32_t* m
 // trajectory is the recorded one, so the end state is and the counts shift by the difference at
 // that checkpoint (a chunk's trajectories typically join within ~1 kbit, so the B passes no
 // longer decode whole chunks) -- and the write pass runs one thread per sub-chunk from the final
-// checkpoints: 8x the threads of one per chunk, each an eighth as long (a single image's write
-// pass was 0.76 ms of serial decoding per thread).
+// checkpoints: many times the threads of one per chunk, each as much shorter (a single image's
+// write pass was 0.76 ms of serial decoding per thread).  256 bits measured best against 128, 512
+// and 1024 (profiles/r05/jpeg/sub_ab_sweep.txt: a joining trajectory stops sooner).
 #ifndef IDN_JPG_SUB  // A/B builds set it
-#define IDN_JPG_SUB 512
+#define IDN_JPG_SUB 256
 #endif
 constexpr uint32_t JPG_SUB = IDN_JPG_SUB;
 __host__ __device__ __forceinline__ uint32_t jpg_nsub(uint32_t chunk_bits) {
