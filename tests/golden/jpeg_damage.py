@@ -62,12 +62,14 @@ def _safe(d: bytes, k: int) -> bool:
 
 
 def _near_safe(d: bytes, k: int) -> int:
-    """the first byte from k on that starts three plain data bytes of one scan"""
+    """the first byte from k on (wrapping to the first scan's data) that starts three plain data
+    bytes of one scan"""
     sp = _spans(d)
-    while not (any(b < k and k + 3 < e for b, e in sp) and _safe(d, k) and _safe(d, k + 1) and
-               _safe(d, k + 2)):
-        k += 1
-    return k
+    ok = [j for b, e in sp for j in range(b + 1, e - 3)
+          if _safe(d, j) and _safe(d, j + 1) and _safe(d, j + 2)]
+    if not ok:
+        raise ValueError("no plain entropy-coded bytes")
+    return next((j for j in ok if j >= k), ok[0])
 
 
 def damage(d: bytes, op: str, arg) -> bytes:
@@ -134,3 +136,21 @@ def key(case) -> str:
     f, op, arg = case
     a = "_".join(str(x) for x in arg) if isinstance(arg, tuple) else str(arg)
     return f"{f}:{op}:{a}"
+
+
+def random_damage(d: bytes, rng) -> bytes:
+    """one random damage of the kinds above at a random place (rng: random.Random); for fuzzing the
+    decoder against the oracle beyond the libjpeg-pinned cases"""
+    op = rng.choice(["cut", "flip", "flip", "ones", "junk", "rstnum", "mix"])
+    rst = [o for o, m in _markers(d) if 0xD0 <= m <= 0xD7]
+    if op == "cut":
+        return damage(d, "cut", rng.random())
+    if op == "flip":
+        return damage(d, "flip", rng.randrange(1000))
+    if op == "ones":
+        return damage(d, "ones", rng.random() * 0.95)
+    if op == "junk":
+        return damage(d, "junk", rng.random() * 0.95)
+    if op == "rstnum" and rst:
+        return damage(d, "rstnum", (rng.randrange(len(rst)), rng.choice([-2, -1, 1, 2, 3, 4])))
+    return damage(damage(d, "flip", rng.randrange(1000)), "cut", 0.3 + 0.7 * rng.random())

@@ -289,3 +289,27 @@ def test_restart_intervals_decode_as_the_same_image_without_them(dev, chunk):
         assert np.array_equal(got[k], got[0]), k
     check = ops.jpeg_decode([files[1]], mode="turbo", chunk_bits=chunk)[0].cpu().numpy()
     assert np.array_equal(check, ops.jpeg_decode([files[0]], mode="turbo")[0].cpu().numpy())
+
+
+def test_random_damaged_files_match_the_oracle(dev):
+    """150 random damages (tests/golden/jpeg_damage.py random_damage: cuts, bit flips, one-bit runs,
+    stray markers, renumbered restart markers) of the small fixtures, GPU against the oracle (itself
+    pinned to libjpeg 9d by the committed damaged variants); tools/jpeg_fuzz.py runs more"""
+    import random
+    from idn import ops
+    from idn._lib import IdnError
+    from oracle import jpeg9
+    jdm = _damaged()
+    rng = random.Random(11)
+    files = [p for p in sorted(JPEG.glob("*.jpg")) if p.stat().st_size < 20000]
+    for i in range(150):
+        p = rng.choice(files)
+        data = jdm.random_damage(p.read_bytes(), rng)
+        try:
+            ref = jpeg9.imread(data)
+        except Exception:
+            with pytest.raises(IdnError):
+                ops.jpeg_decode([data])
+            continue
+        got = ops.jpeg_decode([data])[0].cpu().numpy()
+        assert np.array_equal(got, ref), (i, p.name)
