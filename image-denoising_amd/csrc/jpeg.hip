@@ -84,6 +84,7 @@ struct JpegDev {
   uint32_t scan0, nscan;    // scan path: the image's scans in the batch scan table (0: none)
   int arith;                // arithmetic-coded (the scan path's jpeg_arith_kernel)
   int smooth;               // libjpeg 9d block smoothing (jdcoefct.c decompress_smooth_data)
+  int orient;               // the EXIF orientation cv2.imread applies (1: none; jpg_exif_orientation)
   int8_t cbits[4][6];       // its coef_bits latch per component (zigzag 0..5; -1: never coded)
   uint8_t ph_comp[10], ph_dv[10], ph_dh[10];  // block of the MCU -> component, block row, column
   uint16_t q[4][64];        // quantisation tables, natural order
@@ -178,6 +179,128 @@ static size_t jpg_segment_end(const uint8_t* p, size_t n, size_t i) {
 static int jpg_fail(std::string* err, const char* msg) {
   if (err) *err = msg;
   return IDN_EUNSUPPORTED;
+}
+
+// ---- host: the EXIF orientation cv2.imread applies ----------------------------------------------
+// OpenCV 3.4.2's imread (loadsave.cpp) calls ApplyExifOrientation on the decoded image unless
+// IMREAD_IGNORE_ORIENTATION is set; the tag comes from exif.cpp's ExifReader, which walks the
+// file's markers two bytes at a time (the 0xFF is not checked) and takes the FIRST APP1 segment
+// as EXIF data whatever its identifier.  Restated from the published OpenCV source [recalled: cv2
+// is not importable here], including when it gives up (orientation 1, the image as decoded):
+//   - the walk skips (by their length field) SOF0, SOF2, DHT, DQT, DRI, SOS, RST0-7, APP0,
+//     APP2-15, COM; SOI / EOI have no length; any other code ends the search (no EXIF);
+//   - a length below 2, or an APP1 length <= 6, is a parse error (no EXIF); the APP1 data is
+//     the length - 6 bytes after the 6-byte identifier slot (zero-filled past the end of file);
+//   - the TIFF header: "II" little-endian, "MM" or any other equal pair big-endian, unequal
+//     bytes big-endian too; u16 at 2 must be 42, else no entries; IFD0 at the u32 at 4;
+//   - every IFD0 entry is parsed, and the tags exif.cpp knows read their values: an offset past
+//     the data (getU16 / getU32 bounds, getString's size check) aborts the whole parse, so a
+//     broken MAKE string after a good Orientation still leaves the image unrotated; the first
+//     entry of a tag wins (std::map insert); Orientation = the u16 at entry + 8.
+// 32-bit offset arithmetic wraps as exif.cpp's uint32_t does.
+struct CvExifReader {
+  const uint8_t* d;
+  size_t n;
+  bool intel = false, bad = false;
+  uint32_t u16(size_t o) {
+    if (o + 1 >= n) {
+      bad = true;
+      return 0;
+    }
+    return intel ? (uint32_t)d[o] | (uint32_t)d[o + 1] << 8 : (uint32_t)d[o] << 8 | d[o + 1];
+  }
+  uint32_t u32(size_t o) {
+    if (o + 3 >= n) {
+      bad = true;
+      return 0;
+    }
+    return intel ? (uint32_t)d[o] | (uint32_t)d[o + 1] << 8 | (uint32_t)d[o + 2] << 16 |
+                       (uint32_t)d[o + 3] << 24
+                 : (uint32_t)d[o] << 24 | (uint32_t)d[o + 1] << 16 | (uint32_t)d[o + 2] << 8 |
+                       d[o + 3];
+  }
+  void rationals(size_t entry, int count) {  // getResolution / WhitePoint / ... / RefBW
+    uint32_t r = u32(entry + 8);
+    for (int k = 0; k < count && !bad; ++k, r += 8) {
+      (void)u32(r);
+      (void)u32((uint32_t)(r + 4));
+    }
+  }
+  void string(size_t entry) {  // getString: the size check only
+    const uint32_t size = u32(entry + 4);
+    uint32_t off = 8;
+    if (!bad && size > 4) off = u32(entry + 8);
+    if (!bad && (off > n || (uint32_t)(off + size) > n)) bad = true;
+  }
+};
+
+// the orientation (1..8 acts, anything else is left as decoded) OpenCV 3.4.2 applies to file p
+static int jpg_exif_orientation(const uint8_t* p, size_t n) {
+  size_t i = 0;
+  std::vector<uint8_t> data;
+  bool found = false;
+  while (!found) {
+    if (i + 2 > n) break;  // (a short read ends the search)
+    const uint8_t m = p[i + 1];
+    i += 2;
+    auto field = [&]() -> size_t {  // getFieldSize: 0 on a short read
+      if (i + 2 > n) {
+        i = n;
+        return 0;
+      }
+      const size_t v = (size_t)p[i] << 8 | p[i + 1];
+      i += 2;
+      return v;
+    };
+    if (m == 0xC0 || m == 0xC2 || m == 0xC4 || m == 0xDB || m == 0xDD || m == 0xDA ||
+        (m >= 0xD0 && m <= 0xD7) || m == 0xE0 || (m >= 0xE2 && m <= 0xEF) || m == 0xFE) {
+      const size_t skip = field();
+      if (skip < 2) return 1;
+      i += skip - 2;
+    } else if (m == 0xD8 || m == 0xD9) {
+    } else if (m == 0xE1) {
+      const size_t len = field();
+      if (len <= 6) return 1;
+      data.assign(len - 6, 0);
+      i += 6;
+      if (i < n) memcpy(data.data(), p + i, std::min(len - 6, n - i));
+      found = true;
+    } else {
+      break;
+    }
+  }
+  if (!found) return 1;
+  CvExifReader R{data.data(), data.size()};
+  // getFormat: unequal first bytes -> NONE (read big-endian), 'I' Intel, 'M' or other -> big-endian
+  R.intel = !(data.size() > 1 && data[0] != data[1]) && data[0] == 'I';
+  if (R.u16(2) != 0x2A || R.bad) return 1;  // checkTagMark (a short block throws)
+  uint32_t off = R.u32(4);
+  const uint32_t nent = R.u16(off);
+  if (R.bad) return 1;
+  off += 2;
+  int orient = -1;
+  for (uint32_t e = 0; e < nent; ++e, off += 12) {
+    const uint32_t tag = R.u16(off);
+    switch (tag) {
+      case 0x010E: case 0x010F: case 0x0110: case 0x0131: case 0x0132: case 0x8298:
+        R.string(off);
+        break;  // description, make, model, software, date-time, copyright
+      case 0x0112: {
+        const uint32_t v = R.u16((size_t)off + 8);
+        if (orient < 0) orient = (int)v;
+        break;
+      }
+      case 0x011A: case 0x011B: R.rationals(off, 1); break;  // x / y resolution
+      case 0x0128: case 0x0213: (void)R.u16((size_t)off + 8); break;
+      case 0x013E: R.rationals(off, 2); break;   // white point
+      case 0x013F: R.rationals(off, 6); break;   // primary chromaticities
+      case 0x0211: R.rationals(off, 3); break;   // YCbCr coefficients
+      case 0x0214: R.rationals(off, 6); break;   // reference black / white
+      default: break;                            // EXIF_OFFSET and unknown tags: no value read
+    }
+    if (R.bad) return 1;
+  }
+  return orient >= 1 && orient <= 8 ? orient : 1;
 }
 
 // the end of a scan-path file (EOI or end of data): at least one scan.  libjpeg block-smooths a
@@ -570,7 +693,9 @@ struct JpegLdsScan {
   uint8_t huffval[8][256];
 };
 
-// entry i of mca (see JpegLds) from a table's maxcode[18]
+// entry i of mca (see JpegLds) from a table's maxcode[18]: the codes longer than the fast table,
+// lengths 10 .. 16, so the table must be exactly 9 bits
+static_assert(JPG_LUTB == 9, "jpg_mca and jpg_decode's compare-count assume 9-bit fast tables");
 __device__ __forceinline__ int32_t jpg_mca(const int32_t* __restrict__ maxcode, int i) {
   int32_t m = -1;
   for (int l = 10; l <= 10 + i && l <= 16; ++l)
@@ -699,13 +824,19 @@ constexpr int JRING_W = JRG * 4 + 4;   // ring words per lane (one pad group: la
 //         and one that starts exactly at the end, never past the image's last block
 //   MASK  (a restart interval, whose data the next one's follows) bits from end_bit on read as 0;
 //         stop at dc_limit DC symbols or at an MCU that starts past end_bit
-template <bool WRITE, bool MASK = false>
+//   CLAMP (any other piece of a restart interval: the sync passes, the write pass's inner pieces)
+//         bits from zero_bit (the interval's end) on read as 0, the stop rule unchanged: a symbol
+//         that starts in the piece and runs past the interval's data reads libjpeg's zero fill,
+//         not the next interval's bits
+template <bool WRITE, bool MASK = false, bool CLAMP = false>
 __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T, rsrc_t rs,
                                             uint32_t* __restrict__ ring, uint64_t st,
                                             uint32_t end_bit, ChunkOut* cnt, int32_t blk,
                                             int (&pred)[3], int16_t* __restrict__ coef,
                                             uint32_t dc_limit = 0xFFFFFFFFu, bool tail = false,
-                                            int badlen = 17, uint32_t* badseen = nullptr) {
+                                            int badlen = 17, uint32_t* badseen = nullptr,
+                                            uint32_t zero_bit = 0xFFFFFFFFu) {
+  static_assert(!(MASK && CLAMP), "MASK already zeroes the bits past end_bit");
   uint32_t ndc = 0;
   bool bad_real = false;  // WRITE: a bad code inside the image's blocks
   uint32_t pos = (uint32_t)st, ph = (uint32_t)(st >> 32) & 0xFF, z = (uint32_t)(st >> 40) & 0xFF;
@@ -725,11 +856,11 @@ __device__ __forceinline__ uint64_t jpg_run(const JpgConst& K, const JpegLds& T,
   v4u pend = __builtin_amdgcn_raw_buffer_load_b128(rs, ((wi >> 2) + JRG) * 16u, 0, 0);
   uint64_t acc = 0;
   int nb = 0;
-  // word wix of the stream (MASK: its bits from end_bit on cleared)
+  // word wix of the stream (MASK: its bits from end_bit on cleared; CLAMP: from zero_bit on)
   auto fetch = [&](uint32_t wix) -> uint32_t {
     const uint32_t v = ring[wix & (4 * JRG - 1)];
-    if (!MASK) return v;
-    const int64_t r = (int64_t)end_bit - 32 * (int64_t)wix;
+    if (!MASK && !CLAMP) return v;
+    const int64_t r = (int64_t)(MASK ? end_bit : zero_bit) - 32 * (int64_t)wix;
     return r >= 32 ? v : r <= 0 ? 0u : v & ~(0xFFFFFFFFu >> (uint32_t)r);
   };
   uint32_t nxt = fetch(wi);
@@ -984,7 +1115,8 @@ __global__ __launch_bounds__(256) void jpeg_unstuff_final(const DESC* __restrict
                                                           const uint2* __restrict__ mk,
                                                           uint32_t* __restrict__ ivstart,
                                                           uint32_t* __restrict__ ivend,
-                                                          uint32_t* __restrict__ ublen) {
+                                                          uint32_t* __restrict__ ublen,
+                                                          uint32_t* __restrict__ overflow) {
   const DESC& D = imgs[blockIdx.x];
   __shared__ uint32_t len_s, nmk_s, bad_s;
   if (threadIdx.x < 64) {
@@ -1003,6 +1135,9 @@ __global__ __launch_bounds__(256) void jpeg_unstuff_final(const DESC* __restrict
       len_s = a;
       nmk_s = min(r, D.mk_cap);
       bad_s = 0;
+      // more markers than the table holds (nintervals + JPG_MK_EXTRA: a damaged file full of
+      // stray markers): the dropped ones would resynchronise differently -- the host reports it
+      if (r > D.mk_cap) *overflow = 1u;
     }
   }
   __syncthreads();
@@ -1238,9 +1373,14 @@ __global__ __launch_bounds__(64) void jpeg_sync_kernel(const JpegDev* __restrict
     ckc[j] = co;
     const uint32_t sub_end = min(b0 + (j + 1) * JPG_SUB, b1);
     // a state past the sub-chunk (the predecessor ran over it) ends where it starts
-    if ((uint32_t)e < sub_end)
-      e = jpg_run<false>(K, T, rs, ring + threadIdx.x * JRING_W, e, sub_end, &co, 0, pred, nullptr,
-                         0xFFFFFFFFu, false, badlen);
+    if ((uint32_t)e < sub_end) {
+      if (D.restart)  // (uniform per workgroup) the interval's end reads as zero bits
+        e = jpg_run<false, false, true>(K, T, rs, ring + threadIdx.x * JRING_W, e, sub_end, &co, 0,
+                                        pred, nullptr, 0xFFFFFFFFu, false, badlen, nullptr, cp.end);
+      else
+        e = jpg_run<false>(K, T, rs, ring + threadIdx.x * JRING_W, e, sub_end, &co, 0, pred,
+                           nullptr, 0xFFFFFFFFu, false, badlen);
+    }
   }
   next[D.ch_off + t] = e;
   cnt[D.ch_off + t] = co;
@@ -1384,8 +1524,8 @@ __global__ __launch_bounds__(64) void jpeg_write_kernel(const JpegDev* __restric
   const uint32_t bhi = min((cp.k + 1) * R, mcus) * (uint32_t)D.bpm;
   K.total_blocks = bhi;
   if (!tail) {
-    jpg_run<true>(K, T, rs, myring, st, b1, &dummy, blk, pred, coef, 0xFFFFFFFFu, false, badlen,
-                  badseen);
+    jpg_run<true, false, true>(K, T, rs, myring, st, b1, &dummy, blk, pred, coef, 0xFFFFFFFFu,
+                               false, badlen, badseen, cp.end);
     return;
   }
   // the interval's end: its MCUs to the last one, the bits past its data 0, an MCU decoded only if
@@ -2361,22 +2501,49 @@ __device__ __forceinline__ void jpg_color8(const JpegDev& D, const uint8_t* __re
     o[j] = px[4 * j] | px[4 * j + 1] << 8 | px[4 * j + 2] << 16 | px[4 * j + 3] << 24;
 }
 
-// grid (tiles of 256 x 8 pixels, n)
+// grid (tiles of 256 x 8 decoded pixels, n); (h, w) is the batch's output size, which is the
+// decoded size turned by each image's EXIF orientation (D.orient, OpenCV 3.4.2 loadsave.cpp
+// ApplyExifOrientation: 2 flip(1), 3 flip(-1), 4 flip(0), 5 transpose, 6 transpose + flip(1),
+// 7 transpose + flip(-1), 8 transpose + flip(0)).  Decoded pixel (y, x) of an H x W image goes to
+// the output position below; orientation 1 keeps the coalesced 24-byte row stores
 __global__ __launch_bounds__(256) void jpeg_color8_kernel(const JpegDev* __restrict__ imgs,
                                                           const uint8_t* __restrict__ planes,
                                                           uint8_t* __restrict__ dst, int h, int w,
                                                           int64_t row_stride) {
   const JpegDev& D = imgs[blockIdx.y];
-  const int ow = (w + 7) / 8;
+  const int H = D.height, W = D.width;  // as decoded
+  const int ow = (W + 7) / 8;
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= (int64_t)h * ow) return;
+  if (q >= (int64_t)H * ow) return;
   const int y = (int)(q / ow), x0 = 8 * (int)(q - (int64_t)y * ow);
   uint32_t o[6];
   if (D.ncomp == 1) jpg_color8<1, 1, true>(D, planes, x0, y, o);
   else if (D.up == 0) jpg_color8<1, 1, false>(D, planes, x0, y, o);
   else if (D.up == 1) jpg_color8<2, 1, false>(D, planes, x0, y, o);
   else jpg_color8<2, 2, false>(D, planes, x0, y, o);
-  uint8_t* p = dst + (int64_t)blockIdx.y * h * row_stride + (int64_t)y * row_stride + (int64_t)x0 * 3;
+  uint8_t* const img = dst + (int64_t)blockIdx.y * h * row_stride;
+  if (D.orient > 1) {
+    const int t = D.orient;
+    for (int k = 0; k < 8 && x0 + k < W; ++k) {
+      const int x = x0 + k;
+      int oy, ox;
+      if (t <= 4) {
+        oy = (t == 3 || t == 4) ? H - 1 - y : y;
+        ox = (t == 2 || t == 3) ? W - 1 - x : x;
+      } else {  // transposed: (x, y), then the flip of the W x H result
+        oy = (t == 7 || t == 8) ? W - 1 - x : x;
+        ox = (t == 6 || t == 7) ? H - 1 - y : y;
+      }
+      uint8_t* p = img + (int64_t)oy * row_stride + (int64_t)ox * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int b = 3 * k + c;
+        p[c] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+    return;
+  }
+  uint8_t* p = img + (int64_t)y * row_stride + (int64_t)x0 * 3;
   if (x0 + 8 <= w && ((uintptr_t)p & 7) == 0) {
     uint2* p2 = reinterpret_cast<uint2*>(p);
     p2[0] = make_uint2(o[0], o[1]);
@@ -2444,8 +2611,9 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int h, int w,
                      int flags, JpegPlan& P, std::string* err, bool tables = true) {
   const bool turbo = (flags & IDN_JPEG_TURBO) != 0;
+  const bool orient = (flags & IDN_JPEG_IGNORE_ORIENTATION) == 0;
   const uint32_t chunk_req = (uint32_t)(flags >> 8) & 0xFFFFu;
-  if ((flags & ~(IDN_JPEG_TURBO | (0xFFFF << 8))) != 0 ||
+  if ((flags & ~(IDN_JPEG_TURBO | IDN_JPEG_IGNORE_ORIENTATION | (0xFFFF << 8))) != 0 ||
       (chunk_req != 0 && (chunk_req < 512 || chunk_req % 64 != 0))) {
     if (err) *err = "bad flags";
     return IDN_EINVAL;
@@ -2459,12 +2627,15 @@ static int jpeg_plan(const uint8_t* const* files, const size_t* lens, int n, int
     if (!files[i]) return jpg_fail(err, "null file pointer");
     int rc = jpeg_parse(files[i], lens[i], J, err);
     if (rc != IDN_OK) return rc;
-    if ((h > 0 && J.height != h) || (w > 0 && J.width != w)) {
+    const int ori = orient ? jpg_exif_orientation(files[i], lens[i]) : 1;
+    const bool tr = ori >= 5;  // the output is the transposed size
+    if ((h > 0 && (tr ? J.width : J.height) != h) || (w > 0 && (tr ? J.height : J.width) != w)) {
       if (err) *err = "image size differs from the batch size";
       return IDN_EINVAL;
     }
     JpegDev& D = P.dev[i];
     memset(&D, 0, sizeof(D));
+    D.orient = ori;
     D.width = J.width;
     D.height = J.height;
     D.ncomp = J.ncomp;
@@ -2715,9 +2886,16 @@ extern "C" int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* 
   std::string err;
   const int rc = jpeg_parse(file, len, J, &err);
   if (rc != IDN_OK) return set_error(rc, "idn_jpeg_info: %s", err.c_str());
-  *height = J.height;
-  *width = J.width;
+  const bool tr = jpg_exif_orientation(file, len) >= 5;  // cv2.imread's shape: after the turn
+  *height = tr ? J.width : J.height;
+  *width = tr ? J.height : J.width;
   *components = J.ncomp;
+  return IDN_OK;
+}
+
+extern "C" int idn_jpeg_orientation(const uint8_t* file, size_t len, int* orientation) {
+  IDN_CHECK_ARG(file && orientation, "idn_jpeg_orientation: null pointer");
+  *orientation = jpg_exif_orientation(file, len);
   return IDN_OK;
 }
 
@@ -2825,6 +3003,9 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   uint2* tcnt = reinterpret_cast<uint2*>(ws + P.off_tcnt);
   uint32_t* ck_iv = reinterpret_cast<uint32_t*>(ws + P.off_ck_iv);
   uint32_t* iv_ck = reinterpret_cast<uint32_t*>(ws + P.off_iv_ck);
+  uint32_t* mk_over = flag + 33;  // marker table overflow (jpeg_unstuff_final)
+  if (hipMemsetAsync(mk_over, 0, 4, st) != hipSuccess)
+    return set_error(IDN_EHIP, "idn_jpeg_decode_u8: memset failed");
   {
     const dim3 g((unsigned)P.mt_img, (unsigned)n);
     hipLaunchKernelGGL(jpeg_unstuff_count<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
@@ -2832,7 +3013,7 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     hipLaunchKernelGGL(jpeg_unstuff_write<JpegDev>, g, dim3(1024), 0, st, dimg, ws + P.off_scan,
                        tcnt, P.mt_img, ub, mk);
     hipLaunchKernelGGL(jpeg_unstuff_final<JpegDev>, dim3(n), dim3(256), 0, st, dimg, tcnt,
-                       P.mt_img, ub, mk, ivs, ive, ublen);
+                       P.mt_img, ub, mk, ivs, ive, ublen, mk_over);
   }
   if (P.any_restart)
     hipLaunchKernelGGL(jpeg_chunk_map_kernel, dim3(n), dim3(256), 0, st, dimg, ivs, ive, iv_ck,
@@ -2847,7 +3028,8 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
     hipLaunchKernelGGL(jpeg_unstuff_write<JpegScanDev>, g, dim3(1024), 0, st, dscan,
                        ws + P.off_scan, tcnt, P.mt_scan, ub, mk);
     hipLaunchKernelGGL(jpeg_unstuff_final<JpegScanDev>, dim3(ns), dim3(256), 0, st, dscan, tcnt,
-                       P.mt_scan, ub, mk, ivs, ive, reinterpret_cast<uint32_t*>(ws + P.off_ublen_s));
+                       P.mt_scan, ub, mk, ivs, ive, reinterpret_cast<uint32_t*>(ws + P.off_ublen_s),
+                       mk_over);
   }
   const dim3 gitems((P.max_items + 63) / 64, n);
   uint32_t* badseen = flag + 32;  // (past the sync passes' flags)
@@ -2913,7 +3095,9 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
       hipLaunchKernelGGL((jpeg_idct_kernel<2, 2>), dim3((unsigned)gb), dim3(256), 0, st, dimg, bend,
                          n, P.nblk, coef, ws + P.off_planes);
     {
-      const int64_t gx = ((int64_t)h * ((w + 7) / 8) + 255) / 256;
+      // decoded 8-pixel groups per image: h x ceil(w / 8), or w x ceil(h / 8) for a transposed one
+      const int64_t groups = std::max((int64_t)h * ((w + 7) / 8), (int64_t)w * ((h + 7) / 8));
+      const int64_t gx = (groups + 255) / 256;
       hipLaunchKernelGGL(jpeg_color8_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, dimg,
                          ws + P.off_planes, dst, h, w, row_stride);
     }
@@ -2921,13 +3105,16 @@ extern "C" int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* len
   };
   int drc = decode(P.any_chunked ? 16 : 17);
   if (drc != IDN_OK) return drc;
-  if (P.any_chunked) {  // a bad code on a true trajectory: decode again with libjpeg's rule
-    uint32_t bad = 0;
-    if (hipMemcpyAsync(&bad, badseen, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return set_error(IDN_EHIP, "idn_jpeg_decode_u8: decode failed");
-    if (bad && (drc = decode(17)) != IDN_OK) return drc;
-  }
+  uint32_t bad_over[2] = {0u, 0u};  // badseen, mk_over (adjacent words)
+  if (hipMemcpyAsync(bad_over, badseen, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return set_error(IDN_EHIP, "idn_jpeg_decode_u8: decode failed");
+  if (bad_over[1])
+    return set_error(IDN_EUNSUPPORTED, "idn_jpeg_decode_u8: more markers in an entropy-coded "
+                                       "segment than restart intervals + %u (damaged file)",
+                     JPG_MK_EXTRA);
+  // a bad code on a true trajectory: decode again with libjpeg's rule
+  if (P.any_chunked && bad_over[0] && (drc = decode(17)) != IDN_OK) return drc;
   // the staging buffer is reused by the next call: finish here
   if (hipStreamSynchronize(st) != hipSuccess)
     return set_error(IDN_EHIP, "idn_jpeg_decode_u8: decode failed");

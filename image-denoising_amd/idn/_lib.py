@@ -15,7 +15,7 @@ import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libidn_hip.so"
-ABI_VERSION = 5  # IDN_ABI_VERSION of include/idn.h that SIGNATURES binds
+ABI_VERSION = 6  # IDN_ABI_VERSION of include/idn.h that SIGNATURES binds
 VARIANTS = {"tuning": Path(__file__).resolve().parent / "libidn_hip_tuning.so"}
 
 _c_u8p = ctypes.c_void_p
@@ -41,6 +41,7 @@ SIGNATURES = {
     "idn_noise_workspace_size": (_c_size, [_c_int, _c_int]),
     "idn_poisson_levels": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "idn_jpeg_info": (_c_int, [_c_vp, _c_size, _c_vp, _c_vp, _c_vp]),
+    "idn_jpeg_orientation": (_c_int, [_c_vp, _c_size, _c_vp]),
     "idn_jpeg_workspace_size": (_c_size, [_c_vp, _c_vp, _c_int, _c_int]),
     "idn_jpeg_decode_u8": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_int, _c_i64, _c_int,
                                     _c_vp, _c_size, _c_vp]),

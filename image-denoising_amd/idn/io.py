@@ -10,7 +10,11 @@ does not take raises IdnError.  Other (lossless) formats go through PIL, flipped
 `imread_gpu` is the GPU decode front-end: JPEG files are decoded on the
 device (idn_jpeg_decode_u8), bit-exact with the reference's pinned IJG libjpeg 9d by default or
 with libjpeg-turbo (mode="turbo"), images of one size in one launch; files the decoder does not
-take raise IdnError (no CPU fallback inside the product).
+take raise IdnError (no CPU fallback inside the product).  Like OpenCV 3.4.2's imread, each JPEG
+is turned by its EXIF orientation (APP1 IFD0 tag 0x0112: flips / transposes; idn_jpeg_orientation)
+unless orientation=False (IMREAD_IGNORE_ORIENTATION).  PNG and the other lossless formats never
+carry it in the form OpenCV 3.4.2's EXIF reader walks (it reads JPEG markers), so `_imread_pil`
+leaves them as stored.
 """
 from __future__ import annotations
 
@@ -52,9 +56,10 @@ def _imread_pil(path) -> np.ndarray:
     return np.ascontiguousarray(rgb[..., ::-1])
 
 
-def imread_gpu(paths, mode: str = "libjpeg9"):
+def imread_gpu(paths, mode: str = "libjpeg9", orientation: bool = True):
     """cv2.imread for a list of JPEG paths, decoded on the GPU: a list of (h, w, 3) uint8 BGR
-    device tensors in input order; same-size files share one decode launch."""
+    device tensors in input order, each turned by its EXIF orientation (orientation=False:
+    IMREAD_IGNORE_ORIENTATION); files of the same output size share one decode launch."""
     from . import ops
     datas = []
     for p in paths:
@@ -62,10 +67,10 @@ def imread_gpu(paths, mode: str = "libjpeg9"):
             datas.append(f.read())
     groups = {}
     for i, d in enumerate(datas):
-        groups.setdefault(ops.jpeg_info(d)[:2], []).append(i)
+        groups.setdefault(ops.jpeg_info(d, orientation)[:2], []).append(i)
     out = [None] * len(datas)
     for idx in groups.values():
-        dec = ops.jpeg_decode([datas[i] for i in idx], mode=mode)
+        dec = ops.jpeg_decode([datas[i] for i in idx], mode=mode, orientation=orientation)
         for k, i in enumerate(idx):
             out[i] = dec[k]
     return out

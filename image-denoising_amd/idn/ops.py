@@ -764,35 +764,53 @@ def _file_ptrs(files):
     return bufs, ptrs, lens
 
 
-def jpeg_info(data: bytes) -> Tuple[int, int, int]:
-    """(height, width, components) of a JPEG held in memory; IdnError if the decoder does not
-    take it (progressive, arithmetic, CMYK, ...)."""
+def jpeg_orientation(data: bytes) -> int:
+    """The EXIF orientation (1..8, 1 = none) cv2.imread (OpenCV 3.4.2) applies to this JPEG after
+    decoding (include/idn.h idn_jpeg_orientation)."""
+    lib = _lib.load()
+    o = ctypes.c_int()
+    buf = bytes(data)
+    _lib.check(lib.idn_jpeg_orientation(ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p),
+                                        len(buf), ctypes.byref(o)), "idn_jpeg_orientation")
+    return o.value
+
+
+def jpeg_info(data: bytes, orientation: bool = True) -> Tuple[int, int, int]:
+    """(height, width, components) of a JPEG held in memory, as cv2.imread returns it (the size
+    after its EXIF orientation; orientation=False: the decoded size); IdnError if the decoder
+    does not take it (lossless, hierarchical, 12-bit, ...)."""
     lib = _lib.load()
     h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     buf = bytes(data)
     _lib.check(lib.idn_jpeg_info(ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p), len(buf),
                                  ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)),
                "idn_jpeg_info")
+    if not orientation and jpeg_orientation(buf) >= 5:  # back to the decoded (untransposed) size
+        return w.value, h.value, c.value
     return h.value, w.value, c.value
 
 
 JPEG_MODES = {"libjpeg9": 0, "turbo": 1}  # include/idn.h IDN_JPEG_TURBO
+JPEG_IGNORE_ORIENTATION = 2  # include/idn.h IDN_JPEG_IGNORE_ORIENTATION
 
 
 def jpeg_decode(files, out: Optional[torch.Tensor] = None, device=None, mode: str = "libjpeg9",
-                chunk_bits: int = 0) -> torch.Tensor:
-    """cv2.imread(path) for a batch of same-size baseline JPEG files (bytes in host memory):
+                chunk_bits: int = 0, orientation: bool = True) -> torch.Tensor:
+    """cv2.imread(path) for a batch of same-size JPEG files (bytes in host memory):
     (n, h, w, 3) uint8 BGR on the GPU.  mode "libjpeg9" (default) is bit-exact with the
     reference's pinned IJG libjpeg 9d (requirements.txt:74, under OpenCV 3.4.2: scaled 16x16 /
-    16x8 chroma IDCT); "turbo" with libjpeg-turbo (fancy upsampling).  chunk_bits (0 = default)
-    sets the entropy decoder's chunk size; it does not change the output."""
+    16x8 chroma IDCT); "turbo" with libjpeg-turbo (fancy upsampling).  Each image is turned by its
+    EXIF orientation as OpenCV 3.4.2's imread does (orientation=False: cv2's
+    IMREAD_IGNORE_ORIENTATION); (h, w) is the size after the turn and must agree across the
+    batch.  chunk_bits (0 = default) sets the entropy decoder's chunk size; it does not change
+    the output."""
     files = list(files)
     if not files:
         raise ValueError("jpeg_decode: no files")
     if mode not in JPEG_MODES:
         raise ValueError(f"jpeg_decode: mode must be one of {sorted(JPEG_MODES)}")
-    flags = JPEG_MODES[mode] | (int(chunk_bits) << 8)
-    h, w, _ = jpeg_info(files[0])
+    flags = JPEG_MODES[mode] | (int(chunk_bits) << 8) | (0 if orientation else JPEG_IGNORE_ORIENTATION)
+    h, w, _ = jpeg_info(files[0], orientation)
     n = len(files)
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     if out is None:

@@ -77,8 +77,11 @@ typedef enum idn_wavelet {
  *      (IDN_JPEG_TURBO); the default decode became IJG libjpeg 9d's; idn_noise_filter_u8
  *      (the fused noise -> 3x3 / 5x5 filter) was removed: compose idn_noise_u8 and the filter
  *   4  idn_abi_version added (no signature changed)
- *   5  idn_noise_ycc_u8 and idn_wavelet_denoise_ycc added (no signature changed) */
-#define IDN_ABI_VERSION 5
+ *   5  idn_noise_ycc_u8 and idn_wavelet_denoise_ycc added (no signature changed)
+ *   6  cv2.imread's EXIF orientation: idn_jpeg_decode_u8 turns each image by it (flag
+ *      IDN_JPEG_IGNORE_ORIENTATION keeps the decoded layout), idn_jpeg_info reports the turned
+ *      size, idn_jpeg_orientation added */
+#define IDN_ABI_VERSION 6
 int idn_abi_version(void);
 const char* idn_version(void);
 const char* idn_last_error(void);
@@ -338,8 +341,21 @@ int idn_resize_linear_f32(const float* src, float* dst, int n, int h, int w, int
  * libjpeg decides it (component IDs, JFIF / Adobe markers); four are CMYK or YCCK (Adobe's
  * transform; K sampled as the first component), decoded to libjpeg's CMYK and converted to BGR
  * as OpenCV does (icvCvt_CMYK2BGR_8u_C4C3R).  IDN_EUNSUPPORTED for anything else (lossless,
- * hierarchical, 12-bit, big-gamut colour, DHP / EXP / JPGn / LSE markers, other sampling). */
+ * hierarchical, 12-bit, big-gamut colour, DHP / EXP / JPGn / LSE markers, other sampling).
+ * height x width is the size cv2.imread returns: after the file's EXIF orientation
+ * (idn_jpeg_orientation), so orientations 5..8 report the decoded size transposed. */
 int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int* components);
+
+/* The EXIF orientation (1..8; 1 = none) OpenCV 3.4.2's imread applies to this file after decoding
+ * (loadsave.cpp ApplyExifOrientation, unless IMREAD_IGNORE_ORIENTATION): exif.cpp's ExifReader
+ * reads Orientation (0x0112) from IFD0 of the FIRST APP1 segment (little- or big-endian TIFF);
+ * a marker its walk does not know, or a malformed IFD0 (any offset past the data, a bad tag
+ * value among the tags it parses), means 1, as does a value outside 1..8.  The decode applies
+ * it: 2 flip(1), 3 flip(-1), 4 flip(0), 5 transpose, 6 transpose + flip(1), 7 transpose +
+ * flip(-1), 8 transpose + flip(0) (cv::flip codes).  Restated from OpenCV's published source
+ * (parity vs cv2 unpinned: cv2 is not importable where this was built; the decoded pixels are
+ * pinned by the real libjpeg 9d, the geometry by Pillow's reading of the tag). */
+int idn_jpeg_orientation(const uint8_t* file, size_t len, int* orientation);
 
 /* idn_jpeg_decode_u8 flags.  Default (0): the decode of the reference's pinned libjpeg 9d
  * (requirements.txt:74, linked by its OpenCV 3.4.2): 8x8 ISLOW IDCT for full-size components,
@@ -352,6 +368,8 @@ int idn_jpeg_info(const uint8_t* file, size_t len, int* height, int* width, int*
  * else a multiple of 64, >= 512; does not
  * change the output). */
 #define IDN_JPEG_TURBO 1
+/* cv2.IMREAD_IGNORE_ORIENTATION: store every image as decoded (h x w is then the decoded size) */
+#define IDN_JPEG_IGNORE_ORIENTATION 2
 /* device workspace for decoding these files with these flags (0 if any is unsupported) */
 size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, int n, int flags);
 /* cv2.imread(path) (IMREAD_COLOR) of n JPEG files held in host memory (any mix of the kinds
@@ -363,6 +381,13 @@ size_t idn_jpeg_workspace_size(const uint8_t* const* files, const size_t* lens, 
  * EOI appended, or none), bit errors, bad Huffman codes, lost / renumbered restart markers and
  * stray markers -- the data runs out, the rest of its restart interval stays gray, restart
  * markers resynchronise as jdmarker.c's jpeg_resync_to_restart does.
+ * Each image is turned by its EXIF orientation (idn_jpeg_orientation) unless the flags say
+ * IDN_JPEG_IGNORE_ORIENTATION; h x w is the size after that turn.
+ * Speed: baseline / extended sequential files (the reference's VOC images) take the parallel
+ * self-synchronising entropy decoder.  Progressive and arithmetic-coded files take the scan path,
+ * which is serial within a restart interval (one lane per interval): a 600 x 1000 progressive
+ * file without restart markers decodes SLOWER than one host core running libjpeg (see DESIGN.md,
+ * JPEG section, for the measured figures); batch them to fill the GPU.
  * The entropy-coded segments are copied to the workspace in one transfer; synchronous on
  * `stream`. */
 int idn_jpeg_decode_u8(const uint8_t* const* files, const size_t* lens, int n, uint8_t* dst,

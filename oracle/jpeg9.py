@@ -859,8 +859,20 @@ def _fancy_h2v2(p, dw, dh):
     return out
 
 
-def imread(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
-    """cv2.imread(..., IMREAD_COLOR) of a baseline JPEG: (H, W, 3) uint8 BGR"""
+def imread(data: bytes, mode: str = "libjpeg9", orientation: bool = True) -> np.ndarray:
+    """cv2.imread(..., IMREAD_COLOR) of a JPEG: (H, W, 3) uint8 BGR, turned by the file's EXIF
+    orientation as OpenCV 3.4.2 does (oracle/exif.py; orientation=False:
+    IMREAD_IGNORE_ORIENTATION)"""
+    img = decode(data, mode)
+    if orientation:
+        from . import exif
+        img = exif.apply(img, exif.orientation(data))
+    return img
+
+
+def decode(data: bytes, mode: str = "libjpeg9") -> np.ndarray:
+    """the library's decode of a JPEG as OpenCV receives it (before the EXIF step): (H, W, 3)
+    uint8 BGR"""
     d = parse_and_decode(data)
     W, H, hmax, vmax = d["width"], d["height"], d["hmax"], d["vmax"]
     if d["smooth"] is not None:

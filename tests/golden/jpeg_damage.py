@@ -16,6 +16,10 @@ A recipe is (file name, op, argument):
   junk   f      the data byte at fraction f replaced by the marker FF 08 (below SOF0: libjpeg ends
                 the segment there and resynchronises at the next restart marker)
   rstnum k, d   the k-th RST marker's number moved by d (libjpeg's jpeg_resync_to_restart)
+  shortiv k, r  the data of the restart interval that the k-th RST marker ends cut to its first
+                m bytes (m the largest <= 60 % of them whose unstuffed length is r mod 32, r in
+                1..3): the interval's data run out mid-MCU a few bits past a 256-bit boundary of
+                the decoder's sub-chunks, so symbols that start before it read libjpeg's zero fill
 """
 
 
@@ -103,6 +107,23 @@ def damage(d: bytes, op: str, arg) -> bytes:
         x = bytearray(d)
         x[off + 1] = 0xD0 + ((x[off + 1] - 0xD0 + dd) & 7)
         return bytes(x)
+    if op == "shortiv":
+        k, r = arg
+        rst = [o for o, m in _markers(d) if 0xD0 <= m <= 0xD7]
+        end = rst[k]
+        begin = rst[k - 1] + 2 if k > 0 else next(b for b, e in _spans(d) if b <= end < e)
+        body = d[begin:end]
+        best, n_un = None, 0
+        for m in range(1, len(body)):
+            # unstuffed length of body[:m] (a stuffed FF00 is one data byte); never cut inside a pair
+            n_un += 0 if body[m - 1] == 0x00 and m >= 2 and body[m - 2] == 0xFF else 1
+            if m > 0.6 * len(body):
+                break
+            if body[m - 1] != 0xFF and n_un % 32 == r:
+                best = m
+        if best is None:
+            raise ValueError("interval too short")
+        return d[:begin + best] + d[end:]
     raise ValueError(op)
 
 
@@ -129,6 +150,7 @@ def cases():
     for f in _RST_FILES:
         out += [(f, "cutrst", (3, 0)), (f, "cutrst", (3, 2)), (f, "junk", 0.45),
                 (f, "rstnum", (2, 3)), (f, "rstnum", (2, 1)), (f, "rstnum", (2, -1))]
+        out += [(f, "shortiv", (2, r)) for r in (1, 2, 3)]
     return out
 
 

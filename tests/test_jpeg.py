@@ -363,7 +363,7 @@ def test_damaged_fixture_set_is_complete():
     assert meta["libjpeg"].startswith("9")
     assert sorted(meta["cases"]) == sorted(jd.key(c) for c in jd.cases())
     ops = {c[1] for c in jd.cases()}
-    assert ops == {"cut", "cutrst", "flip", "ones", "junk", "rstnum"}
+    assert ops == {"cut", "cutrst", "flip", "ones", "junk", "rstnum", "shortiv"}
     for c in jd.cases():  # every recipe changes the file (a cut at 0.97 may keep all the data)
         data = (JPEG / c[0]).read_bytes()
         assert jd.damage(data, c[1], c[2]) != data or c[1] == "cut", c
@@ -423,3 +423,75 @@ def test_oracle_turbo_mode_matches_system_pil_on_damaged_files(tmp_path):
     for c in cases:
         data = jd.damage((JPEG / c[0]).read_bytes(), c[1], c[2])
         assert np.array_equal(jpeg9.imread(data, mode="turbo"), ref[jd.key(c)]), jd.key(c)
+
+
+# ---- cv2.imread's EXIF orientation (OpenCV 3.4.2 loadsave.cpp ApplyExifOrientation) -------------
+EXIF = GOLD / "jpeg_exif"
+
+
+def _exif_meta():
+    return json.loads((GOLD / "jpeg_exif.json").read_text())["files"]
+
+
+def test_exif_fixture_set():
+    meta = _exif_meta()
+    assert sorted(meta) == sorted(p.name for p in EXIF.glob("*.jpg"))
+    assert {r["orientation"] for r in meta.values()} == set(range(1, 9))
+    # the malformed cases: OpenCV's reader gives up where Pillow's still finds a tag
+    assert sum(r["orientation"] == 1 and r["pil_orientation"] not in (None, 1)
+               for r in meta.values()) >= 6
+
+
+@pytest.mark.parametrize("name", sorted(_exif_meta()) if (GOLD / "jpeg_exif.json").exists() else [])
+def test_exif_orientation_oracle_and_library(name):
+    """oracle/exif.py and the library's idn_jpeg_orientation (host code, no GPU) give the
+    orientation recorded for the fixture; on well-formed Pillow-written blocks that is Pillow's
+    own reading of the tag"""
+    from oracle import exif
+    from idn import ops
+    rec = _exif_meta()[name]
+    data = (EXIF / name).read_bytes()
+    assert exif.orientation(data) == rec["orientation"]
+    assert ops.jpeg_orientation(data) == rec["orientation"]
+    if "_o" in name and not any(k in name for k in ("bad", "trunc", "xmp", "dup", "o0", "o9",
+                                                    "len6", "mark")):
+        assert rec["pil_orientation"] == rec["orientation"]
+    h, w, c = rec["shape"]
+    assert ops.jpeg_info(data)[:2] == (h, w)
+    if rec["orientation"] >= 5:
+        assert ops.jpeg_info(data, orientation=False)[:2] == (w, h)
+
+
+@pytest.mark.parametrize("name", [n for n in sorted(_exif_meta()) if "600x1000" not in n]
+                         if (GOLD / "jpeg_exif.json").exists() else [])
+def test_exif_oracle_imread_matches_libjpeg9_turned_by_pillow(name):
+    """the oracle's imread (libjpeg 9d restatement + the EXIF step) against the real libjpeg 9d
+    decode turned by Pillow's Image.transpose (an independent statement of the eight turns)"""
+    from oracle import jpeg9
+    rec = _exif_meta()[name]
+    got = jpeg9.imread((EXIF / name).read_bytes())
+    assert np.array_equal(got, np.load(GOLD / "jpeg_exif.npz")[name])
+    assert hashlib.sha256(got.tobytes()).hexdigest() == rec["sha256"]
+
+
+def test_exif_orientation_fuzz_library_vs_oracle():
+    """random damage to EXIF blocks (bytes of the TIFF header, IFD counts, offsets, tag types and
+    values; cut APP1 lengths; files cut inside the block): the library's host parser and the
+    oracle agree on every file"""
+    from oracle import exif
+    from idn import ops
+    rs = np.random.RandomState(7)
+    seeds = [(EXIF / n).read_bytes() for n in sorted(_exif_meta()) if "600x1000" not in n]
+    for k in range(1500):
+        data = bytearray(seeds[rs.randint(len(seeds))])
+        k1 = data.find(b"\xff\xe1")
+        if k1 < 0:
+            continue
+        end = k1 + 4 + 64
+        for _ in range(rs.randint(1, 4)):
+            j = rs.randint(k1 + 2, min(end, len(data)))
+            data[j] = rs.randint(256) if rs.rand() < 0.7 else data[j] ^ (1 << rs.randint(8))
+        if rs.rand() < 0.1:
+            data = data[:rs.randint(2, k1 + 60)]
+        data = bytes(data)
+        assert ops.jpeg_orientation(data) == exif.orientation(data), (k, data[:k1 + 80].hex())

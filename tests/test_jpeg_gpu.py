@@ -313,3 +313,68 @@ def test_random_damaged_files_match_the_oracle(dev):
             continue
         got = ops.jpeg_decode([data])[0].cpu().numpy()
         assert np.array_equal(got, ref), (i, p.name)
+
+
+# ---- cv2.imread's EXIF orientation (OpenCV 3.4.2 loadsave.cpp ApplyExifOrientation) -------------
+EXIF = GOLD / "jpeg_exif"
+EXIF_META = json.loads((GOLD / "jpeg_exif.json").read_text())["files"]
+
+
+def check_exif(name, got):
+    rec = EXIF_META[name]
+    assert list(got.shape) == rec["shape"], name
+    z = np.load(GOLD / "jpeg_exif.npz")
+    if rec.get("full"):
+        d = np.abs(got.astype(int) - z[name].astype(int))
+        assert d.max() == 0, (name, d.max(), np.argwhere(d > 0)[:5])
+    else:
+        for k, (y, x) in enumerate(rec["crops"]):
+            assert np.array_equal(got[y:y + 32, x:x + 32], z[f"{name}:crop{k}"]), (name, k)
+    assert hashlib.sha256(np.ascontiguousarray(got).tobytes()).hexdigest() == rec["sha256"], name
+
+
+@pytest.mark.parametrize("name", sorted(EXIF_META))
+def test_exif_orientation_bitexact(dev, name):
+    """each of the eight orientations (baseline 4:2:0, progressive 4:2:2, grayscale, restart rows,
+    600x1000) and the malformed EXIF blocks: the real libjpeg 9d decode turned as OpenCV 3.4.2
+    turns it (tests/golden/make_jpeg_exif.py)"""
+    from idn import ops
+    got = ops.jpeg_decode([(EXIF / name).read_bytes()])[0].cpu().numpy()
+    check_exif(name, got)
+
+
+def test_exif_orientations_in_one_batch_and_ignore_flag(dev):
+    """the transposed orientations 5..8 of one file share a launch with an unturned file of the
+    transposed size; IMREAD_IGNORE_ORIENTATION returns every one as decoded; imread_gpu groups by
+    the turned size"""
+    from idn import io, ops
+    from oracle import jpeg9
+    names = [f"s420_o{o}_37x53.jpg" for o in (5, 6, 7, 8)] + [f"prog_s422_o{o}_45x67.jpg" for o in (6, 8)]
+    datas = [(EXIF / n).read_bytes() for n in names[:4]]
+    got = ops.jpeg_decode(datas).cpu().numpy()
+    for n, g in zip(names, got):
+        check_exif(n, g)
+    plain = ops.jpeg_decode(datas, orientation=False).cpu().numpy()
+    base = jpeg9.decode(datas[0])
+    for g in plain:
+        assert np.array_equal(g, base)
+    paths = [EXIF / n for n in names] + [EXIF / "s420_o1_37x53.jpg", EXIF / "s420_o3_37x53.jpg"]
+    outs = io.imread_gpu(paths)
+    for p, o in zip(paths, outs):
+        check_exif(p.name, o.cpu().numpy())
+    outs = io.imread_gpu(paths, orientation=False)
+    assert [tuple(o.shape) for o in outs[:4]] == [(37, 53, 3)] * 4
+    from idn._lib import IdnError
+    with pytest.raises(IdnError, match="size"):  # 53x37 turned against 37x53 unturned
+        ops.jpeg_decode([datas[0], (EXIF / "s420_o1_37x53.jpg").read_bytes()])
+
+
+def test_exif_turbo_mode_turns_too(dev):
+    """the turn is OpenCV's step after the library's decode: the turbo mode applies it as well"""
+    from idn import ops
+    from oracle import exif
+    for name in ("s420_o6_37x53.jpg", "prog_s422_o7_45x67.jpg", "gray_o3_29x41.jpg"):
+        data = (EXIF / name).read_bytes()
+        got = ops.jpeg_decode([data], mode="turbo")[0].cpu().numpy()
+        ref = exif.apply(pil_bgr(EXIF / name), EXIF_META[name]["orientation"])
+        assert np.array_equal(got, ref), name
