@@ -391,6 +391,60 @@ def load_traffic(op: str):
         return None
 
 
+# VALU issue peak in lane operations per second: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz (a wave64
+# VALU instruction issues over 4 cycles; fp64 FMA runs at the same per-lane rate on gfx950,
+# MI355X_MICROARCH.md), i.e. 39.3 T lane-ops/s -- the binding roofline of the ops whose counters
+# show VALU issue near saturation (VALU utilisation beside the %HBM figure)
+VALU_PEAK = 256 * 4 * 16 * 2.4e9
+
+
+def load_valu(op: str):
+    """VALU lane operations per pixel of the op (all its kernels) from the newest committed
+    rocprofv3 --pmc record profiles/r*/pmc/<op>.json (SQ_INSTS_VALU x 64 / pixels of the launch),
+    or None.  Not measured in this run: the SQ counters need their own --pmc passes."""
+    recs = sorted(ROOT.glob(f"profiles/r*/pmc/{op}.json"))
+    for p in reversed(recs):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        ks = d.get("kernels", {})
+        vpp = [k["valu_per_pixel"] for k in ks.values() if k.get("valu_per_pixel") is not None]
+        if vpp:
+            main = max(ks.items(), key=lambda kv: kv[1].get("avg_us") or 0.0)[0]
+            return {"valu_per_pixel": round(sum(vpp), 2), "kernels": len(vpp),
+                    "longest_kernel": main, "source": str(p.relative_to(ROOT))}
+    return None
+
+
+def roofline_fields(op, bpp, pixels, avg_kern_ms, traffic, kname):
+    """The roofline object: the HBM roofline (algorithmic bytes / the line's kernel time) and,
+    where a committed PMC record gives the op's VALU lane-ops per pixel, the VALU roofline over
+    the same time; `bound` is whichever fraction is higher and the top-level achieved / peak /
+    unit / frac are that roofline's."""
+    achieved_gbs = bpp * pixels / (avg_kern_ms * 1e-3) / 1e9
+    e2e = op in END_TO_END
+    hbm = {"achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": None if e2e else round(achieved_gbs / HBM_PEAK_GBS, 4)}
+    rl = {"bound": "latency (end-to-end op)" if e2e else "hbm", **hbm, "hbm": dict(hbm),
+          "traffic": traffic,
+          "traffic_source": "profiles/pmc_traffic.json (committed rocprofv3 FETCH_SIZE x2 + "
+                            "WRITE_SIZE passes; not measured in this run)" if traffic else None}
+    v = None if e2e else load_valu(op)
+    if v is not None:
+        lane_ops = v["valu_per_pixel"] * pixels / (avg_kern_ms * 1e-3)
+        rl["valu"] = {"achieved": round(lane_ops / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
+                      "unit": "T lane-ops/s", "frac": round(lane_ops / VALU_PEAK, 4),
+                      "valu_per_pixel": v["valu_per_pixel"],
+                      "valu_source": v["source"] + " (SQ_INSTS_VALU x 64 / pixels; counters "
+                                                   "not measured in this run)"}
+        if rl["valu"]["frac"] > hbm["frac"]:
+            rl.update(bound="valu", achieved=rl["valu"]["achieved"], peak=rl["valu"]["peak"],
+                      unit=rl["valu"]["unit"], frac=rl["valu"]["frac"])
+    rl.update({"kernel": kname, "kernel_ms_avg": round(avg_kern_ms, 5)})
+    return rl, achieved_gbs
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -595,8 +649,9 @@ def main():
 
     pix_step = total_images * H * W
     value = pix_step * args.steps / wall / 1e6
-    achieved_gbs = bpp * my_batch * H * W / (avg_kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.op)
+    roofline, achieved_gbs = roofline_fields(args.op, bpp, my_batch * H * W, avg_kern_ms, traffic,
+                                             kname)
 
     if rank == 0:
         rec = {
@@ -629,16 +684,7 @@ def main():
                 "parallelism": f"image-sharded x{world} (no collective in the timed region)",
             },
             "roofline": {
-                "bound": "hbm" if args.op not in END_TO_END else "latency (end-to-end op)",
-                "achieved": round(achieved_gbs, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if args.op not in END_TO_END else None,
-                "traffic": traffic,
-                "traffic_source": "profiles/pmc_traffic.json (committed rocprofv3 FETCH_SIZE x2 + "
-                                  "WRITE_SIZE passes; not measured in this run)" if traffic else None,
-                "kernel": kname,
-                "kernel_ms_avg": round(avg_kern_ms, 5),
+                **roofline,
                 "timing": ("end-to-end op time (host gather, H2D, synchronous passes), not a "
                            "kernel duration" if args.op in END_TO_END else
                            "HIP events around the K launches on the launch stream"),

@@ -56,3 +56,24 @@ def test_single_gpu_default_is_one_rank():
     assert r.returncode == 0, r.stderr[-2000:]
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == 1 and rec["shards"] == [[0, 0, 256]]
+
+
+def test_roofline_names_the_binding_roof():
+    """The line carries the VALU roofline beside the HBM one where a committed PMC record gives
+    the op's VALU lane-ops per pixel, and `bound` names the higher fraction."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    pix = 256 * bench.H * bench.W
+    # median 5x5 at its measured 0.479 ms: ~110 VALU/px -> ~0.9 of the VALU peak, 0.24 of HBM
+    rl, _ = bench.roofline_fields("median5", 6, pix, 0.479, None, "median_u8")
+    assert rl["bound"] == "valu"
+    assert rl["valu"]["valu_per_pixel"] > 50 and 0.6 < rl["valu"]["frac"] < 1.2
+    assert rl["hbm"]["frac"] < 0.3 and rl["frac"] == rl["valu"]["frac"]
+    assert rl["unit"] == "T lane-ops/s" and rl["valu"]["valu_source"].startswith("profiles/")
+    # the headline stays HBM-bound: 19 VALU/px at 0.151 ms is ~0.5 of the VALU peak
+    rl, gbs = bench.roofline_fields("gauss5", 6, pix, 0.151, 9.4e8, "stencil_u8")
+    assert rl["bound"] == "hbm" and rl["frac"] == rl["hbm"]["frac"] > 0.7
+    assert rl["valu"]["frac"] < rl["hbm"]["frac"] and abs(rl["achieved"] - gbs) < 0.1
+    # end-to-end ops claim no fraction
+    rl, _ = bench.roofline_fields("detect_e2e", 6, bench.H * bench.W, 1.7, None, "e2e")
+    assert rl["frac"] is None and "valu" not in rl
