@@ -1,0 +1,1003 @@
+// Haar L = 3 on u8 images (BASELINE config 5's denoiser: skimage 0.14.2 denoise_wavelet(db1,
+// wavelet_levels=3), lib/roi_data_layer/minibatch_before_curvelet.py:85-87), round 6: two reads of
+// the image and one write.  Included by wavelet.hip inside namespace idn, after the shared helpers
+// (stats layout, haar_int / ycc_w, the exact dd key, select_bin / radix_pass).
+//
+//   wl_h3_window  reads 1/8 of the level-1 rows of every image: per channel a histogram of the
+//                 finest |T| (T = w_c . D_dd, the exact integer that the finest dd is a multiple
+//                 of) and a window [lo, hi] of |T| that holds the median rank with a wide margin
+//   wl_h3_stats   reads the image once: the exact fp64 YCbCr min / max (integer keys per lane,
+//                 the fp64 chain only on the pixels holding a workgroup's extreme key), the integer
+//                 second moments of every detail band (the BayesShrink sums), the count of nonzero
+//                 finest T, the count below the window, the |T| inside the window (appended), and
+//                 the positions where T = 0 but the reference's fp64 dd may be a rounding residue
+//   wl_h3_sigma   per image and channel: the residues evaluated exactly (the nonzero count), the
+//                 median rank selected among the window's |T| (sigma), the sums and thresholds;
+//                 an image whose rank falls outside its window, or is a residue, takes an exact
+//                 full-image selection in the same workgroup
+//   wl_h3_synth   reads the image again: the three levels' coefficients from the integer
+//                 combinations, soft thresholds, synthesis, clip, de-normalisation, YCbCr -> RGB
+//                 and the U8 store, in fp32 (packed where two 2x2 groups run side by side)
+//
+// Sigma: the reference's finest dd is 0.5 T / (255000 range) within 2e-12 / range (the error
+// analysis at wl_haar_stats), and distinct |T| differ by >= 1.96e-6 / range, so the ranks of the
+// fp64 values are the ranks of |T| and T = 0 ranks below every T != 0.  The median is taken as
+// 0.5 |T_k| / (255000 range) in fp64: relative 1e-6 / |T_k| from the reference's value (a few
+// 1e-12 at the usual |T_k| ~ 1e5..1e7), far inside the 1e-5 output tolerance.  The nonzero
+// count stays exact: every T = 0 position that is not an equal-triple pair (exact 0, x - x) is
+// evaluated with the reference's fp64 chain.
+
+constexpr int H3_SEL = 66;   // stats doubles [66, 78): per channel 8 u32 (H3Sel)
+constexpr int H3_CST = 112;  // stats doubles [112, 148): per channel 24 floats (H3Const)
+struct H3Sel {
+  uint32_t lo, hi;  // window of |T| (wl_h3_window)
+  uint32_t n_t;     // nonzero finest T (wl_h3_stats)
+  uint32_t n_lo;    // |T| < lo, zeros included
+  uint32_t n_c;     // |T| appended from the window
+  uint32_t n_r;     // residue positions appended (channel 0's slot counts for the image)
+  uint32_t fb;      // diagnostics: 1 = full-image fallback taken (wl_h3_sigma)
+  uint32_t pad;
+};
+struct H3Const {  // fp32 synthesis constants of one channel (wl_h3_consts)
+  float w1[3], w2[3], w3[3];  // rgb2ycbcr row x 1000 x the level's coefficient scale
+  float t1[3], t2[3], t3[3];  // soft thresholds in the same (folded) units
+  float ka;                   // level-3 approximation offset
+  float rng, mo;              // de-normalisation: v * rng + mo (mo = min - YCbCr offset)
+  float pad[3];
+};
+static_assert(sizeof(H3Const) == 24 * sizeof(float), "24 floats per channel");
+__host__ __device__ inline H3Sel* h3_sel(double* st) { return reinterpret_cast<H3Sel*>(st + H3_SEL); }
+__host__ __device__ inline const H3Const* h3_cst(const double* st) {
+  return reinterpret_cast<const H3Const*>(st + H3_CST);
+}
+
+// The synthesis constants from the stats block (min / max, half thresholds thrh, flag).  With
+// s1 = 0.5 / (255000 range) and k = 2 (offset - min) / range (wl_haar_synth_int), and the idwt's
+// factors 1/2 folded into the coefficients (a power of two commutes with soft()):
+//   level 1 detail  soft(T s1 / 2, thrh(0))          -> w1 = w s1 / 2,  t1 = thrh(0)
+//   level 2 detail  soft(T s1 / 8, thrh(1) / 2)      -> w2 = w s1 / 8,  t2 = thrh(1) / 2
+//   level 3         (w . S64) s1 / 32 + k / 2 +- soft(T s1 / 32, thrh(2) / 4)
+// so each level's approximation enters the next butterfly unscaled.
+__device__ void h3_consts(double* st, int c) {
+  wreal mn, mx;
+  wl_minmax64(st, c, mn, mx);
+  const double inv = mx - mn, s1 = 0.5 / (255000.0 * inv);
+  const double k = 2.0 * ((c == 0 ? 16.0 : 128.0) - mn) / inv;
+  H3Const* q = const_cast<H3Const*>(h3_cst(st)) + c;
+  for (int j = 0; j < 3; ++j) {
+    const double wj = (double)ycc_w(c, j);
+    q->w1[j] = (float)(wj * s1 * 0.5);
+    q->w2[j] = (float)(wj * s1 * 0.125);
+    q->w3[j] = (float)(wj * s1 * 0.03125);
+    q->t1[j] = (float)st[WlStats::thrh(c, 0, j)];
+    q->t2[j] = (float)(0.5 * st[WlStats::thrh(c, 1, j)]);
+    q->t3[j] = (float)(0.25 * st[WlStats::thrh(c, 2, j)]);
+  }
+  q->ka = (float)(0.5 * k);
+  q->rng = (float)inv;
+  q->mo = (float)(mn - (c == 0 ? 16.0 : 128.0));
+}
+__global__ void wl_h3_consts(double* __restrict__ stats, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 3 * n) h3_consts(stats + (size_t)(i / 3) * WL_STATS, i % 3);
+}
+
+// ---- wl_h3_synth ---------------------------------------------------------------------------------
+typedef float h3f2 __attribute__((ext_vector_type(2)));
+// lane value of quad member k (DPP quad_perm broadcast, one VALU op)
+__device__ __forceinline__ int quad_get(int v, int k) {
+  switch (k) {
+    case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);
+    default: return __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, false);
+  }
+}
+__device__ __forceinline__ float soft_f(float x, float t) {
+  return x - __builtin_amdgcn_fmed3f(x, -t, t);
+}
+__device__ __forceinline__ h3f2 soft_f2(h3f2 x, float t) {
+  const h3f2 c = {__builtin_amdgcn_fmed3f(x.x, -t, t), __builtin_amdgcn_fmed3f(x.y, -t, t)};
+  return x - c;
+}
+__device__ __forceinline__ h3f2 fma2(h3f2 a, h3f2 b, h3f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ h3f2 splat2(float v) { return h3f2{v, v}; }
+
+// One thread per 4x4 sub-block; the four sub-blocks of an 8x8 block are consecutive lanes (a
+// quad), which exchange their level-2 approximation sums by DPP for level 3.  Level 1 runs on two
+// 2x2 groups side by side as fp32 pairs (v_pk_fma / add / mul).  Outputs within the 1e-5
+// tolerance of the fp64 form (fp32 throughout: the synthesis is continuous in its inputs and no
+// exact zero depends on it).  GEN = false: u8 output only, dword-aligned rows (the product's
+// case); true: any of u8 (byte stores) / f32 output.
+template <bool GEN>
+__global__ __launch_bounds__(WLH_WG) void wl_h3_synth(const uint8_t* __restrict__ src, int h, int w,
+                                                      int64_t row_stride,
+                                                      const double* __restrict__ stats,
+                                                      uint8_t* __restrict__ out_u8,
+                                                      float* __restrict__ out_f32) {
+  const int img = blockIdx.y;
+  const int nbx = w >> 3, nblk = nbx * (h >> 3);
+  const int tid = blockIdx.x * WLH_WG + threadIdx.x;
+  const int blk = tid >> 2, sub = tid & 3;
+  const bool act = blk < nblk;  // uniform over each quad
+  const double* st = stats + (size_t)img * WL_STATS;
+  const H3Const* K = h3_cst(st);
+  int y0 = 0, x0 = 0;
+  uint32_t q[4][3] = {};
+  const uint8_t* ib = src + (int64_t)img * h * row_stride;
+  if (act) {
+    const int by = blk / nbx, bx = blk - by * nbx;
+    y0 = by * 8 + (sub >> 1) * 4;
+    x0 = bx * 8 + (sub & 1) * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + (int64_t)(y0 + r) * row_stride +
+                                                            (int64_t)x0 * 3);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) q[r][k] = p[k];
+    }
+  }
+  auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+  // level-1 integer combinations of the four 2x2 groups (g = 2 gy + gx), rgb
+  int S4[4][3], D1[4][3][3];  // [group][rgb] sums, [group][band][rgb] details
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const int gy = g >> 1, gx = g & 1;
+      haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
+               px(2 * gy + 1, 6 * gx + 3 + ch), S4[g][ch], D1[g][0][ch], D1[g][1][ch], D1[g][2][ch]);
+    }
+  int S16[3], D2[3][3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch)
+    haar_int(S4[0][ch], S4[1][ch], S4[2][ch], S4[3][ch], S16[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
+  int S64[3], D3[3][3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch)
+    haar_int(quad_get(S16[ch], 0), quad_get(S16[ch], 1), quad_get(S16[ch], 2), quad_get(S16[ch], 3),
+             S64[ch], D3[0][ch], D3[1][ch], D3[2][ch]);
+  if (!act) return;
+  if (st[WlStats::FLAG] != 0.0) {  // image-uniform: zeros (0.14.2's NaN -> U8 0)
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r)
+#pragma unroll 1
+      for (int k = 0; k < 12; ++k) {
+        const int y = y0 + r, xx = x0 + k / 3, c = k % 3;
+        if (out_u8) out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] = 0;
+        if (out_f32) out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = 0.0f;
+      }
+    return;
+  }
+  // lane signs of this sub-block's output in the level-3 butterfly (r = sub >> 1, s = sub & 1)
+  const float sad = (sub & 1) ? -1.f : 1.f, sda = (sub & 2) ? -1.f : 1.f, sdd = sad * sda;
+  float f64s[3], fd3[3][3], fd2[3][3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    f64s[ch] = (float)S64[ch];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      fd3[b][ch] = (float)D3[b][ch];
+      fd2[b][ch] = (float)D2[b][ch];
+    }
+  }
+  // per channel: level 3 -> a2, level 2 -> the four groups' level-1 approximations
+  float A1[3][4];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const H3Const& k = K[c];
+    auto dotw = [&](const float (&wv)[3], const float (&d)[3]) {
+      return __fmaf_rn(wv[2], d[2], __fmaf_rn(wv[1], d[1], wv[0] * d[0]));
+    };
+    float a2 = __fmaf_rn(k.w3[2], f64s[2], __fmaf_rn(k.w3[1], f64s[1], __fmaf_rn(k.w3[0], f64s[0], k.ka)));
+    a2 = __fmaf_rn(sad, soft_f(dotw(k.w3, fd3[0]), k.t3[0]), a2);
+    a2 = __fmaf_rn(sda, soft_f(dotw(k.w3, fd3[1]), k.t3[1]), a2);
+    a2 = __fmaf_rn(sdd, soft_f(dotw(k.w3, fd3[2]), k.t3[2]), a2);
+    const float ad = soft_f(dotw(k.w2, fd2[0]), k.t2[0]);
+    const float da = soft_f(dotw(k.w2, fd2[1]), k.t2[1]);
+    const float dd = soft_f(dotw(k.w2, fd2[2]), k.t2[2]);
+    const float p = a2 + ad, m = a2 - ad, q0 = da + dd, q1 = da - dd;
+    A1[c][0] = p + q0;
+    A1[c][1] = m + q1;
+    A1[c][2] = p - q0;
+    A1[c][3] = m - q1;
+  }
+  // level 1: groups (0, 1) and (2, 3) side by side -> pixel values v[pair][pixel (r, s)][c]
+  constexpr float Rf[3][3] = {
+      {(float)(0.004566210045662101 * 255), (float)(1.1808799897950177e-09 * 255), (float)(0.006258928969943937 * 255)},
+      {(float)(0.004566210045662101 * 255), (float)(-0.0015363236860449021 * 255), (float)(-0.003188110949655707 * 255)},
+      {(float)(0.004566210045662101 * 255), (float)(0.007910716233554741 * 255), (float)(1.1977497040511743e-08 * 255)}};
+  const bool dw = !GEN;
+#pragma unroll
+  for (int gp = 0; gp < 2; ++gp) {  // pair gp: groups 2 gp (x of the pair) and 2 gp + 1 (y)
+    h3f2 v[4][3];                    // [pixel (r, s)][c]: .x group 2 gp, .y group 2 gp + 1
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const H3Const& k = K[c];
+      h3f2 d[3];
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const h3f2 D0 = {(float)D1[2 * gp][b][0], (float)D1[2 * gp + 1][b][0]};
+        const h3f2 Dg = {(float)D1[2 * gp][b][1], (float)D1[2 * gp + 1][b][1]};
+        const h3f2 Db = {(float)D1[2 * gp][b][2], (float)D1[2 * gp + 1][b][2]};
+        d[b] = soft_f2(fma2(splat2(k.w1[2]), Db, fma2(splat2(k.w1[1]), Dg, splat2(k.w1[0]) * D0)), k.t1[b]);
+      }
+      const h3f2 A = {A1[c][2 * gp], A1[c][2 * gp + 1]};
+      const h3f2 p = A + d[0], m = A - d[0], q0 = d[1] + d[2], q1 = d[1] - d[2];
+      v[0][c] = p + q0;
+      v[1][c] = m + q1;
+      v[2][c] = p - q0;
+      v[3][c] = m - q1;
+    }
+    // inner clip [0, 1], de-normalise, YCbCr -> RGB x 255, truncate, saturate to u8
+    uint32_t rowp[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = i >> 1, s = i & 1;
+      h3f2 e[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const h3f2 vc = {__builtin_amdgcn_fmed3f(v[i][c].x, 0.f, 1.f),
+                         __builtin_amdgcn_fmed3f(v[i][c].y, 0.f, 1.f)};
+        e[c] = fma2(vc, splat2(K[c].rng), splat2(K[c].mo));
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const h3f2 o = fma2(e[2], splat2(Rf[c][2]), fma2(e[1], splat2(Rf[c][1]), e[0] * splat2(Rf[c][0])));
+#pragma unroll
+        for (int g2 = 0; g2 < 2; ++g2) {  // group 2 gp + g2: pixel column 2 g2 + s
+          const float of = g2 ? o.y : o.x;
+          const int xx = x0 + 2 * g2 + s, y = y0 + 2 * gp + r;
+          if (dw) {
+            const int bi = (2 * g2 + s) * 3 + c;
+            rowp[r][bi >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_truncf(of), bi & 3,
+                                                              rowp[r][bi >> 2]);
+          } else if (out_u8) {
+            out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] =
+                (uint8_t)min(max((int)of, 0), 255);
+          }
+          if (GEN && out_f32)
+            out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] =
+                __builtin_amdgcn_fmed3f(of, 0.f, 255.f) * (1.f / 255.f);
+        }
+      }
+    }
+    if (dw) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        uint32_t* p = reinterpret_cast<uint32_t*>(out_u8 + (int64_t)img * h * row_stride +
+                                                  (int64_t)(y0 + 2 * gp + r) * row_stride +
+                                                  (int64_t)x0 * 3);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) p[j] = rowp[r][j];
+      }
+    }
+  }
+}
+
+// ---- wl_h3_window ---------------------------------------------------------------------------------
+// |T| histogram bins: floor(log2 |T|) and the next 6 bits (monotone in |T|; |T| < 2^31)
+constexpr int H3_HB = 2048;
+constexpr int H3_WIN_WG = 1024;
+constexpr int H3_SAMPLE = 16;  // every 16th level-1 row (rows 2i, 2i + 1 of the image)
+__device__ __forceinline__ int h3_bin(uint32_t a) {  // a >= 1
+  const int e = 31 - __clz((int)a);
+  const uint32_t m = e >= 6 ? (a >> (e - 6)) & 63u : (a << (6 - e)) & 63u;
+  return e * 64 + (int)m;
+}
+// the largest |T| whose bin is <= b (bins below 64 hold few integers: found by search)
+__device__ uint32_t h3_bin_hi(int b) {
+  const int n = b + 1, e = n >> 6;
+  if (e >= 31) return 0xFFFFFFFFu;
+  if (e >= 6) return ((uint32_t)(64 + (n & 63)) << (e - 6)) - 1u;
+  uint32_t hi = 0;
+  for (uint32_t a = 1; a < 64; ++a)
+    if (h3_bin(a) <= b) hi = a;
+  return hi;
+}
+__device__ __forceinline__ uint32_t h3_bin_lo(int b) {  // the smallest |T| of bin b, 1 below 64
+  const int e = b >> 6;
+  return e >= 6 ? (uint32_t)(64 + (b & 63)) << (e - 6) : 1u;
+}
+// equal RGB triples along the rows or the columns of a 2x2 group: the reference's dd is x - x = 0
+__device__ __forceinline__ bool h3_eqtrip(uint32_t t00, uint32_t t01, uint32_t t10, uint32_t t11) {
+  return (t00 == t01 && t10 == t11) || (t00 == t10 && t01 == t11);
+}
+
+// The sample: level-1 rows i = 0, 16, 32, .. (the finest dd of row i reads image rows 2i, 2i + 1),
+// every column.  Per channel the window of |T| ranks [n (0.5 - rho / 2 - m), n (0.5 + m)] of the
+// sample's n nonzero T, rho the sample's share of residue candidates (T = 0, not an equal-triple
+// pair: each may or may not be a nonzero fp64 residue, so the median's rank among the T != 0 lies
+// up to rho / 2 lower) and m = 4 sample standard errors of the median rank (2 / sqrt(n)) + 0.3 %.
+// A rank outside the window costs wl_h3_sigma its exact full-image path, not correctness.
+__global__ __launch_bounds__(H3_WIN_WG) void wl_h3_window(const uint8_t* __restrict__ src, int h,
+                                                          int w, int64_t row_stride,
+                                                          double* __restrict__ stats,
+                                                          int force_fb = 0) {
+  const int img = blockIdx.x;
+  __shared__ uint32_t hist[3][H3_HB];
+  __shared__ uint32_t nres[3];
+  for (int k = threadIdx.x; k < 3 * H3_HB; k += H3_WIN_WG) (&hist[0][0])[k] = 0u;
+  if (threadIdx.x < 3) nres[threadIdx.x] = 0u;
+  __syncthreads();
+  const int H1 = h >> 1, npair = w >> 2;  // position pairs (4 pixels, 3 dwords) per row
+  const int nrows = (H1 + H3_SAMPLE - 1) / H3_SAMPLE, items = nrows * npair;
+  const uint8_t* ib = src + (int64_t)img * h * row_stride;
+  for (int it = threadIdx.x; it < items; it += H3_WIN_WG) {
+    const int i = (it / npair) * H3_SAMPLE, jp = it - (it / npair) * npair;
+    uint32_t q[2][3];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + (int64_t)(2 * i + r) * row_stride +
+                                                            (int64_t)jp * 12);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) q[r][k] = p[k];
+    }
+    auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+    auto trip = [&](int r, int pix) {
+      return (uint32_t)(px(r, 3 * pix) | (px(r, 3 * pix + 1) << 8) | (px(r, 3 * pix + 2) << 16));
+    };
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      int D[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        D[ch] = px(0, 6 * s + ch) - px(0, 6 * s + 3 + ch) - px(1, 6 * s + ch) + px(1, 6 * s + 3 + ch);
+      const bool eq = h3_eqtrip(trip(0, 2 * s), trip(0, 2 * s + 1), trip(1, 2 * s), trip(1, 2 * s + 1));
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int T = __mul24(ycc_w(c, 0), D[0]) + __mul24(ycc_w(c, 1), D[1]) + __mul24(ycc_w(c, 2), D[2]);
+        if (T != 0) atomicAdd(&hist[c][h3_bin((uint32_t)(T < 0 ? -T : T))], 1u);
+        else if (!eq) atomicAdd(&nres[c], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave >= 3) return;
+  const int c = wave;
+  constexpr int PER = H3_HB / 64;
+  uint32_t own = 0;
+  for (int b = 0; b < PER; ++b) own += hist[c][lane * PER + b];
+  uint32_t inc = own;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+    if (lane >= o) inc += t;
+  }
+  const uint32_t n = (uint32_t)__shfl((int)inc, 63);
+  auto find = [&](uint32_t rank) -> int {  // bin holding sample rank `rank` (< n)
+    const uint32_t excl = inc - own;
+    int bin = H3_HB - 1;
+    if (own && rank >= excl && rank < inc) {
+      uint32_t acc = excl;
+      int b = lane * PER;
+      for (; b < lane * PER + PER - 1; ++b) {
+        if (acc + hist[c][b] > rank) break;
+        acc += hist[c][b];
+      }
+      bin = b;
+    }
+    const unsigned long long m = __ballot(own && rank >= excl && rank < inc);
+    return __shfl(bin, m ? __ffsll((long long)m) - 1 : 0);
+  };
+  uint32_t lo = 1u, hi = 0xFFFFFFFFu;
+  if (n >= 512) {
+    const double rho = fmin((double)nres[c] / (double)n, 1.0);
+    const double m = 2.0 / sqrt((double)n) + 0.003;
+    const double qlo = 0.5 - 0.5 * rho - m, qhi = 0.5 + m;
+    const int64_t klo = (int64_t)floor(qlo * (double)n), khi = (int64_t)ceil(qhi * (double)n);
+    const int blo = klo > 0 ? find((uint32_t)klo) : -1;
+    const int bhi = khi < (int64_t)n - 1 ? find((uint32_t)khi) : -1;
+    if (blo >= 0) lo = h3_bin_lo(blo);
+    if (bhi >= 0) hi = h3_bin_hi(bhi);
+  }
+  if (force_fb) lo = hi = 0xFFFFFFFFu;  // tests: an empty window, every channel takes the exact path
+  if (lane == 0) {
+    H3Sel* s = h3_sel(stats + (size_t)img * WL_STATS) + c;
+    s->lo = lo;
+    s->hi = hi;
+  }
+}
+
+// ---- wl_h3_stats ----------------------------------------------------------------------------------
+#ifndef IDN_H3_IT  // A/B builds set these
+#define IDN_H3_IT 16
+#endif
+#ifndef IDN_H3_K
+#define IDN_H3_K 8
+#endif
+#ifndef IDN_H3_WPE
+#define IDN_H3_WPE 1
+#endif
+#ifndef IDN_H3_MOM  // level-1 moments: 0 v_dot2 on group pairs, 1 24-bit multiply-adds
+#define IDN_H3_MOM 0
+#endif
+#ifndef IDN_H3_PROBE  // timing probes only (wrong results): bit 0 no proxies, 1 no T / counts /
+#define IDN_H3_PROBE 0  // appends, 2 no level-1 moments, 3 no levels 2-3
+#endif
+constexpr int H3_IT = IDN_H3_IT;  // block rows per workgroup (int32 moments: <= 16 steps, 1.07e9)
+// Appends go to per-lane LDS slots (no atomics, no barriers): slot j of lane t of channel c at
+// [c][j][t]; a wave moves its lanes' slots to the image's arrays (one scan, one global atomic per
+// array) once some lane could overflow in the next iteration (4 appends per lane and array).
+constexpr int H3_K = IDN_H3_K;
+constexpr int H3_KR = 4;  // residue slots per lane (overflow: a global atomic each)
+// a wave's per-lane runs buf[j][t] (j < n, the lane's count) to dst[base + exclusive prefix]
+__device__ __forceinline__ void h3_wave_flush(const uint32_t* buf, uint32_t n, uint32_t* dst,
+                                              uint32_t* gcount) {
+  const int lane = threadIdx.x & 63;
+  uint32_t inc = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+    if (lane >= o) inc += t;
+  }
+  const uint32_t tot = (uint32_t)__shfl((int)inc, 63);
+  if (tot == 0) return;
+  uint32_t base = 0;
+  if (lane == 63) base = atomicAdd(gcount, tot);
+  base = (uint32_t)__shfl((int)base, 63) + inc - n;
+  for (uint32_t j = 0; j < n; ++j) dst[base + j] = buf[j * WLH_WG + threadIdx.x];
+}
+typedef short h3s2 __attribute__((ext_vector_type(2)));
+// rgb2ycbcr coefficients as floats: the fp32 proxy of a pixel's YCbCr dot x 255 (|error| < 0.03
+// for bytes: three roundings at magnitude < 2^16 plus the coefficients' own, < 1e-3 each)
+__device__ __forceinline__ float h3_ycf(int c, int k) {
+  constexpr float W[3][3] = {{65.481f, 128.553f, 24.966f}, {-37.797f, -74.203f, 112.0f},
+                             {112.0f, -93.786f, -18.214f}};
+  return W[c][k];
+}
+constexpr float H3_PTOL = 0.0625f;
+__device__ __forceinline__ int ykey(int c, int r, int g, int b) {  // exact YCbCr dot x 255000
+  return __mul24(ycc_w(c, 0), r) + __mul24(ycc_w(c, 1), g) + __mul24(ycc_w(c, 2), b);
+}
+
+// Work split: a workgroup of 128 threads = 32 quads = the 8x8 blocks of 32 consecutive block
+// columns; it walks H3_IT block rows down (one 4x4 sub-block per thread and step: the quad's four
+// sub-blocks are consecutive lanes, as wl_haar_stats), so a thread's column and its level-1
+// position advance by constants (no per-step index division).  Grid: (column strips x row
+// chunks, images).  Workspace (the image's slot): |T| candidates [3][P] u32, residues [P] u32
+// (level-1 position | channel mask << 28), P = (h / 2) (w / 2).
+constexpr int H3_COLS = WLH_WG / 4;  // block columns per workgroup
+__host__ __device__ inline int h3_strips(int w) { return ((w >> 3) + H3_COLS - 1) / H3_COLS; }
+__host__ __device__ inline int h3_chunks(int h) { return ((h >> 3) + H3_IT - 1) / H3_IT; }
+__global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_WPE))) void wl_h3_stats(const uint8_t* __restrict__ src, int h, int w,
+                                                      int64_t row_stride, wreal* __restrict__ ws,
+                                                      size_t img_floats, double* __restrict__ stats,
+                                                      double* __restrict__ part, size_t part_per_img) {
+  constexpr int L = 3;
+  const int img = blockIdx.y;
+  const int nbx = w >> 3, nby = h >> 3;
+  const int strips = h3_strips(w);
+  const int strip = (int)blockIdx.x % strips, chunk = (int)blockIdx.x / strips;
+  const int sub = threadIdx.x & 3, bx = strip * H3_COLS + (threadIdx.x >> 2);
+  const int by0 = chunk * H3_IT, nit = min(H3_IT, nby - by0);  // block rows of this workgroup
+  const bool colact = bx < nbx;
+  const int x0 = bx * 8 + (sub & 1) * 4, sy = (sub >> 1) * 4;
+  double* st = stats + (size_t)img * WL_STATS;
+  H3Sel* sel = h3_sel(st);
+  const uint32_t W1 = (uint32_t)(w >> 1), P = (uint32_t)(h >> 1) * W1;
+  uint32_t* cand = reinterpret_cast<uint32_t*>(ws + img * img_floats);
+  uint32_t* resl = cand + 3 * (size_t)P;
+  __shared__ double red[3 * L * 3][WLH_WG / 64];
+  __shared__ int ml2[3 * 6][WLH_WG];
+  __shared__ int ml3[3 * 6][WLH_WG / 4];
+  __shared__ uint32_t cb[3][H3_K * WLH_WG];  // [channel][slot][thread]
+  __shared__ uint32_t rb[H3_KR * WLH_WG];     // residues [slot][thread]
+  __shared__ uint32_t cnt_s[6];
+  __shared__ float kred[6][WLH_WG / 64];
+  __shared__ double dred[6][WLH_WG / 64];
+#pragma unroll
+  for (int k = 0; k < 3 * 6; ++k) ml2[k][threadIdx.x] = 0;
+  if (threadIdx.x < WLH_WG / 4)
+#pragma unroll
+    for (int k = 0; k < 3 * 6; ++k) ml3[k][threadIdx.x] = 0;
+  if (threadIdx.x < 6) cnt_s[threadIdx.x] = 0u;
+  uint32_t lo[3], span[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    lo[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sel[c].lo);
+    span[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(sel[c].hi - sel[c].lo));
+  }
+  __syncthreads();
+  int mom[3][6];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) mom[b][k] = 0;
+  float pmn[3] = {INFINITY, INFINITY, INFINITY}, pmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  uint32_t ct[3] = {0u, 0u, 0u}, cl[3] = {0u, 0u, 0u};  // per-lane counts
+  uint32_t na[4] = {0u, 0u, 0u, 0u};                    // this lane's filled slots
+  auto mom_lds = [&](int l, int b, int r, int g, int bl) {
+    const int ld = l == 1 ? WLH_WG : WLH_WG / 4;
+    int* m = l == 1 ? &ml2[b * 6][threadIdx.x] : &ml3[b * 6][threadIdx.x >> 2];
+    atomicAdd(m + 0 * ld, __mul24(r, r));
+    atomicAdd(m + 1 * ld, __mul24(g, g));
+    atomicAdd(m + 2 * ld, __mul24(bl, bl));
+    atomicAdd(m + 3 * ld, __mul24(r, g));
+    atomicAdd(m + 4 * ld, __mul24(r, bl));
+    atomicAdd(m + 5 * ld, __mul24(g, bl));
+  };
+  // this thread's sub-block at step it: rows y0 = 8 (by0 + it) + sy, columns x0 .. x0 + 3
+  const uint8_t* ib = src + (int64_t)img * h * row_stride + (int64_t)(8 * by0 + sy) * row_stride +
+                      (int64_t)x0 * 3;
+  const int64_t step_bytes = 8 * row_stride;
+  auto load_q = [&](int it, uint32_t (&qq)[4][3]) {
+    if (!colact || it >= nit) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + it * step_bytes + r * row_stride);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
+    }
+  };
+  auto flush = [&](int a) {  // wave-uniform
+    h3_wave_flush(a < 3 ? cb[a] : rb, na[a], a < 3 ? cand + (size_t)a * P : resl,
+                  a < 3 ? &sel[a].n_c : &sel[0].n_r);
+    na[a] = 0u;
+  };
+  auto put_res = [&](bool cond, uint32_t v) {  // a lane's residue slots full: straight out
+    if (cond) {
+      if (na[3] < (uint32_t)H3_KR) {
+        rb[na[3] * WLH_WG + threadIdx.x] = v;
+        ++na[3];
+      } else {
+        resl[atomicAdd(&sel[0].n_r, 1u)] = v;
+      }
+    }
+  };
+  // level-1 position of group (0, 0) of this thread's sub-block at step 0; + 4 W1 per step
+  const uint32_t pos00 = (uint32_t)(4 * by0 + sy / 2) * W1 + (uint32_t)(x0 / 2);
+  uint32_t qn[4][3] = {};
+  load_q(0, qn);
+#pragma unroll 1
+  for (int it = 0; it < nit; ++it) {
+    const bool act = colact;  // (rows: it < nit, uniform)
+    uint32_t q[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) q[r][k] = qn[r][k];
+    load_q(it + 1, qn);
+    if (!act) {  // lanes past the image: zeros (they add nothing; keys and counts are masked)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) q[r][k] = 0u;
+    }
+    auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+    auto pxf = [&](int r, int k) { return (float)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+    // fp32 proxies of the YCbCr dots (x 255) of pixel pairs: per lane min / max (exact values
+    // only where a lane is within H3_PTOL of the workgroup's extreme, after the loop)
+    if (act && !(IDN_H3_PROBE & 1))
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const h3f2 R = {pxf(r, 6 * pp), pxf(r, 6 * pp + 3)}, G = {pxf(r, 6 * pp + 1), pxf(r, 6 * pp + 4)},
+                   B = {pxf(r, 6 * pp + 2), pxf(r, 6 * pp + 5)};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const h3f2 k2 = fma2(splat2(h3_ycf(c, 2)), B, fma2(splat2(h3_ycf(c, 1)), G, splat2(h3_ycf(c, 0)) * R));
+          pmn[c] = __builtin_fminf(pmn[c], __builtin_fminf(k2.x, k2.y));
+          pmx[c] = __builtin_fmaxf(pmx[c], __builtin_fmaxf(k2.x, k2.y));
+        }
+      }
+    int a1[4][3];
+#pragma unroll
+    for (int gy = 0; gy < 2; ++gy) {
+      int D[2][3][3];  // [gx][band][rgb]
+#pragma unroll
+      for (int gx = 0; gx < 2; ++gx)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+          haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
+                   px(2 * gy + 1, 6 * gx + 3 + ch), a1[gy * 2 + gx][ch], D[gx][0][ch], D[gx][1][ch],
+                   D[gx][2][ch]);
+      // the two groups' moments as 16-bit pairs: one v_dot2 per moment and band (|D| <= 510)
+      if (IDN_H3_MOM == 1 && !(IDN_H3_PROBE & 4))
+#pragma unroll
+        for (int gx = 0; gx < 2; ++gx)
+#pragma unroll
+          for (int b = 0; b < 3; ++b) mom_add(mom[b], D[gx][b][0], D[gx][b][1], D[gx][b][2]);
+#pragma unroll
+      for (int b = 0; b < ((IDN_H3_PROBE & 4) || IDN_H3_MOM == 1 ? 0 : 3); ++b) {
+        h3s2 P[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+          P[ch] = __builtin_bit_cast(h3s2, __builtin_amdgcn_perm(D[1][b][ch], D[0][b][ch], 0x05040100u));
+        mom[b][0] = __builtin_amdgcn_sdot2(P[0], P[0], mom[b][0], false);
+        mom[b][1] = __builtin_amdgcn_sdot2(P[1], P[1], mom[b][1], false);
+        mom[b][2] = __builtin_amdgcn_sdot2(P[2], P[2], mom[b][2], false);
+        mom[b][3] = __builtin_amdgcn_sdot2(P[0], P[1], mom[b][3], false);
+        mom[b][4] = __builtin_amdgcn_sdot2(P[0], P[2], mom[b][4], false);
+        mom[b][5] = __builtin_amdgcn_sdot2(P[1], P[2], mom[b][5], false);
+      }
+#pragma unroll
+      for (int gx = 0; gx < ((IDN_H3_PROBE & 2) ? 0 : 2); ++gx) {
+        const uint32_t pos = pos00 + (uint32_t)(4 * it + gy) * W1 + (uint32_t)gx;
+        int T[3];
+        uint32_t aT[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          T[c] = ykey(c, D[gx][2][0], D[gx][2][1], D[gx][2][2]);
+          aT[c] = (uint32_t)(T[c] < 0 ? -T[c] : T[c]);
+          // branch-free: per-lane counts; the slot store is unconditional (a slot written
+          // without the count moving is overwritten by the next append)
+          ct[c] += aT[c] != 0u ? 1u : 0u;
+          cl[c] += aT[c] < lo[c] ? 1u : 0u;
+          cb[c][na[c] * WLH_WG + threadIdx.x] = aT[c];
+          na[c] += aT[c] - lo[c] <= span[c] ? 1u : 0u;
+        }
+        const bool z = act && min(min(aT[0], aT[1]), aT[2]) == 0u;
+        if (__builtin_amdgcn_ballot_w64(z)) {
+          auto trip = [&](int r, int k) { return (uint32_t)(px(r, k) | (px(r, k + 1) << 8) | (px(r, k + 2) << 16)); };
+          const bool eq = h3_eqtrip(trip(2 * gy, 6 * gx), trip(2 * gy, 6 * gx + 3),
+                                    trip(2 * gy + 1, 6 * gx), trip(2 * gy + 1, 6 * gx + 3));
+          const uint32_t cm = (T[0] == 0 ? 1u : 0u) | (T[1] == 0 ? 2u : 0u) | (T[2] == 0 ? 4u : 0u);
+          put_res(z && !eq, pos | (cm << 28));
+        }
+      }
+    }
+    if (IDN_H3_PROBE & 8) continue;
+    int a2[3], D2[3][3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+      haar_int(a1[0][ch], a1[1][ch], a1[2][ch], a1[3][ch], a2[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
+    if (act)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) mom_lds(1, b, D2[b][0], D2[b][1], D2[b][2]);
+    int D3[3][3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      int aa;
+      haar_int(quad_get(a2[ch], 0), quad_get(a2[ch], 1), quad_get(a2[ch], 2), quad_get(a2[ch], 3), aa,
+               D3[0][ch], D3[1][ch], D3[2][ch]);
+    }
+    if (act && sub == 0)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) mom_lds(2, b, D3[b][0], D3[b][1], D3[b][2]);
+    // a wave moves its slots out once a lane could overflow in the next step (4 appends each)
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+      if (__builtin_amdgcn_ballot_w64(na[a] > (uint32_t)(H3_K - 4))) flush(a);
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) flush(a);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // counts (lanes past the image counted their zero groups: dropped)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    uint32_t a = colact ? ct[c] : 0u, b = colact ? cl[c] : 0u;
+    for (int o = 32; o > 0; o >>= 1) {
+      a += (uint32_t)__shfl_xor((int)a, o);
+      b += (uint32_t)__shfl_xor((int)b, o);
+    }
+    if (lane == 0) {
+      atomicAdd(&cnt_s[c], a);
+      atomicAdd(&cnt_s[3 + c], b);
+    }
+  }
+  // unscaled sums of squares T^2 per (channel, level, band): w_c^T M w_c (wl_h3_sigma scales them)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double w0 = ycc_w(c, 0), w1 = ycc_w(c, 1), w2 = ycc_w(c, 2);
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        int m[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          m[k] = l == 0 ? mom[b][k]
+                 : l == 1 ? ml2[b * 6 + k][threadIdx.x]
+                          : ((threadIdx.x & 3) == 0 ? ml3[b * 6 + k][threadIdx.x >> 2] : 0);
+        double v = w0 * w0 * (double)m[0] + w1 * w1 * (double)m[1] + w2 * w2 * (double)m[2] +
+                   2.0 * (w0 * w1 * (double)m[3] + w0 * w2 * (double)m[4] + w1 * w2 * (double)m[5]);
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) red[(c * L + l) * 3 + b][wave] = v;
+      }
+  }
+  // the workgroup's extreme proxies (lanes past the image hold +-inf)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float a = pmn[c], b = pmx[c];
+    for (int o = 32; o > 0; o >>= 1) {
+      a = __builtin_fminf(a, __shfl_xor(a, o));
+      b = __builtin_fmaxf(b, __shfl_xor(b, o));
+    }
+    if (lane == 0) {
+      kred[c][wave] = a;
+      kred[3 + c][wave] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 * L * 3) {
+    const int k = threadIdx.x, b = k % 3, l = (k / 3) % L, c = k / (3 * L);
+    double t = red[k][0];
+#pragma unroll
+    for (int wv = 1; wv < WLH_WG / 64; ++wv) t += red[k][wv];
+    part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + (size_t)l * gridDim.x +
+         blockIdx.x] = t;
+  }
+  if (threadIdx.x < 3) {
+    atomicAdd(&sel[threadIdx.x].n_t, cnt_s[threadIdx.x]);
+    atomicAdd(&sel[threadIdx.x].n_lo, cnt_s[3 + threadIdx.x]);
+  }
+  float gmn[3], gmx[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    gmn[c] = kred[c][0];
+    gmx[c] = kred[3 + c][0];
+#pragma unroll
+    for (int wv = 1; wv < WLH_WG / 64; ++wv) {
+      gmn[c] = __builtin_fminf(gmn[c], kred[c][wv]);
+      gmx[c] = __builtin_fmaxf(gmx[c], kred[3 + c][wv]);
+    }
+  }
+  // the fp64 chain only where a lane's proxy is within H3_PTOL of the workgroup's extreme: every
+  // pixel there whose proxy is (exact ties differ in the last fp64 bits; the proxy's error is
+  // below 0.03, distinct exact values 0.001 apart, so the extreme is among them)
+  double dmn[3] = {INFINITY, INFINITY, INFINITY}, dmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  bool need = false;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) need |= pmn[c] <= gmn[c] + H3_PTOL || pmx[c] >= gmx[c] - H3_PTOL;
+  if (colact && need) {
+#pragma unroll 1
+    for (int it = 0; it < nit; ++it) {
+      uint32_t q[4][3];
+      load_q(it, q);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int r = k >> 2, p = k & 3;
+        auto px = [&](int kk) { return (int)((q[r][kk >> 2] >> (8 * (kk & 3))) & 0xFFu); };
+        const int R = px(3 * p), G = px(3 * p + 1), B = px(3 * p + 2);
+        bool hit = false;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float pk = __fmaf_rn(h3_ycf(c, 2), (float)B, __fmaf_rn(h3_ycf(c, 1), (float)G, h3_ycf(c, 0) * (float)R));
+          hit |= pk <= gmn[c] + H3_PTOL || pk >= gmx[c] - H3_PTOL;
+        }
+        if (!hit) continue;
+        double d[3];
+        ycc_dots((double)R * (1.0 / 255.0), (double)G * (1.0 / 255.0), (double)B * (1.0 / 255.0), d);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          dmn[c] = fmin(dmn[c], d[c]);
+          dmx[c] = fmax(dmx[c], d[c]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double a = dmn[c], b = dmx[c];
+    for (int o = 32; o > 0; o >>= 1) {
+      a = fmin(a, __shfl_xor(a, o));
+      b = fmax(b, __shfl_xor(b, o));
+    }
+    if (lane == 0) {
+      dred[c][wave] = a;
+      dred[3 + c][wave] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int c = threadIdx.x;
+    double a = dred[c][0], b = dred[3 + c][0];
+#pragma unroll
+    for (int wv = 1; wv < WLH_WG / 64; ++wv) {
+      a = fmin(a, dred[c][wv]);
+      b = fmax(b, dred[3 + c][wv]);
+    }
+    if (a <= b) {  // rounded offsets after the reduction, as wl_color_minmax
+      atomicMinD(st + WlStats::MN64 + c, __dadd_rn(a, ycc_offset(c)));
+      atomicMaxD(st + WlStats::MX64 + c, __dadd_rn(b, ycc_offset(c)));
+    }
+  }
+}
+
+// ---- wl_h3_sigma ----------------------------------------------------------------------------------
+// rank `rank` of v[0..n) (u32), block-wide: three histogram passes of 11 / 11 / 10 bits
+__device__ uint32_t h3_select_u32(const uint32_t* __restrict__ v, uint32_t n, uint32_t rank,
+                                  uint32_t* hist) {
+  uint32_t prefix = 0u, pmask = 0u;
+#pragma unroll 1
+  for (int p = 0; p < 3; ++p) {
+    const int sh = p == 0 ? 21 : p == 1 ? 10 : 0, nb = p == 2 ? 1024 : 2048;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0u;
+    __syncthreads();
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += 4 * blockDim.x) {
+      uint32_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * blockDim.x;
+        x[u] = i < n ? v[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + (uint32_t)u * blockDim.x < n && (x[u] & pmask) == prefix)
+          atomicAdd(&hist[(x[u] >> sh) & (uint32_t)(nb - 1)], 1u);
+    }
+    __syncthreads();
+    const BinSel bs = select_bin(hist, nb, rank, nullptr, false);
+    prefix |= bs.bin << sh;
+    pmask |= (uint32_t)(nb - 1) << sh;
+    rank = bs.rank;
+  }
+  return prefix;
+}
+
+// per (image, channel) workgroup of WLM_WG threads
+__global__ __launch_bounds__(WLM_WG) void wl_h3_sigma(const uint8_t* __restrict__ src,
+                                                      int64_t row_stride, wreal* __restrict__ ws,
+                                                      size_t img_floats, double* __restrict__ stats,
+                                                      WlLayout Lt, const double* __restrict__ part,
+                                                      int nwg) {
+  const int img = blockIdx.x / 3, c = blockIdx.x % 3;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* st = stats + (size_t)img * WL_STATS;
+  H3Sel* sel = h3_sel(st);
+  const uint32_t W1 = (uint32_t)Lt.W[1], P = (uint32_t)Lt.H[1] * W1;
+  const uint32_t* cand = reinterpret_cast<const uint32_t*>(ws + img * img_floats) + (size_t)c * P;
+  const uint32_t* resl = reinterpret_cast<const uint32_t*>(ws + img * img_floats) + 3 * (size_t)P;
+  double* kd = ws + img * img_floats + 2 * (size_t)P + (size_t)c * P;  // fallback keys
+  wreal mn, mx;
+  wl_minmax64(st, c, mn, mx);
+  const wreal inv = mx - mn, rcp = 1.0 / inv;
+  const double sc = 0.5 / (255000.0 * inv);
+  __shared__ uint32_t hist[WLM_NH * WL_FBINS];
+  __shared__ uint32_t red_u[WLM_WG / 64], le_s, gt_s;
+  __shared__ unsigned long long gtk_s;
+  __shared__ uint32_t lek_s;
+  // 1. the residues of this channel: exact fp64 dd (nonzero ones count)
+  const uint32_t nr = sel[0].n_r;
+  uint32_t nz = 0;
+  constexpr int BQ = 6;
+  for (uint32_t t0 = threadIdx.x; t0 < nr; t0 += BQ * WLM_WG) {
+    uint32_t e[BQ];
+    Dd1Raw q[BQ];
+#pragma unroll
+    for (int u = 0; u < BQ; ++u) {
+      e[u] = resl[min(t0 + (uint32_t)u * WLM_WG, nr - 1)];
+      q[u] = wl_dd1_load(src, img, Lt.h, row_stride, e[u] & 0x0FFFFFFFu, (int)W1);
+    }
+#pragma unroll
+    for (int u = 0; u < BQ; ++u)
+      if (t0 + (uint32_t)u * WLM_WG < nr && ((e[u] >> (28 + c)) & 1u))
+        nz += wl_dd1_eval<true>(q[u], c, mn, inv, rcp) != 0ull ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) nz += (uint32_t)__shfl_xor((int)nz, o);
+  if (lane == 0) red_u[wave] = nz;
+  if (threadIdx.x == 0) {
+    le_s = 0u;
+    gt_s = 0xFFFFFFFFu;
+    gtk_s = ~0ull;
+    lek_s = 0u;
+  }
+  __syncthreads();
+  uint32_t nrnz = 0;
+#pragma unroll
+  for (int k = 0; k < WLM_WG / 64; ++k) nrnz += red_u[k];
+  // 2. the median ranks among the nonzero finest dd (residues rank below every T != 0)
+  const uint32_t n_t = sel[c].n_t, n_c = sel[c].n_c;
+  const uint32_t below = sel[c].n_lo - (P - n_t);  // 0 < |T| < lo
+  const uint32_t N = n_t + nrnz;
+  double med = NAN;
+  uint32_t total = N;
+  bool fb = false;
+  if (N) {
+    const uint32_t klo = (N - 1) / 2, khi = N / 2;
+    const uint32_t base = nrnz + below;  // rank of the window's first |T|
+    if (klo >= base && khi < base + n_c) {
+      const uint32_t rlo = klo - base, rhi = khi - base;
+      const uint32_t tlo = h3_select_u32(cand, n_c, rlo, hist);
+      uint32_t thi = tlo;
+      if (rhi != rlo) {  // the upper middle: the same value while enough |T| are <= it
+        uint32_t le = 0, gt = 0xFFFFFFFFu;
+        for (uint32_t i = threadIdx.x; i < n_c; i += WLM_WG) {
+          const uint32_t x = cand[i];
+          if (x <= tlo) ++le;
+          else gt = min(gt, x);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          le += (uint32_t)__shfl_xor((int)le, o);
+          gt = min(gt, (uint32_t)__shfl_xor((int)gt, o));
+        }
+        if (lane == 0) {
+          atomicAdd(&le_s, le);
+          atomicMin(&gt_s, gt);
+        }
+        __syncthreads();
+        if (le_s <= rhi) thi = gt_s;
+      }
+      med = ((double)tlo * sc + (double)thi * sc) / 2.0;
+    } else {
+      fb = true;
+    }
+  }
+  if (fb) {
+    // exact full-image selection: the reference's fp64 |dd| of every position (wl_dd1_key), then
+    // the radix passes of wl_haar_median over them
+    for (uint32_t p0 = threadIdx.x; p0 < P; p0 += BQ * WLM_WG) {
+      Dd1Raw q[BQ];
+#pragma unroll
+      for (int u = 0; u < BQ; ++u)
+        q[u] = wl_dd1_load(src, img, Lt.h, row_stride, min(p0 + (uint32_t)u * WLM_WG, P - 1), (int)W1);
+#pragma unroll
+      for (int u = 0; u < BQ; ++u)
+        if (p0 + (uint32_t)u * WLM_WG < P)
+          kd[p0 + (uint32_t)u * WLM_WG] =
+              __longlong_as_double((long long)wl_dd1_eval<true>(q[u], c, mn, inv, rcp));
+    }
+    __syncthreads();
+    RadixState rsx{0ull, 0ull, 0u};
+    radix_pass(kd, P, 52, 11, rsx, hist, &total);
+    if (total) {
+      radix_pass(kd, P, 41, 11, rsx, hist, nullptr);
+      radix_pass(kd, P, 30, 11, rsx, hist, nullptr);
+      radix_pass(kd, P, 19, 11, rsx, hist, nullptr);
+      radix_pass(kd, P, 8, 11, rsx, hist, nullptr);
+      radix_pass(kd, P, 0, 8, rsx, hist, nullptr);
+      const unsigned long long lo_key = rsx.prefix;
+      const double vlo = __longlong_as_double((long long)lo_key);
+      double vhi = vlo;
+      if ((total - 1) / 2 != total / 2) {
+        uint32_t le = 0;
+        unsigned long long gt = ~0ull;
+        for (uint32_t k = threadIdx.x; k < P; k += WLM_WG) {
+          const unsigned long long key = absbits(kd[k]);
+          if (key == 0ull) continue;
+          if (key <= lo_key) ++le;
+          else gt = key < gt ? key : gt;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          le += (uint32_t)__shfl_xor((int)le, o);
+          const unsigned long long og = (unsigned long long)__shfl_xor((long long)gt, o);
+          gt = og < gt ? og : gt;
+        }
+        if (lane == 0) {
+          atomicAdd(&lek_s, le);
+          atomicMin(&gtk_s, gt);
+        }
+        __syncthreads();
+        if (lek_s <= total / 2) vhi = __longlong_as_double((long long)gtk_s);
+      }
+      med = (vlo + vhi) / 2.0;
+    } else {
+      med = NAN;
+    }
+  }
+  // 3. sums of squares (wl_h3_stats' unscaled partials, in workgroup order) and thresholds
+  __shared__ double sums[9];
+  for (int k = wave; k < 9; k += WLM_WG / 64) {
+    const int l = k / 3, b = k - 3 * l;
+    const double* p = part + img * Lt.part_per_img + (size_t)(c * 3 + b) * (Lt.part_per_img / 9) +
+                      (size_t)l * nwg;
+    double s = 0.0;
+    for (int t = lane; t < nwg; t += 64) s += p[t];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+      const double sl = ldexp(sc, -l);  // level l + 1's coefficient scale
+      sums[k] = s * (sl * sl);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  constexpr int L = 3;
+  st[WlStats::median(c, L)] = med;
+  st[WlStats::DIAG + c] = (double)total;
+  sel[c].fb = fb ? 1u : 0u;
+  const double sigma = med / 0.6744897501960817;
+  const bool bad = !(mx > mn) || !(sigma == sigma);
+  const double var = sigma * sigma;
+  for (int l = 0; l < L; ++l)
+    for (int b = 0; b < 3; ++b) {
+      const double sq = sums[3 * l + b];
+      st[WlStats::sumsq(c, l, b, L)] = sq;
+      const double cnt = (double)Lt.H[l + 1] * Lt.W[l + 1];
+      const double t = var / sqrt(fmax(sq / cnt - var, 2.220446049250313e-16));
+      st[WlStats::thr(c, l, b, L)] = t;
+      st[WlStats::thrh(c, l, b)] = 0.5 * t;
+    }
+  if (bad) st[WlStats::FLAG] = 1.0;
+  h3_consts(st, c);
+}

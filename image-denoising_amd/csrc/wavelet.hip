@@ -3521,6 +3521,8 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
   if (part) wl_sums_thresh(st, part + img * Ls.part_per_img, c, Ls, Lt, med, mn, mx);
 }
 
+#include "haar3.hpp"
+
 template <int L>
 static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8, float* out_f32,
                         const WlLayout& Lt, int64_t row_stride, void* ws, hipStream_t st,
@@ -3533,6 +3535,27 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
   const int nwg = (nthr + WLH_WG - 1) / WLH_WG;
   hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n,
                      ycc_keys);
+  if constexpr (L == 3) {
+    // round 6 (haar3.hpp): window sample, one statistics read, sigma, one synthesis read
+    // (IDN_WAVELET_H3=0: the round-4 passes below)
+    const int nwg1 = h3_strips(Lt.w) * h3_chunks(Lt.h);
+    if (src && !ycc_keys && knob("IDN_WAVELET_H3", 1) && (size_t)(3 * nwg1) <= Lt.part_per_img / 9) {
+      hipLaunchKernelGGL(wl_h3_window, dim3(n), dim3(H3_WIN_WG), 0, st, src, Lt.h, Lt.w, row_stride,
+                         stats, knob("IDN_WAVELET_H3FB", 0));
+      hipLaunchKernelGGL(wl_h3_stats, dim3(nwg1, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+                         row_stride, wsf, Lt.img_floats, stats, part, Lt.part_per_img);
+      hipLaunchKernelGGL(wl_h3_sigma, dim3(n * 3), dim3(WLM_WG), 0, st, src, row_stride, wsf,
+                         Lt.img_floats, stats, Lt, (const double*)part, nwg1);
+      const bool gen = out_f32 || !out_u8 || ((uintptr_t)out_u8 & 3) != 0;
+      if (gen)
+        hipLaunchKernelGGL(wl_h3_synth<true>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+                           row_stride, (const double*)stats, out_u8, out_f32);
+      else
+        hipLaunchKernelGGL(wl_h3_synth<false>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h,
+                           Lt.w, row_stride, (const double*)stats, out_u8, (float*)nullptr);
+      return;
+    }
+  }
   if (!ycc_keys) {
     const int64_t np = (int64_t)Lt.h * Lt.w;
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
@@ -3575,6 +3598,21 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     hipLaunchKernelGGL((wl_haar_median<L>), dim3(n * 3), dim3(WLM_WG), 0, st, src, in64, row_stride,
                        wsf, Lt.img_floats, stats, Lt, (const double*)nullptr, Ls);
     hipLaunchKernelGGL(wl_thresh, dim3(n), dim3(64), 0, st, stats, Lt);
+  }
+  if constexpr (L == 3) {
+    // round 6: fp32 synthesis with the level-1 groups paired (IDN_WAVELET_H3S=0: the round-4
+    // kernel below)
+    if (src && knob("IDN_WAVELET_INTSYNTH", 1) && knob("IDN_WAVELET_H3S", 1)) {
+      hipLaunchKernelGGL(wl_h3_consts, dim3((3 * n + 63) / 64), dim3(64), 0, st, stats, n);
+      const bool gen = out_f32 || !out_u8 || ((uintptr_t)out_u8 & 3) != 0;
+      if (gen)
+        hipLaunchKernelGGL(wl_h3_synth<true>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+                           row_stride, (const double*)stats, out_u8, out_f32);
+      else
+        hipLaunchKernelGGL(wl_h3_synth<false>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h,
+                           Lt.w, row_stride, (const double*)stats, out_u8, (float*)nullptr);
+      return;
+    }
   }
   if constexpr (L >= 2) {
     if (src && knob("IDN_WAVELET_INTSYNTH", 1)) {
