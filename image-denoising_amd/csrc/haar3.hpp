@@ -27,8 +27,12 @@
 // count stays exact: every T = 0 position that is not an equal-triple pair (exact 0, x - x) is
 // evaluated with the reference's fp64 chain.
 
+// wl_h3_stats / wl_h3_synth grid: a workgroup of WLH_WG threads = WLH_WG / 4 quads = the 8x8 blocks
+// of H3_COLS consecutive block columns (a column strip), walking a chunk of block rows
+constexpr int H3_COLS = WLH_WG / 4;
+__host__ __device__ inline int h3_strips(int w) { return ((w >> 3) + H3_COLS - 1) / H3_COLS; }
 constexpr int H3_SEL = 66;   // stats doubles [66, 78): per channel 8 u32 (H3Sel)
-constexpr int H3_CST = 112;  // stats doubles [112, 148): per channel 24 floats (H3Const)
+constexpr int H3_CST = 112;  // stats doubles [112, 154): per channel 28 floats (H3Const)
 struct H3Sel {
   uint32_t lo, hi;  // window of |T| (wl_h3_window)
   uint32_t n_t;     // nonzero finest T (wl_h3_stats)
@@ -43,14 +47,26 @@ struct H3Const {  // fp32 synthesis constants of one channel (wl_h3_consts)
   float t1[3], t2[3], t3[3];  // soft thresholds in the same (folded) units
   float ka;                   // level-3 approximation offset
   float rng, mo;              // de-normalisation: v * rng + mo (mo = min - YCbCr offset)
-  float pad[3];
+  float mr[3], br[3];         // this channel's column of the output map (H3Rgb): 255 R[k][c] rng,
+  float pad;                  // and its part of the offsets, 255 R[k][c] mo
 };
-static_assert(sizeof(H3Const) == 24 * sizeof(float), "24 floats per channel");
+static_assert(sizeof(H3Const) == 28 * sizeof(float), "28 floats per channel");
+struct H3Rgb {     // out_k = sum_c m[k][c] v_c + b[k], v_c the clipped [0, 1] synthesis output of
+  float m[3][3];  // channel c: skimage's ycbcr2rgb rows x 255 x range_c; the de-normalisation
+  float b[3];     // offsets in b (minus 0.5: the U8 cast rounds to nearest, see wl_h3_synth)
+};
 __host__ __device__ inline H3Sel* h3_sel(double* st) { return reinterpret_cast<H3Sel*>(st + H3_SEL); }
 __host__ __device__ inline const H3Const* h3_cst(const double* st) {
   return reinterpret_cast<const H3Const*>(st + H3_CST);
 }
 
+// skimage ycbcr2rgb (the inverse of rgb2ycbcr's matrix, per unit of Y - 16, Cb - 128, Cr - 128)
+__host__ __device__ constexpr double h3_r(int k, int c) {
+  constexpr double R[3][3] = {{0.004566210045662101, 1.1808799897950177e-09, 0.006258928969943937},
+                              {0.004566210045662101, -0.0015363236860449021, -0.003188110949655707},
+                              {0.004566210045662101, 0.007910716233554741, 1.1977497040511743e-08}};
+  return R[k][c];
+}
 // The synthesis constants from the stats block (min / max, half thresholds thrh, flag).  With
 // s1 = 0.5 / (255000 range) and k = 2 (offset - min) / range (wl_haar_synth_int), and the idwt's
 // factors 1/2 folded into the coefficients (a power of two commutes with soft()):
@@ -76,11 +92,30 @@ __device__ void h3_consts(double* st, int c) {
   q->ka = (float)(0.5 * k);
   q->rng = (float)inv;
   q->mo = (float)(mn - (c == 0 ? 16.0 : 128.0));
+  for (int j = 0; j < 3; ++j) {
+    q->mr[j] = (float)(255.0 * h3_r(j, c) * inv);
+    q->br[j] = (float)(255.0 * h3_r(j, c) * (mn - (c == 0 ? 16.0 : 128.0)));
+  }
+}
+__device__ __forceinline__ float uniform_f32(float v) {  // a wave-uniform float into an SGPR
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+// out_k = 255 sum_c R[k][c] (v_c rng_c + mo_c) - 0.5 from the three channels' columns (H3Const)
+__device__ __forceinline__ H3Rgb h3_rgb(const H3Const* K) {
+  H3Rgb o;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o.m[k][c] = K[c].mr[k];
+    o.b[k] = uniform_f32(((K[0].br[k] - 0.5f) + K[1].br[k]) + K[2].br[k]);
+  }
+  return o;
 }
 __global__ void wl_h3_consts(double* __restrict__ stats, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < 3 * n) h3_consts(stats + (size_t)(i / 3) * WL_STATS, i % 3);
 }
+
 
 // ---- wl_h3_synth ---------------------------------------------------------------------------------
 typedef float h3f2 __attribute__((ext_vector_type(2)));
@@ -109,78 +144,107 @@ __device__ __forceinline__ h3f2 splat2(float v) { return h3f2{v, v}; }
 // tolerance of the fp64 form (fp32 throughout: the synthesis is continuous in its inputs and no
 // exact zero depends on it).  GEN = false: u8 output only, dword-aligned rows (the product's
 // case); true: any of u8 (byte stores) / f32 output.
+#ifndef IDN_H3S_IT  // block rows per synthesis thread (A/B builds set it)
+#define IDN_H3S_IT 2
+#endif
+constexpr int H3S_IT = IDN_H3S_IT;
+__host__ __device__ inline int h3s_chunks(int h) { return ((h >> 3) + H3S_IT - 1) / H3S_IT; }
+#ifndef IDN_H3S_WPE
+#define IDN_H3S_WPE 1
+#endif
 template <bool GEN>
-__global__ __launch_bounds__(WLH_WG) void wl_h3_synth(const uint8_t* __restrict__ src, int h, int w,
+__global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_WPE))) void wl_h3_synth(const uint8_t* __restrict__ src, int h, int w,
                                                       int64_t row_stride,
                                                       const double* __restrict__ stats,
                                                       uint8_t* __restrict__ out_u8,
                                                       float* __restrict__ out_f32) {
+  // grid: (column strips of 32 blocks x chunks of H3S_IT block rows, images), as wl_h3_stats
   const int img = blockIdx.y;
-  const int nbx = w >> 3, nblk = nbx * (h >> 3);
-  const int tid = blockIdx.x * WLH_WG + threadIdx.x;
-  const int blk = tid >> 2, sub = tid & 3;
-  const bool act = blk < nblk;  // uniform over each quad
+  const int nbx = w >> 3, nby = h >> 3, strips = h3_strips(w);
+  const int strip = (int)blockIdx.x % strips, chunk = (int)blockIdx.x / strips;
+  const int sub = threadIdx.x & 3, bx = strip * H3_COLS + (threadIdx.x >> 2);
+  const int by0 = chunk * H3S_IT, nit = min(H3S_IT, nby - by0);
+  const bool act = bx < nbx;  // uniform over each quad
   const double* st = stats + (size_t)img * WL_STATS;
   const H3Const* K = h3_cst(st);
-  int y0 = 0, x0 = 0;
-  uint32_t q[4][3] = {};
-  const uint8_t* ib = src + (int64_t)img * h * row_stride;
-  if (act) {
-    const int by = blk / nbx, bx = blk - by * nbx;
-    y0 = by * 8 + (sub >> 1) * 4;
-    x0 = bx * 8 + (sub & 1) * 4;
+  const int x0 = bx * 8 + (sub & 1) * 4;
+  const int64_t img_off = (int64_t)img * h * row_stride;
+  const uint8_t* ib = src + img_off + (int64_t)(8 * by0 + (sub >> 1) * 4) * row_stride + (int64_t)x0 * 3;
+  auto load_q = [&](int it, uint32_t (&qq)[4][3]) {
+    if (!act || it >= nit) return;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + (int64_t)(y0 + r) * row_stride +
-                                                            (int64_t)x0 * 3);
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(ib + (int64_t)it * 8 * row_stride + r * row_stride);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) q[r][k] = p[k];
+      for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
     }
-  }
-  auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
-  // level-1 integer combinations of the four 2x2 groups (g = 2 gy + gx), rgb
-  int S4[4][3], D1[4][3][3];  // [group][rgb] sums, [group][band][rgb] details
+  };
+  uint32_t qn[4][3] = {};
+  load_q(0, qn);
+#pragma unroll 1
+  for (int it = 0; it < nit; ++it) {
+  const int y0 = 8 * (by0 + it) + (sub >> 1) * 4;
+  uint32_t q[4][3];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) q[r][k] = qn[r][k];
+  load_q(it + 1, qn);
+  // the bytes as floats (v_cvt_f32_ubyte): every combination below is an exact small integer
+  auto pxf = [&](int r, int k) { return (float)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+  // level 1 on the group pairs (gx = 0, 1 of row pair gy) as fp32 pairs: S1[gy][rgb] sums,
+  // D1[gy][band][rgb] details
+  h3f2 S1[2][3], D1[2][3][3];
+#pragma unroll
+  for (int gy = 0; gy < 2; ++gy)
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-      const int gy = g >> 1, gx = g & 1;
-      haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
-               px(2 * gy + 1, 6 * gx + 3 + ch), S4[g][ch], D1[g][0][ch], D1[g][1][ch], D1[g][2][ch]);
+      const h3f2 x00 = {pxf(2 * gy, ch), pxf(2 * gy, 6 + ch)}, x01 = {pxf(2 * gy, 3 + ch), pxf(2 * gy, 9 + ch)};
+      const h3f2 x10 = {pxf(2 * gy + 1, ch), pxf(2 * gy + 1, 6 + ch)},
+                 x11 = {pxf(2 * gy + 1, 3 + ch), pxf(2 * gy + 1, 9 + ch)};
+      const h3f2 lo0 = x00 + x10, lo1 = x01 + x11, hi0 = x00 - x10, hi1 = x01 - x11;
+      S1[gy][ch] = lo0 + lo1;
+      D1[gy][0][ch] = lo0 - lo1;
+      D1[gy][1][ch] = hi0 + hi1;
+      D1[gy][2][ch] = hi0 - hi1;
     }
-  int S16[3], D2[3][3];
+  // level 2 on the four groups' sums (g0 g1 / g2 g3 = S1[0].x .y / S1[1].x .y)
+  float S16[3], fd2[3][3];
 #pragma unroll
-  for (int ch = 0; ch < 3; ++ch)
-    haar_int(S4[0][ch], S4[1][ch], S4[2][ch], S4[3][ch], S16[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
-  int S64[3], D3[3][3];
+  for (int ch = 0; ch < 3; ++ch) {
+    const h3f2 lo = S1[0][ch] + S1[1][ch], hi = S1[0][ch] - S1[1][ch];
+    S16[ch] = lo.x + lo.y;
+    fd2[0][ch] = lo.x - lo.y;
+    fd2[1][ch] = hi.x + hi.y;
+    fd2[2][ch] = hi.x - hi.y;
+  }
+  // level 3 across the quad
+  float f64s[3], fd3[3][3];
 #pragma unroll
-  for (int ch = 0; ch < 3; ++ch)
-    haar_int(quad_get(S16[ch], 0), quad_get(S16[ch], 1), quad_get(S16[ch], 2), quad_get(S16[ch], 3),
-             S64[ch], D3[0][ch], D3[1][ch], D3[2][ch]);
-  if (!act) return;
+  for (int ch = 0; ch < 3; ++ch) {
+    const int b16 = __float_as_int(S16[ch]);
+    const float x00 = __int_as_float(quad_get(b16, 0)), x01 = __int_as_float(quad_get(b16, 1));
+    const float x10 = __int_as_float(quad_get(b16, 2)), x11 = __int_as_float(quad_get(b16, 3));
+    const float lo0 = x00 + x10, lo1 = x01 + x11, hi0 = x00 - x10, hi1 = x01 - x11;
+    f64s[ch] = lo0 + lo1;
+    fd3[0][ch] = lo0 - lo1;
+    fd3[1][ch] = hi0 + hi1;
+    fd3[2][ch] = hi0 - hi1;
+  }
+  if (!act) continue;
   if (st[WlStats::FLAG] != 0.0) {  // image-uniform: zeros (0.14.2's NaN -> U8 0)
 #pragma unroll 1
     for (int r = 0; r < 4; ++r)
 #pragma unroll 1
       for (int k = 0; k < 12; ++k) {
         const int y = y0 + r, xx = x0 + k / 3, c = k % 3;
-        if (out_u8) out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] = 0;
+        if (out_u8) out_u8[img_off + (int64_t)y * row_stride + (int64_t)xx * 3 + c] = 0;
         if (out_f32) out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] = 0.0f;
       }
-    return;
+    continue;
   }
   // lane signs of this sub-block's output in the level-3 butterfly (r = sub >> 1, s = sub & 1)
   const float sad = (sub & 1) ? -1.f : 1.f, sda = (sub & 2) ? -1.f : 1.f, sdd = sad * sda;
-  float f64s[3], fd3[3][3], fd2[3][3];
-#pragma unroll
-  for (int ch = 0; ch < 3; ++ch) {
-    f64s[ch] = (float)S64[ch];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      fd3[b][ch] = (float)D3[b][ch];
-      fd2[b][ch] = (float)D2[b][ch];
-    }
-  }
   // per channel: level 3 -> a2, level 2 -> the four groups' level-1 approximations
   float A1[3][4];
 #pragma unroll
@@ -203,10 +267,7 @@ __global__ __launch_bounds__(WLH_WG) void wl_h3_synth(const uint8_t* __restrict_
     A1[c][3] = m - q1;
   }
   // level 1: groups (0, 1) and (2, 3) side by side -> pixel values v[pair][pixel (r, s)][c]
-  constexpr float Rf[3][3] = {
-      {(float)(0.004566210045662101 * 255), (float)(1.1808799897950177e-09 * 255), (float)(0.006258928969943937 * 255)},
-      {(float)(0.004566210045662101 * 255), (float)(-0.0015363236860449021 * 255), (float)(-0.003188110949655707 * 255)},
-      {(float)(0.004566210045662101 * 255), (float)(0.007910716233554741 * 255), (float)(1.1977497040511743e-08 * 255)}};
+  const H3Rgb M = h3_rgb(K);
   const bool dw = !GEN;
 #pragma unroll
   for (int gp = 0; gp < 2; ++gp) {  // pair gp: groups 2 gp (x of the pair) and 2 gp + 1 (y)
@@ -216,12 +277,9 @@ __global__ __launch_bounds__(WLH_WG) void wl_h3_synth(const uint8_t* __restrict_
       const H3Const& k = K[c];
       h3f2 d[3];
 #pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const h3f2 D0 = {(float)D1[2 * gp][b][0], (float)D1[2 * gp + 1][b][0]};
-        const h3f2 Dg = {(float)D1[2 * gp][b][1], (float)D1[2 * gp + 1][b][1]};
-        const h3f2 Db = {(float)D1[2 * gp][b][2], (float)D1[2 * gp + 1][b][2]};
-        d[b] = soft_f2(fma2(splat2(k.w1[2]), Db, fma2(splat2(k.w1[1]), Dg, splat2(k.w1[0]) * D0)), k.t1[b]);
-      }
+      for (int b = 0; b < 3; ++b)
+        d[b] = soft_f2(fma2(splat2(k.w1[2]), D1[gp][b][2],
+                            fma2(splat2(k.w1[1]), D1[gp][b][1], splat2(k.w1[0]) * D1[gp][b][0])), k.t1[b]);
       const h3f2 A = {A1[c][2 * gp], A1[c][2 * gp + 1]};
       const h3f2 p = A + d[0], m = A - d[0], q0 = d[1] + d[2], q1 = d[1] - d[2];
       v[0][c] = p + q0;
@@ -229,50 +287,48 @@ __global__ __launch_bounds__(WLH_WG) void wl_h3_synth(const uint8_t* __restrict_
       v[2][c] = p - q0;
       v[3][c] = m - q1;
     }
-    // inner clip [0, 1], de-normalise, YCbCr -> RGB x 255, truncate, saturate to u8
+    // inner clip [0, 1]; de-normalisation, YCbCr -> RGB x 255 and the offsets in one affine map
+    // (H3Rgb, its bias minus 0.5); the cast: round to nearest with saturation
     uint32_t rowp[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = i >> 1, s = i & 1;
-      h3f2 e[3];
+      h3f2 vc[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        vc[c] = h3f2{__builtin_amdgcn_fmed3f(v[i][c].x, 0.f, 1.f), __builtin_amdgcn_fmed3f(v[i][c].y, 0.f, 1.f)};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const h3f2 vc = {__builtin_amdgcn_fmed3f(v[i][c].x, 0.f, 1.f),
-                         __builtin_amdgcn_fmed3f(v[i][c].y, 0.f, 1.f)};
-        e[c] = fma2(vc, splat2(K[c].rng), splat2(K[c].mo));
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const h3f2 o = fma2(e[2], splat2(Rf[c][2]), fma2(e[1], splat2(Rf[c][1]), e[0] * splat2(Rf[c][0])));
+        const h3f2 o = fma2(vc[2], splat2(M.m[c][2]),
+                            fma2(vc[1], splat2(M.m[c][1]), fma2(vc[0], splat2(M.m[c][0]), splat2(M.b[c]))));
 #pragma unroll
         for (int g2 = 0; g2 < 2; ++g2) {  // group 2 gp + g2: pixel column 2 g2 + s
-          const float of = g2 ? o.y : o.x;
+          const float of = g2 ? o.y : o.x;  // out - 0.5
           const int xx = x0 + 2 * g2 + s, y = y0 + 2 * gp + r;
           if (dw) {
             const int bi = (2 * g2 + s) * 3 + c;
-            rowp[r][bi >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_truncf(of), bi & 3,
-                                                              rowp[r][bi >> 2]);
+            rowp[r][bi >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(of, bi & 3, rowp[r][bi >> 2]);
           } else if (out_u8) {
-            out_u8[(int64_t)img * h * row_stride + (int64_t)y * row_stride + (int64_t)xx * 3 + c] =
-                (uint8_t)min(max((int)of, 0), 255);
+            out_u8[img_off + (int64_t)y * row_stride + (int64_t)xx * 3 + c] =
+                (uint8_t)(__builtin_amdgcn_cvt_pk_u8_f32(of, 0, 0u) & 0xFFu);
           }
           if (GEN && out_f32)
             out_f32[(((int64_t)img * h + y) * w + xx) * 3 + c] =
-                __builtin_amdgcn_fmed3f(of, 0.f, 255.f) * (1.f / 255.f);
+                __builtin_amdgcn_fmed3f(of + 0.5f, 0.f, 255.f) * (1.f / 255.f);
         }
       }
     }
     if (dw) {
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        uint32_t* p = reinterpret_cast<uint32_t*>(out_u8 + (int64_t)img * h * row_stride +
-                                                  (int64_t)(y0 + 2 * gp + r) * row_stride +
+        uint32_t* p = reinterpret_cast<uint32_t*>(out_u8 + img_off + (int64_t)(y0 + 2 * gp + r) * row_stride +
                                                   (int64_t)x0 * 3);
 #pragma unroll
         for (int j = 0; j < 3; ++j) p[j] = rowp[r][j];
       }
     }
   }
+  }  // it
 }
 
 // ---- wl_h3_window ---------------------------------------------------------------------------------
@@ -456,8 +512,6 @@ __device__ __forceinline__ int ykey(int c, int r, int g, int b) {  // exact YCbC
 // position advance by constants (no per-step index division).  Grid: (column strips x row
 // chunks, images).  Workspace (the image's slot): |T| candidates [3][P] u32, residues [P] u32
 // (level-1 position | channel mask << 28), P = (h / 2) (w / 2).
-constexpr int H3_COLS = WLH_WG / 4;  // block columns per workgroup
-__host__ __device__ inline int h3_strips(int w) { return ((w >> 3) + H3_COLS - 1) / H3_COLS; }
 __host__ __device__ inline int h3_chunks(int h) { return ((h >> 3) + H3_IT - 1) / H3_IT; }
 __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_WPE))) void wl_h3_stats(const uint8_t* __restrict__ src, int h, int w,
                                                       int64_t row_stride, wreal* __restrict__ ws,

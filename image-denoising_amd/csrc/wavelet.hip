@@ -3548,10 +3548,10 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
                          Lt.img_floats, stats, Lt, (const double*)part, nwg1);
       const bool gen = out_f32 || !out_u8 || ((uintptr_t)out_u8 & 3) != 0;
       if (gen)
-        hipLaunchKernelGGL(wl_h3_synth<true>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+        hipLaunchKernelGGL(wl_h3_synth<true>, dim3(h3_strips(Lt.w) * h3s_chunks(Lt.h), n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
                            row_stride, (const double*)stats, out_u8, out_f32);
       else
-        hipLaunchKernelGGL(wl_h3_synth<false>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h,
+        hipLaunchKernelGGL(wl_h3_synth<false>, dim3(h3_strips(Lt.w) * h3s_chunks(Lt.h), n), dim3(WLH_WG), 0, st, src, Lt.h,
                            Lt.w, row_stride, (const double*)stats, out_u8, (float*)nullptr);
       return;
     }
@@ -3606,10 +3606,10 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
       hipLaunchKernelGGL(wl_h3_consts, dim3((3 * n + 63) / 64), dim3(64), 0, st, stats, n);
       const bool gen = out_f32 || !out_u8 || ((uintptr_t)out_u8 & 3) != 0;
       if (gen)
-        hipLaunchKernelGGL(wl_h3_synth<true>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+        hipLaunchKernelGGL(wl_h3_synth<true>, dim3(h3_strips(Lt.w) * h3s_chunks(Lt.h), n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
                            row_stride, (const double*)stats, out_u8, out_f32);
       else
-        hipLaunchKernelGGL(wl_h3_synth<false>, dim3(nwg, n), dim3(WLH_WG), 0, st, src, Lt.h,
+        hipLaunchKernelGGL(wl_h3_synth<false>, dim3(h3_strips(Lt.w) * h3s_chunks(Lt.h), n), dim3(WLH_WG), 0, st, src, Lt.h,
                            Lt.w, row_stride, (const double*)stats, out_u8, (float*)nullptr);
       return;
     }
