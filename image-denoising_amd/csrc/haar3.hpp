@@ -152,16 +152,22 @@ __host__ __device__ inline int h3s_chunks(int h) { return ((h >> 3) + H3S_IT - 1
 #ifndef IDN_H3S_WPE
 #define IDN_H3S_WPE 1
 #endif
+#ifndef IDN_H3S_XCD
+#define IDN_H3S_XCD 0
+#endif
 template <bool GEN>
 __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_WPE))) void wl_h3_synth(const uint8_t* __restrict__ src, int h, int w,
                                                       int64_t row_stride,
                                                       const double* __restrict__ stats,
                                                       uint8_t* __restrict__ out_u8,
                                                       float* __restrict__ out_f32) {
-  // grid: (column strips of 32 blocks x chunks of H3S_IT block rows, images), as wl_h3_stats
-  const int img = blockIdx.y;
+  // grid: (column strips of 32 blocks x chunks of H3S_IT block rows, images); IDN_H3S_XCD: in
+  // XCD-contiguous order, as wl_h3_stats
+  const int lin0 = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  const int lin = IDN_H3S_XCD ? xcd_contiguous_block(lin0, (int)(gridDim.x * gridDim.y)) : lin0;
+  const int img = lin / (int)gridDim.x, wg = lin - img * (int)gridDim.x;
   const int nbx = w >> 3, nby = h >> 3, strips = h3_strips(w);
-  const int strip = (int)blockIdx.x % strips, chunk = (int)blockIdx.x / strips;
+  const int strip = wg % strips, chunk = wg / strips;
   const int sub = threadIdx.x & 3, bx = strip * H3_COLS + (threadIdx.x >> 2);
   const int by0 = chunk * H3S_IT, nit = min(H3S_IT, nby - by0);
   const bool act = bx < nbx;  // uniform over each quad
@@ -502,6 +508,19 @@ __device__ __forceinline__ float h3_ycf(int c, int k) {
   return W[c][k];
 }
 constexpr float H3_PTOL = 0.0625f;
+// the RGB cube corner (bits: r g b = 255) where channel c's YCbCr dot is lowest / highest
+__device__ __forceinline__ int h3_corner(int c, bool hi) {
+  constexpr int C[3][2] = {{0b000, 0b111}, {0b110, 0b001}, {0b011, 0b100}};
+  return C[c][hi ? 1 : 0];
+}
+__device__ __forceinline__ float h3_corner_proxy(int k, int c) {  // as the loop's proxy (x 255)
+  const float R = (k & 4) ? 255.f : 0.f, G = (k & 2) ? 255.f : 0.f, B = (k & 1) ? 255.f : 0.f;
+  return __fmaf_rn(h3_ycf(c, 2), B, __fmaf_rn(h3_ycf(c, 1), G, h3_ycf(c, 0) * R));
+}
+__device__ __forceinline__ void h3_corner_dots(int k, double (&d)[3]) {  // wl_color_minmax's chain
+  const double v = 255.0 * (1.0 / 255.0);
+  ycc_dots((k & 4) ? v : 0.0, (k & 2) ? v : 0.0, (k & 1) ? v : 0.0, d);
+}
 __device__ __forceinline__ int ykey(int c, int r, int g, int b) {  // exact YCbCr dot x 255000
   return __mul24(ycc_w(c, 0), r) + __mul24(ycc_w(c, 1), g) + __mul24(ycc_w(c, 2), b);
 }
@@ -518,10 +537,12 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
                                                       size_t img_floats, double* __restrict__ stats,
                                                       double* __restrict__ part, size_t part_per_img) {
   constexpr int L = 3;
-  const int img = blockIdx.y;
+  // XCD-contiguous order over (image, chunk, strip): a strip's neighbours share its edge lines
+  const int lin = xcd_contiguous_block((int)(blockIdx.y * gridDim.x + blockIdx.x), (int)(gridDim.x * gridDim.y));
+  const int img = lin / (int)gridDim.x, wg = lin - img * (int)gridDim.x;
   const int nbx = w >> 3, nby = h >> 3;
   const int strips = h3_strips(w);
-  const int strip = (int)blockIdx.x % strips, chunk = (int)blockIdx.x / strips;
+  const int strip = wg % strips, chunk = wg / strips;
   const int sub = threadIdx.x & 3, bx = strip * H3_COLS + (threadIdx.x >> 2);
   const int by0 = chunk * H3_IT, nit = min(H3_IT, nby - by0);  // block rows of this workgroup
   const bool colact = bx < nbx;
@@ -558,6 +579,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
     for (int k = 0; k < 6; ++k) mom[b][k] = 0;
   float pmn[3] = {INFINITY, INFINITY, INFINITY}, pmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  uint32_t smn[3] = {0u, 0u, 0u}, smx[3] = {0u, 0u, 0u};  // steps near the lane's extremes
   uint32_t ct[3] = {0u, 0u, 0u}, cl[3] = {0u, 0u, 0u};  // per-lane counts
   uint32_t na[4] = {0u, 0u, 0u, 0u};                    // this lane's filled slots
   auto mom_lds = [&](int l, int b, int r, int g, int bl) {
@@ -621,20 +643,33 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     auto pxf = [&](int r, int k) { return (float)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
     // fp32 proxies of the YCbCr dots (x 255) of pixel pairs: per lane min / max (exact values
     // only where a lane is within H3_PTOL of the workgroup's extreme, after the loop)
-    if (act && !(IDN_H3_PROBE & 1))
+    // Per extreme, a mask of the steps whose pixels come within H3_PTOL of the lane's running
+    // extreme (reset when the extreme moves past it): at the end it holds every step with a pixel
+    // within H3_PTOL of the lane's final extreme, the only steps a rescan reads.
+    if (act && !(IDN_H3_PROBE & 1)) {
+      float imn[3] = {INFINITY, INFINITY, INFINITY}, imx[3] = {-INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int pp = 0; pp < 2; ++pp) {
-        const h3f2 R = {pxf(r, 6 * pp), pxf(r, 6 * pp + 3)}, G = {pxf(r, 6 * pp + 1), pxf(r, 6 * pp + 4)},
-                   B = {pxf(r, 6 * pp + 2), pxf(r, 6 * pp + 5)};
+        for (int pp = 0; pp < 2; ++pp) {
+          const h3f2 R = {pxf(r, 6 * pp), pxf(r, 6 * pp + 3)}, G = {pxf(r, 6 * pp + 1), pxf(r, 6 * pp + 4)},
+                     B = {pxf(r, 6 * pp + 2), pxf(r, 6 * pp + 5)};
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const h3f2 k2 = fma2(splat2(h3_ycf(c, 2)), B, fma2(splat2(h3_ycf(c, 1)), G, splat2(h3_ycf(c, 0)) * R));
-          pmn[c] = __builtin_fminf(pmn[c], __builtin_fminf(k2.x, k2.y));
-          pmx[c] = __builtin_fmaxf(pmx[c], __builtin_fmaxf(k2.x, k2.y));
+          for (int c = 0; c < 3; ++c) {
+            const h3f2 k2 = fma2(splat2(h3_ycf(c, 2)), B, fma2(splat2(h3_ycf(c, 1)), G, splat2(h3_ycf(c, 0)) * R));
+            imn[c] = __builtin_fminf(imn[c], __builtin_fminf(k2.x, k2.y));
+            imx[c] = __builtin_fmaxf(imx[c], __builtin_fmaxf(k2.x, k2.y));
+          }
         }
+      const uint32_t bit = 1u << it;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        smn[c] = imn[c] < pmn[c] - H3_PTOL ? bit : (imn[c] <= pmn[c] + H3_PTOL ? smn[c] | bit : smn[c]);
+        smx[c] = imx[c] > pmx[c] + H3_PTOL ? bit : (imx[c] >= pmx[c] - H3_PTOL ? smx[c] | bit : smx[c]);
+        pmn[c] = __builtin_fminf(pmn[c], imn[c]);
+        pmx[c] = __builtin_fmaxf(pmx[c], imx[c]);
       }
+    }
     int a1[4][3];
 #pragma unroll
     for (int gy = 0; gy < 2; ++gy) {
@@ -770,7 +805,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
     for (int wv = 1; wv < WLH_WG / 64; ++wv) t += red[k][wv];
     part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + (size_t)l * gridDim.x +
-         blockIdx.x] = t;
+         (size_t)wg] = t;
   }
   if (threadIdx.x < 3) {
     atomicAdd(&sel[threadIdx.x].n_t, cnt_s[threadIdx.x]);
@@ -791,12 +826,33 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   // pixel there whose proxy is (exact ties differ in the last fp64 bits; the proxy's error is
   // below 0.03, distinct exact values 0.001 apart, so the extreme is among them)
   double dmn[3] = {INFINITY, INFINITY, INFINITY}, dmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  bool need = false;
+  // An extreme at the RGB cube's own (a corner: 0 / 255 channels, as saturated noise reaches) is
+  // that corner's value exactly: each corner is the only triple with its exact key and the next
+  // triple lies >= 18 proxy units away.  No rescan for those.
+  uint32_t steps = 0u;  // the steps that may hold a workgroup extreme
 #pragma unroll
-  for (int c = 0; c < 3; ++c) need |= pmn[c] <= gmn[c] + H3_PTOL || pmx[c] >= gmx[c] - H3_PTOL;
-  if (colact && need) {
+  for (int c = 0; c < 3; ++c) {
+    const int cmn = h3_corner(c, false), cmx = h3_corner(c, true);
+    const bool at_mn = gmn[c] <= h3_corner_proxy(cmn, c) + H3_PTOL;
+    const bool at_mx = gmx[c] >= h3_corner_proxy(cmx, c) - H3_PTOL;
+    double d[3];
+    if (at_mn) {
+      h3_corner_dots(cmn, d);
+      dmn[c] = d[c];
+    } else if (pmn[c] <= gmn[c] + H3_PTOL) {
+      steps |= smn[c];
+    }
+    if (at_mx) {
+      h3_corner_dots(cmx, d);
+      dmx[c] = d[c];
+    } else if (pmx[c] >= gmx[c] - H3_PTOL) {
+      steps |= smx[c];
+    }
+  }
+  if (colact && steps && !(IDN_H3_PROBE & 16)) {
 #pragma unroll 1
-    for (int it = 0; it < nit; ++it) {
+    for (; steps; steps &= steps - 1u) {
+      const int it = __builtin_ctz(steps);
       uint32_t q[4][3];
       load_q(it, q);
 #pragma unroll

@@ -136,4 +136,12 @@ __device__ __forceinline__ double u01_closed_open(uint32_t a, uint32_t b) {
   return (double)v * (1.0 / 9007199254740992.0);
 }
 
+// Workgroup renumbering for the 8 XCDs (dispatch places workgroup b on XCD b % 8): the returned
+// ids of each XCD's workgroups form one contiguous run, so neighbouring work items (halo rows, the
+// partial 128-byte lines at a strip's edges) run on the same XCD and meet in its L2
+__device__ __forceinline__ int xcd_contiguous_block(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 }  // namespace idn

@@ -233,10 +233,6 @@ __device__ __forceinline__ StripeGeom stripe_geom(int item, int lane, int rb, in
 //          blocks renumbered so each XCD walks a contiguous run of bands: vertical neighbours
 //          run on the same XCD at about the same time and their halo rows hit its L2
 //   map 2: as 1 without the XCD renumbering
-__device__ __forceinline__ int xcd_contiguous_block(int b, int nb) {
-  const int q = nb >> 3, r = nb & 7, x = b & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-}
 __device__ __forceinline__ int stripe_item(int map, int nseg) {
   const int wave = threadIdx.x >> 6;
   if (map == 0) return __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave);
