@@ -906,26 +906,38 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 }
 
 // ---- wl_h3_sigma ----------------------------------------------------------------------------------
-// rank `rank` of v[0..n) (u32), block-wide: three histogram passes of 11 / 11 / 10 bits
+// rank `rank` of v[0..n) (u32, all in [lo, lo + span]), block-wide: radix passes of up to 11 bits
+// over v - lo, as many as span needs (a 5 % window spans ~2^19: two passes), into H3_NH
+// histogram copies by lane (the values crowd into few bins; one copy serialises the LDS atomics)
+constexpr int H3_NH = 4;
 __device__ uint32_t h3_select_u32(const uint32_t* __restrict__ v, uint32_t n, uint32_t rank,
-                                  uint32_t* hist) {
+                                  uint32_t lo, uint32_t span, uint32_t* hist) {
+  const int nbits = max(32 - __clz((int)span), 1);  // bits of the largest offset
   uint32_t prefix = 0u, pmask = 0u;
 #pragma unroll 1
-  for (int p = 0; p < 3; ++p) {
-    const int sh = p == 0 ? 21 : p == 1 ? 10 : 0, nb = p == 2 ? 1024 : 2048;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0u;
+  for (int top = nbits; top > 0; top -= 11) {
+    const int wd = min(top, 11), sh = top - wd, nb = 1 << wd;
+    for (int k = threadIdx.x; k < H3_NH * nb; k += blockDim.x) hist[k] = 0u;
     __syncthreads();
+    uint32_t* hc = hist + (threadIdx.x & (H3_NH - 1)) * nb;
     for (uint32_t i0 = threadIdx.x; i0 < n; i0 += 4 * blockDim.x) {
       uint32_t x[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t i = i0 + (uint32_t)u * blockDim.x;
-        x[u] = i < n ? v[i] : 0u;
+        x[u] = i < n ? v[i] - lo : 0u;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (i0 + (uint32_t)u * blockDim.x < n && (x[u] & pmask) == prefix)
-          atomicAdd(&hist[(x[u] >> sh) & (uint32_t)(nb - 1)], 1u);
+          atomicAdd(&hc[(x[u] >> sh) & (uint32_t)(nb - 1)], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int cp = 0; cp < H3_NH; ++cp) t += hist[cp * nb + b];
+      hist[b] = t;
     }
     __syncthreads();
     const BinSel bs = select_bin(hist, nb, rank, nullptr, false);
@@ -933,7 +945,7 @@ __device__ uint32_t h3_select_u32(const uint32_t* __restrict__ v, uint32_t n, ui
     pmask |= (uint32_t)(nb - 1) << sh;
     rank = bs.rank;
   }
-  return prefix;
+  return prefix + lo;
 }
 
 // per (image, channel) workgroup of WLM_WG threads
@@ -999,7 +1011,8 @@ __global__ __launch_bounds__(WLM_WG) void wl_h3_sigma(const uint8_t* __restrict_
     const uint32_t base = nrnz + below;  // rank of the window's first |T|
     if (klo >= base && khi < base + n_c) {
       const uint32_t rlo = klo - base, rhi = khi - base;
-      const uint32_t tlo = h3_select_u32(cand, n_c, rlo, hist);
+      const uint32_t wlo = sel[c].lo, wspan = sel[c].hi - sel[c].lo;
+      const uint32_t tlo = h3_select_u32(cand, n_c, rlo, wlo, wspan, hist);
       uint32_t thi = tlo;
       if (rhi != rlo) {  // the upper middle: the same value while enough |T| are <= it
         uint32_t le = 0, gt = 0xFFFFFFFFu;
