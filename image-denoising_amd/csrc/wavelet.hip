@@ -86,6 +86,7 @@ inline int wl_max_level(int n, int F) {
 constexpr int WL_MAXL = 12;
 constexpr int RB_TY = 8, RB_TX = 32, RB_R = 4;  // analysis tile (wl_dwt_rb)
 constexpr int WL_STATS = 256;  // doubles of per-image stats
+constexpr int WL_N32U = 156;   // stats [156, 159): u32 counts of the N32 analysis' uncertain codes
 
 struct WlLayout {
   int n, h, w, F, L;
@@ -744,6 +745,66 @@ template <int SRC> constexpr int ws_pf() {
 }
 
 
+__device__ __forceinline__ double uniform_f64(double v) {  // a wave-uniform double into SGPRs
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)b);
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ int ycc_w(int c, int k) {  // rgb2ycbcr coefficients x 1000
+  constexpr int W[3][3] = {{65481, 128553, 24966}, {-37797, -74203, 112000}, {112000, -93786, -18214}};
+  return W[c][k];
+}
+// bior1.5: the level-1 highpass has two taps, so a finest dd is the 2x2 combination of the
+// normalised samples at rows 2i-4, 2i-3 and columns 2j-4, 2j-3 (pywt 'symmetric' indices), in
+// wl_dwt_stream's op order: the column highpass (two products, then their sum) of both columns,
+// then the row highpass.  The sigma median recomputes the few exact values it needs from the input
+// (wl_haar_median<1, true, true>), so the analysis keeps the level-1 dd band in fp32 only -- all
+// that the synthesis reads of it.
+__device__ __forceinline__ double bior_dd2x2(double x00, double x01, double x10, double x11) {
+  const double h0 = (-S2) * x10 + S2 * x00, h1 = (-S2) * x11 + S2 * x01;  // x[row][column]
+  return (-S2) * h1 + S2 * h0;
+}
+struct BiorDdRaw {  // u8: the dword holding each sample's 3 bytes, and the bit offset of the pixel
+  uint32_t v[2][2];
+  uint32_t sh[2];
+};
+__device__ __forceinline__ BiorDdRaw wl_bior_dd1_load(rsrc_t rs, int h, int w, int64_t row_stride,
+                                                      uint32_t pos, int W1) {
+  const int i = (int)(pos / (uint32_t)W1), j = (int)(pos - (uint32_t)i * (uint32_t)W1);
+  const int y[2] = {sym_idx(2 * i - 4, h), sym_idx(2 * i - 3, h)};
+  const int x[2] = {sym_idx(2 * j - 4, w), sym_idx(2 * j - 3, w)};
+  BiorDdRaw q;
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) q.sh[cc] = x[cc] > 0 ? 8u : 0u;
+  // bytes 3x - 1 .. 3x + 2 (0 .. 3 at x = 0): never past the end.  The whole offset goes in the
+  // per-lane operand (a per-lane row offset in the scalar one becomes a loop over the lanes)
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+      q.v[rr][cc] = __builtin_amdgcn_raw_buffer_load_b32(
+          rs, (uint32_t)((int64_t)y[rr] * row_stride) + (x[cc] > 0 ? 3u * (uint32_t)x[cc] - 1u : 0u),
+          0u, 0);
+  return q;
+}
+__device__ __forceinline__ unsigned long long wl_bior_dd1_eval(const BiorDdRaw& q, int c, wreal mn,
+                                                               wreal inv, wreal rcp) {
+  double r[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      double px[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        px[ch] = (double)((q.v[rr][cc] >> (q.sh[cc] + 8 * ch)) & 0xFFu) * (1.0 / 255.0);
+      const wreal a = ycbcr_c(px, c) - mn;  // wl_dwt_stream's norm (u8: reciprocal + Markstein)
+      const wreal q0 = a * rcp;
+      r[rr][cc] = __fma_rn(__fma_rn(-q0, inv, a), rcp, q0);
+    }
+  return absbits(bior_dd2x2(r[0][0], r[0][1], r[1][0], r[1][1]));
+}
 // TL / TH: arithmetic of the lowpass / highpass paths.  fp64 throughout is pywt's precision; the
 // product runs the lowpass outputs (aa, ad, da: continuous inputs of the thresholds' fp64 sums of
 // squares and of the synthesis) in fp32, and at level 1 keeps the normalisation, the column
@@ -770,9 +831,16 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
   // (u & 1) * WS_MAXT / 2 + u / 2) so that the row threads' 16-byte reads (lane stride 4 columns)
   // fill whole bank rows -- interleaved fp64 columns put two lanes on every 16-byte slot
   constexpr bool SEPF = !std::is_same<TL, TH>::value;  // a separate TL copy of the highpass
+  // N32 (round 6; u8 level 1 with an fp32 highpass): the normalisation is one fp32 affine map of
+  // the bytes per channel, and the finest dd's codes come from the exact integer T = K00 - K10 -
+  // K01 + K11 of the pixels' YCbCr keys K = w . rgb (the dd is 0.5 T / (255000 range) within
+  // 2e-12 / range, as for the fused Haar: wl_haar_stats' certainty rule, the exact fp64 key where
+  // it is not certain) -- sigma stays bit-identical while every coefficient runs in fp32
+  constexpr bool N32 = SRC == 0 && std::is_same<TH, float>::value && CODES != 0;
   __shared__ TL VL[2][3][NT];
   __shared__ TL VF[SEPF ? 2 : 1][SEPF ? 3 : 1][SEPF ? NT : 1];
   __shared__ TH VH[2][3][NT];
+  __shared__ int VK[N32 ? 2 : 1][N32 ? 3 : 1][N32 ? NT : 1];  // key column highpass, VH's layout
   __shared__ double RED[3][NT];
   const int img = blockIdx.z;
   const int strip = (int)blockIdx.x % strips, band = (int)blockIdx.x / strips;
@@ -800,6 +868,18 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
       wl_minmax64(st, c, mn[c], mx);
       inv[c] = mx - mn[c];
       rcp[c] = 1.0 / inv[c];
+    }
+  }
+  // N32: x_c = sum_k A[c][k] b_k + Bc[c] (b the bytes) = ((w_c . b) / 255000 + off_c - min_c) / range_c
+  float A32c[3][3] = {}, B32c[3] = {};
+  double sc1[3] = {0.0, 0.0, 0.0};  // the finest dd per unit of T: 0.5 / (255000 range)
+  if constexpr (N32) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      sc1[c] = uniform_f64(0.5 / (255000.0 * inv[c]));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) A32c[c][k] = (float)((double)ycc_w(c, k) / (255000.0 * inv[c]));
+      B32c[c] = (float)(((c == 0 ? 16.0 : 128.0) - mn[c]) / inv[c]);
     }
   }
   rsrc_t rs;
@@ -855,8 +935,10 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
   };
   TL acc[3][5];              // running column lowpass of outputs k .. k+4 (slot = output % 5)
   TH hd0[3], hd1[3];         // column highpass of pairs k-1, k-2 (hi[i] is pair i-2's)
+  int kd0[3], kd1[3];        // N32: the key highpass K(row 2k) - K(row 2k+1) of the same pairs
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
+    kd0[c] = kd1[c] = 0;
     hd0[c] = hd1[c] = (TH)0;
 #pragma unroll
     for (int r = 0; r < 5; ++r) acc[c][r] = (TL)0;
@@ -899,12 +981,36 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
       if (colt) {
         const int slot = r % PF;  // PF divides 5 (compile-time after unrolling)
         const WsRaw<SRC>& cur = rq[slot];
+        float bf[2][3];   // N32: the pixel bytes as floats
+        int bi[2][3];     //      and as integers
+        if constexpr (N32) {
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+            for (int k3 = 0; k3 < 3; ++k3) {
+              bi[h2][k3] = (int)((cur.p[h2] >> (qsh + 8 * k3)) & 0xFFu);
+              bf[h2][k3] = (float)bi[h2][k3];
+            }
+        }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          const auto x0 = norm(cur, 0, c), x1 = norm(cur, 1, c);
-          const TL l0 = (TL)x0, l1 = (TL)x1;
+          TH h0, h1;
+          TL l0, l1;
+          if constexpr (N32) {
+            const float y0 = __fmaf_rn(A32c[c][2], bf[0][2], __fmaf_rn(A32c[c][1], bf[0][1], __fmaf_rn(A32c[c][0], bf[0][0], B32c[c])));
+            const float y1 = __fmaf_rn(A32c[c][2], bf[1][2], __fmaf_rn(A32c[c][1], bf[1][1], __fmaf_rn(A32c[c][0], bf[1][0], B32c[c])));
+            l0 = (TL)y0;
+            l1 = (TL)y1;
+            h0 = (TH)y0;
+            h1 = (TH)y1;
+          } else {
+            const auto x0 = norm(cur, 0, c), x1 = norm(cur, 1, c);
+            l0 = (TL)x0;
+            l1 = (TL)x1;
+            h0 = (TH)x0;
+            h1 = (TH)x1;
+          }
           const TL sk = l0 + l1, ek = l1 - l0;
-          const TH h0 = (TH)x0, h1 = (TH)x1;
           const TH hk = (TH)(-S2) * h1 + (TH)S2 * h0;  // pywt: mul, add (no contraction)
           // pair k's contributions; slot (k + j) % 5 == (r + j) % 5 for the unrolled r
           acc[c][(r + 4) % 5] = (TL)(-B1) * ek;
@@ -916,9 +1022,15 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
             VL[buf][c][t] = lo;
             VH[buf][c][(t & 1) * (NT / 2) + (t >> 1)] = hd1[c];
             if constexpr (SEPF) VF[buf][c][t] = (TL)hd1[c];
+            if constexpr (N32) VK[buf][c][(t & 1) * (NT / 2) + (t >> 1)] = kd1[c];
           }
           hd1[c] = hd0[c];
           hd0[c] = hk;
+          if constexpr (N32) {
+            kd1[c] = kd0[c];
+            kd0[c] = (__mul24(ycc_w(c, 0), bi[0][0]) + __mul24(ycc_w(c, 1), bi[0][1]) + __mul24(ycc_w(c, 2), bi[0][2])) -
+                     (__mul24(ycc_w(c, 0), bi[1][0]) + __mul24(ycc_w(c, 1), bi[1][1]) + __mul24(ycc_w(c, 2), bi[1][2]));
+          }
         }
       }
       // refill the slot PF steps ahead, after its last use and outside the column threads' branch
@@ -976,8 +1088,25 @@ __global__ __launch_bounds__(NT, IDN_WS_WPE) void wl_dwt_stream(
           sq[0] = __fma_rn(v1, v1, sq[0]);  // (exact squares for the fp32 bands: = mul + add)
           sq[1] = __fma_rn(v2, v2, sq[1]);
           sq[2] = __fma_rn(v3, v3, sq[2]);
-          const unsigned long long key = absbits((double)odd[d]);
-          code[d] = key ? wl_fbin(key) + 1 : 0;
+          if constexpr (N32) {
+            const int* vke = &VK[buf][rc][jj];
+            const int* vko = &VK[buf][rc][NT / 2 + jj];
+            const int T = vke[d + 2] - vko[d + 2];  // elements 2d + 4 (even), 2d + 5 (odd)
+            const uint32_t aT = (uint32_t)(T < 0 ? -T : T);
+            const uint32_t hi = (uint32_t)__double2hiint((double)aT * sc1[rc]);
+            code[d] = (uint32_t)min(max((int)(hi >> 16) - (1023 - 61) * 16, 0), WL_FBINS - 1) + 1u;
+            if (!(aT >= 3u && (hi & 0xFFFFu) - 2u <= 0xFFFBu)) {
+              // rare: the median workgroup sets this code from the exact fp64 key (the list sits
+              // after the channel's codes, where the median's key scratch starts later)
+              code[d] = 0u;
+              uint32_t* lst = reinterpret_cast<uint32_t*>(base + (size_t)rc * Hin * Win + (bsz + 3) / 4);
+              lst[atomicAdd(reinterpret_cast<uint32_t*>(const_cast<double*>(stats) + (size_t)img * WL_STATS + WL_N32U + rc), 1u)] =
+                  (uint32_t)(i * Wo + oj + d);
+            }
+          } else {
+            const unsigned long long key = absbits((double)odd[d]);
+            code[d] = key ? wl_fbin(key) + 1 : 0;
+          }
         }
         if (emit_codes) {  // the pair's two codes as one dword where it is aligned
           uint16_t* cp = reinterpret_cast<uint16_t*>(base + (size_t)rc * Hin * Win) + e0;
@@ -2568,56 +2697,6 @@ __device__ __forceinline__ unsigned long long wl_dd1_eval(const Dd1Raw& q, int c
   return absbits(dd);
 }
 
-// bior1.5: the level-1 highpass has two taps, so a finest dd is the 2x2 combination of the
-// normalised samples at rows 2i-4, 2i-3 and columns 2j-4, 2j-3 (pywt 'symmetric' indices), in
-// wl_dwt_stream's op order: the column highpass (two products, then their sum) of both columns,
-// then the row highpass.  The sigma median recomputes the few exact values it needs from the input
-// (wl_haar_median<1, true, true>), so the analysis keeps the level-1 dd band in fp32 only -- all
-// that the synthesis reads of it.
-__device__ __forceinline__ double bior_dd2x2(double x00, double x01, double x10, double x11) {
-  const double h0 = (-S2) * x10 + S2 * x00, h1 = (-S2) * x11 + S2 * x01;  // x[row][column]
-  return (-S2) * h1 + S2 * h0;
-}
-struct BiorDdRaw {  // u8: the dword holding each sample's 3 bytes, and the bit offset of the pixel
-  uint32_t v[2][2];
-  uint32_t sh[2];
-};
-__device__ __forceinline__ BiorDdRaw wl_bior_dd1_load(rsrc_t rs, int h, int w, int64_t row_stride,
-                                                      uint32_t pos, int W1) {
-  const int i = (int)(pos / (uint32_t)W1), j = (int)(pos - (uint32_t)i * (uint32_t)W1);
-  const int y[2] = {sym_idx(2 * i - 4, h), sym_idx(2 * i - 3, h)};
-  const int x[2] = {sym_idx(2 * j - 4, w), sym_idx(2 * j - 3, w)};
-  BiorDdRaw q;
-#pragma unroll
-  for (int cc = 0; cc < 2; ++cc) q.sh[cc] = x[cc] > 0 ? 8u : 0u;
-  // bytes 3x - 1 .. 3x + 2 (0 .. 3 at x = 0): never past the end.  The whole offset goes in the
-  // per-lane operand (a per-lane row offset in the scalar one becomes a loop over the lanes)
-#pragma unroll
-  for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
-      q.v[rr][cc] = __builtin_amdgcn_raw_buffer_load_b32(
-          rs, (uint32_t)((int64_t)y[rr] * row_stride) + (x[cc] > 0 ? 3u * (uint32_t)x[cc] - 1u : 0u),
-          0u, 0);
-  return q;
-}
-__device__ __forceinline__ unsigned long long wl_bior_dd1_eval(const BiorDdRaw& q, int c, wreal mn,
-                                                               wreal inv, wreal rcp) {
-  double r[2][2];
-#pragma unroll
-  for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      double px[3];
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch)
-        px[ch] = (double)((q.v[rr][cc] >> (q.sh[cc] + 8 * ch)) & 0xFFu) * (1.0 / 255.0);
-      const wreal a = ycbcr_c(px, c) - mn;  // wl_dwt_stream's norm (u8: reciprocal + Markstein)
-      const wreal q0 = a * rcp;
-      r[rr][cc] = __fma_rn(__fma_rn(-q0, inv, a), rcp, q0);
-    }
-  return absbits(bior_dd2x2(r[0][0], r[0][1], r[1][0], r[1][1]));
-}
 __device__ unsigned long long wl_bior_dd1_key64(const double* __restrict__ in64, int img, int h,
                                                 int w, uint32_t pos, int W1, int c, wreal mn,
                                                 wreal inv) {
@@ -2662,12 +2741,6 @@ __device__ unsigned long long wl_bior_dd1_key64(const double* __restrict__ in64,
 // Channels whose range is only rounding noise (Cb / Cr of a gray image, range ~1e-14) get sums
 // that differ from the fp64 planes' (which are noise themselves); their thresholds cannot move the
 // output, which is min + v * range for such a channel.
-__device__ __forceinline__ double uniform_f64(double v) {  // a wave-uniform double into SGPRs
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readfirstlane((int)b);
-  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
-}
 constexpr int WLS_IT = 16;  // sub-blocks per thread (int32 moments stay below 2^31: <= 1.07e9)
 constexpr int WLS_XMAX = WLH_WG * 12;  // uncertain codes one iteration can queue (12 per thread)
 constexpr int WLS_XCAP = 2 * WLS_XMAX;  // the queue is evaluated once more than half full
@@ -2686,10 +2759,6 @@ __device__ __forceinline__ void mom_add(int (&m)[6], int r, int g, int b) {
   m[3] += __mul24(r, g);
   m[4] += __mul24(r, b);
   m[5] += __mul24(g, b);
-}
-__device__ __forceinline__ int ycc_w(int c, int k) {  // rgb2ycbcr coefficients x 1000
-  constexpr int W[3][3] = {{65481, 128553, 24966}, {-37797, -74203, 112000}, {112000, -93786, -18214}};
-  return W[c][k];
 }
 
 template <int L>
@@ -3261,6 +3330,22 @@ __global__ __launch_bounds__(WLM_WG) void wl_haar_median(const uint8_t* __restri
   __shared__ uint32_t hist[WLM_NH * WL_FBINS];
   __shared__ uint32_t m_s, mn_s, le_s, next_s;
   __shared__ unsigned long long nmin_s, gt_s;
+  if (BAND && BIOR && !in64) {
+    // the codes the N32 analysis could not certify (wl_dwt_stream): the exact fp64 key's code
+    const uint32_t nu = *reinterpret_cast<const uint32_t*>(stats + (size_t)img * WL_STATS + WL_N32U + c);
+    if (nu) {
+      const uint32_t* lst = reinterpret_cast<const uint32_t*>(slot + (bsz + 3) / 4);
+      uint16_t* cw = reinterpret_cast<uint16_t*>(slot);
+      const rsrc_t rs = make_rsrc(src + (int64_t)img * Lt.h * row_stride, (uint32_t)((int64_t)Lt.h * row_stride));
+      for (uint32_t t = threadIdx.x; t < nu; t += WLM_WG) {
+        const uint32_t pos = lst[t];
+        const unsigned long long key =
+            wl_bior_dd1_eval(wl_bior_dd1_load(rs, Lt.h, Lt.w, row_stride, pos, W1), c, mn, inv, rcp);
+        cw[pos] = (uint16_t)(key ? (uint32_t)wl_fbin(key) + 1u : 0u);
+      }
+      __syncthreads();
+    }
+  }
   for (int k = threadIdx.x; k < WLM_NH * WL_FBINS; k += WLM_WG) hist[k] = 0u;
   if (threadIdx.x == 0) {
     m_s = 0;
@@ -3683,7 +3768,11 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       const dim3 grid((unsigned)(strips * bands), 1, (unsigned)n);
       const dim3 blk((unsigned)((2 * sw + 8 + 63) / 64 * 64));
       const int Hi = Lt.H[l - 1], Wi = Lt.W[l - 1], emit = (l == 1 && codes) ? 1 : 0;
-      // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32
+      // IDN_WAVELET_A32 bit 0: level 1's lowpass path in fp32; bit 1: deeper levels in fp32;
+      // bit 2 (with bit 0, u8 input and the code median): level 1's normalisation and highpass
+      // in fp32 too, the codes from exact integer keys (wl_dwt_stream's N32; sigma bit-identical
+      // by test, but 1041 vs 849 us per 256 images: gfx950 issues fp64 FMA at the fp32 rate, and
+      // the key staging adds instructions and registers -- profiles/r06/wavelet/n32_ab.txt)
 #define IDN_WS_(SRC, TL, TH, FMC, CC, EMIT)                                                        \
   hipLaunchKernelGGL((wl_dwt_stream<SRC, TL, TH, FMC, CC>), grid, blk, 0, st, wsf, Lt.img_floats,  \
                      stats, in_off, Hi, Wi, Lt.off_band[l], Lt.H[l], Lt.W[l], sw, strips, bands,   \
@@ -3713,6 +3802,9 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
       } else if (in64) {
         if (f1) IDN_WS(1, float, wreal, emit);
         else IDN_WS(1, wreal, wreal, emit);
+      } else if (f1 && (a32 & 4) && emit && dd32) {
+        // the whole level-1 analysis in fp32, codes from the exact integer keys (N32; A/B form)
+        IDN_WS(0, float, float, emit);
       } else {
         if (f1) IDN_WS(0, float, wreal, emit);
         else IDN_WS(0, wreal, wreal, emit);

@@ -316,10 +316,12 @@ def _bior_stats(monkeypatch, img, env):
 
 
 @pytest.mark.parametrize("shape", [(600, 1000), (130, 77), (37, 53), (9, 11)])
-@pytest.mark.parametrize("a32", ["1", "2", "3"])
+@pytest.mark.parametrize("a32", ["1", "2", "3", "7"])
 def test_wavelet_bior15_fp32_analysis(dev, monkeypatch, shape, a32):
     """IDN_WAVELET_A32 (bit 0: level 1's lowpass path aa / ad / da in fp32, the normalisation,
-    column highpass and dd in fp64; bit 1: deeper levels in fp32) against the fp64 analysis:
+    column highpass and dd in fp64; bit 1: deeper levels in fp32; bit 2 (round 6, A/B form):
+    level 1's normalisation and highpass in fp32 too, the finest dd's codes from the exact
+    integer keys) against the fp64 analysis:
     the finest dd -- hence the sigma medians and the nonzero counts -- bit-identical, outputs
     within 2e-6, small images within TOL of the oracle"""
     import oracle
@@ -337,6 +339,31 @@ def test_wavelet_bior15_fp32_analysis(dev, monkeypatch, shape, a32):
         ref = oracle.wavelet.denoise_wavelet(img, "bior1.5", None)
         assert np.abs(fb - ref).max() <= TOL
         check_u8(u8b, ref, oracle.sk.to_u8(255 * ref))
+
+
+def test_wavelet_bior15_n32_stat_images(dev, monkeypatch):
+    """the fp32 level-1 analysis with integer-key codes (IDN_WAVELET_A32=7) against the product's
+    fp64-highpass form (3) on images with exact zeros, rounding residues (gray: T = 0), |T| < 3
+    combinations, bin-edge values and saturated channels -- every code the analysis cannot certify
+    is set by the median workgroup from the exact fp64 key: sigma medians and nonzero counts
+    bit-identical, outputs within 2e-6"""
+    import torch
+    from idn import _lib
+    x = torch.from_numpy(np.concatenate([_stat_images(96, 160),
+                                         np.stack([_clipped(96, 160, 5)])])).cuda()
+    out = {}
+    for a32 in ("3", "7"):
+        monkeypatch.setenv("IDN_WAVELET_A32", a32)
+        with _lib.variant("tuning"):
+            out[a32] = _stats_after_w(x, "bior1.5", None)
+    (u8a, fa, sa), (u8b, fb, sb) = out["3"], out["7"]
+    lv = 1  # 96 x 160: max(dwt_max_level - 3, 1)
+    med = slice(8 + 9 * lv, 8 + 9 * lv + 3)
+    np.testing.assert_array_equal(sa[:, med].view(np.uint64), sb[:, med].view(np.uint64))
+    np.testing.assert_array_equal(sa[:, 248:251], sb[:, 248:251])
+    assert np.abs(fa - fb).max() <= 2e-6
+    # U8 flips only on rounding boundaries (the flat / gray images sit on exact k / 255 values)
+    check_u8(u8b, fa.astype(np.float64), u8a)
 
 
 @pytest.mark.parametrize("shape", [(600, 1000), (130, 77), (37, 53)])
