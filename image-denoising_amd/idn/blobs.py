@@ -18,6 +18,18 @@ def _to_device(im):
     return torch.from_numpy(np.ascontiguousarray(im)).cuda()
 
 
+def _to_host(t: torch.Tensor) -> np.ndarray:
+    """A device tensor as a host numpy array, through page-locked memory from torch's caching host
+    allocator: a 600x1000 float32 blob (7.2 MB) copied into fresh pageable memory paid its page
+    faults on every call (~0.9 ms against ~0.15 ms); the block returns to the cache when the array
+    is dropped, as the test loop drops each image's blobs."""
+    if t.device.type != "cuda":
+        return t.numpy()
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h.numpy()
+
+
 def im_scale_for(shape, target_size: int, max_size: int) -> float:
     """prep_im_for_blob's scale rule (blob.py:37-43)."""
     im_size_min = float(min(shape[0:2]))
@@ -43,7 +55,7 @@ def prep_im_for_blob(im, pixel_means, target_size, max_size, flip: bool = False,
             raise TypeError("prep_im_for_blob: a deferred GaussianBlur needs a uint8 image")
         if not flip and im_scale_for(x.shape, target_size, max_size) == 1.0:
             f = ops.gaussian_blob(x, int(gaussian_ksize), means)[0]
-            return (f if as_tensor else f.cpu().numpy()), 1.0
+            return (f if as_tensor else _to_host(f)), 1.0
         x = ops.gaussian_blur(x, int(gaussian_ksize))
     if x.dtype == torch.uint8:
         f = ops.blob(x, means, flip=flip)[0]
@@ -56,15 +68,17 @@ def prep_im_for_blob(im, pixel_means, target_size, max_size, flip: bool = False,
     im_scale = im_scale_for(f.shape, target_size, max_size)
     if im_scale != 1.0:
         f = ops.resize_linear(f, im_scale, im_scale)
-    return (f if as_tensor else f.cpu().numpy()), im_scale
+    return (f if as_tensor else _to_host(f)), im_scale
 
 
 def im_list_to_blob(ims, as_tensor: bool = False):
     """Zero-padded NHWC float32 blob of prepared images (numpy or device tensors)."""
     xs = [_to_device(im) for im in ims]
+    if len(xs) == 1 and not as_tensor:  # nothing to pad: straight to the host
+        return _to_host(xs[0].float().unsqueeze(0))
     hmax = max(int(x.shape[0]) for x in xs)
     wmax = max(int(x.shape[1]) for x in xs)
     blob = torch.zeros((len(xs), hmax, wmax, 3), dtype=torch.float32, device=xs[0].device)
     for i, x in enumerate(xs):
         blob[i, : x.shape[0], : x.shape[1], :] = x.float()
-    return blob if as_tensor else blob.cpu().numpy()
+    return blob if as_tensor else _to_host(blob)

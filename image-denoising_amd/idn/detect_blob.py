@@ -48,7 +48,7 @@ def apply_noise(img, noise: str, mode: str = "test_v0", image_id: int = 0,
     if key not in _PRE:
         _PRE[key] = Preprocessor(noise, mode, seed=cfg.RNG_SEED, rng=_random, noise_rng=noise_rng)
     outs, _ = _PRE[key](_blob._to_device(img)[None], image_ids=[image_id])
-    return outs[0] if as_tensor else outs[0].cpu().numpy()
+    return outs[0] if as_tensor else _blob._to_host(outs[0])
 
 
 def _get_image_blob(im, as_tensor: bool = False):

@@ -74,3 +74,82 @@ def imread_gpu(paths, mode: str = "libjpeg9", orientation: bool = True):
         for k, i in enumerate(idx):
             out[i] = dec[k]
     return out
+
+
+class ImageReader:
+    """The test loop's image reads (lib/model/test.py:189-191: `for i in range(num_images):
+    img = cv2.imread(imdb.image_path_at(i))`) with read-ahead: reader[i] is
+    imread_gpu([paths[i]])[0], but the files are decoded `batch` at a time (one decode launch per
+    window of same-size files), and while the caller works on the images of window b, window
+    b + 1 decodes on a side stream from a worker thread.  A single file's decode is latency-bound
+    (its entropy passes keep ~16 waves busy for ~1.3 ms while the host waits on their
+    convergence flags) and a window of 8 takes about as long as one, so read-ahead turns the
+    decode from the loop's largest stage into one hidden behind the current image's noise,
+    wavelet and blob work and its copy to the host.  Results are those of imread_gpu (the decode
+    is per file; batching does not change a byte); access is expected in order (an index outside
+    the windows in flight decodes its own window on demand).
+
+        reader = ImageReader([imdb.image_path_at(i) for i in range(num_images)])
+        for i in range(num_images):
+            im = apply_noise(reader[i], noise, decode="gpu", as_tensor=True)
+            ...
+    """
+
+    def __init__(self, paths, mode: str = "libjpeg9", orientation: bool = True, prefetch: bool = True,
+                 batch: int = 8):
+        import concurrent.futures
+        import torch
+        if batch < 1:
+            raise ValueError("ImageReader: batch must be >= 1")
+        self.paths = [str(p) for p in paths]
+        self.mode, self.orientation, self.batch = mode, orientation, int(batch)
+        self._dev = torch.cuda.current_device()
+        self._side = torch.cuda.Stream(self._dev)
+        self._pool = concurrent.futures.ThreadPoolExecutor(1) if prefetch else None
+        self._pending = {}  # window -> future of (images, event)
+        self._win = None    # (window, images, event) being read
+
+    def __len__(self):
+        return len(self.paths)
+
+    def _decode(self, b):
+        import torch
+        lo = b * self.batch
+        with torch.cuda.device(self._dev), torch.cuda.stream(self._side):
+            ims = imread_gpu(self.paths[lo:lo + self.batch], self.mode, self.orientation)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return ims, ev
+
+    def __getitem__(self, i: int):
+        import torch
+        if not 0 <= i < len(self.paths):
+            raise IndexError(i)
+        b = i // self.batch
+        if self._win is None or self._win[0] != b:
+            fut = self._pending.pop(b, None)
+            ims, ev = fut.result() if fut is not None else self._decode(b)
+            self._win = (b, ims, ev)
+            if (self._pool is not None and (b + 1) * self.batch < len(self.paths)
+                    and b + 1 not in self._pending):
+                self._pending[b + 1] = self._pool.submit(self._decode, b + 1)
+        _, ims, ev = self._win
+        im = ims[i - b * self.batch]
+        cur = torch.cuda.current_stream(self._dev)
+        cur.wait_event(ev)
+        im.record_stream(cur)  # decoded on the side stream, used on the caller's
+        return im
+
+    def close(self):
+        for f in self._pending.values():
+            f.result()
+        self._pending.clear()
+        self._win = None
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

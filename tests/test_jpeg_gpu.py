@@ -378,3 +378,34 @@ def test_exif_turbo_mode_turns_too(dev):
         got = ops.jpeg_decode([data], mode="turbo")[0].cpu().numpy()
         ref = exif.apply(pil_bgr(EXIF / name), EXIF_META[name]["orientation"])
         assert np.array_equal(got, ref), name
+
+
+def test_image_reader_prefetch_matches_imread_gpu(dev):
+    """idn.io.ImageReader (the test loop's reads, test.py:189-191, decoded in windows with the
+    next window decoded ahead on a side stream): every image equals imread_gpu's, in order and on demand out of
+    order, and the per-image body run on its images (noise + wavelet + blob, the bench's
+    detect_e2e_pipelined) gives the same blobs as on imread_gpu's"""
+    import torch
+    from idn import detect_blob
+    from idn import io as idn_io
+    names = sorted(p.name for p in JPEG.glob("demo_*.jpg"))
+    assert len(names) >= 3
+    paths = [str(JPEG / n) for n in names] * 2
+    ref = [idn_io.imread_gpu([p])[0] for p in paths]
+    for batch in (1, 4, 8):  # windows of mixed sizes (several decode launches) and a partial one
+        with idn_io.ImageReader(paths, batch=batch) as rd:
+            for i in range(len(paths)):
+                assert torch.equal(rd[i], ref[i]), (batch, paths[i])
+            assert torch.equal(rd[1], ref[1])  # out of order: its window decoded on demand
+    import random
+    with idn_io.ImageReader(paths) as rd:
+        for i in range(len(paths)):
+            random.seed(1000 + i)  # test_v0 draws the gaussian level from the random module
+            a = detect_blob.apply_noise(rd[i], "gaussian_wavelet_var0.1", mode="test_v0",
+                                        image_id=i, as_tensor=True)
+            random.seed(1000 + i)
+            b = detect_blob.apply_noise(ref[i], "gaussian_wavelet_var0.1", mode="test_v0",
+                                        image_id=i, as_tensor=True)
+            ba, _ = detect_blob._get_blobs(a)
+            bb, _ = detect_blob._get_blobs(b)
+            np.testing.assert_array_equal(ba["data"], bb["data"])

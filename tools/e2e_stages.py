@@ -5,7 +5,8 @@ test_net body, lib/model/test.py:189-191 (cv2.imread), 1678-1684 (gaussian noise
   python tools/e2e_stages.py [--iters 200] [--out file.json]
 
 Each stage is bracketed by torch.cuda.synchronize() and timed on the host clock (medians over the
-iterations); the whole step is also timed without the inner synchronisations, as the bench does."""
+iterations); the whole step is also timed without the inner synchronisations, as the bench does, and the loop
+over eight distinct files with read-ahead (idn.io.ImageReader), as bench.py's detect_e2e_pipelined."""
 import argparse
 import json
 import os
@@ -19,6 +20,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "image-denoising_amd"))
 sys.path.insert(0, str(ROOT))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -63,6 +65,30 @@ def main():
         step()
     torch.cuda.synchronize()
     whole = (time.perf_counter() - t0) * 1e3 / args.iters
+    # the loop with read-ahead (idn.io.ImageReader: windows of 8 files, the next one decoded on a
+    # side stream while this window's images run)
+    paths = []
+    for j in range(8):
+        pj = os.path.join(d, f"ra{j}.jpg")
+        Image.fromarray(np.roll(x[0].cpu().numpy()[..., ::-1], 37 * j, axis=1)).save(
+            pj, "JPEG", quality=90, subsampling=2)
+        paths.append(pj)
+    reader = idn_io.ImageReader(paths * (args.iters // 8 + 8), batch=8)
+
+    def step_ra(k):
+        im = detect_blob.apply_noise(reader[k], "gaussian_wavelet_var0.1", mode="test_v0",
+                                     decode="gpu", as_tensor=True)
+        detect_blob._get_blobs(im)
+
+    for k in range(32):
+        step_ra(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(32, 32 + args.iters):
+        step_ra(k)
+    torch.cuda.synchronize()
+    read_ahead = (time.perf_counter() - t0) * 1e3 / args.iters
+    reader.close()
     # stages
     orig = (idn_io.imread_gpu, ops.random_noise_ycc, ops.denoise_wavelet, ops.blob,
             blobs.im_list_to_blob, ops.random_noise)
@@ -75,7 +101,7 @@ def main():
 
     def im_list_to_blob(ims, as_tensor=False):
         b = timed("im_list_to_blob (pad + copy, device)", ilb)(ims, as_tensor=True)
-        return b if as_tensor else timed("D2H (blob to host numpy)", lambda t: t.cpu().numpy())(b)
+        return b if as_tensor else timed("D2H (blob to host numpy, pinned)", blobs._to_host)(b)
     blobs.im_list_to_blob = im_list_to_blob
     detect_blob._blob.im_list_to_blob = im_list_to_blob
     TIMES.clear()
@@ -84,7 +110,8 @@ def main():
         step()
     torch.cuda.synchronize()
     synced = (time.perf_counter() - t0) * 1e3 / args.iters
-    rec = {"ms_per_image_unsynced": round(whole, 4), "ms_per_image_with_stage_syncs": round(synced, 4),
+    rec = {"ms_per_image_unsynced": round(whole, 4), "ms_per_image_read_ahead": round(read_ahead, 4),
+           "ms_per_image_with_stage_syncs": round(synced, 4),
            "stages_ms_median": {k: round(statistics.median(v), 4) for k, v in TIMES.items()},
            "iters": args.iters}
     rec["stages_sum_ms"] = round(sum(rec["stages_ms_median"].values()), 4)
