@@ -32,7 +32,17 @@ struct BilateralTaps {
   double gcc;                                       // -0.5 / sigma_color^2
   float sw[(2 * BL_MAXR + 1) * (2 * BL_MAXR + 1)];  // space weight at (i+R)*(2R+1)+(j+R)
   float swq[BL_MAXR * BL_MAXR + 1];                 // space weight by r^2 = i^2 + j^2
+  float kc;                                         // gcc * log2(e) (computed colour weights)
+  float ksq[BL_MAXR * BL_MAXR + 1];                 // log2(space weight) by r^2
 };
+// computed weights (A/B, bilateral_u8_pre2_kernel): bit k set = the taps of the k-th distinct r^2
+// take exp2(dist^2 * kc + log2(space weight)) on v_exp_f32 instead of the LDS table read
+#ifndef IDN_BL_CW
+#define IDN_BL_CW 0
+#endif
+#ifndef IDN_BL2_WGD  // resident workgroups per CU of the two-column kernel
+#define IDN_BL2_WGD 2
+#endif
 constexpr int BL_LUT = 3 * 255 + 1;
 
 template <int C>
@@ -291,15 +301,18 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
   constexpr int TH = BLP_NW * RPT;
   constexpr int LH = TH + 2 * R;
   constexpr Rsq<R> RS;
+  constexpr uint32_t ALL = (1u << RS.n) - 1u;
+  constexpr bool TABLE = (IDN_BL_CW & ALL) != ALL;  // some taps still read the table
   __shared__ uint32_t tile[LH * LW];
-  __shared__ float wt[RS.n * BL_LUT];
+  __shared__ float wt[TABLE ? RS.n * BL_LUT : 1];
 
   // wt[k][i] = space_weight(r^2 = q_k) * color_weight[i], OpenCV's float product
-  for (int i = threadIdx.x; i < BL_LUT; i += NT) {
-    const float cwv = (float)exp((double)(i * i) * taps.gcc);
+  if (TABLE)
+    for (int i = threadIdx.x; i < BL_LUT; i += NT) {
+      const float cwv = (float)exp((double)(i * i) * taps.gcc);
 #pragma unroll
-    for (int k = 0; k < RS.n; ++k) wt[k * BL_LUT + i] = taps.swq[RS.q[k]] * cwv;
-  }
+      for (int k = 0; k < RS.n; ++k) wt[k * BL_LUT + i] = taps.swq[RS.q[k]] * cwv;
+    }
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -357,7 +370,7 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
     // looked up at the first of the two visits in the walk order and kept in a register for the
     // second; the centre tap's weight is the constant wt[slot(0)][0].  Each output's sum keeps
     // its order, so the results are unchanged bit for bit.
-    const float w00 = wt[RS.slot[0] * BL_LUT];
+    const float w00 = TABLE ? wt[RS.slot[0] * BL_LUT] : 1.f;  // float(exp(0)) * float(exp(0))
     float wsh[RPT * 2][RPT * 2];
 #pragma unroll
     for (int dy = -R; dy < RPT + R; ++dy) {
@@ -392,7 +405,12 @@ __global__ __launch_bounds__(64 * BLP_NW) void bilateral_u8_pre2_kernel(
               wv = wsh[ky][kx];  // looked up when the walk passed the output's own position
             } else {
               const uint32_t dist = __builtin_amdgcn_sad_u8(p, p0[o][cc], 0u);
-              wv = wt[RS.slot[i * i + j * j] * BL_LUT + dist];
+              if ((IDN_BL_CW >> RS.slot[i * i + j * j]) & 1) {
+                const float df = (float)dist;
+                wv = __builtin_amdgcn_exp2f(__fmaf_rn(df * df, taps.kc, taps.ksq[i * i + j * j]));
+              } else {
+                wv = wt[RS.slot[i * i + j * j] * BL_LUT + dist];
+              }
               if (SYM && own) wsh[kx][ky] = wv;
             }
             const f32x2 w2 = {wv, wv};
@@ -443,7 +461,7 @@ static void launch_bl_pre2(const uint8_t* src, uint8_t* dst, int n, int h, int w
   const int tiles_x = (w + BL2_TW - 1) / BL2_TW;
   const int tiles_y = (h + BLP_NW * 4 - 1) / (BLP_NW * 4);
   const int64_t ntiles = (int64_t)n * tiles_x * tiles_y;
-  const int64_t res = (int64_t)cu_count() * knob("IDN_BL2_WG", 2);  // resident workgroups per CU
+  const int64_t res = (int64_t)cu_count() * knob("IDN_BL2_WG", IDN_BL2_WGD);  // resident workgroups per CU
   const int64_t grid = ntiles < res ? ntiles : res;
   if (knob("IDN_BL2_SYM", 1))
     hipLaunchKernelGGL((bilateral_u8_pre2_kernel<R, true>), dim3((unsigned)grid), dim3(64 * BLP_NW),
@@ -537,7 +555,9 @@ extern "C" int idn_bilateral_u8(const uint8_t* src, uint8_t* dst, int n, int h, 
       if (r > radius) continue;
       taps.sw[(i + radius) * (2 * radius + 1) + (j + radius)] = (float)exp(r * r * gsc);  // OpenCV's
       taps.swq[i * i + j * j] = (float)exp(r * r * gsc);
+      taps.ksq[i * i + j * j] = (float)log2((double)taps.swq[i * i + j * j]);
     }
+  taps.kc = (float)(gcc * 1.4426950408889634);
   hipStream_t st = as_stream(stream);
 #define IDN_BL(CC)                                                          \
   switch (radius) {                                                         \
