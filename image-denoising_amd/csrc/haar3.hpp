@@ -137,6 +137,24 @@ __device__ __forceinline__ h3f2 soft_f2(h3f2 x, float t) {
 }
 __device__ __forceinline__ h3f2 fma2(h3f2 a, h3f2 b, h3f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ h3f2 splat2(float v) { return h3f2{v, v}; }
+// a + b and a - b clamped to [0, 1] by the packed add's clamp bit (LLVM clamps each half with a
+// v_max_f32 instead: one instruction per value)
+__device__ __forceinline__ h3f2 pk_add_clamp(h3f2 a, h3f2 b) {
+  h3f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ h3f2 pk_sub_clamp(h3f2 a, h3f2 b) {
+  h3f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1] clamp" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+#ifndef IDN_H3S_Q3  // 1: level 3 of the synthesis split across the quad's lanes (A/B; 207 against
+#define IDN_H3S_Q3 0    // 187 us with each lane forming all: the DPP round trips lengthen the chain)
+#endif
+#ifndef IDN_H3S_CLAMP  // 1: the inner clip as the clamp bit of the packed adds (A/B: 0 = v_max clamp)
+#define IDN_H3S_CLAMP 1
+#endif
 
 // One thread per 4x4 sub-block; the four sub-blocks of an 8x8 block are consecutive lanes (a
 // quad), which exchange their level-2 approximation sums by DPP for level 3.  Level 1 runs on two
@@ -185,6 +203,16 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
       for (int k = 0; k < 3; ++k) qq[r][k] = p[k];
     }
   };
+  // IDN_H3S_Q3: this lane's level-3 signs over x01, x10, x11 (haar_int's bands ad, da, dd for
+  // sub = 0, 1, 2; the approximation for 3), chain start (ka for the approximation) and threshold
+  const float q3s[3] = {sub == 1 || sub == 3 ? 1.f : -1.f, sub == 0 || sub == 3 ? 1.f : -1.f,
+                        sub >= 2 ? 1.f : -1.f};
+  float q3b[3], q3t[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    q3b[c] = sub == 3 ? K[c].ka : 0.f;
+    q3t[c] = sub == 3 ? 0.f : (sub == 0 ? K[c].t3[0] : sub == 1 ? K[c].t3[1] : K[c].t3[2]);
+  }
   uint32_t qn[4][3] = {};
   load_q(0, qn);
 #pragma unroll 1
@@ -225,7 +253,18 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
     fd2[2][ch] = hi.x - hi.y;
   }
   // level 3 across the quad
-  float f64s[3], fd3[3][3];
+  float f64s[3], fd3[3][3], y3[3];
+  if (IDN_H3S_Q3) {
+    // quad lane `sub` forms one of the quad's level-3 sums: band sub (< 3) or the approximation
+    // (3), exact small integers in any order
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const int b16 = __float_as_int(S16[ch]);
+      const float x00 = __int_as_float(quad_get(b16, 0)), x01 = __int_as_float(quad_get(b16, 1));
+      const float x10 = __int_as_float(quad_get(b16, 2)), x11 = __int_as_float(quad_get(b16, 3));
+      y3[ch] = __fmaf_rn(q3s[2], x11, __fmaf_rn(q3s[1], x10, __fmaf_rn(q3s[0], x01, x00)));
+    }
+  } else
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
     const int b16 = __float_as_int(S16[ch]);
@@ -259,10 +298,22 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
     auto dotw = [&](const float (&wv)[3], const float (&d)[3]) {
       return __fmaf_rn(wv[2], d[2], __fmaf_rn(wv[1], d[1], wv[0] * d[0]));
     };
-    float a2 = __fmaf_rn(k.w3[2], f64s[2], __fmaf_rn(k.w3[1], f64s[1], __fmaf_rn(k.w3[0], f64s[0], k.ka)));
-    a2 = __fmaf_rn(sad, soft_f(dotw(k.w3, fd3[0]), k.t3[0]), a2);
-    a2 = __fmaf_rn(sda, soft_f(dotw(k.w3, fd3[1]), k.t3[1]), a2);
-    a2 = __fmaf_rn(sdd, soft_f(dotw(k.w3, fd3[2]), k.t3[2]), a2);
+    float a2;
+    if (IDN_H3S_Q3) {
+      // this lane's term: the soft-thresholded band (threshold 0 leaves the approximation term,
+      // whose chain starts at ka), then the quad's four terms in the chain's order
+      const float tq = soft_f(__fmaf_rn(k.w3[2], y3[2], __fmaf_rn(k.w3[1], y3[1], __fmaf_rn(k.w3[0], y3[0], q3b[c]))), q3t[c]);
+      const int ti = __float_as_int(tq);
+      a2 = __int_as_float(quad_get(ti, 3));
+      a2 = __fmaf_rn(sad, __int_as_float(quad_get(ti, 0)), a2);
+      a2 = __fmaf_rn(sda, __int_as_float(quad_get(ti, 1)), a2);
+      a2 = __fmaf_rn(sdd, __int_as_float(quad_get(ti, 2)), a2);
+    } else {
+      a2 = __fmaf_rn(k.w3[2], f64s[2], __fmaf_rn(k.w3[1], f64s[1], __fmaf_rn(k.w3[0], f64s[0], k.ka)));
+      a2 = __fmaf_rn(sad, soft_f(dotw(k.w3, fd3[0]), k.t3[0]), a2);
+      a2 = __fmaf_rn(sda, soft_f(dotw(k.w3, fd3[1]), k.t3[1]), a2);
+      a2 = __fmaf_rn(sdd, soft_f(dotw(k.w3, fd3[2]), k.t3[2]), a2);
+    }
     const float ad = soft_f(dotw(k.w2, fd2[0]), k.t2[0]);
     const float da = soft_f(dotw(k.w2, fd2[1]), k.t2[1]);
     const float dd = soft_f(dotw(k.w2, fd2[2]), k.t2[2]);
@@ -288,10 +339,17 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
                             fma2(splat2(k.w1[1]), D1[gp][b][1], splat2(k.w1[0]) * D1[gp][b][0])), k.t1[b]);
       const h3f2 A = {A1[c][2 * gp], A1[c][2 * gp + 1]};
       const h3f2 p = A + d[0], m = A - d[0], q0 = d[1] + d[2], q1 = d[1] - d[2];
-      v[0][c] = p + q0;
-      v[1][c] = m + q1;
-      v[2][c] = p - q0;
-      v[3][c] = m - q1;
+      if (IDN_H3S_CLAMP) {  // v already clipped to [0, 1]
+        v[0][c] = pk_add_clamp(p, q0);
+        v[1][c] = pk_add_clamp(m, q1);
+        v[2][c] = pk_sub_clamp(p, q0);
+        v[3][c] = pk_sub_clamp(m, q1);
+      } else {
+        v[0][c] = p + q0;
+        v[1][c] = m + q1;
+        v[2][c] = p - q0;
+        v[3][c] = m - q1;
+      }
     }
     // inner clip [0, 1]; de-normalisation, YCbCr -> RGB x 255 and the offsets in one affine map
     // (H3Rgb, its bias minus 0.5); the cast: round to nearest with saturation
@@ -302,7 +360,8 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
       h3f2 vc[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c)
-        vc[c] = h3f2{__builtin_amdgcn_fmed3f(v[i][c].x, 0.f, 1.f), __builtin_amdgcn_fmed3f(v[i][c].y, 0.f, 1.f)};
+        vc[c] = IDN_H3S_CLAMP ? v[i][c]
+                              : h3f2{__builtin_amdgcn_fmed3f(v[i][c].x, 0.f, 1.f), __builtin_amdgcn_fmed3f(v[i][c].y, 0.f, 1.f)};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const h3f2 o = fma2(vc[2], splat2(M.m[c][2]),
@@ -468,15 +527,27 @@ __global__ __launch_bounds__(H3_WIN_WG) void wl_h3_window(const uint8_t* __restr
 #ifndef IDN_H3_K
 #define IDN_H3_K 8
 #endif
-#ifndef IDN_H3_WPE
-#define IDN_H3_WPE 1
+#ifndef IDN_H3_WPE  // waves per EU the statistics kernel is built for: 3 caps it at 168 VGPRs (the
+#define IDN_H3_WPE 3    // branch-free loop body takes 242 uncapped: two waves, 352 against 308.5 us)
 #endif
 #ifndef IDN_H3_MOM  // level-1 moments: 0 v_dot2 on group pairs, 1 24-bit multiply-adds
 #define IDN_H3_MOM 0
 #endif
-#ifndef IDN_H3_PROBE  // timing probes only (wrong results): bit 0 no proxies, 1 no T / counts /
-#define IDN_H3_PROBE 0  // appends, 2 no level-1 moments, 3 no levels 2-3
+#ifndef IDN_H3_BRW  // 1: below-window count from the borrow of |T| - lo (A/B: 308.8 against 308.5)
+#define IDN_H3_BRW 0
 #endif
+#ifndef IDN_H3_ZC  // 1: zero |T| counted on the residue branch (the nonzero count derived; A/B:
+#define IDN_H3_ZC 0    // 331 against 308.5 us)
+#endif
+#ifndef IDN_H3_L3Q  // 1: level-3 moments by band across the quad's lanes; 0: the first lane all
+#define IDN_H3_L3Q 1    // (308.5 against 340 us)
+#endif
+#ifndef IDN_H3_UNR  // unroll of the block-row loop
+#define IDN_H3_UNR 1
+#endif
+#ifndef IDN_H3_PROBE  // timing probes only (wrong results): bit 0 no proxies, 1 no T / counts /
+#define IDN_H3_PROBE 0  // appends, 2 no level-1 moments, 3 no levels 2-3, 5 flush without its
+#endif                  // global atomic, 6 no flush
 constexpr int H3_IT = IDN_H3_IT;  // block rows per workgroup (int32 moments: <= 16 steps, 1.07e9)
 // Appends go to per-lane LDS slots (no atomics, no barriers): slot j of lane t of channel c at
 // [c][j][t]; a wave moves its lanes' slots to the image's arrays (one scan, one global atomic per
@@ -493,9 +564,9 @@ __device__ __forceinline__ void h3_wave_flush(const uint32_t* buf, uint32_t n, u
     if (lane >= o) inc += t;
   }
   const uint32_t tot = (uint32_t)__shfl((int)inc, 63);
-  if (tot == 0) return;
+  if (tot == 0 || (IDN_H3_PROBE & 64)) return;
   uint32_t base = 0;
-  if (lane == 63) base = atomicAdd(gcount, tot);
+  if (lane == 63 && !(IDN_H3_PROBE & 32)) base = atomicAdd(gcount, tot);
   base = (uint32_t)__shfl((int)base, 63) + inc - n;
   for (uint32_t j = 0; j < n; ++j) dst[base + j] = buf[j * WLH_WG + threadIdx.x];
 }
@@ -580,7 +651,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     for (int k = 0; k < 6; ++k) mom[b][k] = 0;
   float pmn[3] = {INFINITY, INFINITY, INFINITY}, pmx[3] = {-INFINITY, -INFINITY, -INFINITY};
   uint32_t smn[3] = {0u, 0u, 0u}, smx[3] = {0u, 0u, 0u};  // steps near the lane's extremes
-  uint32_t ct[3] = {0u, 0u, 0u}, cl[3] = {0u, 0u, 0u};  // per-lane counts
+  uint32_t ct[3] = {0u, 0u, 0u}, cl[3] = {0u, 0u, 0u};  // per-lane counts: zero / below-window |T|
   uint32_t na[4] = {0u, 0u, 0u, 0u};                    // this lane's filled slots
   auto mom_lds = [&](int l, int b, int r, int g, int bl) {
     const int ld = l == 1 ? WLH_WG : WLH_WG / 4;
@@ -622,9 +693,14 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   };
   // level-1 position of group (0, 0) of this thread's sub-block at step 0; + 4 W1 per step
   const uint32_t pos00 = (uint32_t)(4 * by0 + sy / 2) * W1 + (uint32_t)(x0 / 2);
+  // haar_int's band signs of x01, x10, x11 for band `sub` (ad: - + -, da: + - -, dd: - - +)
+  const int s3b[3] = {sub == 1 ? 1 : -1, sub == 0 ? 1 : -1, sub == 2 ? 1 : -1};
   uint32_t qn[4][3] = {};
   load_q(0, qn);
-#pragma unroll 1
+  // Lanes past the image hold zero pixels throughout (load_q never fills them): their moments
+  // add nothing, and their proxies, counts and masks are dropped after the loop, so the body runs
+  // without per-lane branches (only the residue appends test `act`).
+#pragma unroll IDN_H3_UNR
   for (int it = 0; it < nit; ++it) {
     const bool act = colact;  // (rows: it < nit, uniform)
     uint32_t q[4][3];
@@ -633,12 +709,6 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
       for (int k = 0; k < 3; ++k) q[r][k] = qn[r][k];
     load_q(it + 1, qn);
-    if (!act) {  // lanes past the image: zeros (they add nothing; keys and counts are masked)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) q[r][k] = 0u;
-    }
     auto px = [&](int r, int k) { return (int)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
     auto pxf = [&](int r, int k) { return (float)((q[r][k >> 2] >> (8 * (k & 3))) & 0xFFu); };
     // fp32 proxies of the YCbCr dots (x 255) of pixel pairs: per lane min / max (exact values
@@ -646,8 +716,8 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     // Per extreme, a mask of the steps whose pixels come within H3_PTOL of the lane's running
     // extreme (reset when the extreme moves past it): at the end it holds every step with a pixel
     // within H3_PTOL of the lane's final extreme, the only steps a rescan reads.
-    if (act && !(IDN_H3_PROBE & 1)) {
-      float imn[3] = {INFINITY, INFINITY, INFINITY}, imx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (!(IDN_H3_PROBE & 1)) {
+      float imn[3], imx[3];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -657,15 +727,17 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const h3f2 k2 = fma2(splat2(h3_ycf(c, 2)), B, fma2(splat2(h3_ycf(c, 1)), G, splat2(h3_ycf(c, 0)) * R));
-            imn[c] = __builtin_fminf(imn[c], __builtin_fminf(k2.x, k2.y));
-            imx[c] = __builtin_fmaxf(imx[c], __builtin_fmaxf(k2.x, k2.y));
+            const float lo2 = __builtin_fminf(k2.x, k2.y), hi2 = __builtin_fmaxf(k2.x, k2.y);
+            imn[c] = r + pp == 0 ? lo2 : __builtin_fminf(imn[c], lo2);
+            imx[c] = r + pp == 0 ? hi2 : __builtin_fmaxf(imx[c], hi2);
           }
         }
       const uint32_t bit = 1u << it;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        smn[c] = imn[c] < pmn[c] - H3_PTOL ? bit : (imn[c] <= pmn[c] + H3_PTOL ? smn[c] | bit : smn[c]);
-        smx[c] = imx[c] > pmx[c] + H3_PTOL ? bit : (imx[c] >= pmx[c] - H3_PTOL ? smx[c] | bit : smx[c]);
+        // branch-free: a new extreme past the tolerance restarts the mask; within it, adds the step
+        smn[c] = (imn[c] < pmn[c] - H3_PTOL ? 0u : smn[c]) | (imn[c] <= pmn[c] + H3_PTOL ? bit : 0u);
+        smx[c] = (imx[c] > pmx[c] + H3_PTOL ? 0u : smx[c]) | (imx[c] >= pmx[c] - H3_PTOL ? bit : 0u);
         pmn[c] = __builtin_fminf(pmn[c], imn[c]);
         pmx[c] = __builtin_fmaxf(pmx[c], imx[c]);
       }
@@ -711,13 +783,24 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
           aT[c] = (uint32_t)(T[c] < 0 ? -T[c] : T[c]);
           // branch-free: per-lane counts; the slot store is unconditional (a slot written
           // without the count moving is overwritten by the next append)
-          ct[c] += aT[c] != 0u ? 1u : 0u;
-          cl[c] += aT[c] < lo[c] ? 1u : 0u;
-          cb[c][na[c] * WLH_WG + threadIdx.x] = aT[c];
-          na[c] += aT[c] - lo[c] <= span[c] ? 1u : 0u;
+          // (IDN_H3_ZC: nonzero counts as the groups less the zeros, counted on the residue branch)
+          if (!IDN_H3_ZC) ct[c] += aT[c] != 0u ? 1u : 0u;
+          if (IDN_H3_BRW) {  // the subtraction's borrow as the below-window test
+            uint32_t dl;
+            cl[c] += __builtin_sub_overflow(aT[c], lo[c], &dl) ? 1u : 0u;
+            cb[c][na[c] * WLH_WG + threadIdx.x] = aT[c];
+            na[c] += dl <= span[c] ? 1u : 0u;
+          } else {
+            cl[c] += aT[c] < lo[c] ? 1u : 0u;
+            cb[c][na[c] * WLH_WG + threadIdx.x] = aT[c];
+            na[c] += aT[c] - lo[c] <= span[c] ? 1u : 0u;
+          }
         }
         const bool z = act && min(min(aT[0], aT[1]), aT[2]) == 0u;
         if (__builtin_amdgcn_ballot_w64(z)) {
+          if (IDN_H3_ZC)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) ct[c] += aT[c] == 0u ? 1u : 0u;  // zeros (past the image: dropped)
           auto trip = [&](int r, int k) { return (uint32_t)(px(r, k) | (px(r, k + 1) << 8) | (px(r, k + 2) << 16)); };
           const bool eq = h3_eqtrip(trip(2 * gy, 6 * gx), trip(2 * gy, 6 * gx + 3),
                                     trip(2 * gy + 1, 6 * gx), trip(2 * gy + 1, 6 * gx + 3));
@@ -731,19 +814,29 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch)
       haar_int(a1[0][ch], a1[1][ch], a1[2][ch], a1[3][ch], a2[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
-    if (act)
 #pragma unroll
-      for (int b = 0; b < 3; ++b) mom_lds(1, b, D2[b][0], D2[b][1], D2[b][2]);
-    int D3[3][3];
+    for (int b = 0; b < 3; ++b) mom_lds(1, b, D2[b][0], D2[b][1], D2[b][2]);  // (zeros past the image)
+    // level 3: quad lane `sub` < 3 takes band `sub` of the quad's group (haar_int's signs over
+    // the quad's four level-2 sums), its moments into the quad's LDS column of that band
+    if (IDN_H3_L3Q) {
+      int D3[3];
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      int aa;
-      haar_int(quad_get(a2[ch], 0), quad_get(a2[ch], 1), quad_get(a2[ch], 2), quad_get(a2[ch], 3), aa,
-               D3[0][ch], D3[1][ch], D3[2][ch]);
+      for (int ch = 0; ch < 3; ++ch)
+        D3[ch] = quad_get(a2[ch], 0) + __mul24(s3b[0], quad_get(a2[ch], 1)) +
+                 __mul24(s3b[1], quad_get(a2[ch], 2)) + __mul24(s3b[2], quad_get(a2[ch], 3));
+      if (sub < 3) mom_lds(2, sub, D3[0], D3[1], D3[2]);
+    } else {  // the quad's first lane, all three bands
+      int D3[3][3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        int aa;
+        haar_int(quad_get(a2[ch], 0), quad_get(a2[ch], 1), quad_get(a2[ch], 2), quad_get(a2[ch], 3), aa,
+                 D3[0][ch], D3[1][ch], D3[2][ch]);
+      }
+      if (sub == 0)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) mom_lds(2, b, D3[b][0], D3[b][1], D3[b][2]);
     }
-    if (act && sub == 0)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) mom_lds(2, b, D3[b][0], D3[b][1], D3[b][2]);
     // a wave moves its slots out once a lane could overflow in the next step (4 appends each)
 #pragma unroll
     for (int a = 0; a < 3; ++a)
@@ -755,7 +848,8 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   // counts (lanes past the image counted their zero groups: dropped)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    uint32_t a = colact ? ct[c] : 0u, b = colact ? cl[c] : 0u;
+    uint32_t a = colact ? (IDN_H3_ZC ? 4u * (uint32_t)nit - ct[c] : ct[c]) : 0u;  // nonzero |T|
+    uint32_t b = colact ? cl[c] : 0u;
     for (int o = 32; o > 0; o >>= 1) {
       a += (uint32_t)__shfl_xor((int)a, o);
       b += (uint32_t)__shfl_xor((int)b, o);
@@ -788,7 +882,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   // the workgroup's extreme proxies (lanes past the image hold +-inf)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    float a = pmn[c], b = pmx[c];
+    float a = colact ? pmn[c] : INFINITY, b = colact ? pmx[c] : -INFINITY;  // (lanes past the image)
     for (int o = 32; o > 0; o >>= 1) {
       a = __builtin_fminf(a, __shfl_xor(a, o));
       b = __builtin_fmaxf(b, __shfl_xor(b, o));

@@ -18,6 +18,9 @@ bash tools/bench_ops.sh "${1:-record}" gauss5 gauss3 box3 median5 median3 bilate
 timeout -k 10 300 python bench.py --op detect_e2e --no-cpu --no-copy --steps 200 --warmup 20 \
   >> "$OUT/bench.jsonl" 2> "$OUT/e2e.err" || exit 1
 tail -1 "$OUT/bench.jsonl"
+timeout -k 10 300 python bench.py --op detect_e2e_pipelined --no-cpu --no-copy --steps 400 --warmup 40 \
+  >> "$OUT/bench.jsonl" 2> "$OUT/e2e.err" || exit 1
+tail -1 "$OUT/bench.jsonl"
 timeout -k 10 300 python bench.py > "$OUT/default.json" 2> "$OUT/default.err" || exit 1
 cat "$OUT/default.json"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$(pwd)/$OUT/ks_default" -o k \
