@@ -170,8 +170,8 @@ __host__ __device__ inline int h3s_chunks(int h) { return ((h >> 3) + H3S_IT - 1
 #ifndef IDN_H3S_WPE
 #define IDN_H3S_WPE 1
 #endif
-#ifndef IDN_H3S_XCD
-#define IDN_H3S_XCD 0
+#ifndef IDN_H3S_XCD  // XCD-contiguous workgroup order: neighbouring strips share their edge lines
+#define IDN_H3S_XCD 1    // in one L2 (FETCH 536 -> 461 MB per 256 images, 187.9 -> 185.7 us)
 #endif
 template <bool GEN>
 __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_WPE))) void wl_h3_synth(const uint8_t* __restrict__ src, int h, int w,
