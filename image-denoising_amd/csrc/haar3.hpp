@@ -438,6 +438,13 @@ __global__ __launch_bounds__(H3_WIN_WG) void wl_h3_window(const uint8_t* __restr
   const int img = blockIdx.x;
   __shared__ uint32_t hist[3][H3_HB];
   __shared__ uint32_t nres[3];
+  {  // this image's statistics block as wl_init_stats leaves it (no colour keys): min keys ~0,
+     // max keys 0, the rest 0.0 -- the first kernel of the path, so no separate launch
+    double* st = stats + (size_t)img * WL_STATS;
+    for (int k = threadIdx.x; k < WL_STATS; k += H3_WIN_WG)
+      reinterpret_cast<unsigned long long*>(st)[k] =
+          k >= WlStats::MN64 && k < WlStats::MN64 + 3 ? ~0ull : 0ull;
+  }
   for (int k = threadIdx.x; k < 3 * H3_HB; k += H3_WIN_WG) (&hist[0][0])[k] = 0u;
   if (threadIdx.x < 3) nres[threadIdx.x] = 0u;
   __syncthreads();
@@ -571,6 +578,22 @@ __device__ __forceinline__ void h3_wave_flush(const uint32_t* buf, uint32_t n, u
   for (uint32_t j = 0; j < n; ++j) dst[base + j] = buf[j * WLH_WG + threadIdx.x];
 }
 typedef short h3s2 __attribute__((ext_vector_type(2)));
+#ifndef IDN_H3_MIN3  // one v_min3 / v_max3 per pixel pair in the proxies (309 -> 298 us)
+#define IDN_H3_MIN3 1
+#endif
+#ifndef IDN_H3_PK  // level 1 of the statistics on 16-bit pairs (the two groups side by side)
+#define IDN_H3_PK 1
+#endif
+__device__ __forceinline__ float h3_min3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float h3_max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 // rgb2ycbcr coefficients as floats: the fp32 proxy of a pixel's YCbCr dot x 255 (|error| < 0.03
 // for bytes: three roundings at magnitude < 2^16 plus the coefficients' own, < 1e-3 each)
 __device__ __forceinline__ float h3_ycf(int c, int k) {
@@ -727,9 +750,14 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const h3f2 k2 = fma2(splat2(h3_ycf(c, 2)), B, fma2(splat2(h3_ycf(c, 1)), G, splat2(h3_ycf(c, 0)) * R));
-            const float lo2 = __builtin_fminf(k2.x, k2.y), hi2 = __builtin_fmaxf(k2.x, k2.y);
-            imn[c] = r + pp == 0 ? lo2 : __builtin_fminf(imn[c], lo2);
-            imx[c] = r + pp == 0 ? hi2 : __builtin_fmaxf(imx[c], hi2);
+            if (IDN_H3_MIN3) {  // one v_min3 / v_max3 per pair (LLVM: min + min3 + canonicalising max)
+              imn[c] = r + pp == 0 ? h3_min3(k2.x, k2.x, k2.y) : h3_min3(imn[c], k2.x, k2.y);
+              imx[c] = r + pp == 0 ? h3_max3(k2.x, k2.x, k2.y) : h3_max3(imx[c], k2.x, k2.y);
+            } else {
+              const float lo2 = __builtin_fminf(k2.x, k2.y), hi2 = __builtin_fmaxf(k2.x, k2.y);
+              imn[c] = r + pp == 0 ? lo2 : __builtin_fminf(imn[c], lo2);
+              imx[c] = r + pp == 0 ? hi2 : __builtin_fmaxf(imx[c], hi2);
+            }
           }
         }
       const uint32_t bit = 1u << it;
@@ -746,13 +774,42 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
 #pragma unroll
     for (int gy = 0; gy < 2; ++gy) {
       int D[2][3][3];  // [gx][band][rgb]
+      h3s2 PD[3][3];   // IDN_H3_PK: [band][rgb] as 16-bit pairs (gx = 0 low, 1 high)
+      if (IDN_H3_PK) {
+        // the two groups side by side in 16-bit lanes: each pixel pair is one v_perm of the row
+        // dwords (bytes k and k + 6, zero-extended), the butterflies are v_pk_add / v_pk_sub_u16
+        // (|D| <= 510, sums <= 1020: no wrap), and the moments take the pairs as they are
+        auto pk = [&](int r, int k) {  // bytes k (gx 0) and k + 6 (gx 1) of row r
+          const int k1 = k + 6;
+          const uint32_t sel = (uint32_t)(k & 3) | 0x0C00u | ((uint32_t)(4 + (k1 & 3)) << 16) | 0x0C000000u;
+          return __builtin_bit_cast(h3s2, __builtin_amdgcn_perm(q[r][k1 >> 2], q[r][k >> 2], sel));
+        };
 #pragma unroll
-      for (int gx = 0; gx < 2; ++gx)
+        for (int ch = 0; ch < 3; ++ch) {
+          const h3s2 x00 = pk(2 * gy, ch), x01 = pk(2 * gy, 3 + ch), x10 = pk(2 * gy + 1, ch),
+                     x11 = pk(2 * gy + 1, 3 + ch);
+          const h3s2 lo0 = x00 + x10, lo1 = x01 + x11, hi0 = x00 - x10, hi1 = x01 - x11;
+          const h3s2 A = lo0 + lo1;
+          PD[0][ch] = lo0 - lo1;
+          PD[1][ch] = hi0 + hi1;
+          PD[2][ch] = hi0 - hi1;
+          a1[gy * 2][ch] = A.x;
+          a1[gy * 2 + 1][ch] = A.y;
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-          haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
-                   px(2 * gy + 1, 6 * gx + 3 + ch), a1[gy * 2 + gx][ch], D[gx][0][ch], D[gx][1][ch],
-                   D[gx][2][ch]);
+          for (int b = 0; b < 3; ++b) {
+            D[0][b][ch] = PD[b][ch].x;
+            D[1][b][ch] = PD[b][ch].y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int gx = 0; gx < 2; ++gx)
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch)
+            haar_int(px(2 * gy, 6 * gx + ch), px(2 * gy, 6 * gx + 3 + ch), px(2 * gy + 1, 6 * gx + ch),
+                     px(2 * gy + 1, 6 * gx + 3 + ch), a1[gy * 2 + gx][ch], D[gx][0][ch], D[gx][1][ch],
+                     D[gx][2][ch]);
+      }
       // the two groups' moments as 16-bit pairs: one v_dot2 per moment and band (|D| <= 510)
       if (IDN_H3_MOM == 1 && !(IDN_H3_PROBE & 4))
 #pragma unroll
@@ -764,7 +821,8 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
         h3s2 P[3];
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch)
-          P[ch] = __builtin_bit_cast(h3s2, __builtin_amdgcn_perm(D[1][b][ch], D[0][b][ch], 0x05040100u));
+          P[ch] = IDN_H3_PK ? PD[b][ch]
+                            : __builtin_bit_cast(h3s2, __builtin_amdgcn_perm(D[1][b][ch], D[0][b][ch], 0x05040100u));
         mom[b][0] = __builtin_amdgcn_sdot2(P[0], P[0], mom[b][0], false);
         mom[b][1] = __builtin_amdgcn_sdot2(P[1], P[1], mom[b][1], false);
         mom[b][2] = __builtin_amdgcn_sdot2(P[2], P[2], mom[b][2], false);

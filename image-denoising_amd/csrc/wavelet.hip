@@ -3618,11 +3618,10 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
   const int n = Lt.n;
   const int nthr = (Lt.h >> L) * (Lt.w >> L) * HaarSplit<L>::NS;
   const int nwg = (nthr + WLH_WG - 1) / WLH_WG;
-  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n,
-                     ycc_keys);
   if constexpr (L == 3) {
     // round 6 (haar3.hpp): window sample, one statistics read, sigma, one synthesis read
-    // (IDN_WAVELET_H3=0: the round-4 passes below)
+    // (IDN_WAVELET_H3=0: the round-4 passes below); the window kernel also clears its image's
+    // statistics block (wl_init_stats' values)
     const int nwg1 = h3_strips(Lt.w) * h3_chunks(Lt.h);
     if (src && !ycc_keys && knob("IDN_WAVELET_H3", 1) && (size_t)(3 * nwg1) <= Lt.part_per_img / 9) {
       hipLaunchKernelGGL(wl_h3_window, dim3(n), dim3(H3_WIN_WG), 0, st, src, Lt.h, Lt.w, row_stride,
@@ -3641,6 +3640,8 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
       return;
     }
   }
+  hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n,
+                     ycc_keys);
   if (!ycc_keys) {
     const int64_t np = (int64_t)Lt.h * Lt.w;
     // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
