@@ -119,6 +119,7 @@ __global__ void wl_h3_consts(double* __restrict__ stats, int n) {
 
 // ---- wl_h3_synth ---------------------------------------------------------------------------------
 typedef float h3f2 __attribute__((ext_vector_type(2)));
+typedef short h3s2 __attribute__((ext_vector_type(2)));
 // lane value of quad member k (DPP quad_perm broadcast, one VALU op)
 __device__ __forceinline__ int quad_get(int v, int k) {
   switch (k) {
@@ -151,6 +152,9 @@ __device__ __forceinline__ h3f2 pk_sub_clamp(h3f2 a, h3f2 b) {
 }
 #ifndef IDN_H3S_Q3  // 1: level 3 of the synthesis split across the quad's lanes (A/B; 207 against
 #define IDN_H3S_Q3 0    // 187 us with each lane forming all: the DPP round trips lengthen the chain)
+#endif
+#ifndef IDN_H3S_PK  // level 1 of the synthesis's analysis on 16-bit integer pairs
+#define IDN_H3S_PK 1
 #endif
 #ifndef IDN_H3S_CLAMP  // 1: the inner clip as the clamp bit of the packed adds (A/B: 0 = v_max clamp)
 #define IDN_H3S_CLAMP 1
@@ -229,6 +233,28 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
   // level 1 on the group pairs (gx = 0, 1 of row pair gy) as fp32 pairs: S1[gy][rgb] sums,
   // D1[gy][band][rgb] details
   h3f2 S1[2][3], D1[2][3][3];
+  if (IDN_H3S_PK) {
+    // as wl_h3_stats: the two groups side by side in 16-bit lanes (v_perm of the row dwords,
+    // v_pk_add / sub_u16: exact), then each 16-bit result to float
+    auto pk = [&](int r, int k) {  // bytes k (gx 0) and k + 6 (gx 1) of row r
+      const int k1 = k + 6;
+      const uint32_t sel = (uint32_t)(k & 3) | 0x0C00u | ((uint32_t)(4 + (k1 & 3)) << 16) | 0x0C000000u;
+      return __builtin_bit_cast(h3s2, __builtin_amdgcn_perm(q[r][k1 >> 2], q[r][k >> 2], sel));
+    };
+    auto f2 = [](h3s2 v) { return h3f2{(float)v.x, (float)v.y}; };
+#pragma unroll
+    for (int gy = 0; gy < 2; ++gy)
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const h3s2 x00 = pk(2 * gy, ch), x01 = pk(2 * gy, 3 + ch), x10 = pk(2 * gy + 1, ch),
+                   x11 = pk(2 * gy + 1, 3 + ch);
+        const h3s2 lo0 = x00 + x10, lo1 = x01 + x11, hi0 = x00 - x10, hi1 = x01 - x11;
+        S1[gy][ch] = f2(lo0 + lo1);
+        D1[gy][0][ch] = f2(lo0 - lo1);
+        D1[gy][1][ch] = f2(hi0 + hi1);
+        D1[gy][2][ch] = f2(hi0 - hi1);
+      }
+  } else
 #pragma unroll
   for (int gy = 0; gy < 2; ++gy)
 #pragma unroll
@@ -577,9 +603,11 @@ __device__ __forceinline__ void h3_wave_flush(const uint32_t* buf, uint32_t n, u
   base = (uint32_t)__shfl((int)base, 63) + inc - n;
   for (uint32_t j = 0; j < n; ++j) dst[base + j] = buf[j * WLH_WG + threadIdx.x];
 }
-typedef short h3s2 __attribute__((ext_vector_type(2)));
 #ifndef IDN_H3_MIN3  // one v_min3 / v_max3 per pixel pair in the proxies (309 -> 298 us)
 #define IDN_H3_MIN3 1
+#endif
+#ifndef IDN_H3_MICRO  // running extremes by v_min3 / v_max3, level 2 from the packed sums, the
+#define IDN_H3_MICRO 1   // residue test's ballot straight from the compare
 #endif
 #ifndef IDN_H3_PK  // level 1 of the statistics on 16-bit pairs (the two groups side by side)
 #define IDN_H3_PK 1
@@ -718,6 +746,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   const uint32_t pos00 = (uint32_t)(4 * by0 + sy / 2) * W1 + (uint32_t)(x0 / 2);
   // haar_int's band signs of x01, x10, x11 for band `sub` (ad: - + -, da: + - -, dd: - - +)
   const int s3b[3] = {sub == 1 ? 1 : -1, sub == 0 ? 1 : -1, sub == 2 ? 1 : -1};
+  const uint64_t actmask = __builtin_amdgcn_ballot_w64(colact);  // lanes inside the image
   uint32_t qn[4][3] = {};
   load_q(0, qn);
   // Lanes past the image hold zero pixels throughout (load_q never fills them): their moments
@@ -766,11 +795,12 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
         // branch-free: a new extreme past the tolerance restarts the mask; within it, adds the step
         smn[c] = (imn[c] < pmn[c] - H3_PTOL ? 0u : smn[c]) | (imn[c] <= pmn[c] + H3_PTOL ? bit : 0u);
         smx[c] = (imx[c] > pmx[c] + H3_PTOL ? 0u : smx[c]) | (imx[c] >= pmx[c] - H3_PTOL ? bit : 0u);
-        pmn[c] = __builtin_fminf(pmn[c], imn[c]);
-        pmx[c] = __builtin_fmaxf(pmx[c], imx[c]);
+        pmn[c] = IDN_H3_MICRO ? h3_min3(pmn[c], imn[c], imn[c]) : __builtin_fminf(pmn[c], imn[c]);
+        pmx[c] = IDN_H3_MICRO ? h3_max3(pmx[c], imx[c], imx[c]) : __builtin_fmaxf(pmx[c], imx[c]);
       }
     }
     int a1[4][3];
+    h3s2 Apk[2][3];  // IDN_H3_PK: the level-1 sums of row pair gy as 16-bit pairs (gx = 0 low)
 #pragma unroll
     for (int gy = 0; gy < 2; ++gy) {
       int D[2][3][3];  // [gx][band][rgb]
@@ -795,6 +825,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
           PD[2][ch] = hi0 - hi1;
           a1[gy * 2][ch] = A.x;
           a1[gy * 2 + 1][ch] = A.y;
+          Apk[gy][ch] = A;
 #pragma unroll
           for (int b = 0; b < 3; ++b) {
             D[0][b][ch] = PD[b][ch].x;
@@ -855,7 +886,8 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
           }
         }
         const bool z = act && min(min(aT[0], aT[1]), aT[2]) == 0u;
-        if (__builtin_amdgcn_ballot_w64(z)) {
+        if (IDN_H3_MICRO ? (__builtin_amdgcn_ballot_w64(min(min(aT[0], aT[1]), aT[2]) == 0u) & actmask) != 0ull
+                         : __builtin_amdgcn_ballot_w64(z) != 0ull) {
           if (IDN_H3_ZC)
 #pragma unroll
             for (int c = 0; c < 3; ++c) ct[c] += aT[c] == 0u ? 1u : 0u;  // zeros (past the image: dropped)
@@ -871,7 +903,15 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     int a2[3], D2[3][3];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch)
-      haar_int(a1[0][ch], a1[1][ch], a1[2][ch], a1[3][ch], a2[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
+      if (IDN_H3_PK && IDN_H3_MICRO) {  // level 2 from the packed level-1 sums of the two row pairs
+        const h3s2 L = Apk[0][ch] + Apk[1][ch], H = Apk[0][ch] - Apk[1][ch];  // {lo0, lo1}, {hi0, hi1}
+        a2[ch] = L.x + L.y;
+        D2[0][ch] = L.x - L.y;
+        D2[1][ch] = H.x + H.y;
+        D2[2][ch] = H.x - H.y;
+      } else {
+        haar_int(a1[0][ch], a1[1][ch], a1[2][ch], a1[3][ch], a2[ch], D2[0][ch], D2[1][ch], D2[2][ch]);
+      }
 #pragma unroll
     for (int b = 0; b < 3; ++b) mom_lds(1, b, D2[b][0], D2[b][1], D2[b][2]);  // (zeros past the image)
     // level 3: quad lane `sub` < 3 takes band `sub` of the quad's group (haar_int's signs over

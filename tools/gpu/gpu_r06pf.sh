@@ -2,7 +2,7 @@
 # round 6: the product after the Haar L3 changes -- wavelet / config / jpeg GPU tests, bench lines of
 # wavelet_haar3 and cfg5, kernel stats
 set -u
-OUT=gpurun_out/r06pj
+OUT=gpurun_out/r06pp
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_wavelet_gpu.py tests/test_configs_gpu.py tests/test_live_path_gpu.py -q --timeout 300 \
