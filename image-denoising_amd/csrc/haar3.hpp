@@ -560,8 +560,8 @@ __global__ __launch_bounds__(H3_WIN_WG) void wl_h3_window(const uint8_t* __restr
 #ifndef IDN_H3_K
 #define IDN_H3_K 8
 #endif
-#ifndef IDN_H3_WPE  // waves per EU the statistics kernel is built for: 3 caps it at 168 VGPRs (the
-#define IDN_H3_WPE 3    // branch-free loop body takes 242 uncapped: two waves, 352 against 308.5 us)
+#ifndef IDN_H3_WPE  // waves per EU the statistics kernel is scheduled for (~158 VGPRs either way:
+#define IDN_H3_WPE 3    // without the hint LLVM's schedule of the branch-free body ran 352 us, with 3 308.5)
 #endif
 #ifndef IDN_H3_MOM  // level-1 moments: 0 v_dot2 on group pairs, 1 24-bit multiply-adds
 #define IDN_H3_MOM 0
@@ -654,6 +654,9 @@ __device__ __forceinline__ int ykey(int c, int r, int g, int b) {  // exact YCbC
 // chunks, images).  Workspace (the image's slot): |T| candidates [3][P] u32, residues [P] u32
 // (level-1 position | channel mask << 28), P = (h / 2) (w / 2).
 __host__ __device__ inline int h3_chunks(int h) { return ((h >> 3) + H3_IT - 1) / H3_IT; }
+// MM = true: the exact fp64 YCbCr min / max alone (the proxies, their rescans and the keys), for
+// the other wavelets' u8 input in place of wl_color_minmax (ws / part unused)
+template <bool MM>
 __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_WPE))) void wl_h3_stats(const uint8_t* __restrict__ src, int h, int w,
                                                       int64_t row_stride, wreal* __restrict__ ws,
                                                       size_t img_floats, double* __restrict__ stats,
@@ -682,18 +685,21 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   __shared__ uint32_t cnt_s[6];
   __shared__ float kred[6][WLH_WG / 64];
   __shared__ double dred[6][WLH_WG / 64];
+  if constexpr (!MM) {
 #pragma unroll
-  for (int k = 0; k < 3 * 6; ++k) ml2[k][threadIdx.x] = 0;
-  if (threadIdx.x < WLH_WG / 4)
+    for (int k = 0; k < 3 * 6; ++k) ml2[k][threadIdx.x] = 0;
+    if (threadIdx.x < WLH_WG / 4)
 #pragma unroll
-    for (int k = 0; k < 3 * 6; ++k) ml3[k][threadIdx.x] = 0;
-  if (threadIdx.x < 6) cnt_s[threadIdx.x] = 0u;
-  uint32_t lo[3], span[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    lo[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sel[c].lo);
-    span[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(sel[c].hi - sel[c].lo));
+      for (int k = 0; k < 3 * 6; ++k) ml3[k][threadIdx.x] = 0;
+    if (threadIdx.x < 6) cnt_s[threadIdx.x] = 0u;
   }
+  uint32_t lo[3] = {0u, 0u, 0u}, span[3] = {0u, 0u, 0u};
+  if constexpr (!MM)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      lo[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sel[c].lo);
+      span[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(sel[c].hi - sel[c].lo));
+    }
   __syncthreads();
   int mom[3][6];
 #pragma unroll
@@ -799,6 +805,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
         pmx[c] = IDN_H3_MICRO ? h3_max3(pmx[c], imx[c], imx[c]) : __builtin_fmaxf(pmx[c], imx[c]);
       }
     }
+    if constexpr (MM) continue;  // (the min / max alone)
     int a1[4][3];
     h3s2 Apk[2][3];  // IDN_H3_PK: the level-1 sums of row pair gy as 16-bit pairs (gx = 0 low)
 #pragma unroll
@@ -899,7 +906,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
         }
       }
     }
-    if (IDN_H3_PROBE & 8) continue;
+    if (MM || (IDN_H3_PROBE & 8)) continue;
     int a2[3], D2[3][3];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch)
@@ -940,9 +947,10 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     for (int a = 0; a < 3; ++a)
       if (__builtin_amdgcn_ballot_w64(na[a] > (uint32_t)(H3_K - 4))) flush(a);
   }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if constexpr (!MM) {
 #pragma unroll
   for (int a = 0; a < 4; ++a) flush(a);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // counts (lanes past the image counted their zero groups: dropped)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -977,6 +985,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
         if (lane == 0) red[(c * L + l) * 3 + b][wave] = v;
       }
   }
+  }  // !MM
   // the workgroup's extreme proxies (lanes past the image hold +-inf)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -991,7 +1000,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     }
   }
   __syncthreads();
-  if (threadIdx.x < 3 * L * 3) {
+  if (!MM && threadIdx.x < 3 * L * 3) {
     const int k = threadIdx.x, b = k % 3, l = (k / 3) % L, c = k / (3 * L);
     double t = red[k][0];
 #pragma unroll
@@ -999,7 +1008,7 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
     part[img * part_per_img + (size_t)(c * 3 + b) * (part_per_img / 9) + (size_t)l * gridDim.x +
          (size_t)wg] = t;
   }
-  if (threadIdx.x < 3) {
+  if (!MM && threadIdx.x < 3) {
     atomicAdd(&sel[threadIdx.x].n_t, cnt_s[threadIdx.x]);
     atomicAdd(&sel[threadIdx.x].n_lo, cnt_s[3 + threadIdx.x]);
   }

@@ -3626,7 +3626,7 @@ static void wl_run_haar(const uint8_t* src, const double* in64, uint8_t* out_u8,
     if (src && !ycc_keys && knob("IDN_WAVELET_H3", 1) && (size_t)(3 * nwg1) <= Lt.part_per_img / 9) {
       hipLaunchKernelGGL(wl_h3_window, dim3(n), dim3(H3_WIN_WG), 0, st, src, Lt.h, Lt.w, row_stride,
                          stats, knob("IDN_WAVELET_H3FB", 0));
-      hipLaunchKernelGGL(wl_h3_stats, dim3(nwg1, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
+      hipLaunchKernelGGL(wl_h3_stats<false>, dim3(nwg1, n), dim3(WLH_WG), 0, st, src, Lt.h, Lt.w,
                          row_stride, wsf, Lt.img_floats, stats, part, Lt.part_per_img);
       hipLaunchKernelGGL(wl_h3_sigma, dim3(n * 3), dim3(WLM_WG), 0, st, src, row_stride, wsf,
                          Lt.img_floats, stats, Lt, (const double*)part, nwg1);
@@ -3737,12 +3737,22 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
   hipLaunchKernelGGL(wl_init_stats, dim3((n * WL_STATS + 255) / 256), dim3(256), 0, st, stats, n,
                      ycc_keys);
   if (!ycc_keys) {
-    const int64_t np = (int64_t)Lt.h * Lt.w;
-    // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
-    int gx = (int)((np / 4 + 255) / 256);
-    if (gx > 24) gx = 24;
-    hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
-                       row_stride, stats);
+    // u8 input in whole 8x8 blocks with dword-aligned rows: the Haar path's proxy min / max
+    // (wl_h3_stats<true>: fp32 proxies, fp64 rescans of the steps near an extreme); else the
+    // fp64 chain on every pixel
+    if (src && knob("IDN_WAVELET_MMPROXY", 1) && Lt.h % 8 == 0 && Lt.w % 8 == 0 && row_stride % 4 == 0 &&
+        ((uintptr_t)src & 3) == 0) {
+      hipLaunchKernelGGL(wl_h3_stats<true>, dim3(h3_strips(Lt.w) * h3_chunks(Lt.h), n), dim3(WLH_WG), 0, st,
+                         src, Lt.h, Lt.w, row_stride, wsf, Lt.img_floats, stats, (double*)nullptr,
+                         (size_t)0);
+    } else {
+      const int64_t np = (int64_t)Lt.h * Lt.w;
+      // a few long-lived workgroups per image: per-wave reduction + atomics are the fixed cost
+      int gx = (int)((np / 4 + 255) / 256);
+      if (gx > 24) gx = 24;
+      hipLaunchKernelGGL(wl_color_minmax, dim3(gx, n), dim3(256), 0, st, src, in64, Lt.h, Lt.w,
+                         row_stride, stats);
+    }
   }
   double* part = (double*)((char*)ws + Lt.part_off);
   // sigma from level-1 dd codes (wl_haar_median<.., true>) when the channel's input-plane slot
