@@ -654,6 +654,13 @@ __device__ __forceinline__ int ykey(int c, int r, int g, int b) {  // exact YCbC
 // chunks, images).  Workspace (the image's slot): |T| candidates [3][P] u32, residues [P] u32
 // (level-1 position | channel mask << 28), P = (h / 2) (w / 2).
 __host__ __device__ inline int h3_chunks(int h) { return ((h >> 3) + H3_IT - 1) / H3_IT; }
+// the min / max form's block rows per workgroup: its workgroups are short and light, so more
+// of them even out the last round of the grid
+#ifndef IDN_H3_ITMM
+#define IDN_H3_ITMM 8  // (A/B, bior1.5 u8: 4 132.2, 8 123.9, 16 128.4 us; the statistics at 8 instead of 16: 314 against 274)
+#endif
+constexpr int H3_IT_MM = IDN_H3_ITMM;
+__host__ __device__ inline int h3_chunks_mm(int h) { return ((h >> 3) + H3_IT_MM - 1) / H3_IT_MM; }
 // MM = true: the exact fp64 YCbCr min / max alone (the proxies, their rescans and the keys), for
 // the other wavelets' u8 input in place of wl_color_minmax (ws / part unused)
 template <bool MM>
@@ -669,7 +676,8 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3_W
   const int strips = h3_strips(w);
   const int strip = wg % strips, chunk = wg / strips;
   const int sub = threadIdx.x & 3, bx = strip * H3_COLS + (threadIdx.x >> 2);
-  const int by0 = chunk * H3_IT, nit = min(H3_IT, nby - by0);  // block rows of this workgroup
+  constexpr int IT = MM ? H3_IT_MM : H3_IT;
+  const int by0 = chunk * IT, nit = min(IT, nby - by0);  // block rows of this workgroup
   const bool colact = bx < nbx;
   const int x0 = bx * 8 + (sub & 1) * 4, sy = (sub >> 1) * 4;
   double* st = stats + (size_t)img * WL_STATS;

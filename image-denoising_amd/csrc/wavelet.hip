@@ -3742,7 +3742,7 @@ static int wl_run(const uint8_t* src, const double* in64, uint8_t* out_u8, float
     // fp64 chain on every pixel
     if (src && knob("IDN_WAVELET_MMPROXY", 1) && Lt.h % 8 == 0 && Lt.w % 8 == 0 && row_stride % 4 == 0 &&
         ((uintptr_t)src & 3) == 0) {
-      hipLaunchKernelGGL(wl_h3_stats<true>, dim3(h3_strips(Lt.w) * h3_chunks(Lt.h), n), dim3(WLH_WG), 0, st,
+      hipLaunchKernelGGL(wl_h3_stats<true>, dim3(h3_strips(Lt.w) * h3_chunks_mm(Lt.h), n), dim3(WLH_WG), 0, st,
                          src, Lt.h, Lt.w, row_stride, wsf, Lt.img_floats, stats, (double*)nullptr,
                          (size_t)0);
     } else {
