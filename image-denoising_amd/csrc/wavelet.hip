@@ -1746,6 +1746,9 @@ __device__ __forceinline__ T abs_t(T x) {
   if constexpr (sizeof(T) == 4) return __builtin_fabsf(x);
   else return __builtin_fabs(x);
 }
+#ifndef IDN_SOFT_MED3  // fp32 soft thresholds as d - med3(d, -t, t) (A/B: 0 = compare / copysign)
+#define IDN_SOFT_MED3 1
+#endif
 template <typename T>
 __device__ __forceinline__ T clip01_t(T x) {
   if constexpr (sizeof(T) == 4) return __builtin_fminf(__builtin_fmaxf(x, 0.f), 1.f);
@@ -1753,9 +1756,16 @@ __device__ __forceinline__ T clip01_t(T x) {
 }
 template <typename T>
 __device__ __forceinline__ T soft_t(T d, T t) {
-  const T m = abs_t<T>(d) - t;
-  if constexpr (sizeof(T) == 4) return m > 0.f ? __builtin_copysignf(m, d) : 0.f;
-  else return m > 0.0 ? __builtin_copysign(m, d) : 0.0;
+  // fp32: d - clamp(d, -t, t), one v_med3 and a subtraction -- the same value (d -+ t rounds as
+  // |d| - t does, +0 inside the threshold) for the compare / copysign / select of the fp64 form
+  if constexpr (sizeof(T) == 4) {
+    if (IDN_SOFT_MED3) return d - __builtin_amdgcn_fmed3f(d, -t, t);
+    const T m = abs_t<T>(d) - t;
+    return m > 0.f ? __builtin_copysignf(m, d) : 0.f;
+  } else {
+    const T m = abs_t<T>(d) - t;
+    return m > 0.0 ? __builtin_copysign(m, d) : 0.0;
+  }
 }
 template <typename T>
 __device__ __forceinline__ T dot3_t(T x0, T x1, T x2, T m0, T m1, T m2) {
