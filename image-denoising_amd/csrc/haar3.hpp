@@ -423,28 +423,33 @@ __global__ __launch_bounds__(WLH_WG) __attribute__((amdgpu_waves_per_eu(IDN_H3S_
 }
 
 // ---- wl_h3_window ---------------------------------------------------------------------------------
-// |T| histogram bins: floor(log2 |T|) and the next 6 bits (monotone in |T|; |T| < 2^31)
-constexpr int H3_HB = 2048;
+// |T| histogram bins: floor(log2 |T|) and the next H3_MB bits (monotone in |T|; |T| < 2^31)
+#ifndef IDN_H3_MB  // mantissa bits of the window histogram (finer bins: a narrower window)
+#define IDN_H3_MB 6
+#endif
+constexpr int H3_MB = IDN_H3_MB;
+constexpr uint32_t H3_MM = (1u << H3_MB) - 1u;
+constexpr int H3_HB = 32 << H3_MB;
 constexpr int H3_WIN_WG = 1024;
 constexpr int H3_SAMPLE = 16;  // every 16th level-1 row (rows 2i, 2i + 1 of the image)
 __device__ __forceinline__ int h3_bin(uint32_t a) {  // a >= 1
   const int e = 31 - __clz((int)a);
-  const uint32_t m = e >= 6 ? (a >> (e - 6)) & 63u : (a << (6 - e)) & 63u;
-  return e * 64 + (int)m;
+  const uint32_t m = e >= H3_MB ? (a >> (e - H3_MB)) & H3_MM : (a << (H3_MB - e)) & H3_MM;
+  return (e << H3_MB) + (int)m;
 }
-// the largest |T| whose bin is <= b (bins below 64 hold few integers: found by search)
+// the largest |T| whose bin is <= b (bins below 2^H3_MB hold few integers: found by search)
 __device__ uint32_t h3_bin_hi(int b) {
-  const int n = b + 1, e = n >> 6;
+  const int n = b + 1, e = n >> H3_MB;
   if (e >= 31) return 0xFFFFFFFFu;
-  if (e >= 6) return ((uint32_t)(64 + (n & 63)) << (e - 6)) - 1u;
+  if (e >= H3_MB) return ((uint32_t)((1 << H3_MB) + (n & (int)H3_MM)) << (e - H3_MB)) - 1u;
   uint32_t hi = 0;
-  for (uint32_t a = 1; a < 64; ++a)
+  for (uint32_t a = 1; a < (1u << H3_MB); ++a)
     if (h3_bin(a) <= b) hi = a;
   return hi;
 }
-__device__ __forceinline__ uint32_t h3_bin_lo(int b) {  // the smallest |T| of bin b, 1 below 64
-  const int e = b >> 6;
-  return e >= 6 ? (uint32_t)(64 + (b & 63)) << (e - 6) : 1u;
+__device__ __forceinline__ uint32_t h3_bin_lo(int b) {  // the smallest |T| of bin b, 1 below 2^H3_MB
+  const int e = b >> H3_MB;
+  return e >= H3_MB ? (uint32_t)((1 << H3_MB) + (b & (int)H3_MM)) << (e - H3_MB) : 1u;
 }
 // equal RGB triples along the rows or the columns of a 2x2 group: the reference's dd is x - x = 0
 __device__ __forceinline__ bool h3_eqtrip(uint32_t t00, uint32_t t01, uint32_t t10, uint32_t t11) {
